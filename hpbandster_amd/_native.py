@@ -1,0 +1,95 @@
+"""ctypes binding of libhbx.so (include/hbx.h).
+
+The engine has exactly one compute path: the HIP kernels in this library.  There is no CPU
+fallback -- if the library is missing or cannot be loaded, every engine call raises.
+"""
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libhbx.so")
+
+_lock = threading.Lock()
+_lib = None
+
+c_i32, c_i64, c_f64p, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p
+
+# name -> (restype, argtypes); every pointer is passed as an integer address (c_void_p)
+SIGNATURES = {
+    "hbx_last_error": (ctypes.c_char_p, []),
+    "hbx_version": (ctypes.c_char_p, []),
+    "hbx_kde_param_bytes": (c_i64, []),
+    "hbx_kde_est_bytes": (c_i64, []),
+    "hbx_acq_result_bytes": (c_i64, []),
+    "hbx_max_dims": (c_i32, []),
+    "hbx_sort_scratch_bytes": (c_i64, [c_i64]),
+    "hbx_seg_argsort": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_kde_fit": (c_i32, [c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp, c_vp]),
+    "hbx_kde_bucket": (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "hbx_kde_prepare": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_logpdf": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "hbx_kde_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "hbx_kde_acquire": (c_i32, [c_vp, c_i64, c_i32, c_i64,
+                                c_vp, c_vp, c_vp, c_vp, c_i32,
+                                c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
+                                c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_kde_result_ptr": (c_vp, [c_vp]),
+    "hbx_kde_pdf_scratch_bytes": (c_i64, [c_i64]),
+    "hbx_kde_pdf_exact": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_sh_promote": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+}
+
+
+class HbxError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libhbx.so (once).  Raises if it is not built: there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HbxError("libhbx.so not found at %s -- build it with `python -m hpbandster_amd.build` "
+                           "(the engine has no CPU fallback)" % LIB_PATH)
+        # torch first: its bundled libamdhip64.so.7 then satisfies libhbx's HIP dependency (same
+        # SONAME), so kernels and torch's allocator/streams share one HIP runtime.
+        import torch  # noqa: F401
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().hbx_last_error()
+        raise HbxError("libhbx error %d: %s" % (rc, msg.decode() if msg else "?"))
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args))
+
+
+def ptr(t):
+    """Device/host address of a torch tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,106 @@
+// hbx_common.h -- shared definitions for the MI355X (gfx950) KDE-acquisition / SH-promotion engine.
+//
+// Everything in this directory is compiled by hipcc --offload-arch=gfx950 into ONE shared library
+// (hpbandster_amd/_lib/libhbx.so) whose extern "C" entry points are declared in include/hbx.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HBX_MAX_D 256          // largest configuration-space dimension the engine accepts
+#define HBX_WAVE 64            // CDNA wavefront width
+
+#include "hbx.h"  // the public C ABI (include/hbx.h): every definition here must match it
+
+// Sets the thread-local error message returned by hbx_last_error(); returns `code`.
+int hbx_fail(int code, const char* fmt, ...);
+
+#define HBX_HIP(call)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (call);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return hbx_fail(HBX_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), \
+                      __FILE__, __LINE__);                                            \
+  } while (0)
+
+#define HBX_LAUNCH_CHECK()                                                            \
+  do {                                                                                \
+    hipError_t _e = hipGetLastError();                                                \
+    if (_e != hipSuccess)                                                             \
+      return hbx_fail(HBX_ERR_HIP, "kernel launch failed: %s (%s:%d)",               \
+                      hipGetErrorString(_e), __FILE__, __LINE__);                    \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// KDE model parameters, one block per KDE (good or bad).  Written on the device by
+// kde_params_kernel from (data rows, bandwidths, level counts); read by the scoring kernels.
+// Python never looks inside: it only allocates hbx_kde_param_bytes() bytes.
+struct KdeParams {
+  int32_t n;          // observations in this KDE
+  int32_t D;          // total dims
+  int32_t dc;         // continuous dims
+  int32_t du;         // active categorical dims (num_levels > 1)
+  int32_t nconst;     // categorical dims with a single observed level (bw == 0)
+  int32_t nan_all;    // a continuous bandwidth is 0 -> reference pdf is NaN everywhere
+  int32_t has_neg;    // some active categorical dim has 1 - h < 0 (signed sums needed)
+  int32_t unsupported;// bandwidth/level combination the engine does not model (error)
+  int32_t stride;     // floats per observation row of the fp32 table
+  int32_t dc_pad;     // continuous slots in the table (template bucket)
+  int32_t du_pad;     // categorical slots in the table (template bucket)
+  int32_t pad0;
+  double log_norm;    // ln pdf = ln(S) + log_norm  (S = sum of 2^(t - M0))
+  double m0_log2;     // M0: upper bound of the per-pair log2 kernel product
+  double lb_sum;      // sum over active categorical dims of log2(h/(c-1))
+  double prod_bw_c;   // sequential product of continuous bandwidths (reference op order)
+  float cmax;         // max_j |C_j| over the table (error bound)
+  float sum_abs_delta;// sum |delta_u| over finite deltas (error bound)
+  int32_t cont_dim[HBX_MAX_D];
+  double cont_scale[HBX_MAX_D];     // s_c = sqrt(log2(e) / 2) / h_c
+  double center[HBX_MAX_D];         // per continuous slot: mean of the KDE's data (coordinates are
+                                    // centred before scaling so the fp32 expansion keeps precision)
+  float xmax[HBX_MAX_D];            // max_j |X'_jc| (error bound)
+  int32_t cat_dim[HBX_MAX_D];
+  float cat_delta[HBX_MAX_D];       // log2|1-h| - log2(h/(c-1)); -1e30 when 1-h == 0
+  float cat_negf[HBX_MAX_D];        // 1.0 when 1-h < 0
+  int32_t const_dim[HBX_MAX_D];
+  double const_level[HBX_MAX_D];
+  // exact fp64 re-score (reference arithmetic)
+  int32_t vartype[HBX_MAX_D];       // 0 = continuous 'c', 1 = unordered categorical 'u'
+  int32_t nlev[HBX_MAX_D];
+  double bw[HBX_MAX_D];
+};
+
+// Per-candidate output of the fp32 log-domain scoring kernel, one per KDE.
+struct KdeEst {
+  float lpos;   // ln(sum of positive terms) + log_norm   (NaN: structural NaN pdf)
+  float lneg;   // ln(sum of negative terms) + log_norm   (-inf when none)
+  float err;    // relative error bound on each sum
+  float pad;
+};
+
+// Result of one acquisition on one device.
+struct AcqResult {
+  int64_t index;     // winning candidate (global index), -1 when no finite score exists
+  double score;      // its exact fp64 score max(1e-8, g) / max(l, 1e-8)
+  double pdf_l;      // exact fp64 l(x) of the winner
+  double pdf_g;      // exact fp64 g(x) of the winner
+  int64_t shortlist; // candidates re-scored in fp64
+  int32_t flags;     // bit0: fp64 overflow risk -> every candidate re-scored
+  int32_t pad;
+};
+
+// float <-> order-preserving uint32 (for atomicMin on floats of either sign)
+__device__ __forceinline__ uint32_t hbx_f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float hbx_ord2f(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// double -> order-preserving uint64 with every NaN mapped past +inf
+__device__ __forceinline__ uint64_t hbx_d2ord(double d) {
+  if (d != d) return ~0ull;
+  uint64_t u = (uint64_t)__double_as_longlong(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}

@@ -1,0 +1,194 @@
+// hbx_fit.hip -- batched BOHB KDE refit on MI355X: per-budget (segment) stable argsort of the
+// losses, good/bad split and normal-reference bandwidths + observed level counts.
+//
+// Reference: bohb.py:220-246 (argsort, good = head, bad = tail, KDEMultivariate(..., 'normal_reference'))
+// -> SM:_kernel_base.py:250-265 (bw = 1.06 * np.std(X, axis=0) * n**(-1/(4+D))) and
+// SM:kernels.py:59-60 (num_levels = np.unique(column).size).
+//
+// Bit-exactness: np.std(X, axis=0) is reproduced operation for operation -- mean = sum / n,
+// var = sum((x - mean)^2) / n, sqrt -- with numpy's reduction order: sequential down each column
+// for D > 1, and (D == 1, where numpy reduces a contiguous vector) pairwise summation over
+// 8192-element buffers.  The factor n**(-1/(4+D)) is a host-side glibc pow() per segment, passed in,
+// because the device pow() is not guaranteed to round the same way.
+#include "hbx_common.h"
+#include "hbx_sort.h"
+
+__device__ double np_pairwise_gather(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
+                                     double mean, bool sq);
+
+// sum of (x) or ((x - mean)^2) over a gathered column, numpy pairwise order (one leaf <= 128)
+__device__ double pw_leaf(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n, double mean,
+                          bool sq) {
+  auto v = [&](int64_t i) -> double {
+    const double x = X[rows[i] * (int64_t)D + d];
+    if (!sq) return x;
+    const double t = x - mean;
+    return t * t;
+  };
+  if (n < 8) {
+    double res = 0.0;
+    for (int64_t i = 0; i < n; ++i) res += v(i);
+    return res;
+  }
+  double r0 = v(0), r1 = v(1), r2 = v(2), r3 = v(3), r4 = v(4), r5 = v(5), r6 = v(6), r7 = v(7);
+  int64_t i;
+  for (i = 8; i < n - (n % 8); i += 8) {
+    r0 += v(i + 0); r1 += v(i + 1); r2 += v(i + 2); r3 += v(i + 3);
+    r4 += v(i + 4); r5 += v(i + 5); r6 += v(i + 6); r7 += v(i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += v(i);
+  return res;
+}
+
+__device__ double np_pairwise_gather(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
+                                     double mean, bool sq) {
+  if (n <= 128) return pw_leaf(X, D, d, rows, n, mean, sq);
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  // depth <= log2(8192/128) + 1 here (called per 8192 buffer) -> bounded recursion
+  return np_pairwise_gather(X, D, d, rows, n2, mean, sq) +
+         np_pairwise_gather(X, D, d, rows + n2, n - n2, mean, sq);
+}
+
+__device__ double np_sum_column(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
+                                double mean, bool sq) {
+  if (D > 1) {  // axis-0 reduction of an (n, D) C-array: sequential down the column
+    double acc = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+      const double x = X[rows[i] * (int64_t)D + d];
+      if (sq) {
+        const double t = x - mean;
+        acc = acc + t * t;
+      } else {
+        acc = acc + x;
+      }
+    }
+    return acc;
+  }
+  double acc = 0.0;  // contiguous vector: pairwise per 8192-element ufunc buffer
+  for (int64_t c = 0; c < n; c += 8192)
+    acc = acc + np_pairwise_gather(X, D, d, rows + c, (n - c) < 8192 ? (n - c) : 8192, mean, sq);
+  return acc;
+}
+
+// one workgroup per segment: stable argsort of the segment's losses
+__global__ __launch_bounds__(256) void seg_argsort_kernel(const double* __restrict__ loss,
+                                                          const int64_t* __restrict__ seg_off, int tile,
+                                                          uint64_t* gk, int32_t* gi, uint64_t* gk2, int32_t* gi2,
+                                                          int64_t* __restrict__ order) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint64_t* lk = (uint64_t*)smem;
+  int32_t* li = (int32_t*)(smem + sizeof(uint64_t) * tile);
+  const int64_t b = blockIdx.x;
+  const int64_t s = seg_off[b], e = seg_off[b + 1];
+  block_sort_segment<false>(loss + s, e - s, tile, lk, li, gk + s, gi + s, gk2 + s, gi2 + s, order + s);
+}
+
+// one thread per (segment, set in {good, bad}, dim): bandwidth and observed level count
+__global__ __launch_bounds__(128) void kde_fit_stats_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
+    const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
+    const double* __restrict__ fac_good, const double* __restrict__ fac_bad, const int32_t* __restrict__ vartype,
+    double* __restrict__ bw_good, double* __restrict__ bw_bad, int32_t* __restrict__ nlev_good,
+    int32_t* __restrict__ nlev_bad) {
+  __shared__ uint32_t bits[128][33];  // 1024-level bitmap per thread (+1 pad: bank spread)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = B * 2 * D;
+  if (t >= total) return;
+  const int32_t d = (int32_t)(t % D);
+  const int64_t bs = t / D;
+  const int64_t b = bs >> 1;
+  const bool good = (bs & 1) == 0;
+  const int64_t ns = good ? n_good[b] : n_bad[b];
+  const int64_t s0 = seg_off[b], len = seg_off[b + 1] - s0;
+  double* bwo = (good ? bw_good : bw_bad) + b * D + d;
+  int32_t* nlo = (good ? nlev_good : nlev_bad) + b * D + d;
+  if (ns <= 0 || ns > len) {  // segment not refit (host decided) -> leave a NaN marker
+    *bwo = NAN;
+    *nlo = 0;
+    return;
+  }
+  // rows of the set: good = head of the argsort, bad = tail (bohb.py:231-232)
+  const int64_t* ord = order + s0 + (good ? 0 : (len - ns));
+  // order holds positions local to the segment -> shift X to the segment's first row
+  const double* Xs = X + s0 * (int64_t)D;
+  const double mean = np_sum_column(Xs, D, d, ord, ns, 0.0, false) / (double)ns;
+  const double var = np_sum_column(Xs, D, d, ord, ns, mean, true) / (double)ns;
+  const double sd = sqrt(var);
+  *bwo = (1.06 * sd) * (good ? fac_good[b] : fac_bad[b]);
+  if (vartype[d] == 0) {
+    *nlo = 0;
+    return;
+  }
+  uint32_t* bm = bits[threadIdx.x];
+  for (int w = 0; w < 32; ++w) bm[w] = 0u;
+  int32_t cnt = 0;
+  for (int64_t i = 0; i < ns; ++i) {
+    const double x = Xs[ord[i] * (int64_t)D + d];
+    const int v = (int)x;
+    if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
+      cnt = -1;  // categorical codes must be integers in [0, 1024)
+      break;
+    }
+    const uint32_t m = 1u << (v & 31);
+    if (!(bm[v >> 5] & m)) {
+      bm[v >> 5] |= m;
+      ++cnt;
+    }
+  }
+  *nlo = cnt;
+}
+
+extern "C" {
+
+// Scratch bytes hbx_kde_fit / hbx_sh_promote need for N total rows.
+int64_t hbx_sort_scratch_bytes(int64_t N) { return (int64_t)(2 * (sizeof(uint64_t) + sizeof(int32_t)) * N + 64); }
+
+static int sort_tile(int64_t max_seg) {
+  int tile = 64;
+  while (tile < max_seg && tile < 4096) tile <<= 1;
+  return tile;
+}
+
+// Stable argsort of each segment's losses (np.argsort order; ties by position).  seg_off: device
+// int64[B+1]; max_seg: host upper bound on segment length; order: device int64[N] (segment-local).
+int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                    int64_t* order, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!loss || !seg_off || !order || (!scratch && N > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort: null");
+  if (B <= 0) return HBX_OK;
+  if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
+  const int tile = sort_tile(max_seg);
+  char* sc = (char*)scratch;
+  uint64_t* gk = (uint64_t*)sc;
+  uint64_t* gk2 = gk + N;
+  int32_t* gi = (int32_t*)(gk2 + N);
+  int32_t* gi2 = gi + N;
+  hipLaunchKernelGGL(seg_argsort_kernel, dim3((unsigned)B), dim3(256), (sizeof(uint64_t) + sizeof(int32_t)) * tile,
+                     (hipStream_t)stream, loss, seg_off, tile, gk, gi, gk2, gi2, order);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// Batched KDE refit.  X: device fp64 [N][D] (segment b = rows seg_off[b]..seg_off[b+1]);
+// order: output of hbx_seg_argsort; n_good/n_bad: device int64[B] (0 = segment not refit);
+// fac_good/fac_bad: device fp64[B] = n**(-1/(4+D)) from host pow(); vartype: device int32[D].
+// Outputs: bw_good/bw_bad fp64[B][D], nlev_good/nlev_bad int32[B][D] (-1: code not an integer in [0,1024)).
+int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, const int64_t* order,
+                const int64_t* n_good, const int64_t* n_bad, const double* fac_good, const double* fac_bad,
+                const int32_t* vartype, double* bw_good, double* bw_bad, int32_t* nlev_good, int32_t* nlev_bad,
+                void* stream) {
+  if (!X || !seg_off || !order || !n_good || !n_bad || !fac_good || !fac_bad || !vartype || !bw_good ||
+      !bw_bad || !nlev_good || !nlev_bad)
+    return hbx_fail(HBX_ERR_ARG, "hbx_kde_fit: null pointer");
+  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
+  if (B <= 0) return HBX_OK;
+  const int64_t total = B * 2 * D;
+  hipLaunchKernelGGL(kde_fit_stats_kernel, dim3((unsigned)((total + 127) / 128)), dim3(128), 0,
+                     (hipStream_t)stream, X, D, seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype,
+                     bw_good, bw_bad, nlev_good, nlev_bad);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+}  // extern "C"

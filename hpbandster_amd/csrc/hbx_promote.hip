@@ -1,0 +1,69 @@
+// hbx_promote.hip -- batched successive-halving promotion on MI355X.
+//
+// Reference: HB_iteration.py:179-182 (SuccessiveHalving.process_results)
+//     ranks = np.argsort(np.argsort(losses)); advance = ranks < num_configs[SH_iter]
+// and HB_iteration.py:240-242 (SuccessiveResampling: ranks < max(1, n * (1 - 0.5))).
+// Only REVIEW configurations (finite losses) are ranked; CRASHED ones (non-finite, register_result
+// HB_iteration.py:102-106) never advance.  One workgroup per bracket: stable sort of the losses in
+// LDS (hbx_sort.h), then advance[position] = (rank < k).  Ties are ranked by position (stable);
+// numpy's argsort is unstable, so on tied losses the reference's choice is platform dependent.
+#include "hbx_common.h"
+#include "hbx_sort.h"
+
+__global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restrict__ loss,
+                                                         const int64_t* __restrict__ seg_off,
+                                                         const double* __restrict__ k, int tile, uint64_t* gk,
+                                                         int32_t* gi, uint64_t* gk2, int32_t* gi2,
+                                                         int64_t* __restrict__ order,
+                                                         uint8_t* __restrict__ advance,
+                                                         int64_t* __restrict__ n_advance) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint64_t* lk = (uint64_t*)smem;
+  int32_t* li = (int32_t*)(smem + sizeof(uint64_t) * tile);
+  __shared__ int cnt;
+  const int64_t b = blockIdx.x;
+  const int64_t s = seg_off[b], e = seg_off[b + 1], n = e - s;
+  if (threadIdx.x == 0) cnt = 0;
+  block_sort_segment<true>(loss + s, n, tile, lk, li, gk + s, gi + s, gk2 + s, gi2 + s, order + s);
+  const double kb = k[b];
+  int mine = 0;
+  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
+    const int64_t p = order[s + r];
+    const double v = loss[s + p];
+    const bool adv = (v - v == 0.0) && ((double)r < kb);
+    advance[s + p] = adv ? 1 : 0;
+    mine += adv;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && n_advance) n_advance[b] = cnt;
+}
+
+extern "C" {
+
+int64_t hbx_sort_scratch_bytes(int64_t N);
+
+// loss: device fp64[N] (non-finite = not ranked); seg_off: device int64[B+1]; k: device fp64[B];
+// max_seg: host bound on the longest bracket; order: device int64[N] scratch/output (sorted
+// positions per bracket); advance: device uint8[N]; n_advance: device int64[B] (nullable).
+int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                   const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
+                   int64_t scratch_bytes, void* stream) {
+  if (!loss || !seg_off || !k || !order || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
+  if (B <= 0) return HBX_OK;
+  if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
+  int tile = 64;
+  while (tile < max_seg && tile < 4096) tile <<= 1;
+  char* sc = (char*)scratch;
+  uint64_t* gk = (uint64_t*)sc;
+  uint64_t* gk2 = gk + N;
+  int32_t* gi = (int32_t*)(gk2 + N);
+  int32_t* gi2 = gi + N;
+  hipLaunchKernelGGL(sh_promote_kernel, dim3((unsigned)B), dim3(256), (sizeof(uint64_t) + sizeof(int32_t)) * tile,
+                     (hipStream_t)stream, loss, seg_off, k, tile, gk, gi, gk2, gi2, order, advance, n_advance);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+}  // extern "C"

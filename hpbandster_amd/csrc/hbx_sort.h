@@ -1,0 +1,128 @@
+// hbx_sort.h -- per-segment stable sort of fp64 losses for one workgroup (device code).
+//
+// A segment (one budget's observations for the KDE refit, or one bracket's losses for the SH
+// promotion) is sorted by (key, position): keys are order-preserving 64-bit images of the fp64
+// losses, the position breaks ties, so the order is total and stable.  Segments up to `tile`
+// elements are bitonic-sorted in LDS; longer segments are cut into LDS-sorted runs of `tile`
+// elements that are merged pairwise through global scratch (every output element finds its slot
+// with one binary search in the partner run -- no data-dependent control flow between threads).
+#pragma once
+
+#include "hbx_common.h"
+
+// argsort order of numpy (np.argsort on fp64): -inf < finite < +inf < NaN
+__device__ __forceinline__ uint64_t key_argsort(double v) { return hbx_d2ord(v); }
+// promotion order: finite losses ranked, every non-finite loss (CRASHED) after them
+__device__ __forceinline__ uint64_t key_promote(double v) {
+  return (v - v == 0.0) ? hbx_d2ord(v) : ~0ull;
+}
+
+__device__ __forceinline__ bool kv_less(uint64_t ka, int32_t ia, uint64_t kb, int32_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+// Bitonic sort of P (power of two) pairs in LDS, whole block participates.
+__device__ void block_bitonic(uint64_t* k, int32_t* ix, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const bool gt = kv_less(k[j], ix[j], k[i], ix[i]);
+          if (gt == up) {
+            const uint64_t tk = k[i];
+            k[i] = k[j];
+            k[j] = tk;
+            const int32_t ti = ix[i];
+            ix[i] = ix[j];
+            ix[j] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Sort one segment of n losses; writes the sorted positions (0..n-1) to `order` (int64) and, if
+// `sorted_keys` is non-null, the keys.  lds_k / lds_i hold `tile` entries; gk/gi (and gk2/gi2) are
+// global scratch of n entries each, needed only when n > tile.  PROMOTE selects the key order.
+template <bool PROMOTE>
+__device__ void block_sort_segment(const double* __restrict__ loss, int64_t n, int tile, uint64_t* lds_k,
+                                   int32_t* lds_i, uint64_t* gk, int32_t* gi, uint64_t* gk2, int32_t* gi2,
+                                   int64_t* __restrict__ order) {
+  if (n <= 0) return;
+  if (n <= tile) {
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+      if (i < n) {
+        lds_k[i] = PROMOTE ? key_promote(loss[i]) : key_argsort(loss[i]);
+        lds_i[i] = i;
+      } else {
+        lds_k[i] = ~0ull;
+        lds_i[i] = 0x7fffffff;
+      }
+    }
+    __syncthreads();
+    block_bitonic(lds_k, lds_i, P);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) order[i] = lds_i[i];
+    __syncthreads();
+    return;
+  }
+  // 1) LDS-sorted runs of `tile`
+  for (int64_t base = 0; base < n; base += tile) {
+    const int len = (int)((n - base) < tile ? (n - base) : tile);
+    for (int i = threadIdx.x; i < tile; i += blockDim.x) {
+      if (i < len) {
+        lds_k[i] = PROMOTE ? key_promote(loss[base + i]) : key_argsort(loss[base + i]);
+        lds_i[i] = (int32_t)(base + i);
+      } else {
+        lds_k[i] = ~0ull;
+        lds_i[i] = 0x7fffffff;
+      }
+    }
+    __syncthreads();
+    block_bitonic(lds_k, lds_i, tile);
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+      gk[base + i] = lds_k[i];
+      gi[base + i] = lds_i[i];
+    }
+    __syncthreads();
+  }
+  // 2) pairwise merges of runs (width doubles each pass); ping-pong gk/gi <-> gk2/gi2
+  uint64_t *sk = gk, *dk = gk2;
+  int32_t *si = gi, *di = gi2;
+  for (int64_t width = tile; width < n; width <<= 1) {
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+      const int64_t run = e / width;
+      const int64_t lstart = (run & ~1ll) * width;
+      const int64_t rstart = lstart + width;
+      const bool left = (run & 1) == 0;
+      const int64_t o_start = left ? rstart : lstart;              // partner run
+      const int64_t o_end = left ? (rstart + width < n ? rstart + width : n) : rstart;
+      const uint64_t k = sk[e];
+      const int32_t ix = si[e];
+      int64_t lo = o_start, hi = o_end;  // count partner elements less than (k, ix)
+      if (!left || rstart < n) {
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (kv_less(sk[mid], si[mid], k, ix)) lo = mid + 1; else hi = mid;
+        }
+      } else {
+        lo = o_start;
+      }
+      const int64_t mine = e - (left ? lstart : rstart);
+      const int64_t pos = lstart + mine + (lo - o_start);
+      dk[pos] = k;
+      di[pos] = ix;
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint64_t* tk = sk; sk = dk; dk = tk;
+    int32_t* ti = si; si = di; di = ti;
+  }
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) order[i] = si[i];
+  __syncthreads();
+}

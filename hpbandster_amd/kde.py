@@ -1,0 +1,282 @@
+"""Device-resident BOHB KDE models: fit (refit per budget), scoring and exact acquisition.
+
+The arithmetic mirrors the reference path exactly:
+
+* split:      bohb.py:220-237 -- argsort the losses, good = head n_good, bad = tail n_bad
+* bandwidth:  statsmodels 0.12.2 _kernel_base.py:250-265 -- 1.06 * np.std(X, 0) * n**(-1/(4+D))
+* levels:     statsmodels kernels.py:59-60 -- observed np.unique(column).size per categorical dim
+* pdf:        statsmodels kernel_density.py:162-196 / _kernel_base.py:456-518 (gpke)
+* selection:  bohb.py:129,149-152 -- max(1e-8, g)/max(l, 1e-8), strict '<', first index wins
+
+Everything that touches observations x candidates runs in libhbx.so (HIP, gfx950).  The host
+side does O(D) bookkeeping only: the BOHB size rule, the pow() factor of the bandwidth rule (so it
+rounds exactly like the reference's Python pow), and the small parameter block upload.
+"""
+
+import math
+import struct
+
+import numpy as np
+
+from . import _native as N
+
+RESULT_FMT = "<qdddqii"  # AcqResult: index, score, pdf_l, pdf_g, shortlist, flags, pad
+RESULT_BYTES = struct.calcsize(RESULT_FMT)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def default_device():
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise N.HbxError("hpbandster_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                         "the engine has no CPU path")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def var_type_codes(var_type):
+    return np.array([0 if c == "c" else 1 for c in var_type], dtype=np.int32)
+
+
+def bohb_split_sizes(n, min_points, top_n_percent=15):
+    """bohb.py:224-225."""
+    return (max(min_points, (top_n_percent * n) // 100),
+            max(min_points, ((100 - top_n_percent) * n) // 100))
+
+
+def bandwidth_factor(nobs, D):
+    """n**(-1/(4+D)) exactly as SM:_kernel_base.py:265 evaluates it (Python int ** float)."""
+    return int(nobs) ** (-1. / (4 + int(D)))
+
+
+class AcqResult(object):
+    __slots__ = ("index", "score", "pdf_l", "pdf_g", "shortlist", "flags")
+
+    def __init__(self, index, score, pdf_l, pdf_g, shortlist, flags):
+        self.index, self.score, self.pdf_l, self.pdf_g = int(index), score, pdf_l, pdf_g
+        self.shortlist, self.flags = int(shortlist), int(flags)
+
+    @classmethod
+    def from_bytes(cls, b):
+        idx, score, l, g, sl, fl, _ = struct.unpack(RESULT_FMT, bytes(b))
+        return cls(idx, score, l, g, sl, fl)
+
+    def __repr__(self):
+        return "AcqResult(index=%d, score=%r, pdf_l=%r, pdf_g=%r, shortlist=%d, flags=%d)" % (
+            self.index, self.score, self.pdf_l, self.pdf_g, self.shortlist, self.flags)
+
+
+class DeviceKDE(object):
+    """One fitted KDE (good or bad) on the GPU, with the statsmodels surface BOHB reads.
+
+    ``data``/``bw``/``nobs``/``var_type``/``k_vars`` match ``KDEMultivariate`` (bohb.py:126-139
+    reads ``.data``, ``.bw`` and ``.pdf``); ``pdf`` evaluates the exact fp64 density on the GPU.
+    """
+
+    def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None):
+        torch = _torch()
+        L = N.lib()
+        self.var_type = var_type
+        self.k_vars = len(var_type)
+        self.bw = np.asarray(bw, dtype=np.float64)
+        self.nlev = np.asarray(nlev, dtype=np.int32)
+        self.data = data_host
+        self.nobs = int(rows_dev.shape[0])
+        self.X_dev = X_dev
+        self.rows_dev = rows_dev
+        self.device = X_dev.device
+        D = self.k_vars
+        vt = var_type_codes(var_type)
+        dc, du = int((vt == 0).sum()), int((vt == 1).sum())
+        dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+        N.check(L.hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
+        self.stride = int(stride[0])
+        self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
+        self.table = torch.empty(self.nobs * self.stride, dtype=torch.float32, device=self.device)
+        info = np.zeros(8, dtype=np.int32)
+        bw_c = np.ascontiguousarray(self.bw)
+        nlev_c = np.ascontiguousarray(self.nlev)
+        N.check(L.hbx_kde_prepare(N.ptr(X_dev), D, N.ptr(rows_dev), self.nobs, N.ptr(vt), N.ptr(bw_c),
+                                  N.ptr(nlev_c), N.ptr(self.params), N.ptr(self.table), self.table.numel(),
+                                  N.ptr(info), N.stream_handle(stream)))
+        self.has_neg, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
+            [int(v) for v in info]
+        if unsupported:
+            raise N.HbxError("KDE bandwidth/level combination not modelled (bw=%r, nlev=%r)" % (self.bw, self.nlev))
+
+    def pdf(self, data_predict=None, stream=None):
+        """Exact fp64 pdf on the GPU (KDEMultivariate.pdf semantics, np.squeeze'd)."""
+        torch = _torch()
+        L = N.lib()
+        if data_predict is None:
+            pts = np.asarray(self.data, dtype=np.float64)
+        else:
+            pts = np.asarray(data_predict, dtype=np.float64)
+            if pts.ndim <= 1:
+                pts = pts.reshape(-1, self.k_vars) if pts.size != self.k_vars else pts.reshape(1, -1)
+        pts = np.ascontiguousarray(pts.reshape(-1, self.k_vars))
+        p_dev = torch.from_numpy(pts).to(self.device)
+        out = torch.empty(pts.shape[0], dtype=torch.float64, device=self.device)
+        sb = int(L.hbx_kde_pdf_scratch_bytes(self.nobs))
+        scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
+        N.check(L.hbx_kde_pdf_exact(N.ptr(p_dev), pts.shape[0], self.k_vars, N.ptr(self.params), N.ptr(self.X_dev),
+                                    N.ptr(self.rows_dev), self.nobs, N.ptr(out), N.ptr(scratch), sb,
+                                    N.stream_handle(stream)))
+        return np.squeeze(out.cpu().numpy())
+
+    def logpdf_est(self, cand_dev, stream=None):
+        """fp32 log-domain estimate per candidate -> (lpos, lneg, err) numpy arrays."""
+        torch = _torch()
+        L = N.lib()
+        Nc = int(cand_dev.shape[0])
+        est = torch.empty((Nc, 4), dtype=torch.float32, device=self.device)
+        N.check(L.hbx_kde_logpdf(N.ptr(cand_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
+                                 self.dc_pad, self.du_pad, self.has_neg, N.ptr(est), N.stream_handle(stream)))
+        e = est.cpu().numpy()
+        return e[:, 0], e[:, 1], e[:, 2]
+
+
+class KDEPair(object):
+    """The (good, bad) KDE pair of one budget -- BOHB's ``kde_models[budget]`` entry.
+
+    Immutable once built; BOHB replaces the whole entry on refit (bohb.py:248-251), so a
+    concurrent ``get_config`` always sees a consistent snapshot.
+    """
+
+    def __init__(self, good, bad):
+        self.good = good
+        self.bad = bad
+        if (good.dc_pad, good.du_pad) != (bad.dc_pad, bad.du_pad):
+            raise N.HbxError("good/bad KDEs prepared for different kernel buckets")
+        self.nmax = max(good.nobs, bad.nobs)
+
+    def __getitem__(self, key):  # cg.kde_models[b]['good'] like the reference dict
+        if key == "good":
+            return self.good
+        if key == "bad":
+            return self.bad
+        raise KeyError(key)
+
+    def keys(self):
+        return ["good", "bad"]
+
+    def workspace_bytes(self, Nc):
+        return int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
+
+    def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True):
+        """Select the first index minimising max(1e-8, g)/max(l, 1e-8) over the candidates.
+
+        ``cands``: [Nc, D] float64 (numpy or a device tensor).  Returns AcqResult (index -1 when no
+        candidate has a finite score: the reference then falls back to a random configuration).
+        With ``logs`` the fp32 ln l(x), ln g(x) estimates are returned as well.
+        With ``sync=False`` the result stays on the device: returns the result tensor view.
+        """
+        torch = _torch()
+        L = N.lib()
+        dev = self.good.device
+        if isinstance(cands, np.ndarray):
+            c_dev = torch.from_numpy(np.ascontiguousarray(cands, dtype=np.float64)).to(dev)
+        else:
+            c_dev = cands
+            if c_dev.dtype != torch.float64 or not c_dev.is_contiguous():
+                raise N.HbxError("candidate tensor must be contiguous float64 [Nc, D]")
+        Nc = int(c_dev.shape[0])
+        D = self.good.k_vars
+        if Nc > 0 and (c_dev.dim() != 2 or int(c_dev.shape[1]) != D):
+            raise N.HbxError("candidates must be [Nc, %d], got %s" % (D, tuple(c_dev.shape)))
+        wsb = self.workspace_bytes(Nc)
+        ws = workspace if workspace is not None else torch.empty(wsb, dtype=torch.uint8, device=dev)
+        if ws.numel() < wsb:
+            raise N.HbxError("workspace too small")
+        logl = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
+        logg = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
+        g, b = self.good, self.bad
+        N.check(L.hbx_kde_acquire(N.ptr(c_dev), Nc, D, int(index_base),
+                                  N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.has_neg,
+                                  N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.has_neg,
+                                  g.dc_pad, g.du_pad, self.nmax, N.ptr(logl), N.ptr(logg), N.ptr(ws), ws.numel(),
+                                  N.stream_handle(stream)))
+        off = int(L.hbx_kde_result_ptr(N.ptr(ws))) - N.ptr(ws)
+        rview = ws[off:off + RESULT_BYTES]
+        if not sync:
+            return rview
+        res = AcqResult.from_bytes(rview.cpu().numpy().tobytes())
+        if logs:
+            return res, logl.cpu().numpy(), logg.cpu().numpy()
+        return res
+
+
+def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=None, stream=None,
+             split_rule="bohb"):
+    """Refit the good/bad KDEs of one budget on the GPU (BOHB.new_result, bohb.py:220-251).
+
+    Returns a KDEPair, or None where the reference returns without building a model.
+    ``split_rule`` 'bohb' uses integer floor sizes (bohb.py:224-225) and requires rows > D;
+    'kde_ei' uses int(max(top%*N/100., mp)) (kde_ei.py:190-191) and requires rows >= D.
+    """
+    torch = _torch()
+    L = N.lib()
+    device = device or default_device()
+    X = np.ascontiguousarray(np.asarray(configs, dtype=np.float64))
+    loss = np.ascontiguousarray(np.asarray(losses, dtype=np.float64))
+    n, D = X.shape
+    if split_rule == "bohb":
+        n_good, n_bad = bohb_split_sizes(n, min_points, top_n_percent)
+        if min(n_good, n) <= D or min(n_bad, n) <= D:
+            return None
+    else:
+        n_good = int(max(top_n_percent * n / 100., min_points))
+        n_bad = int(max((100 - top_n_percent) * n / 100., min_points))
+        if min(n_good, n) < D or min(n_bad, n) < D:
+            return None
+        if min(n_good, n) <= D or min(n_bad, n) <= D:
+            # KDEMultivariate raises here (kernel_density.py:107-109), as the reference does
+            raise ValueError("The number of observations must be larger than the number of variables.")
+    # numpy slicing semantics: idx[:n_good] / idx[-n_bad:] clip at n
+    n_good, n_bad = min(n_good, n), min(n_bad, n)
+    vt = var_type_codes(var_type)
+    X_dev = torch.from_numpy(X).to(device)
+    loss_dev = torch.from_numpy(loss).to(device)
+    seg = torch.tensor([0, n], dtype=torch.int64, device=device)
+    order = torch.empty(n, dtype=torch.int64, device=device)
+    sb = int(L.hbx_sort_scratch_bytes(n))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=device)
+    sh = N.stream_handle(stream)
+    N.check(L.hbx_seg_argsort(N.ptr(loss_dev), N.ptr(seg), 1, n, n, N.ptr(order), N.ptr(scratch), sb, sh))
+    ng = torch.tensor([n_good], dtype=torch.int64, device=device)
+    nb = torch.tensor([n_bad], dtype=torch.int64, device=device)
+    fg = torch.tensor([bandwidth_factor(n_good, D)], dtype=torch.float64, device=device)
+    fb = torch.tensor([bandwidth_factor(n_bad, D)], dtype=torch.float64, device=device)
+    vt_dev = torch.from_numpy(vt).to(device)
+    bw_g = torch.empty(D, dtype=torch.float64, device=device)
+    bw_b = torch.empty(D, dtype=torch.float64, device=device)
+    nl_g = torch.empty(D, dtype=torch.int32, device=device)
+    nl_b = torch.empty(D, dtype=torch.int32, device=device)
+    N.check(L.hbx_kde_fit(N.ptr(X_dev), D, N.ptr(seg), 1, N.ptr(order), N.ptr(ng), N.ptr(nb), N.ptr(fg), N.ptr(fb),
+                          N.ptr(vt_dev), N.ptr(bw_g), N.ptr(bw_b), N.ptr(nl_g), N.ptr(nl_b), sh))
+    order_h = order.cpu().numpy()
+    bw_gh, bw_bh = bw_g.cpu().numpy(), bw_b.cpu().numpy()
+    nl_gh, nl_bh = nl_g.cpu().numpy(), nl_b.cpu().numpy()
+    if (nl_gh < 0).any() or (nl_bh < 0).any():
+        raise N.HbxError("categorical codes must be integers in [0, 1024)")
+    rows_g = order[:n_good]
+    rows_b = order[n - n_bad:]
+    good = DeviceKDE(X_dev, rows_g, var_type, bw_gh, nl_gh, X[order_h[:n_good]], stream)
+    bad = DeviceKDE(X_dev, rows_b, var_type, bw_bh, nl_bh, X[order_h[n - n_bad:]], stream)
+    return KDEPair(good, bad)
+
+
+def fit_pair_from_rows(X, good_rows, bad_rows, var_type, bw_good, bw_bad, nlev_good, nlev_bad, device=None):
+    """Build a KDEPair from an explicit split and bandwidths (tests / externally fitted models)."""
+    torch = _torch()
+    device = device or default_device()
+    X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
+    X_dev = torch.from_numpy(X).to(device)
+    rg = torch.from_numpy(np.asarray(good_rows, dtype=np.int64)).to(device)
+    rb = torch.from_numpy(np.asarray(bad_rows, dtype=np.int64)).to(device)
+    good = DeviceKDE(X_dev, rg, var_type, bw_good, nlev_good, X[np.asarray(good_rows)])
+    bad = DeviceKDE(X_dev, rb, var_type, bw_bad, nlev_bad, X[np.asarray(bad_rows)])
+    return KDEPair(good, bad)

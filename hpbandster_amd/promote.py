@@ -1,0 +1,50 @@
+"""Batched successive-halving promotion on the GPU (HB_iteration.py:149-190, 203-250).
+
+``advance = argsort(argsort(losses)) < k`` per bracket, over the REVIEW (finite-loss) entries;
+CRASHED entries (non-finite loss) never advance.  Many brackets are ranked in one launch
+(one workgroup per bracket), which is what config #5 of the benchmark exercises.
+"""
+
+import numpy as np
+
+from . import _native as N
+from .kde import default_device
+
+
+def promote_segments(loss, seg_off, k, device=None, stream=None, return_order=False):
+    """loss: fp64 [N] (numpy or device tensor); seg_off: int64 [B+1]; k: per-bracket threshold [B].
+
+    Returns a bool numpy mask [N] (or the device uint8 tensor with ``return_device``).
+    """
+    import torch
+    L = N.lib()
+    device = device or default_device()
+
+    def dev(a, dt):
+        if isinstance(a, np.ndarray) or not hasattr(a, "data_ptr"):
+            return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=dt))).to(device)
+        return a
+
+    loss_d = dev(loss, np.float64)
+    seg_h = np.asarray(seg_off.cpu().numpy() if hasattr(seg_off, "cpu") else seg_off, dtype=np.int64)
+    seg_d = dev(seg_h, np.int64)
+    k_d = dev(np.asarray(k, dtype=np.float64), np.float64)
+    B = seg_h.shape[0] - 1
+    Ntot = int(loss_d.shape[0])
+    max_seg = int(np.max(np.diff(seg_h))) if B > 0 else 0
+    order = torch.empty(Ntot, dtype=torch.int64, device=device)
+    adv = torch.empty(Ntot, dtype=torch.uint8, device=device)
+    nadv = torch.empty(max(B, 1), dtype=torch.int64, device=device)
+    sb = int(L.hbx_sort_scratch_bytes(Ntot))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=device)
+    N.check(L.hbx_sh_promote(N.ptr(loss_d), N.ptr(seg_d), B, max_seg, Ntot, N.ptr(k_d), N.ptr(order), N.ptr(adv),
+                             N.ptr(nadv), N.ptr(scratch), sb, N.stream_handle(stream)))
+    if return_order:
+        return adv, order, nadv
+    return adv.cpu().numpy().astype(bool)
+
+
+def advance_mask(losses, k, device=None):
+    """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182)."""
+    losses = np.asarray(losses, dtype=np.float64)
+    return promote_segments(losses, np.array([0, losses.shape[0]], dtype=np.int64), [k], device=device)

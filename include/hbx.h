@@ -1,0 +1,124 @@
+/* hbx.h -- C ABI of libhbx.so, the MI355X (gfx950) engine for HpBandSter's data-parallel hot path:
+ * BOHB's KDE acquisition (good/bad product-kernel KDE fit, l(x)/g(x) scoring, argmin) and the
+ * successive-halving promotion.
+ *
+ * Conventions
+ *   - Every pointer marked "device" is a HIP device pointer (e.g. torch.Tensor.data_ptr() of a
+ *     ROCm tensor); "host" pointers are ordinary CPU memory.  The library allocates nothing
+ *     per call: callers own outputs, workspaces and scratch (sized by the *_bytes helpers).
+ *   - `stream` is a hipStream_t (NULL = default stream).  Calls only enqueue work, except
+ *     hbx_kde_prepare, which synchronises `stream` once to upload the model parameters.
+ *   - Return value 0 on success, a negative HBX_ERR_* code otherwise; the message is available
+ *     from hbx_last_error() (thread-local).  Calls are reentrant; nothing is cached globally.
+ *
+ * Reference interfaces replaced (paths relative to the HpBandSter snapshot):
+ *   hbx_seg_argsort + hbx_kde_fit   <- bohb.py:220-246 (BOHB.new_result refit:
+ *                                      np.argsort + sm.nonparametric.KDEMultivariate(..,'normal_reference'))
+ *   hbx_kde_prepare                 <- KDEMultivariate.__init__ model state (statsmodels 0.12.2
+ *                                      kernel_density.py:101-115)
+ *   hbx_kde_acquire                 <- bohb.py:124-169 (the num_samples loop: pdf of l and g per
+ *                                      candidate, minimize_me, strict-'<' argmin)
+ *   hbx_kde_logpdf                  <- KDEMultivariate.pdf (kernel_density.py:162-196), fp32 log domain
+ *   hbx_kde_pdf_exact               <- KDEMultivariate.pdf, fp64, reference operation order
+ *   hbx_sh_promote                  <- HB_iteration.py:149-190 (SuccessiveHalving.process_results ranks)
+ */
+#ifndef HBX_H_
+#define HBX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBX_OK 0
+#define HBX_ERR_ARG (-1)
+#define HBX_ERR_HIP (-2)
+#define HBX_ERR_UNSUPPORTED (-3)
+
+/* ---- introspection ---------------------------------------------------------------------- */
+const char* hbx_last_error(void);
+const char* hbx_version(void);
+int64_t hbx_kde_param_bytes(void);     /* bytes of one prepared KDE parameter block (device) */
+int64_t hbx_kde_est_bytes(void);       /* bytes per candidate of hbx_kde_logpdf output */
+int64_t hbx_acq_result_bytes(void);    /* bytes of the acquisition result record */
+int32_t hbx_max_dims(void);            /* largest D accepted */
+
+/* ---- KDE refit (BOHB.new_result) --------------------------------------------------------- */
+int64_t hbx_sort_scratch_bytes(int64_t N);
+
+/* Stable argsort of every segment's fp64 losses (np.argsort order: -inf < finite < +inf < NaN,
+ * ties by position).  loss: device f64[N]; seg_off: device i64[B+1]; max_seg: host bound on the
+ * longest segment; order: device i64[N], positions local to each segment. */
+int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                    int64_t* order, void* scratch, int64_t scratch_bytes, void* stream);
+
+/* Normal-reference bandwidths and observed level counts of the good (head n_good of the argsort)
+ * and bad (tail n_bad) rows of every segment, bit-exact with numpy's np.std.
+ * X: device f64[N][D]; order: from hbx_seg_argsort; n_good/n_bad: device i64[B] (0 = skip);
+ * fac_good/fac_bad: device f64[B] = n**(-1/(4+D)) computed on the host with pow();
+ * vartype: device i32[D] (0 = continuous, 1 = categorical).
+ * Outputs: bw_* device f64[B][D]; nlev_* device i32[B][D] (-1 = categorical code not an
+ * integer in [0, 1024)). */
+int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, const int64_t* order,
+                const int64_t* n_good, const int64_t* n_bad, const double* fac_good, const double* fac_bad,
+                const int32_t* vartype, double* bw_good, double* bw_bad, int32_t* nlev_good, int32_t* nlev_bad,
+                void* stream);
+
+/* ---- KDE model preparation ----------------------------------------------------------------- */
+/* Template bucket of the scoring kernel for dc continuous / du categorical dims. */
+int hbx_kde_bucket(int32_t dc, int32_t du, int32_t* dc_pad, int32_t* du_pad, int32_t* stride);
+
+/* Build one KDE for scoring.  X: device f64[*][D]; rows: device i64[n] (this KDE's rows, in
+ * the reference's order); vartype/bw/nlev: host arrays of length D.  params: device buffer of
+ * hbx_kde_param_bytes(); table: device f32[n * stride].  info: host i32[8] =
+ * {has_neg, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}. */
+int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, const int32_t* vartype,
+                    const double* bw, const int32_t* nlev, void* params, float* table, int64_t table_floats,
+                    int32_t* info, void* stream);
+
+/* ---- scoring ------------------------------------------------------------------------------- */
+/* fp32 log-domain sums for Nc candidates (device f64[Nc][D]) against one prepared KDE;
+ * est_out: device, Nc * hbx_kde_est_bytes() ({ln S+, ln S-, rel. bound, pad} per candidate). */
+int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
+                   int32_t dc_pad, int32_t du_pad, int32_t signed_sum, void* est_out, void* stream);
+
+int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
+
+/* One acquisition: l = good KDE, g = bad KDE; selects the first index of the minimum of
+ * max(1e-8, g)/max(l, 1e-8) over the candidates, exactly (fp64 re-score of every candidate whose
+ * fp32 score interval reaches the minimum).  index_base is added to the reported index (GPU
+ * sharding).  logl_out/logg_out: nullable device f32[Nc] (ln pdf estimates; -inf for pdf <= 0,
+ * NaN for NaN).  The result record lives in the workspace: hbx_kde_result_ptr(workspace). */
+int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
+                    const void* params_good, const float* table_good, const double* X_good,
+                    const int64_t* rows_good, int32_t signed_good,
+                    const void* params_bad, const float* table_bad, const double* X_bad,
+                    const int64_t* rows_bad, int32_t signed_bad, int32_t dc_pad, int32_t du_pad,
+                    int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
+                    void* stream);
+
+/* Device address of the result record {i64 index, f64 score, f64 pdf_l, f64 pdf_g,
+ * i64 shortlist, i32 flags, i32 pad} inside an acquisition workspace. */
+void* hbx_kde_result_ptr(void* workspace);
+
+int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax);
+
+/* Exact fp64 pdf of one prepared KDE at Np points (device f64[Np][D]) -> out (device f64[Np]). */
+int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
+                      const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
+                      void* stream);
+
+/* ---- successive-halving promotion -------------------------------------------------------- */
+/* advance[i] = rank_i < k[b] among the finite losses of bracket b (non-finite = CRASHED, never
+ * advance).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B]; order: device
+ * i64[N] (sorted positions, output); advance: device u8[N]; n_advance: device i64[B], nullable. */
+int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                   const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
+                   int64_t scratch_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HBX_H_ */

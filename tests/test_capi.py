@@ -1,0 +1,54 @@
+"""The C-ABI library loads and exports every entry point include/hbx.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "hbx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = header_functions()
+    assert "hbx_kde_acquire" in names and "hbx_sh_promote" in names and "hbx_kde_fit" in names
+    assert len(names) >= 18
+
+
+def test_library_exports_every_header_symbol():
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    for name in header_functions():
+        assert hasattr(L, name), name
+        assert name in N.SIGNATURES, "ctypes signature missing for %s" % name
+
+
+def test_host_side_helpers():
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    assert L.hbx_version().decode().startswith("hbx")
+    assert L.hbx_max_dims() == 256
+    assert L.hbx_kde_param_bytes() > 0 and L.hbx_acq_result_bytes() == 48
+    assert L.hbx_kde_est_bytes() == 16
+    a, b, s = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+    assert L.hbx_kde_bucket(24, 8, a.ctypes.data, b.ctypes.data, s.ctypes.data) == 0
+    assert (a[0], b[0], s[0]) == (24, 8, 36)
+    assert L.hbx_kde_bucket(100, 0, a.ctypes.data, b.ctypes.data, s.ctypes.data) == -3
+    assert b"continuous" in L.hbx_last_error()
+    assert L.hbx_kde_workspace_bytes(1000, 100) > 1000 * 16
+
+
+def test_errors_are_reported_not_swallowed():
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    rc = L.hbx_kde_acquire(None, 10, 3, 0, None, None, None, None, 0, None, None, None, None, 0, 4, 0,
+                           10, None, None, None, 0, None)
+    assert rc == -1
+    with pytest.raises(N.HbxError):
+        N.check(rc)

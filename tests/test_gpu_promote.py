@@ -1,0 +1,87 @@
+"""GPU parity: batched successive-halving promotion against the reference's golden masks."""
+import numpy as np
+import pytest
+
+from oracle import kde_oracle as O
+from tests import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+
+def test_promotion_matches_reference(device):
+    from hpbandster_amd import promote
+    for c in G.load_sh():
+        losses = np.where(c["crashed"], np.nan, c["losses"])
+        adv = promote.advance_mask(losses, c["k"], device=device)
+        np.testing.assert_array_equal(adv, c["sh_adv"])
+        adv = promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device)
+        np.testing.assert_array_equal(adv, c["sr_adv"])
+
+
+@pytest.mark.parametrize("B,n", [(1, 1), (3, 5000), (64, 1000), (1000, 81), (7, 4097)])
+def test_batched_promotion_matches_oracle(device, B, n):
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(B * 7 + n)
+    lens = rs.randint(max(1, n // 2), n + 1, size=B)
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = rs.rand(seg[-1])
+    loss[rs.rand(seg[-1]) < 0.05] = np.inf
+    loss[rs.rand(seg[-1]) < 0.02] = np.nan
+    loss[rs.rand(seg[-1]) < 0.01] = -np.inf
+    k = np.maximum(lens // 3, 1).astype(np.float64)
+    adv = promote.promote_segments(loss, seg, k, device=device)
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(adv[s:e], O.sh_advance(loss[s:e], k[b]))
+
+
+def test_promotion_ties_are_stable(device):
+    from hpbandster_amd import promote
+    loss = np.array([1.0] * 40 + [0.5] * 10)
+    adv = promote.advance_mask(loss, 15, device=device)
+    assert adv[40:].all() and adv[:5].all() and not adv[5:40].any()
+
+
+def test_config5_shape_with_fit(device):
+    """B=1e3 brackets x 1e3 configs (config #5 at 1/10 the brackets): promotion + per-bracket refit."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    B, n, D = 1000, 1000, 8
+    losses = S.make_bracket_losses(B, n)
+    seg = np.arange(B + 1, dtype=np.int64) * n
+    from hpbandster_amd import promote
+    adv = promote.promote_segments(losses.reshape(-1), seg, np.full(B, 333.0), device=device)
+    assert adv.reshape(B, n).sum(1).tolist() == [333] * B
+    for b in (0, 17, B - 1):
+        np.testing.assert_array_equal(adv.reshape(B, n)[b], O.sh_advance(losses[b], 333))
+    # batched KDE refit of every bracket (D=8 continuous)
+    X = np.random.RandomState(4).rand(B * n, D)
+    L = N.lib()
+    dev = device
+    Xd = torch.from_numpy(X).to(dev)
+    ld = torch.from_numpy(losses.reshape(-1)).to(dev)
+    segd = torch.from_numpy(seg).to(dev)
+    order = torch.empty(B * n, dtype=torch.int64, device=dev)
+    sb = int(L.hbx_sort_scratch_bytes(B * n))
+    scr = torch.empty(sb, dtype=torch.uint8, device=dev)
+    N.call("hbx_seg_argsort", N.ptr(ld), N.ptr(segd), B, n, B * n, N.ptr(order), N.ptr(scr), sb, N.stream_handle())
+    ng, nb = kde.bohb_split_sizes(n, D + 1)
+    ngd = torch.full((B,), ng, dtype=torch.int64, device=dev)
+    nbd = torch.full((B,), nb, dtype=torch.int64, device=dev)
+    fg = torch.full((B,), kde.bandwidth_factor(ng, D), dtype=torch.float64, device=dev)
+    fb = torch.full((B,), kde.bandwidth_factor(nb, D), dtype=torch.float64, device=dev)
+    vt = torch.zeros(D, dtype=torch.int32, device=dev)
+    bwg = torch.empty((B, D), dtype=torch.float64, device=dev)
+    bwb = torch.empty((B, D), dtype=torch.float64, device=dev)
+    nlg = torch.empty((B, D), dtype=torch.int32, device=dev)
+    nlb = torch.empty((B, D), dtype=torch.int32, device=dev)
+    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(order), N.ptr(ngd), N.ptr(nbd), N.ptr(fg), N.ptr(fb),
+           N.ptr(vt), N.ptr(bwg), N.ptr(bwb), N.ptr(nlg), N.ptr(nlb), N.stream_handle())
+    bwg, bwb = bwg.cpu().numpy(), bwb.cpu().numpy()
+    for b in (0, 5, B - 1):
+        Xb, Lb = X[b * n:(b + 1) * n], losses[b]
+        good, bad = O.bohb_split(Xb, Lb, D + 1)
+        np.testing.assert_array_equal(bwg[b], O.normal_reference_bw(Xb[good]))
+        np.testing.assert_array_equal(bwb[b], O.normal_reference_bw(Xb[bad]))
