@@ -35,7 +35,10 @@ SIGNATURES = {
     "hbx_kde_acquire": (c_i32, [c_vp, c_i64, c_i32, c_i64,
                                 c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
-                                c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+                                c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_event_create": (c_i32, [c_vp]),
+    "hbx_event_destroy": (c_i32, [c_vp]),
+    "hbx_event_elapsed_ms": (c_i32, [c_vp, c_vp, c_vp]),
     "hbx_kde_result_ptr": (c_vp, [c_vp]),
     "hbx_kde_pdf_scratch_bytes": (c_i64, [c_i64]),
     "hbx_kde_pdf_exact": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),

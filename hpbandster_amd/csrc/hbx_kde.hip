@@ -706,7 +706,7 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
                     const void* params_bad, const float* table_bad, const double* X_bad,
                     const int64_t* rows_bad, int32_t signed_bad, int32_t dc_pad, int32_t du_pad,
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
-                    void* stream) {
+                    void* events, void* stream) {
   if ((!cand && Nc > 0) || !params_good || !table_good || !X_good || !rows_good || !params_bad || !table_bad ||
       !X_bad || !rows_bad || !workspace)
     return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire: null pointer");
@@ -737,10 +737,14 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   HBX_LAUNCH_CHECK();
   if (Nc > 0) {
     const dim3 grid((unsigned)((Nc + 255) / 256));
+    hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
+    if (ev) HBX_HIP(hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(fg, grid, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_good, table_good, el);
     HBX_LAUNCH_CHECK();
+    if (ev) HBX_HIP(hipEventRecord(ev[1], s));
     hipLaunchKernelGGL(fb, grid, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_bad, table_bad, eg);
     HBX_LAUNCH_CHECK();
+    if (ev) HBX_HIP(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, logl_out, logg_out, lo, hi, U,
                        flags);
     HBX_LAUNCH_CHECK();
@@ -772,6 +776,20 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
   hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, pts, Np, D,
                      (const KdeParams*)params, X, rows, out, (double*)scratch, n);
   HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// Timing events (hipEvent_t) for hbx_kde_acquire's `events` argument.
+int hbx_event_create(void** ev) {
+  HBX_HIP(hipEventCreate((hipEvent_t*)ev));
+  return HBX_OK;
+}
+int hbx_event_destroy(void* ev) {
+  HBX_HIP(hipEventDestroy((hipEvent_t)ev));
+  return HBX_OK;
+}
+int hbx_event_elapsed_ms(void* start, void* stop, float* ms) {
+  HBX_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
   return HBX_OK;
 }
 

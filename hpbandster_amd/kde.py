@@ -166,7 +166,7 @@ class KDEPair(object):
     def workspace_bytes(self, Nc):
         return int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
 
-    def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True):
+    def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True, events=None):
         """Select the first index minimising max(1e-8, g)/max(l, 1e-8) over the candidates.
 
         ``cands``: [Nc, D] float64 (numpy or a device tensor).  Returns AcqResult (index -1 when no
@@ -198,7 +198,7 @@ class KDEPair(object):
                                   N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.has_neg,
                                   N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.has_neg,
                                   g.dc_pad, g.du_pad, self.nmax, N.ptr(logl), N.ptr(logg), N.ptr(ws), ws.numel(),
-                                  N.stream_handle(stream)))
+                                  events.address if events is not None else None, N.stream_handle(stream)))
         off = int(L.hbx_kde_result_ptr(N.ptr(ws))) - N.ptr(ws)
         rview = ws[off:off + RESULT_BYTES]
         if not sync:
@@ -207,6 +207,37 @@ class KDEPair(object):
         if logs:
             return res, logl.cpu().numpy(), logg.cpu().numpy()
         return res
+
+
+class ScoreEvents(object):
+    """Three hipEvents bracketing the two scoring launches of one acquisition (bench timing)."""
+
+    def __init__(self):
+        import ctypes
+        L = N.lib()
+        self._ev = (ctypes.c_void_p * 3)()
+        for i in range(3):
+            h = ctypes.c_void_p()
+            N.check(L.hbx_event_create(ctypes.addressof(h)))
+            self._ev[i] = h.value
+        self.address = ctypes.addressof(self._ev)
+
+    def elapsed_ms(self):
+        """(l launch ms, g launch ms) of the last recorded acquisition (events must be complete)."""
+        import ctypes
+        L = N.lib()
+        a, b = ctypes.c_float(), ctypes.c_float()
+        N.check(L.hbx_event_elapsed_ms(self._ev[0], self._ev[1], ctypes.addressof(a)))
+        N.check(L.hbx_event_elapsed_ms(self._ev[1], self._ev[2], ctypes.addressof(b)))
+        return a.value, b.value
+
+    def __del__(self):
+        try:
+            L = N.lib()
+            for i in range(3):
+                L.hbx_event_destroy(self._ev[i])
+        except Exception:
+            pass
 
 
 def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=None, stream=None,

@@ -89,14 +89,21 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
  * max(1e-8, g)/max(l, 1e-8) over the candidates, exactly (fp64 re-score of every candidate whose
  * fp32 score interval reaches the minimum).  index_base is added to the reported index (GPU
  * sharding).  logl_out/logg_out: nullable device f32[Nc] (ln pdf estimates; -inf for pdf <= 0,
- * NaN for NaN).  The result record lives in the workspace: hbx_kde_result_ptr(workspace). */
+ * NaN for NaN).  The result record lives in the workspace: hbx_kde_result_ptr(workspace).
+ * events: NULL or hipEvent_t[3] (see hbx_event_create). */
 int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
                     const void* params_good, const float* table_good, const double* X_good,
                     const int64_t* rows_good, int32_t signed_good,
                     const void* params_bad, const float* table_bad, const double* X_bad,
                     const int64_t* rows_bad, int32_t signed_bad, int32_t dc_pad, int32_t du_pad,
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
-                    void* stream);
+                    void* events, void* stream);
+
+/* Optional timing: `events` of hbx_kde_acquire is NULL or an array of three hipEvent_t recorded on
+ * `stream` before the l scoring launch, between l and g, and after g. */
+int hbx_event_create(void** ev);
+int hbx_event_destroy(void* ev);
+int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
 /* Device address of the result record {i64 index, f64 score, f64 pdf_l, f64 pdf_g,
  * i64 shortlist, i32 flags, i32 pad} inside an acquisition workspace. */

@@ -1,0 +1,51 @@
+"""ORACLE -- test infrastructure only: ctypes wrapper of oracle/_build/libkde_oracle.so."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_build", "libkde_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            build()
+        L = ctypes.CDLL(SO)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        L.oracle_kde_pdf.argtypes = [vp, i64, i32, vp, vp, vp, vp, i64, vp, i32]
+        L.oracle_kde_pdf.restype = None
+        L.oracle_bohb_select.argtypes = [vp, vp, i64, vp]
+        L.oracle_bohb_select.restype = i64
+        L.oracle_max_threads.restype = i32
+        _lib = L
+    return _lib
+
+
+def kde_pdf(data, bw, var_type, nlev, pts, nthreads=0):
+    data = np.ascontiguousarray(data, dtype=np.float64)
+    pts = np.ascontiguousarray(np.atleast_2d(pts), dtype=np.float64)
+    vt = np.array([0 if c == "c" else 1 for c in var_type], dtype=np.int32)
+    bw = np.ascontiguousarray(bw, dtype=np.float64)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    out = np.empty(pts.shape[0])
+    lib().oracle_kde_pdf(data.ctypes.data, data.shape[0], data.shape[1], vt.ctypes.data, bw.ctypes.data,
+                         nlev.ctypes.data, pts.ctypes.data, pts.shape[0], out.ctypes.data, int(nthreads))
+    return out
+
+
+def bohb_select(pdf_l, pdf_g):
+    l = np.ascontiguousarray(pdf_l, dtype=np.float64)
+    g = np.ascontiguousarray(pdf_g, dtype=np.float64)
+    best = np.zeros(1)
+    i = lib().oracle_bohb_select(l.ctypes.data, g.ctypes.data, l.shape[0], best.ctypes.data)
+    return int(i), float(best[0])

@@ -1,0 +1,85 @@
+/* ORACLE -- test infrastructure only.
+ *
+ * Plain-C fp64 restatement of the reference KDE arithmetic, used as (a) a second checker in
+ * tests/ and (b) the `cpu_baseline` leg of bench.py (OpenMP over candidates on the host cores).
+ * Never linked into, loaded by or called from the engine (hpbandster_amd/).
+ *
+ * Follows, per (candidate, observation) pair:
+ *   gaussian          statsmodels 0.12.2 nonparametric/kernels.py:108-125
+ *                     (1/sqrt(2*pi)) * exp(-(Xi - x)**2 / (h**2 * 2.))
+ *   aitchison_aitken  kernels.py:23-65: 1 - h if Xi == x else h / (num_levels - 1)
+ *   gpke              _kernel_base.py:509-516: prod over dims / prod(bw[continuous]), sum over obs
+ *   pdf               kernel_density.py:190-193: gpke / nobs
+ *   minimize_me       hpbandster bohb.py:129 max(1e-8, g) / max(l, 1e-8) (Python max semantics)
+ *   argmin            bohb.py:149-152 strict '<' against best = +inf (first index wins)
+ * The observation sum is sequential (numpy sums pairwise), so values agree with the reference to
+ * rounding (~1e-15 relative), not bit for bit; selections agree on tie-free inputs.
+ *
+ * Build: oracle/Makefile (gcc -O3 -fopenmp -shared) -> oracle/_build/libkde_oracle.so.
+ */
+#include <math.h>
+#include <stdint.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static const double INV_SQRT_2PI = 0.3989422804014327; /* 1. / np.sqrt(2 * np.pi) */
+
+/* pdf of one KDE (data [n][D]) at Np points (pts [Np][D]) -> out[Np].  vartype: 0 = 'c', 1 = 'u'. */
+void oracle_kde_pdf(const double* data, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
+                    const int32_t* nlev, const double* pts, int64_t Np, double* out, int32_t nthreads) {
+  double prod_bw_c = 1.0;
+  for (int d = 0; d < D; ++d)
+    if (vartype[d] == 0) prod_bw_c *= bw[d];
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t p = 0; p < Np; ++p) {
+    const double* x = pts + p * D;
+    double acc = 0.0;
+    for (int64_t j = 0; j < n; ++j) {
+      const double* xr = data + j * D;
+      double prod = 1.0;
+      for (int d = 0; d < D; ++d) {
+        const double h = bw[d];
+        double k;
+        if (vartype[d] == 0) {
+          const double diff = xr[d] - x[d];
+          k = INV_SQRT_2PI * exp(-(diff * diff) / ((h * h) * 2.));
+        } else {
+          k = (xr[d] == x[d]) ? (1. - h) : (h / (double)(nlev[d] - 1));
+        }
+        prod = (d == 0) ? k : prod * k;
+      }
+      acc += prod / prod_bw_c;
+    }
+    out[p] = acc / (double)n;
+  }
+}
+
+/* first index of the minimum of max(1e-8, g)/max(l, 1e-8) over finite scores; -1 if none */
+int64_t oracle_bohb_select(const double* pdf_l, const double* pdf_g, int64_t Np, double* best_out) {
+  double best = INFINITY;
+  int64_t bi = -1;
+  for (int64_t i = 0; i < Np; ++i) {
+    const double g = pdf_g[i], l = pdf_l[i];
+    const double G = (g > 1e-8) ? g : 1e-8;  /* max(1e-8, g): NaN -> 1e-8 */
+    const double L = (1e-8 > l) ? 1e-8 : l;  /* max(l, 1e-8): NaN -> NaN  */
+    const double v = G / L;
+    if (v < best) {
+      best = v;
+      bi = i;
+    }
+  }
+  if (best_out) *best_out = best;
+  return bi;
+}
+
+int32_t oracle_max_threads(void) {
+#ifdef _OPENMP
+  return (int32_t)omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

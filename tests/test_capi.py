@@ -48,7 +48,7 @@ def test_errors_are_reported_not_swallowed():
     from hpbandster_amd import _native as N
     L = N.lib()
     rc = L.hbx_kde_acquire(None, 10, 3, 0, None, None, None, None, 0, None, None, None, None, 0, 4, 0,
-                           10, None, None, None, 0, None)
+                           10, None, None, None, 0, None, None)
     assert rc == -1
     with pytest.raises(N.HbxError):
         N.check(rc)

@@ -79,3 +79,15 @@ def test_hb_brackets_match_reference():
             s, ns = O.hb_bracket(it["it"], t["eta"], m)
             assert ns == it["num_configs"]
             np.testing.assert_allclose(budgets[(-s - 1):], np.array(it["budgets"]), rtol=5e-16, atol=0)
+
+
+@pytest.mark.parametrize("name", G.kde_case_names())
+def test_c_oracle_matches_reference(name):
+    from oracle import c_oracle
+    c = G.load_kde_case(name)
+    X, C = c["X"], c["cands"]
+    l = c_oracle.kde_pdf(X[c["good_idx"]], c["bw_good"], c["var_type"], c["nlev_good"], C)
+    g = c_oracle.kde_pdf(X[c["bad_idx"]], c["bw_bad"], c["var_type"], c["nlev_bad"], C)
+    np.testing.assert_allclose(l, c["pdf_l"], rtol=1e-12, atol=0, equal_nan=True)
+    np.testing.assert_allclose(g, c["pdf_g"], rtol=1e-12, atol=0, equal_nan=True)
+    assert c_oracle.bohb_select(l, g)[0] == c["chosen"]
