@@ -26,6 +26,7 @@
 #define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
 #define EXACT_GRID 128
 #define SUM_BLOCK 32
+#define LDS_ROWS 128  // observation rows per LDS chunk of the scoring kernel
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -94,125 +95,187 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// fp32 log-domain scoring: one candidate per lane, all observations of one KDE
+// fp32 log-domain scoring: CPT candidates per lane, all observations of one KDE
+//
+// Per (candidate i, observation j), in log2 units and minus the static bound M0:
+//   t_ij = c_i + C_j + sum_c x''_ic X'_jc + sum_u delta_u [x_iu == X_ju]
+// with X' = s (X - mu), x'' = 2 s (x - mu), c_i = -|x'_i|^2, C_j = -|X'_j|^2 + lb_sum - M0
+// (the expansion of -|x' - X'|^2: one FMA per continuous dim).  The observation row is wave-uniform
+// and arrives through scalar loads (s_load_dwordx16) as SGPR operands of the FMAs.  Each lane keeps
+// CPT candidates in registers: CPT independent dependency chains per observation, and every scalar
+// load is amortised over CPT*64 candidates.  The categorical match uses m = clamp(1 - d*d) on the
+// integer codes (d = x - X), which stays in the VALU (no VCC round trip).
 
-template <int DCP, int DUP, bool SIGNED>
+__device__ __forceinline__ float cat_match(float a, float b) {
+  const float d = a - b;
+  return __builtin_amdgcn_fmed3f(fmaf(-d, d, 1.f), 0.f, 1.f);
+}
+
+template <int DCP, int DUP, bool SIGNED, int CPT>
 __global__ __launch_bounds__(256) void kde_logpdf_kernel(const double* __restrict__ cand, int64_t Nc,
                                                          int32_t D, const KdeParams* __restrict__ P,
                                                          const float* __restrict__ table,
                                                          KdeEst* __restrict__ out) {
   constexpr int STRIDE = (1 + DCP + DUP + 3) & ~3;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = i < Nc;
-  const double* x = cand + (valid ? i : (Nc - 1)) * (int64_t)D;
+  constexpr int NC = DCP > 0 ? DCP : 1;
+  constexpr int NU = DUP > 0 ? DUP : 1;
   const int n = P->n;
   const int dc = P->dc, du = P->du;
 
-  // candidate in registers: x''_c = 2 s_c x_c, c_i = -sum x'_c^2, categorical codes
-  float xs[DCP > 0 ? DCP : 1];
-  float ci = 0.f, bnd = 0.f;
+  int64_t idx[CPT];
+  bool valid[CPT], nan_c[CPT];
+  float xs[CPT][NC], xu[CPT][NU], ci[CPT], bnd[CPT];
 #pragma unroll
-  for (int k = 0; k < DCP; ++k) {
-    float v = 0.f;
-    if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-    ci = fmaf(-v, v, ci);
-    xs[k] = 2.f * v;
-    if (k < dc) bnd = fmaf(fabsf(xs[k]), P->xmax[k], bnd);
+  for (int c = 0; c < CPT; ++c) {
+    idx[c] = (int64_t)blockIdx.x * (256 * CPT) + c * 256 + threadIdx.x;
+    valid[c] = idx[c] < Nc;
+    const double* x = cand + (valid[c] ? idx[c] : (Nc - 1)) * (int64_t)D;
+    ci[c] = 0.f;
+    bnd[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < DCP; ++k) {
+      float v = 0.f;
+      if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+      ci[c] = fmaf(-v, v, ci[c]);
+      xs[c][k] = 2.f * v;
+      if (k < dc) bnd[c] = fmaf(fabsf(xs[c][k]), P->xmax[k], bnd[c]);
+    }
+#pragma unroll
+    for (int u = 0; u < DUP; ++u) {
+      float v = -1.f;
+      if (u < du) {
+        const double xv = x[P->cat_dim[u]];
+        // codes are integers; anything else (incl. NaN) never equals an observed code
+        v = (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
+      }
+      xu[c][u] = v;
+    }
+    nan_c[c] = P->nan_all != 0;
+    for (int q = 0; q < P->nconst; ++q)
+      if (x[P->const_dim[q]] != P->const_level[q]) nan_c[c] = true;
   }
-  float xu[DUP > 0 ? DUP : 1], dl[DUP > 0 ? DUP : 1], ng[DUP > 0 ? DUP : 1];
+  float dl[NU], ng[NU];
 #pragma unroll
   for (int u = 0; u < DUP; ++u) {
-    if (u < du) {
-      xu[u] = (float)x[P->cat_dim[u]];
-      dl[u] = P->cat_delta[u];
-      ng[u] = P->cat_negf[u];
-    } else {
-      xu[u] = -1.f;
-      dl[u] = 0.f;
-      ng[u] = 0.f;
-    }
+    dl[u] = (u < du) ? P->cat_delta[u] : 0.f;
+    ng[u] = (u < du) ? P->cat_negf[u] : 0.f;
   }
-  bool nan_c = P->nan_all != 0;
-  for (int q = 0; q < P->nconst; ++q)
-    if (x[P->const_dim[q]] != P->const_level[q]) nan_c = true;
 
-  // t_j (log2 units, minus the bound M0) for observation row r; q = parity of negative matches
-  auto pair_t = [&](const float* __restrict__ r, float& q) -> float {
-    float t = ci + r[0];
+  // t (log2 units, minus M0) of candidate slot c against observation row r; q = parity of
+  // matches in dims whose Aitchison-Aitken match weight 1-h is negative
+  auto pair_t = [&](const float* __restrict__ r, int c, float& q) -> float {
+    float t = ci[c] + r[0];
 #pragma unroll
-    for (int k = 0; k < DCP; ++k) t = fmaf(xs[k], r[1 + k], t);
+    for (int k = 0; k < DCP; ++k) t = fmaf(xs[c][k], r[1 + k], t);
     q = 0.f;
 #pragma unroll
     for (int u = 0; u < DUP; ++u) {
-      const float m = (xu[u] == r[1 + DCP + u]) ? 1.f : 0.f;
+      const float m = cat_match(xu[c][u], r[1 + DCP + u]);
       t = fmaf(dl[u], m, t);
       if (SIGNED) q = fmaf(m, ng[u], -fabsf(q));
     }
     return t;
   };
 
-  float S = 0.f, Sn = 0.f;
-  for (int jb = 0; jb < n; jb += SUM_BLOCK) {
-    const int je = min(jb + SUM_BLOCK, n);
-    float Sb = 0.f, Snb = 0.f;
-#pragma unroll 2
-    for (int j = jb; j < je; ++j) {
-      float q;
-      const float t = pair_t(table + (int64_t)j * STRIDE, q);
-      const float e = __builtin_amdgcn_exp2f(t);
-      Sb += e;
-      if (SIGNED) Snb = fmaf(fabsf(q), e, Snb);
+  float S[CPT], Sn[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) S[c] = Sn[c] = 0.f;
+  // observation rows are staged through LDS, LDS_ROWS at a time (whole block, 16-B loads), and
+  // read back as wave-wide broadcasts; the sum over one chunk is a partial sum (blocked summation)
+  __shared__ __align__(16) float rows_lds[LDS_ROWS * STRIDE];
+  for (int j0 = 0; j0 < n; j0 += LDS_ROWS) {
+    const int nr = min(LDS_ROWS, n - j0);
+    {
+      const float4* __restrict__ src = (const float4*)(table + (int64_t)j0 * STRIDE);
+      float4* dst = (float4*)rows_lds;
+      for (int q = threadIdx.x; q < nr * (STRIDE / 4); q += 256) dst[q] = src[q];
     }
-    S += Sb;
-    if (SIGNED) Sn += Snb;
+    __syncthreads();
+    float Sb[CPT], Snb[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) Sb[c] = Snb[c] = 0.f;
+#pragma unroll 2
+    for (int j = 0; j < nr; ++j) {
+      float r[STRIDE];
+      const float4* rp = (const float4*)(rows_lds + j * STRIDE);
+#pragma unroll
+      for (int q = 0; q < STRIDE / 4; ++q) {
+        const float4 v = rp[q];
+        r[4 * q] = v.x;
+        r[4 * q + 1] = v.y;
+        r[4 * q + 2] = v.z;
+        r[4 * q + 3] = v.w;
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        float q;
+        const float t = pair_t(r, c, q);
+        const float e = __builtin_amdgcn_exp2f(t);
+        Sb[c] += e;
+        if (SIGNED) Snb[c] = fmaf(fabsf(q), e, Snb[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      S[c] += Sb[c];
+      if (SIGNED) Sn[c] += Snb[c];
+    }
+    __syncthreads();
   }
 
-  // rescue: every term sits far below the static bound -> two-pass (max, then sum) for this lane
-  float off = 0.f;
-  const bool need = valid && !nan_c && (S < 0x1p-64f);
-  if (__any(need)) {
-    if (need) {
-      float mx = -INFINITY, q;
-      for (int j = 0; j < n; ++j) mx = fmaxf(mx, pair_t(table + (int64_t)j * STRIDE, q));
-      S = 0.f;
-      Sn = 0.f;
-      if (mx > -INFINITY) {
-        for (int jb = 0; jb < n; jb += SUM_BLOCK) {
-          const int je = min(jb + SUM_BLOCK, n);
-          float Sb = 0.f, Snb = 0.f;
-          for (int j = jb; j < je; ++j) {
-            const float t = pair_t(table + (int64_t)j * STRIDE, q);
-            const float e = __builtin_amdgcn_exp2f(t - mx);
-            Sb += e;
-            if (SIGNED) Snb = fmaf(fabsf(q), e, Snb);
+  // rescue: every term sits far below the static bound -> two-pass (max, then sum) for that slot
+  float off[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    off[c] = 0.f;
+    const bool need = valid[c] && !nan_c[c] && (S[c] < 0x1p-64f);
+    if (__any(need)) {
+      if (need) {
+        float mx = -INFINITY, q;
+        for (int j = 0; j < n; ++j) mx = fmaxf(mx, pair_t(table + (int64_t)j * STRIDE, c, q));
+        float s = 0.f, sn = 0.f;
+        if (mx > -INFINITY) {
+          for (int jb = 0; jb < n; jb += SUM_BLOCK) {
+            const int je = min(jb + SUM_BLOCK, n);
+            float Sb = 0.f, Snb = 0.f;
+            for (int j = jb; j < je; ++j) {
+              const float t = pair_t(table + (int64_t)j * STRIDE, c, q);
+              const float e = __builtin_amdgcn_exp2f(t - mx);
+              Sb += e;
+              if (SIGNED) Snb = fmaf(fabsf(q), e, Snb);
+            }
+            s += Sb;
+            if (SIGNED) sn += Snb;
           }
-          S += Sb;
-          if (SIGNED) Sn += Snb;
+          off[c] = mx;
         }
-        off = mx;
+        S[c] = s;
+        Sn[c] = sn;
       }
     }
   }
 
-  if (valid) {
+  const float lnorm = (float)P->log_norm;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    if (!valid[c]) continue;
     KdeEst o;
-    const float lnorm = (float)P->log_norm;
-    if (nan_c || S != S) {
+    if (nan_c[c] || S[c] != S[c]) {
       o.lpos = NAN;
       o.lneg = -INFINITY;
       o.err = 0.f;
     } else {
-      const float Sp = SIGNED ? (S - Sn) : S;
-      o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off) * HBX_LN2f + lnorm : -INFINITY;
-      o.lneg = (SIGNED && Sn > 0.f) ? (__log2f(Sn) + off) * HBX_LN2f + lnorm : -INFINITY;
+      const float Sp = SIGNED ? (S[c] - Sn[c]) : S[c];
+      o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off[c]) * HBX_LN2f + lnorm : -INFINITY;
+      o.lneg = (SIGNED && Sn[c] > 0.f) ? (__log2f(Sn[c]) + off[c]) * HBX_LN2f + lnorm : -INFINITY;
       const float u = 0x1p-24f;
-      const float Mabs = fabsf(ci) + P->cmax + bnd + P->sum_abs_delta;
+      const float Mabs = fabsf(ci[c]) + P->cmax + bnd[c] + P->sum_abs_delta;
       const float dt = 3.f * (float)(dc + du + 4) * u * Mabs;  // |error of t|, log2 units
-      const float es = ((float)SUM_BLOCK + (float)n / (float)SUM_BLOCK + 8.f) * u * (SIGNED ? 3.f : 1.f);
+      const float es = ((float)LDS_ROWS + (float)n / (float)LDS_ROWS + 8.f) * u * (SIGNED ? 3.f : 1.f);
       o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
     }
     o.pad = 0.f;
-    out[i] = o;
+    out[idx[c]] = o;
   }
 }
 
@@ -503,9 +566,10 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
 
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 
+#define LOGPDF_CPT 2  // candidates per lane
 template <int DCP, int DUP>
 static logpdf_fn pick_signed(bool sgn) {
-  return sgn ? kde_logpdf_kernel<DCP, DUP, true> : kde_logpdf_kernel<DCP, DUP, false>;
+  return sgn ? kde_logpdf_kernel<DCP, DUP, true, LOGPDF_CPT> : kde_logpdf_kernel<DCP, DUP, false, LOGPDF_CPT>;
 }
 
 template <int DCP>
@@ -691,7 +755,8 @@ int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params
   if (Nc <= 0) return HBX_OK;
   logpdf_fn f = pick_logpdf(dc_pad, du_pad, signed_sum != 0);
   if (!f) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
-  hipLaunchKernelGGL(f, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, (hipStream_t)stream, cand, Nc, D,
+  hipLaunchKernelGGL(f, dim3((unsigned)((Nc + 256 * LOGPDF_CPT - 1) / (256 * LOGPDF_CPT))), dim3(256), 0,
+                     (hipStream_t)stream, cand, Nc, D,
                      (const KdeParams*)params, table, (KdeEst*)est_out);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
@@ -737,12 +802,13 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   HBX_LAUNCH_CHECK();
   if (Nc > 0) {
     const dim3 grid((unsigned)((Nc + 255) / 256));
+    const dim3 grid_s((unsigned)((Nc + 256 * LOGPDF_CPT - 1) / (256 * LOGPDF_CPT)));
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     if (ev) HBX_HIP(hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(fg, grid, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_good, table_good, el);
+    hipLaunchKernelGGL(fg, grid_s, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_good, table_good, el);
     HBX_LAUNCH_CHECK();
     if (ev) HBX_HIP(hipEventRecord(ev[1], s));
-    hipLaunchKernelGGL(fb, grid, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_bad, table_bad, eg);
+    hipLaunchKernelGGL(fb, grid_s, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_bad, table_bad, eg);
     HBX_LAUNCH_CHECK();
     if (ev) HBX_HIP(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, logl_out, logg_out, lo, hi, U,
