@@ -29,6 +29,7 @@ SIGNATURES = {
     "hbx_kde_fit": (c_i32, [c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                             c_vp, c_vp]),
     "hbx_kde_bucket": (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "hbx_kde_table_floats": (c_i64, [c_i32, c_i32, c_i32]),
     "hbx_kde_prepare": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_logpdf": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "hbx_kde_workspace_bytes": (c_i64, [c_i64, c_i64]),

@@ -54,6 +54,15 @@ struct KdeParams {
   double prod_bw_c;   // sequential product of continuous bandwidths (reference op order)
   float cmax;         // max_j |C_j| over the table (error bound)
   float sum_abs_delta;// sum |delta_u| over finite deltas (error bound)
+  int32_t kc;         // categorical mode: 0 = VALU match on codes, k >= 1 = one-hot on f16 MFMA,
+                      // k steps of K=32 (2 * oh_total <= 32 k)
+  int32_t chunk_floats; // floats per 64-observation chunk of this KDE's table (layout depends on kc)
+  int32_t oh_total;   // one-hot width: sum over active categorical dims of (max observed code + 1)
+  const double* X;    // the KDE's data (device): X[rows[j]] is observation j (rescue / exact paths)
+  const int64_t* rows;
+  int32_t oh_dim[64];   // one-hot slot -> active categorical dim u
+  int32_t oh_level[64]; // one-hot slot -> code level
+  int32_t cat_maxcode[HBX_MAX_D]; // per active categorical dim: max observed code (-1: not an integer code)
   int32_t cont_dim[HBX_MAX_D];
   double cont_scale[HBX_MAX_D];     // s_c = sqrt(log2(e) / 2) / h_c
   double center[HBX_MAX_D];         // per continuous slot: mean of the KDE's data (coordinates are

@@ -26,7 +26,9 @@
 #define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
 #define EXACT_GRID 128
 #define SUM_BLOCK 32
-#define LDS_ROWS 128  // observation rows per LDS chunk of the scoring kernel
+#define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
+#define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
+#define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -42,7 +44,54 @@ static void bucket_dims(int dc, int du, int* dc_pad, int* du_pad) {
     if (du <= b) { *du_pad = b; break; }
 }
 
-static int table_stride(int dc_pad, int du_pad) { return (1 + dc_pad + du_pad + 3) & ~3; }
+// Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
+//   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0
+//   [64][du_pad]        categorical codes (float), observation-major
+// KP = dc_pad + 2 rounded up to a multiple of 4 (MFMA 16x16x4 K step).  Observations past n in the
+// last chunk are padding with C_j = -1e30 (their terms are exactly 0).
+//
+// Categorical part when kc >= 1 (one-hot mode): 64 observations x kc*32 f16, observation-major,
+// slot k = 2*t + p of one-hot position t = (dim u, level) holds delta_u's f16 hi (p=0) / lo (p=1)
+// part when the observation has that level, else 0; for signed KDEs a second block of the same
+// shape holds 1 in the hi slot of matches in dims with negative match weight (parity count).
+#define OH_MAX_KC 4  // one-hot mode up to 4 f16 MFMA K-steps: sum over dims of levels <= 64
+__host__ __device__ constexpr int kp_of(int dc_pad) { return (dc_pad + 2 + 3) & ~3; }
+__host__ __device__ constexpr int cat_floats(int du_pad, int kc, int sgn) {
+  return kc == 0 ? OBS_CHUNK * du_pad : OBS_CHUNK * kc * 16 * (sgn ? 2 : 1);
+}
+__host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 0, int sgn = 0) {
+  return kp_of(dc_pad) * KROW + cat_floats(du_pad, kc, sgn);
+}
+static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }  // floats per chunk
+static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
+// capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket
+static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
+  const int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
+  return n_chunks(n) * (int64_t)(a > b ? a : b);
+}
+
+// Per active categorical dim (one block each): max observed code, -1 if some code is not an
+// integer in [0, 1024) (then the one-hot mode is not used).
+__global__ __launch_bounds__(256) void kde_maxcode_kernel(const double* __restrict__ X, int32_t D,
+                                                          const int64_t* __restrict__ rows,
+                                                          KdeParams* __restrict__ P) {
+  __shared__ int red[256];
+  const int u = blockIdx.x;
+  const int d = P->cat_dim[u];
+  int m = -1, bad = 0;
+  for (int j = threadIdx.x; j < P->n; j += blockDim.x) {
+    const double v = X[rows[j] * (int64_t)D + d];
+    if (!(v >= 0.0 && v < 1024.0) || v != floor(v)) bad = 1;
+    else m = max(m, (int)v);
+  }
+  red[threadIdx.x] = bad ? 100000 : m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) P->cat_maxcode[u] = red[0] >= 100000 ? -1 : red[0];
+}
 
 // Per continuous slot: mean of the KDE's data column (centre of the scaled coordinates).
 __global__ void kde_center_kernel(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
@@ -56,37 +105,65 @@ __global__ void kde_center_kernel(const double* __restrict__ X, int32_t D, const
   }
 }
 
-// Fill the per-observation fp32 table: [C_j, X'_1..X'_dcpad, code_1..code_dupad, pad].
-// C_j = -sum_c X'_jc^2 + lb_sum - M0  (log2 units), X'_jc = s_c * (X_jc - mu_c).
+// Fill the chunked observation table (layout above).  X'_jc = s_c * (X_jc - mu_c),
+// C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per table slot j < nchunks*64.
 __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict__ X, int32_t D,
                                                         const int64_t* __restrict__ rows,
                                                         KdeParams* __restrict__ P,
                                                         float* __restrict__ table) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = P->n;
+  const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
   const bool ok = j < n;
+  const bool slot = j < nslots;
   const double* x = X + (ok ? rows[j] : rows[0]) * (int64_t)D;
-  float* row = table + (int64_t)(ok ? j : 0) * P->stride;
   const int dc = P->dc, du = P->du, dcp = P->dc_pad, dup = P->du_pad;
+  const int KP = kp_of(dcp);
+  float* ch = table + (int64_t)(j / OBS_CHUNK) * P->chunk_floats;
+  const int jj = j % OBS_CHUNK;
   double C = 0.0;
-  for (int k = 0; k < dcp; ++k) {
+  for (int k = 0; k < KP - 2; ++k) {
     float v = 0.f;
-    if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+    if (ok && k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
     C -= (double)v * (double)v;
-    if (ok) row[1 + k] = v;
-    float a = ok ? fabsf(v) : 0.f;
+    if (slot) ch[(2 + k) * KROW + jj] = v;
+    float a = fabsf(v);
     for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
     if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&P->xmax[k], __float_as_uint(a));
   }
-  for (int u = 0; u < dup; ++u) {
-    float v = (u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
-    if (ok) row[1 + dcp + u] = v;
+  if (P->kc == 0) {
+    for (int u = 0; u < dup; ++u) {
+      const float v = (ok && u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
+      if (slot) ch[KP * KROW + jj * dup + u] = v;
+    }
+  } else if (slot) {
+    const int W = P->kc * 32;  // halves per observation
+    _Float16* oh = (_Float16*)(ch + KP * KROW) + jj * W;
+    _Float16* par = (_Float16*)(ch + KP * KROW) + OBS_CHUNK * W + jj * W;
+    for (int k = 0; k < W; ++k) {
+      const int t = k >> 1, p = k & 1;
+      float v = 0.f, pv = 0.f;
+      if (ok && t < P->oh_total) {
+        const int u = P->oh_dim[t];
+        if (x[P->cat_dim[u]] == (double)P->oh_level[t]) {
+          const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
+          const float hi = (float)(_Float16)dl;
+          v = (p == 0) ? hi : (fabsf(dl) < 60000.f ? dl - hi : 0.f);
+          pv = (p == 0 && P->cat_negf[u] != 0.f) ? 1.f : 0.f;
+        }
+      }
+      oh[k] = (_Float16)v;
+      if (P->has_neg) par[k] = (_Float16)pv;
+    }
   }
-  for (int p = 1 + dcp + dup; p < P->stride; ++p)
-    if (ok) row[p] = 0.f;
   C += P->lb_sum - P->m0_log2;
-  const float Cf = (float)C;
-  if (ok) row[0] = Cf;
+  const float Cf = ok ? (float)C : -1e30f;
+  if (slot) {
+    ch[0 * KROW + jj] = Cf;
+    ch[1 * KROW + jj] = 1.f;
+    if (jj < KROW - OBS_CHUNK)  // zero the pad columns of every k-row once per chunk
+      for (int k = 0; k < KP; ++k) ch[k * KROW + OBS_CHUNK + jj] = 0.f;
+  }
   float a = ok ? fabsf(Cf) : 0.f;
   for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
   if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)&P->cmax, __float_as_uint(a));
@@ -95,64 +172,109 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// fp32 log-domain scoring: CPT candidates per lane, all observations of one KDE
+// fp32 log-domain scoring
 //
 // Per (candidate i, observation j), in log2 units and minus the static bound M0:
-//   t_ij = c_i + C_j + sum_c x''_ic X'_jc + sum_u delta_u [x_iu == X_ju]
+//   t_ij = C_j + c_i + sum_c x''_ic X'_jc + sum_u delta_u [x_iu == X_ju]
 // with X' = s (X - mu), x'' = 2 s (x - mu), c_i = -|x'_i|^2, C_j = -|X'_j|^2 + lb_sum - M0
-// (the expansion of -|x' - X'|^2: one FMA per continuous dim).  The observation row is wave-uniform
-// and arrives through scalar loads (s_load_dwordx16) as SGPR operands of the FMAs.  Each lane keeps
-// CPT candidates in registers: CPT independent dependency chains per observation, and every scalar
-// load is amortised over CPT*64 candidates.  The categorical match uses m = clamp(1 - d*d) on the
-// integer codes (d = x - X), which stays in the VALU (no VCC round trip).
+// (the expansion of -|x' - X'|^2).  The first three terms are one GEMM-shaped product
+// [candidates x K] . [K x observations] with K = 2 + Dc: they run on the f32 matrix cores
+// (v_mfma_f32_16x16x4_f32, an exact fp32 FMA chain in k order).  The categorical match,
+// exp2 and the sums run on the VALU beside them.  The categorical match is m = clamp(1 - d*d) on
+// the integer codes (d = x - X), which stays in the VALU (no VCC round trip).
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float cat_match(float a, float b) {
   const float d = a - b;
   return __builtin_amdgcn_fmed3f(fmaf(-d, d, 1.f), 0.f, 1.f);
 }
 
-template <int DCP, int DUP, bool SIGNED, int CPT>
-__global__ __launch_bounds__(256) void kde_logpdf_kernel(const double* __restrict__ cand, int64_t Nc,
-                                                         int32_t D, const KdeParams* __restrict__ P,
-                                                         const float* __restrict__ table,
-                                                         KdeEst* __restrict__ out) {
-  constexpr int STRIDE = (1 + DCP + DUP + 3) & ~3;
-  constexpr int NC = DCP > 0 ? DCP : 1;
-  constexpr int NU = DUP > 0 ? DUP : 1;
-  const int n = P->n;
-  const int dc = P->dc, du = P->du;
+__device__ __forceinline__ float cand_code(double xv) {
+  // codes are integers; anything else (incl. NaN) never equals an observed code
+  return (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
+}
 
-  int64_t idx[CPT];
-  bool valid[CPT], nan_c[CPT];
-  float xs[CPT][NC], xu[CPT][NU], ci[CPT], bnd[CPT];
+// Per-candidate epilogue: ln S+, ln S-, error bound (or the rescue marker err = -1)
+__device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, float S, float Sn, float off,
+                                             bool nan_c, float ci, float bnd, bool SIGNED, int chunk) {
+  KdeEst o;
+  o.pad = 0.f;
+  if (nan_c || S != S) {
+    o.lpos = NAN;
+    o.lneg = -INFINITY;
+    o.err = 0.f;
+    return o;
+  }
+  const float lnorm = (float)P->log_norm;
+  const float Sp = SIGNED ? (S - Sn) : S;
+  o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off) * HBX_LN2f + lnorm : -INFINITY;
+  o.lneg = (SIGNED && Sn > 0.f) ? (__log2f(Sn) + off) * HBX_LN2f + lnorm : -INFINITY;
+  const float u = 0x1p-24f;
+  const float Mabs = fabsf(ci) + P->cmax + bnd + P->sum_abs_delta;
+  const float dt = 3.f * (float)(P->dc + P->du + 4) * u * Mabs;  // |error of t|, log2 units
+  const float es = ((float)chunk + (float)P->n / (float)chunk + 24.f) * u * (SIGNED ? 3.f : 1.f);
+  o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
+  return o;
+}
+
+template <int DCP, int DUP, bool SIGNED>
+__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_kernel(const double* __restrict__ cand, int64_t Nc,
+                                                                    int32_t D, const KdeParams* __restrict__ P,
+                                                                    const float* __restrict__ table,
+                                                                    KdeEst* __restrict__ out) {
+  constexpr int KP = kp_of(DCP);
+  constexpr int NS = KP / 4;
+  constexpr int CHF = chunk_floats(DCP, DUP);
+  constexpr int NU = DUP > 0 ? DUP : 1;
+  __shared__ __align__(16) float lds[2 * CHF];  // double-buffered observation chunks
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;  // this wave's 16 candidates
+  const int n = P->n, dc = P->dc, du = P->du;
+  const int ia = lane & 15, kq = lane >> 4;
+
+  // A fragments: lane holds A[i = ia][k = 4s + kq]; A[i][0] = 1 (x C_j), A[i][1] = c_i, A[i][2+c] = x''_ic
+  float a[NS];
+  float ci_a = 0.f, bnd_a = 0.f;
+  {
+    int64_t ii = cbase + ia;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+    for (int k = 0; k < dc; ++k) {
+      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+      ci_a = fmaf(-v, v, ci_a);
+      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
+    }
 #pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    idx[c] = (int64_t)blockIdx.x * (256 * CPT) + c * 256 + threadIdx.x;
-    valid[c] = idx[c] < Nc;
-    const double* x = cand + (valid[c] ? idx[c] : (Nc - 1)) * (int64_t)D;
-    ci[c] = 0.f;
-    bnd[c] = 0.f;
-#pragma unroll
-    for (int k = 0; k < DCP; ++k) {
+    for (int s = 0; s < NS; ++s) {
+      const int k = 4 * s + kq;
       float v = 0.f;
-      if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-      ci[c] = fmaf(-v, v, ci[c]);
-      xs[c][k] = 2.f * v;
-      if (k < dc) bnd[c] = fmaf(fabsf(xs[c][k]), P->xmax[k], bnd[c]);
-    }
-#pragma unroll
-    for (int u = 0; u < DUP; ++u) {
-      float v = -1.f;
-      if (u < du) {
-        const double xv = x[P->cat_dim[u]];
-        // codes are integers; anything else (incl. NaN) never equals an observed code
-        v = (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
+      if (k == 0) {
+        v = 1.f;
+      } else if (k == 1) {
+        v = ci_a;
+      } else if (k - 2 < dc) {
+        const int c = k - 2;
+        v = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
       }
-      xu[c][u] = v;
+      a[s] = v;
     }
-    nan_c[c] = P->nan_all != 0;
-    for (int q = 0; q < P->nconst; ++q)
-      if (x[P->const_dim[q]] != P->const_level[q]) nan_c[c] = true;
+  }
+  // epilogue rows: the accumulator of lane holds candidates 4*kq + q (q = 0..3), observation ia
+  float xu[4][NU];
+  bool nanc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int64_t ii = cbase + 4 * kq + q;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+#pragma unroll
+    for (int u = 0; u < DUP; ++u) xu[q][u] = (u < du) ? cand_code(x[P->cat_dim[u]]) : -1.f;
+    bool nn = P->nan_all != 0;
+    for (int c = 0; c < P->nconst; ++c)
+      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
+    nanc[q] = nn;
   }
   float dl[NU], ng[NU];
 #pragma unroll
@@ -161,122 +283,392 @@ __global__ __launch_bounds__(256) void kde_logpdf_kernel(const double* __restric
     ng[u] = (u < du) ? P->cat_negf[u] : 0.f;
   }
 
-  // t (log2 units, minus M0) of candidate slot c against observation row r; q = parity of
-  // matches in dims whose Aitchison-Aitken match weight 1-h is negative
-  auto pair_t = [&](const float* __restrict__ r, int c, float& q) -> float {
-    float t = ci[c] + r[0];
+  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
+  constexpr int NT = 64 * MFMA_WAVES;                 // threads per block
+  constexpr int NV4 = CHF / 4;                        // float4 per chunk
+  constexpr int PER = (NV4 + NT - 1) / NT;            // float4 per thread per chunk
+  float4 pre[PER];
+  // stage chunk 0; later chunks are prefetched into registers during the previous chunk's math
+  {
+    const float4* __restrict__ src = (const float4*)table;
 #pragma unroll
-    for (int k = 0; k < DCP; ++k) t = fmaf(xs[c][k], r[1 + k], t);
-    q = 0.f;
+    for (int q = 0; q < PER; ++q) {
+      const int v = threadIdx.x + q * NT;
+      if (v < NV4) ((float4*)lds)[v] = src[v];
+    }
+  }
+  __syncthreads();
+
+  // one 16x16 tile: B fragments and categorical codes of observation column jt*16 + ia
+  auto load_tile = [&](const float* buf, int jt, float* b, float* xo) {
 #pragma unroll
-    for (int u = 0; u < DUP; ++u) {
-      const float m = cat_match(xu[c][u], r[1 + DCP + u]);
-      t = fmaf(dl[u], m, t);
-      if (SIGNED) q = fmaf(m, ng[u], -fabsf(q));
+    for (int s2 = 0; s2 < NS; ++s2) b[s2] = buf[(4 * s2 + kq) * KROW + jt * 16 + ia];
+#pragma unroll
+    for (int u = 0; u < DUP; ++u) xo[u] = buf[KP * KROW + (jt * 16 + ia) * DUP + u];
+  };
+  auto epilogue = [&](const f32x4& acc, const float* xo, float* Sb, float* Snb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float t = acc[q];
+      float par = 0.f;
+#pragma unroll
+      for (int u = 0; u < DUP; ++u) {
+        const float m = cat_match(xu[q][u], xo[u]);
+        t = fmaf(dl[u], m, t);
+        if (SIGNED) par = fmaf(m, ng[u], -fabsf(par));
+      }
+      const float e = __builtin_amdgcn_exp2f(t);
+      Sb[q] += e;
+      if (SIGNED) Snb[q] = fmaf(fabsf(par), e, Snb[q]);
+    }
+  };
+
+  for (int c = 0; c < nchunks; ++c) {
+    float* buf = lds + (c & 1) * CHF;
+    const bool more = c + 1 < nchunks;
+    if (more) {  // prefetch the next chunk into registers (lands during this chunk's math)
+      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) pre[q] = src[v];
+      }
+    }
+    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
+    // software pipeline over tile pairs: MFMAs of pair p+1 are issued before the VALU epilogue of p
+    float b0[NS], b1[NS], xo0[NU], xo1[NU];
+    f32x4 acc0, acc1;
+    load_tile(buf, 0, b0, xo0);
+    load_tile(buf, 1, b1, xo1);
+    acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b0[s2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b1[s2], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
+      f32x4 n0 = acc0, n1 = acc1;
+      float c0[NU], c1[NU];
+#pragma unroll
+      for (int u = 0; u < DUP; ++u) {
+        c0[u] = xo0[u];
+        c1[u] = xo1[u];
+      }
+      if (p + 1 < OBS_CHUNK / 32) {
+        load_tile(buf, 2 * p + 2, b0, xo0);
+        load_tile(buf, 2 * p + 3, b1, xo1);
+        acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b0[s2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b1[s2], acc1, 0, 0, 0);
+        }
+      }
+      epilogue(n0, c0, Sb, Snb);
+      epilogue(n1, c1, Sb, Snb);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      S[q] += Sb[q];
+      if (SIGNED) Sn[q] += Snb[q];
+    }
+    if (more) {  // publish the prefetched chunk into the other buffer
+      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) dst[v] = pre[q];
+      }
+    }
+    __syncthreads();
+  }
+  // reduce over the 16 lanes (observation columns) that share kq
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      S[q] += __shfl_xor(S[q], o);
+      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
+    }
+  }
+  // lane ia = q of group kq writes candidate 4*kq + q; c_i / bound of that candidate live in lane
+  // (4*kq + q) & 15 + 16*anything of the A layout -> fetch with a shuffle
+  const int src_lane = (4 * kq + (ia & 3)) & 15;
+  const float ci_q = __shfl(ci_a, src_lane);
+  const float bnd_q = __shfl(bnd_a, src_lane);
+  if (ia < 4) {
+    const int q = ia;
+    const int64_t ii = cbase + 4 * kq + q;
+    float Sq = S[0], Snq = Sn[0];
+    bool nq = nanc[0];
+    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
+    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
+    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
+    if (ii < Nc) {
+      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;  // rescue marker (kde_rescue_kernel)
+      out[ii] = o;
+    }
+  }
+}
+
+// One-hot mode: the categorical sum  sum_u delta_u [x_u == X_u]  is a second matrix product,
+// (candidate one-hot) x (delta-weighted observation one-hot), on the f16 matrix cores: operands are
+// 0/1 and the f16 hi+lo parts of delta_u, so every product is exact and only the fp32 accumulation
+// rounds.  It continues the same accumulator as the f32 continuous product, leaving the VALU only
+// exp2 and the running sums.  Signed KDEs add one more f16 product that counts matches in dims with
+// a negative match weight (the sign of the term is (-1)^count).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int DCP, int KC, bool SIGNED>
+__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_oh_kernel(const double* __restrict__ cand,
+                                                                       int64_t Nc, int32_t D,
+                                                                       const KdeParams* __restrict__ P,
+                                                                       const float* __restrict__ table,
+                                                                       KdeEst* __restrict__ out) {
+  constexpr int KP = kp_of(DCP);
+  constexpr int NS = KP / 4;
+  constexpr int W = KC * 32;  // one-hot halves per observation
+  constexpr int CHF = chunk_floats(DCP, 0, KC, SIGNED ? 1 : 0);
+  __shared__ __align__(16) float lds[2 * CHF];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;
+  const int n = P->n, dc = P->dc;
+  const int ia = lane & 15, kq = lane >> 4;
+
+  float a[NS];
+  f16x8 ah[KC];
+  float ci_a = 0.f, bnd_a = 0.f;
+  {
+    int64_t ii = cbase + ia;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+    for (int k = 0; k < dc; ++k) {
+      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+      ci_a = fmaf(-v, v, ci_a);
+      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int k = 4 * s + kq;
+      float v = 0.f;
+      if (k == 0) {
+        v = 1.f;
+      } else if (k == 1) {
+        v = ci_a;
+      } else if (k - 2 < dc) {
+        const int c = k - 2;
+        v = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
+      }
+      a[s] = v;
+    }
+    // candidate one-hot: lane holds A[row ia][k = 32 s + 8 kq + j]
+    const int tot = P->oh_total;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = (32 * s + 8 * kq + j) >> 1;
+        float v = 0.f;
+        if (t < tot && x[P->cat_dim[P->oh_dim[t]]] == (double)P->oh_level[t]) v = 1.f;
+        ah[s][j] = (_Float16)v;
+      }
+    }
+  }
+  bool nanc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int64_t ii = cbase + 4 * kq + q;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+    bool nn = P->nan_all != 0;
+    for (int c = 0; c < P->nconst; ++c)
+      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
+    nanc[q] = nn;
+  }
+
+  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
+  constexpr int NT = 64 * MFMA_WAVES;
+  constexpr int NV4 = CHF / 4;
+  constexpr int PER = (NV4 + NT - 1) / NT;
+  float4 pre[PER];
+  {
+    const float4* __restrict__ src = (const float4*)table;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int v = threadIdx.x + q * NT;
+      if (v < NV4) ((float4*)lds)[v] = src[v];
+    }
+  }
+  __syncthreads();
+
+  // accumulate one 16x16 tile: f32 continuous product, then the f16 one-hot product
+  auto tile = [&](const float* buf, int jt, f32x4& acc, f32x4& accp) {
+    const _Float16* ohb = (const _Float16*)(buf + KP * KROW);
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], buf[(4 * s + kq) * KROW + jt * 16 + ia], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      const f16x8 b = *(const f16x8*)(ohb + (jt * 16 + ia) * W + 32 * s + 8 * kq);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], b, acc, 0, 0, 0);
+    }
+    if (SIGNED) {
+      accp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+        const f16x8 b = *(const f16x8*)(ohb + OBS_CHUNK * W + (jt * 16 + ia) * W + 32 * s + 8 * kq);
+        accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], b, accp, 0, 0, 0);
+      }
+    }
+  };
+  auto epilogue = [&](const f32x4& acc, const f32x4& accp, float* Sb, float* Snb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e = __builtin_amdgcn_exp2f(acc[q]);
+      Sb[q] += e;
+      if (SIGNED) {
+        const float odd = 2.f * __builtin_amdgcn_fractf(0.5f * accp[q]);  // count mod 2
+        Snb[q] = fmaf(odd, e, Snb[q]);
+      }
+    }
+  };
+
+  for (int c = 0; c < nchunks; ++c) {
+    float* buf = lds + (c & 1) * CHF;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) pre[q] = src[v];
+      }
+    }
+    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0, acc1, ap0, ap1;
+    tile(buf, 0, acc0, ap0);
+    tile(buf, 1, acc1, ap1);
+#pragma unroll
+    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
+      const f32x4 n0 = acc0, n1 = acc1, m0 = ap0, m1 = ap1;
+      if (p + 1 < OBS_CHUNK / 32) {
+        tile(buf, 2 * p + 2, acc0, ap0);
+        tile(buf, 2 * p + 3, acc1, ap1);
+      }
+      epilogue(n0, m0, Sb, Snb);
+      epilogue(n1, m1, Sb, Snb);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      S[q] += Sb[q];
+      if (SIGNED) Sn[q] += Snb[q];
+    }
+    if (more) {
+      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) dst[v] = pre[q];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      S[q] += __shfl_xor(S[q], o);
+      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
+    }
+  }
+  const int src_lane = (4 * kq + (ia & 3)) & 15;
+  const float ci_q = __shfl(ci_a, src_lane);
+  const float bnd_q = __shfl(bnd_a, src_lane);
+  if (ia < 4) {
+    const int q = ia;
+    const int64_t ii = cbase + 4 * kq + q;
+    float Sq = S[0], Snq = Sn[0];
+    bool nq = nanc[0];
+    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
+    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
+    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
+    if (ii < Nc) {
+      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
+      out[ii] = o;
+    }
+  }
+}
+
+// Rescue (rare): candidates whose every term sits far below the static bound M0 are recomputed
+// with a true maximum (two passes over the observations), one candidate per thread on the VALU.
+// Continuous coordinates come from the table's f32 part, categorical codes straight from the data.
+template <int DCP, bool SIGNED>
+__global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                         const KdeParams* __restrict__ P,
+                                                         const float* __restrict__ table,
+                                                         KdeEst* __restrict__ out) {
+  constexpr int NC = DCP > 0 ? DCP : 1;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool need = i < Nc && out[i].err == -1.f;
+  if (!__any(need)) return;
+  if (!need) return;
+  const double* x = cand + i * (int64_t)D;
+  const int n = P->n, dc = P->dc, du = P->du, CHF = P->chunk_floats;
+  const double* __restrict__ Xo = P->X;
+  const int64_t* __restrict__ rows = P->rows;
+  float xs[NC], ci = 0.f, bnd = 0.f;
+#pragma unroll
+  for (int k = 0; k < DCP; ++k) {
+    float v = 0.f;
+    if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+    ci = fmaf(-v, v, ci);
+    xs[k] = 2.f * v;
+    if (k < dc) bnd = fmaf(fabsf(xs[k]), P->xmax[k], bnd);
+  }
+  auto pair_t = [&](int j, float& par) -> float {
+    const float* ch = table + (int64_t)(j / OBS_CHUNK) * CHF;
+    const int jj = j % OBS_CHUNK;
+    float t = fmaf(1.f, ch[jj], 0.f);
+    t = fmaf(ci, 1.f, t);
+#pragma unroll
+    for (int k = 0; k < DCP; ++k) t = fmaf(xs[k], ch[(2 + k) * KROW + jj], t);
+    par = 0.f;
+    const double* xo = Xo + rows[j] * (int64_t)D;
+    for (int u = 0; u < du; ++u) {
+      const int d = P->cat_dim[u];
+      const float m = (x[d] == xo[d]) ? 1.f : 0.f;
+      t = fmaf(P->cat_delta[u], m, t);
+      if (SIGNED) par = fmaf(m, P->cat_negf[u], -fabsf(par));
     }
     return t;
   };
-
-  float S[CPT], Sn[CPT];
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) S[c] = Sn[c] = 0.f;
-  // observation rows are staged through LDS, LDS_ROWS at a time (whole block, 16-B loads), and
-  // read back as wave-wide broadcasts; the sum over one chunk is a partial sum (blocked summation)
-  __shared__ __align__(16) float rows_lds[LDS_ROWS * STRIDE];
-  for (int j0 = 0; j0 < n; j0 += LDS_ROWS) {
-    const int nr = min(LDS_ROWS, n - j0);
-    {
-      const float4* __restrict__ src = (const float4*)(table + (int64_t)j0 * STRIDE);
-      float4* dst = (float4*)rows_lds;
-      for (int q = threadIdx.x; q < nr * (STRIDE / 4); q += 256) dst[q] = src[q];
-    }
-    __syncthreads();
-    float Sb[CPT], Snb[CPT];
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) Sb[c] = Snb[c] = 0.f;
-#pragma unroll 2
-    for (int j = 0; j < nr; ++j) {
-      float r[STRIDE];
-      const float4* rp = (const float4*)(rows_lds + j * STRIDE);
-#pragma unroll
-      for (int q = 0; q < STRIDE / 4; ++q) {
-        const float4 v = rp[q];
-        r[4 * q] = v.x;
-        r[4 * q + 1] = v.y;
-        r[4 * q + 2] = v.z;
-        r[4 * q + 3] = v.w;
+  float mx = -INFINITY, par;
+  for (int j = 0; j < n; ++j) mx = fmaxf(mx, pair_t(j, par));
+  float S = 0.f, Sn = 0.f;
+  if (mx > -INFINITY) {
+    for (int j0 = 0; j0 < n; j0 += OBS_CHUNK) {
+      float Sb = 0.f, Snb = 0.f;
+      for (int j = j0; j < min(n, j0 + OBS_CHUNK); ++j) {
+        const float e = __builtin_amdgcn_exp2f(pair_t(j, par) - mx);
+        Sb += e;
+        if (SIGNED) Snb = fmaf(fabsf(par), e, Snb);
       }
-#pragma unroll
-      for (int c = 0; c < CPT; ++c) {
-        float q;
-        const float t = pair_t(r, c, q);
-        const float e = __builtin_amdgcn_exp2f(t);
-        Sb[c] += e;
-        if (SIGNED) Snb[c] = fmaf(fabsf(q), e, Snb[c]);
-      }
+      S += Sb;
+      Sn += Snb;
     }
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      S[c] += Sb[c];
-      if (SIGNED) Sn[c] += Snb[c];
-    }
-    __syncthreads();
+  } else {
+    mx = 0.f;
   }
-
-  // rescue: every term sits far below the static bound -> two-pass (max, then sum) for that slot
-  float off[CPT];
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    off[c] = 0.f;
-    const bool need = valid[c] && !nan_c[c] && (S[c] < 0x1p-64f);
-    if (__any(need)) {
-      if (need) {
-        float mx = -INFINITY, q;
-        for (int j = 0; j < n; ++j) mx = fmaxf(mx, pair_t(table + (int64_t)j * STRIDE, c, q));
-        float s = 0.f, sn = 0.f;
-        if (mx > -INFINITY) {
-          for (int jb = 0; jb < n; jb += SUM_BLOCK) {
-            const int je = min(jb + SUM_BLOCK, n);
-            float Sb = 0.f, Snb = 0.f;
-            for (int j = jb; j < je; ++j) {
-              const float t = pair_t(table + (int64_t)j * STRIDE, c, q);
-              const float e = __builtin_amdgcn_exp2f(t - mx);
-              Sb += e;
-              if (SIGNED) Snb = fmaf(fabsf(q), e, Snb);
-            }
-            s += Sb;
-            if (SIGNED) sn += Snb;
-          }
-          off[c] = mx;
-        }
-        S[c] = s;
-        Sn[c] = sn;
-      }
-    }
-  }
-
-  const float lnorm = (float)P->log_norm;
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    if (!valid[c]) continue;
-    KdeEst o;
-    if (nan_c[c] || S[c] != S[c]) {
-      o.lpos = NAN;
-      o.lneg = -INFINITY;
-      o.err = 0.f;
-    } else {
-      const float Sp = SIGNED ? (S[c] - Sn[c]) : S[c];
-      o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off[c]) * HBX_LN2f + lnorm : -INFINITY;
-      o.lneg = (SIGNED && Sn[c] > 0.f) ? (__log2f(Sn[c]) + off[c]) * HBX_LN2f + lnorm : -INFINITY;
-      const float u = 0x1p-24f;
-      const float Mabs = fabsf(ci[c]) + P->cmax + bnd[c] + P->sum_abs_delta;
-      const float dt = 3.f * (float)(dc + du + 4) * u * Mabs;  // |error of t|, log2 units
-      const float es = ((float)LDS_ROWS + (float)n / (float)LDS_ROWS + 8.f) * u * (SIGNED ? 3.f : 1.f);
-      o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
-    }
-    o.pad = 0.f;
-    out[idx[c]] = o;
-  }
+  out[i] = finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -565,36 +957,66 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
 // launch-side dispatch over the (dc_pad, du_pad, signed) template buckets
 
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
+struct ScoreFns {
+  logpdf_fn main, rescue;
+};
 
-#define LOGPDF_CPT 2  // candidates per lane
+// variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1.. = kc
+template <int DCP, int DUP, bool SG>
+static ScoreFns pick_kc(int kc) {
+  const logpdf_fn r = kde_rescue_kernel<DCP, SG>;
+  switch (kc) {
+    case 0: return {kde_logpdf_kernel<DCP, DUP, SG>, r};
+    case 1: return {kde_logpdf_oh_kernel<DCP, 1, SG>, r};
+    case 2: return {kde_logpdf_oh_kernel<DCP, 2, SG>, r};
+    case 3: return {kde_logpdf_oh_kernel<DCP, 3, SG>, r};
+    case 4: return {kde_logpdf_oh_kernel<DCP, 4, SG>, r};
+  }
+  return {nullptr, nullptr};
+}
+
 template <int DCP, int DUP>
-static logpdf_fn pick_signed(bool sgn) {
-  return sgn ? kde_logpdf_kernel<DCP, DUP, true, LOGPDF_CPT> : kde_logpdf_kernel<DCP, DUP, false, LOGPDF_CPT>;
+static ScoreFns pick_signed(int variant) {
+  const int kc = variant >> 1;
+  return (variant & 1) ? pick_kc<DCP, DUP, true>(kc) : pick_kc<DCP, DUP, false>(kc);
 }
 
 template <int DCP>
-static logpdf_fn pick_du(int du_pad, bool sgn) {
+static ScoreFns pick_du(int du_pad, int variant) {
   switch (du_pad) {
-    case 0: return pick_signed<DCP, 0>(sgn);
-    case 4: return pick_signed<DCP, 4>(sgn);
-    case 8: return pick_signed<DCP, 8>(sgn);
-    case 16: return pick_signed<DCP, 16>(sgn);
-    case 32: return pick_signed<DCP, 32>(sgn);
+    case 0: return pick_signed<DCP, 0>(variant & 1);  // no categorical dims: kc irrelevant
+    case 4: return pick_signed<DCP, 4>(variant);
+    case 8: return pick_signed<DCP, 8>(variant);
+    case 16: return pick_signed<DCP, 16>(variant);
+    case 32: return pick_signed<DCP, 32>(variant);
   }
-  return nullptr;
+  return {nullptr, nullptr};
 }
 
-static logpdf_fn pick_logpdf(int dc_pad, int du_pad, bool sgn) {
+static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   switch (dc_pad) {
-    case 0: return pick_du<0>(du_pad, sgn);
-    case 4: return pick_du<4>(du_pad, sgn);
-    case 8: return pick_du<8>(du_pad, sgn);
-    case 16: return pick_du<16>(du_pad, sgn);
-    case 24: return pick_du<24>(du_pad, sgn);
-    case 32: return pick_du<32>(du_pad, sgn);
-    case 64: return pick_du<64>(du_pad, sgn);
+    case 0: return pick_du<0>(du_pad, variant);
+    case 4: return pick_du<4>(du_pad, variant);
+    case 8: return pick_du<8>(du_pad, variant);
+    case 16: return pick_du<16>(du_pad, variant);
+    case 24: return pick_du<24>(du_pad, variant);
+    case 32: return pick_du<32>(du_pad, variant);
+    case 64: return pick_du<64>(du_pad, variant);
   }
-  return nullptr;
+  return {nullptr, nullptr};
+}
+
+// launch main + rescue scoring for one KDE
+static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
+                        KdeEst* est, hipStream_t s) {
+  const unsigned gm = (unsigned)((Nc + 16 * MFMA_WAVES - 1) / (16 * MFMA_WAVES));
+  hipLaunchKernelGGL(f.main, dim3(gm), dim3(64 * MFMA_WAVES), 0, s, cand, Nc, D, (const KdeParams*)params, table,
+                     est);
+  HBX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(f.rescue, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D,
+                     (const KdeParams*)params, table, est);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
 }
 
 // workspace layout (bytes), shared by hbx_kde_workspace_bytes and hbx_kde_acquire
@@ -629,6 +1051,8 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax) {
 
 extern "C" {
 
+int64_t hbx_kde_table_floats(int32_t n, int32_t dc_pad, int32_t du_pad) { return table_floats(n, dc_pad, du_pad); }
+
 int hbx_kde_bucket(int32_t dc, int32_t du, int32_t* dc_pad, int32_t* du_pad, int32_t* stride) {
   int a, b;
   bucket_dims(dc, du, &a, &b);
@@ -646,9 +1070,9 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax) { return (int64_t)ws_l
 // Build one KDE (good or bad) for scoring.  Host arrays: vartype[D] (0='c', 1='u'), bw[D], nlev[D].
 // Device arrays: X[N][D] fp64 (rows of the whole budget), rows[n] int64 (this KDE's rows, in the
 // reference's order).  Outputs: params (device, hbx_kde_param_bytes()), table (device fp32,
-// n * stride floats), info[8] (host): {has_neg, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}.
+// hbx_kde_table_floats(n, dc_pad, du_pad) floats), info[8] (host): {has_neg, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}.
 int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, const int32_t* vartype,
-                    const double* bw, const int32_t* nlev, void* params, float* table, int64_t table_floats,
+                    const double* bw, const int32_t* nlev, void* params, float* table, int64_t table_floats_,
                     int32_t* info, void* stream) {
   if (!X || !rows || !vartype || !bw || !nlev || !params || !table || !info)
     return hbx_fail(HBX_ERR_ARG, "hbx_kde_prepare: null pointer");
@@ -670,10 +1094,10 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   P->dc_pad = dcp;
   P->du_pad = dup;
   P->stride = table_stride(dcp, dup);
-  if (table_floats < (int64_t)n * P->stride) {
+  if (table_floats_ < table_floats(n, dcp, dup)) {
     free(P);
-    return hbx_fail(HBX_ERR_ARG, "table too small: %lld < %lld floats", (long long)table_floats,
-                    (long long)n * P->stride);
+    return hbx_fail(HBX_ERR_ARG, "table too small: %lld < %lld floats", (long long)table_floats_,
+                    (long long)table_floats(n, dcp, dup));
   }
   const double LOG2E = 1.4426950408889634;
   double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
@@ -726,7 +1150,47 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   P->prod_bw_c = prod_bw_c;
   P->sum_abs_delta = sad;
   P->log_norm = -log((double)n) - sum_ln_h - 0.5 * (double)P->dc * log(2.0 * M_PI) + m0 * M_LN2;
-  info[0] = P->has_neg;
+  P->X = X;
+  P->rows = rows;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
+  // categorical mode: one-hot on the f16 matrix cores when every active dim has integer codes in
+  // [0, 1024) and the one-hot width sum(max code + 1) fits OH_MAX_KC K-steps; else VALU matching
+  if (e == hipSuccess && P->du > 0) {
+    hipLaunchKernelGGL(kde_maxcode_kernel, dim3(P->du), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
+    e = hipGetLastError();
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(P->cat_maxcode, ((KdeParams*)params)->cat_maxcode, sizeof(int32_t) * HBX_MAX_D,
+                         hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+  }
+  if (e != hipSuccess) {
+    free(P);
+    return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
+  }
+  P->kc = 0;
+  P->oh_total = 0;
+  if (P->du > 0) {
+    int tot = 0;
+    bool ok = true;
+    for (int u = 0; u < P->du; ++u) {
+      if (P->cat_maxcode[u] < 0) ok = false;
+      else tot += P->cat_maxcode[u] + 1;
+    }
+    if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
+      P->kc = (2 * tot + 31) / 32;
+      P->oh_total = tot;
+      int t = 0;
+      for (int u = 0; u < P->du; ++u)
+        for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
+          P->oh_dim[t] = u;
+          P->oh_level[t] = l;
+          ++t;
+        }
+    }
+  }
+  P->chunk_floats = chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
+  info[0] = P->has_neg | (P->kc << 1);  // scoring variant (hbx_kde_logpdf / hbx_kde_acquire)
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
@@ -734,32 +1198,28 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   info[5] = P->nconst;
   info[6] = P->dc_pad;
   info[7] = P->du_pad;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
+  e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   free(P);
   if (e != hipSuccess) return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
   hipLaunchKernelGGL(kde_center_kernel, dim3(1), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
   HBX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kde_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, X, D, rows, (KdeParams*)params,
-                     table);
+  const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
+  hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
+                     (KdeParams*)params, table);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
 
 // fp32 log-domain scoring of Nc candidates (fp64 [Nc][D] row-major) against one prepared KDE
 int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
-                   int32_t dc_pad, int32_t du_pad, int32_t signed_sum, void* est_out, void* stream) {
+                   int32_t dc_pad, int32_t du_pad, int32_t variant, void* est_out, void* stream) {
   if ((!cand || !est_out) && Nc > 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf: null pointer");
   if (!params || !table) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf: null pointer");
   if (Nc <= 0) return HBX_OK;
-  logpdf_fn f = pick_logpdf(dc_pad, du_pad, signed_sum != 0);
-  if (!f) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
-  hipLaunchKernelGGL(f, dim3((unsigned)((Nc + 256 * LOGPDF_CPT - 1) / (256 * LOGPDF_CPT))), dim3(256), 0,
-                     (hipStream_t)stream, cand, Nc, D,
-                     (const KdeParams*)params, table, (KdeEst*)est_out);
-  HBX_LAUNCH_CHECK();
-  return HBX_OK;
+  ScoreFns f = pick_logpdf(dc_pad, du_pad, variant);
+  if (!f.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
+  return launch_score(f, cand, Nc, D, params, table, (KdeEst*)est_out, (hipStream_t)stream);
 }
 
 // One acquisition: score every candidate against l (good) and g (bad), shortlist, exact re-score,
@@ -767,9 +1227,9 @@ int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params
 // (AcqResult) stays in the workspace; hbx_kde_result_ptr() gives its device address.
 int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
                     const void* params_good, const float* table_good, const double* X_good,
-                    const int64_t* rows_good, int32_t signed_good,
+                    const int64_t* rows_good, int32_t variant_good,
                     const void* params_bad, const float* table_bad, const double* X_bad,
-                    const int64_t* rows_bad, int32_t signed_bad, int32_t dc_pad, int32_t du_pad,
+                    const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
                     void* events, void* stream) {
   if ((!cand && Nc > 0) || !params_good || !table_good || !X_good || !rows_good || !params_bad || !table_bad ||
@@ -780,9 +1240,9 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   if ((size_t)ws_bytes < w.total)
     return hbx_fail(HBX_ERR_ARG, "workspace too small: %lld < %lld bytes", (long long)ws_bytes,
                     (long long)w.total);
-  logpdf_fn fg = pick_logpdf(dc_pad, du_pad, signed_good != 0);
-  logpdf_fn fb = pick_logpdf(dc_pad, du_pad, signed_bad != 0);
-  if (!fg || !fb) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
+  ScoreFns fg = pick_logpdf(dc_pad, du_pad, variant_good);
+  ScoreFns fb = pick_logpdf(dc_pad, du_pad, variant_bad);
+  if (!fg.main || !fb.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
   char* ws = (char*)workspace;
   uint32_t* U = (uint32_t*)(ws + w.U);
   int32_t* count = (int32_t*)(ws + w.count);
@@ -802,14 +1262,13 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   HBX_LAUNCH_CHECK();
   if (Nc > 0) {
     const dim3 grid((unsigned)((Nc + 255) / 256));
-    const dim3 grid_s((unsigned)((Nc + 256 * LOGPDF_CPT - 1) / (256 * LOGPDF_CPT)));
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     if (ev) HBX_HIP(hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(fg, grid_s, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_good, table_good, el);
-    HBX_LAUNCH_CHECK();
+    int rc = launch_score(fg, cand, Nc, D, params_good, table_good, el, s);
+    if (rc) return rc;
     if (ev) HBX_HIP(hipEventRecord(ev[1], s));
-    hipLaunchKernelGGL(fb, grid_s, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params_bad, table_bad, eg);
-    HBX_LAUNCH_CHECK();
+    rc = launch_score(fb, cand, Nc, D, params_bad, table_bad, eg, s);
+    if (rc) return rc;
     if (ev) HBX_HIP(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, logl_out, logg_out, lo, hi, U,
                        flags);

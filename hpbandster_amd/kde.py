@@ -95,15 +95,17 @@ class DeviceKDE(object):
         N.check(L.hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
         self.stride = int(stride[0])
         self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
-        self.table = torch.empty(self.nobs * self.stride, dtype=torch.float32, device=self.device)
+        tf = int(L.hbx_kde_table_floats(self.nobs, int(dcp[0]), int(dup[0])))
+        self.table = torch.empty(tf, dtype=torch.float32, device=self.device)
         info = np.zeros(8, dtype=np.int32)
         bw_c = np.ascontiguousarray(self.bw)
         nlev_c = np.ascontiguousarray(self.nlev)
         N.check(L.hbx_kde_prepare(N.ptr(X_dev), D, N.ptr(rows_dev), self.nobs, N.ptr(vt), N.ptr(bw_c),
                                   N.ptr(nlev_c), N.ptr(self.params), N.ptr(self.table), self.table.numel(),
                                   N.ptr(info), N.stream_handle(stream)))
-        self.has_neg, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
+        self.variant, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
             [int(v) for v in info]
+        self.has_neg, self.kc = self.variant & 1, self.variant >> 1
         if unsupported:
             raise N.HbxError("KDE bandwidth/level combination not modelled (bw=%r, nlev=%r)" % (self.bw, self.nlev))
 
@@ -134,7 +136,7 @@ class DeviceKDE(object):
         Nc = int(cand_dev.shape[0])
         est = torch.empty((Nc, 4), dtype=torch.float32, device=self.device)
         N.check(L.hbx_kde_logpdf(N.ptr(cand_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
-                                 self.dc_pad, self.du_pad, self.has_neg, N.ptr(est), N.stream_handle(stream)))
+                                 self.dc_pad, self.du_pad, self.variant, N.ptr(est), N.stream_handle(stream)))
         e = est.cpu().numpy()
         return e[:, 0], e[:, 1], e[:, 2]
 
@@ -195,8 +197,8 @@ class KDEPair(object):
         logg = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         g, b = self.good, self.bad
         N.check(L.hbx_kde_acquire(N.ptr(c_dev), Nc, D, int(index_base),
-                                  N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.has_neg,
-                                  N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.has_neg,
+                                  N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.variant,
+                                  N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.variant,
                                   g.dc_pad, g.du_pad, self.nmax, N.ptr(logl), N.ptr(logg), N.ptr(ws), ws.numel(),
                                   events.address if events is not None else None, N.stream_handle(stream)))
         off = int(L.hbx_kde_result_ptr(N.ptr(ws))) - N.ptr(ws)

@@ -66,13 +66,18 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
                 void* stream);
 
 /* ---- KDE model preparation ----------------------------------------------------------------- */
-/* Template bucket of the scoring kernel for dc continuous / du categorical dims. */
+/* Template bucket of the scoring kernel for dc continuous / du categorical dims
+ * (stride = floats per 64-observation table chunk). */
 int hbx_kde_bucket(int32_t dc, int32_t du, int32_t* dc_pad, int32_t* du_pad, int32_t* stride);
+/* floats of the observation table of an n-row KDE in bucket (dc_pad, du_pad) */
+int64_t hbx_kde_table_floats(int32_t n, int32_t dc_pad, int32_t du_pad);
 
 /* Build one KDE for scoring.  X: device f64[*][D]; rows: device i64[n] (this KDE's rows, in
  * the reference's order); vartype/bw/nlev: host arrays of length D.  params: device buffer of
- * hbx_kde_param_bytes(); table: device f32[n * stride].  info: host i32[8] =
- * {has_neg, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}. */
+ * hbx_kde_param_bytes(); table: device f32[hbx_kde_table_floats(n, dc_pad, du_pad)].  info: host i32[8] =
+ * {variant, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}; variant = has_neg | kc << 1 selects
+ * the scoring kernel (kc = 0: categorical matching on the VALU; kc >= 1: categorical one-hot product
+ * on the f16 matrix cores with kc K-steps) and is passed back to hbx_kde_logpdf / hbx_kde_acquire. */
 int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, const int32_t* vartype,
                     const double* bw, const int32_t* nlev, void* params, float* table, int64_t table_floats,
                     int32_t* info, void* stream);
@@ -81,7 +86,7 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
 /* fp32 log-domain sums for Nc candidates (device f64[Nc][D]) against one prepared KDE;
  * est_out: device, Nc * hbx_kde_est_bytes() ({ln S+, ln S-, rel. bound, pad} per candidate). */
 int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
-                   int32_t dc_pad, int32_t du_pad, int32_t signed_sum, void* est_out, void* stream);
+                   int32_t dc_pad, int32_t du_pad, int32_t variant, void* est_out, void* stream);
 
 int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
 
@@ -93,9 +98,9 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
  * events: NULL or hipEvent_t[3] (see hbx_event_create). */
 int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
                     const void* params_good, const float* table_good, const double* X_good,
-                    const int64_t* rows_good, int32_t signed_good,
+                    const int64_t* rows_good, int32_t variant_good,
                     const void* params_bad, const float* table_bad, const double* X_bad,
-                    const int64_t* rows_bad, int32_t signed_bad, int32_t dc_pad, int32_t du_pad,
+                    const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
                     void* events, void* stream);
 
