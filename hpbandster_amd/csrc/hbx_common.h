@@ -56,6 +56,8 @@ struct KdeParams {
   float sum_abs_delta;// sum |delta_u| over finite deltas (error bound)
   int32_t kc;         // categorical mode: 0 = VALU match on codes, k >= 1 = one-hot on f16 MFMA,
                       // k steps of K=32 (2 * oh_total <= 32 k)
+  int32_t hmode;      // 1: continuous product on f16 matrix cores too (hi/lo split coordinates)
+  int32_t nsc;        // hmode: f16 K-steps (of 32) of the continuous product = ceil(4 dc_pad / 32)
   int32_t chunk_floats; // floats per 64-observation chunk of this KDE's table (layout depends on kc)
   int32_t oh_total;   // one-hot width: sum over active categorical dims of (max observed code + 1)
   const double* X;    // the KDE's data (device): X[rows[j]] is observation j (rescue / exact paths)

@@ -62,12 +62,24 @@ __host__ __device__ constexpr int cat_floats(int du_pad, int kc, int sgn) {
 __host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 0, int sgn = 0) {
   return kp_of(dc_pad) * KROW + cat_floats(du_pad, kc, sgn);
 }
+// hmode (all-f16) chunk: [64 f32: C_j] [64 obs x KTP halves: hi/lo continuous + one-hot] [signed:
+// 64 obs x KPP halves parity]; continuous slot k = 4c + pt of dim c holds (pt even ? Xh_c : Xl_c) so
+// the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl).
+// Rows are padded by 8 halves (16 B) so the 16 observation rows a wave reads are spread over banks.
+__host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) / 32; }
+__host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 8; }
+__host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 8; }
+__host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
+  return OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0);
+}
 static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }  // floats per chunk
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 // capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
-  const int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
-  return n_chunks(n) * (int64_t)(a > b ? a : b);
+  int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
+  const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1);
+  a = a > b ? a : b;
+  return n_chunks(n) * (int64_t)(a > c ? a : c);
 }
 
 // Per active categorical dim (one block each): max observed code, -1 if some code is not an
@@ -121,15 +133,34 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   const int KP = kp_of(dcp);
   float* ch = table + (int64_t)(j / OBS_CHUNK) * P->chunk_floats;
   const int jj = j % OBS_CHUNK;
+  const bool hm = P->hmode != 0;
+  const int KTP = h_ktp(dcp, P->kc);
+  _Float16* hrow = (_Float16*)(ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
-  for (int k = 0; k < KP - 2; ++k) {
+  for (int k = 0; k < (hm ? dcp : KP - 2); ++k) {
     float v = 0.f;
     if (ok && k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
     C -= (double)v * (double)v;
-    if (slot) ch[(2 + k) * KROW + jj] = v;
+    if (slot) {
+      if (hm) {
+        const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
+        const _Float16 h = (_Float16)vc;
+        const _Float16 l = (_Float16)(vc - (float)h);
+        hrow[4 * k + 0] = h;
+        hrow[4 * k + 1] = l;
+        hrow[4 * k + 2] = h;
+        hrow[4 * k + 3] = l;
+      } else {
+        ch[(2 + k) * KROW + jj] = v;
+      }
+    }
     float a = fabsf(v);
     for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
     if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&P->xmax[k], __float_as_uint(a));
+  }
+  if (hm && slot) {
+    for (int k = 4 * dcp; k < 32 * P->nsc; ++k) hrow[k] = (_Float16)0.f;
+    for (int k = KTP - 8; k < KTP; ++k) hrow[k] = (_Float16)0.f;
   }
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
@@ -137,9 +168,16 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
       if (slot) ch[KP * KROW + jj * dup + u] = v;
     }
   } else if (slot) {
-    const int W = P->kc * 32;  // halves per observation
-    _Float16* oh = (_Float16*)(ch + KP * KROW) + jj * W;
-    _Float16* par = (_Float16*)(ch + KP * KROW) + OBS_CHUNK * W + jj * W;
+    const int W = P->kc * 32;  // one-hot halves per observation
+    _Float16* oh;
+    _Float16* par;
+    if (hm) {
+      oh = hrow + 32 * P->nsc;
+      par = (_Float16*)(ch + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jj * h_kpp(P->kc);
+    } else {
+      oh = (_Float16*)(ch + KP * KROW) + jj * W;
+      par = (_Float16*)(ch + KP * KROW) + OBS_CHUNK * W + jj * W;
+    }
     for (int k = 0; k < W; ++k) {
       const int t = k >> 1, p = k & 1;
       float v = 0.f, pv = 0.f;
@@ -155,14 +193,20 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
       oh[k] = (_Float16)v;
       if (P->has_neg) par[k] = (_Float16)pv;
     }
+    if (hm && P->has_neg)
+      for (int k = W; k < h_kpp(P->kc); ++k) par[k] = (_Float16)0.f;
   }
   C += P->lb_sum - P->m0_log2;
   const float Cf = ok ? (float)C : -1e30f;
   if (slot) {
-    ch[0 * KROW + jj] = Cf;
-    ch[1 * KROW + jj] = 1.f;
-    if (jj < KROW - OBS_CHUNK)  // zero the pad columns of every k-row once per chunk
-      for (int k = 0; k < KP; ++k) ch[k * KROW + OBS_CHUNK + jj] = 0.f;
+    if (hm) {
+      ch[jj] = Cf;
+    } else {
+      ch[0 * KROW + jj] = Cf;
+      ch[1 * KROW + jj] = 1.f;
+      if (jj < KROW - OBS_CHUNK)  // zero the pad columns of every k-row once per chunk
+        for (int k = 0; k < KP; ++k) ch[k * KROW + OBS_CHUNK + jj] = 0.f;
+    }
   }
   float a = ok ? fabsf(Cf) : 0.f;
   for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
@@ -608,6 +652,191 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_oh_kernel(const do
   }
 }
 
+// hmode: the whole exponent is one f16 matrix product.  Continuous coordinates are split into f16
+// hi + lo parts and all four cross products are summed (every f16 x f16 product is exact in fp32, so
+// the only extra error is the 2^-22 representation error of each coordinate -- accounted in the
+// bound); the one-hot categorical product follows in the same K loop.  C_j + c_i seed the
+// accumulator.  VALU work per pair: one add, exp2, one add.
+template <int NSC, int KC, bool SIGNED>
+__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const double* __restrict__ cand,
+                                                                      int64_t Nc, int32_t D,
+                                                                      const KdeParams* __restrict__ P,
+                                                                      const float* __restrict__ table,
+                                                                      KdeEst* __restrict__ out) {
+  constexpr int NSH = NSC + KC;           // f16 K-steps of 32
+  constexpr int KTP = 32 * NSH + 8;       // halves per observation row (padded)
+  constexpr int KPP = 32 * KC + 8;
+  constexpr int CHF = OBS_CHUNK + OBS_CHUNK * KTP / 2 + (SIGNED ? OBS_CHUNK * KPP / 2 : 0);
+  __shared__ __align__(16) float lds[2 * CHF];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;
+  const int n = P->n, dc = P->dc;
+  const int ia = lane & 15, kq = lane >> 4;
+
+  f16x8 ah[NSH];
+  float ci_a = 0.f, bnd_a = 0.f;
+  {
+    int64_t ii = cbase + ia;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+    for (int k = 0; k < dc; ++k) {
+      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+      ci_a = fmaf(-v, v, ci_a);
+      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
+    }
+#pragma unroll
+    for (int s = 0; s < NSC; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * kq + j;
+        const int c = k >> 2, pt = k & 3;
+        float v = 0.f;
+        if (c < dc) {
+          const float xx = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
+          const float xc = fminf(fmaxf(xx, -60000.f), 60000.f);
+          const float hi = (float)(_Float16)xc;
+          v = (pt < 2) ? hi : (xc - hi);
+        }
+        ah[s][j] = (_Float16)v;
+      }
+    }
+    const int tot = P->oh_total;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = (32 * s + 8 * kq + j) >> 1;
+        float v = 0.f;
+        if (t < tot && x[P->cat_dim[P->oh_dim[t]]] == (double)P->oh_level[t]) v = 1.f;
+        ah[NSC + s][j] = (_Float16)v;
+      }
+    }
+  }
+  bool nanc[4];
+  float ciq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int64_t ii = cbase + 4 * kq + q;
+    if (ii >= Nc) ii = Nc - 1;
+    const double* x = cand + ii * (int64_t)D;
+    bool nn = P->nan_all != 0;
+    for (int c = 0; c < P->nconst; ++c)
+      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
+    nanc[q] = nn;
+    ciq[q] = __shfl(ci_a, 4 * kq + q);
+  }
+
+  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
+  constexpr int NT = 64 * MFMA_WAVES;
+  constexpr int NV4 = CHF / 4;
+  constexpr int PER = (NV4 + NT - 1) / NT;
+  float4 pre[PER];
+  {
+    const float4* __restrict__ src = (const float4*)table;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int v = threadIdx.x + q * NT;
+      if (v < NV4) ((float4*)lds)[v] = src[v];
+    }
+  }
+  __syncthreads();
+
+  auto tile = [&](const float* buf, int jt, f32x4& acc, f32x4& accp) {
+    const int jo = jt * 16 + ia;
+    const float Cj = buf[jo];
+    const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
+    acc = f32x4{ciq[0] + Cj, ciq[1] + Cj, ciq[2] + Cj, ciq[3] + Cj};
+#pragma unroll
+    for (int s = 0; s < NSH; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], *(const f16x8*)(hb + 32 * s), acc, 0, 0, 0);
+    if (SIGNED) {
+      const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
+      accp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KC; ++s)
+        accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[NSC + s], *(const f16x8*)(pb + 32 * s), accp, 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](const f32x4& acc, const f32x4& accp, float* Sb, float* Snb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e = __builtin_amdgcn_exp2f(acc[q]);
+      Sb[q] += e;
+      if (SIGNED) Snb[q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * accp[q]), e, Snb[q]);
+    }
+  };
+
+  for (int c = 0; c < nchunks; ++c) {
+    float* buf = lds + (c & 1) * CHF;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) pre[q] = src[v];
+      }
+    }
+    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0, acc1, ap0, ap1;
+    tile(buf, 0, acc0, ap0);
+    tile(buf, 1, acc1, ap1);
+#pragma unroll
+    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
+      const f32x4 n0 = acc0, n1 = acc1, m0 = ap0, m1 = ap1;
+      if (p + 1 < OBS_CHUNK / 32) {
+        tile(buf, 2 * p + 2, acc0, ap0);
+        tile(buf, 2 * p + 3, acc1, ap1);
+      }
+      epilogue(n0, m0, Sb, Snb);
+      epilogue(n1, m1, Sb, Snb);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      S[q] += Sb[q];
+      if (SIGNED) Sn[q] += Snb[q];
+    }
+    if (more) {
+      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = threadIdx.x + q * NT;
+        if (v < NV4) dst[v] = pre[q];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      S[q] += __shfl_xor(S[q], o);
+      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
+    }
+  }
+  const int src_lane = (4 * kq + (ia & 3)) & 15;
+  const float ci_q = __shfl(ci_a, src_lane);
+  const float bnd_q = __shfl(bnd_a, src_lane);
+  if (ia < 4) {
+    const int q = ia;
+    const int64_t ii = cbase + 4 * kq + q;
+    float Sq = S[0], Snq = Sn[0];
+    bool nq = nanc[0];
+    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
+    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
+    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
+    if (ii < Nc) {
+      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+      // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
+      if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
+      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
+      out[ii] = o;
+    }
+  }
+}
+
 // Rescue (rare): candidates whose every term sits far below the static bound M0 are recomputed
 // with a true maximum (two passes over the observations), one candidate per thread on the VALU.
 // Continuous coordinates come from the table's f32 part, categorical codes straight from the data.
@@ -622,7 +851,7 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
   if (!__any(need)) return;
   if (!need) return;
   const double* x = cand + i * (int64_t)D;
-  const int n = P->n, dc = P->dc, du = P->du, CHF = P->chunk_floats;
+  const int n = P->n, dc = P->dc, du = P->du;
   const double* __restrict__ Xo = P->X;
   const int64_t* __restrict__ rows = P->rows;
   float xs[NC], ci = 0.f, bnd = 0.f;
@@ -635,14 +864,23 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
     if (k < dc) bnd = fmaf(fabsf(xs[k]), P->xmax[k], bnd);
   }
   auto pair_t = [&](int j, float& par) -> float {
-    const float* ch = table + (int64_t)(j / OBS_CHUNK) * CHF;
-    const int jj = j % OBS_CHUNK;
-    float t = fmaf(1.f, ch[jj], 0.f);
+    // observation row rebuilt exactly as kde_table_kernel writes it (f32 X', f64 C_j rounded once)
+    const double* xo = Xo + rows[j] * (int64_t)D;
+    float Xp[NC];
+    double Cd = 0.0;
+#pragma unroll
+    for (int k = 0; k < DCP; ++k) {
+      float v = 0.f;
+      if (k < dc) v = (float)(P->cont_scale[k] * (xo[P->cont_dim[k]] - P->center[k]));
+      Cd -= (double)v * (double)v;
+      Xp[k] = v;
+    }
+    const float Cj = (float)(Cd + P->lb_sum - P->m0_log2);
+    float t = fmaf(1.f, Cj, 0.f);
     t = fmaf(ci, 1.f, t);
 #pragma unroll
-    for (int k = 0; k < DCP; ++k) t = fmaf(xs[k], ch[(2 + k) * KROW + jj], t);
+    for (int k = 0; k < DCP; ++k) t = fmaf(xs[k], Xp[k], t);
     par = 0.f;
-    const double* xo = Xo + rows[j] * (int64_t)D;
     for (int u = 0; u < du; ++u) {
       const int d = P->cat_dim[u];
       const float m = (x[d] == xo[d]) ? 1.f : 0.f;
@@ -961,10 +1199,27 @@ struct ScoreFns {
   logpdf_fn main, rescue;
 };
 
-// variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1.. = kc
+// variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
+// bit 4 = hmode (whole exponent on the f16 matrix cores)
+template <int NSC, bool SG>
+static logpdf_fn pick_h(int kc) {
+  switch (kc) {
+    case 0: return kde_logpdf_h_kernel<NSC, 0, SG>;
+    case 1: return kde_logpdf_h_kernel<NSC, 1, SG>;
+    case 2: return kde_logpdf_h_kernel<NSC, 2, SG>;
+    case 3: return kde_logpdf_h_kernel<NSC, 3, SG>;
+    case 4: return kde_logpdf_h_kernel<NSC, 4, SG>;
+  }
+  return nullptr;
+}
+
 template <int DCP, int DUP, bool SG>
-static ScoreFns pick_kc(int kc) {
+static ScoreFns pick_kc(int kc, bool hm) {
   const logpdf_fn r = kde_rescue_kernel<DCP, SG>;
+  if (hm) {
+    if constexpr (DCP >= 16) return {pick_h<nsc_of(DCP), SG>(kc), r};
+    return {nullptr, nullptr};
+  }
   switch (kc) {
     case 0: return {kde_logpdf_kernel<DCP, DUP, SG>, r};
     case 1: return {kde_logpdf_oh_kernel<DCP, 1, SG>, r};
@@ -977,14 +1232,15 @@ static ScoreFns pick_kc(int kc) {
 
 template <int DCP, int DUP>
 static ScoreFns pick_signed(int variant) {
-  const int kc = variant >> 1;
-  return (variant & 1) ? pick_kc<DCP, DUP, true>(kc) : pick_kc<DCP, DUP, false>(kc);
+  const int kc = (variant >> 1) & 7;
+  const bool hm = (variant >> 4) & 1;
+  return (variant & 1) ? pick_kc<DCP, DUP, true>(kc, hm) : pick_kc<DCP, DUP, false>(kc, hm);
 }
 
 template <int DCP>
 static ScoreFns pick_du(int du_pad, int variant) {
   switch (du_pad) {
-    case 0: return pick_signed<DCP, 0>(variant & 1);  // no categorical dims: kc irrelevant
+    case 0: return pick_signed<DCP, 0>(variant & 0x11);  // no categorical dims: kc irrelevant
     case 4: return pick_signed<DCP, 4>(variant);
     case 8: return pick_signed<DCP, 8>(variant);
     case 16: return pick_signed<DCP, 16>(variant);
@@ -1189,8 +1445,17 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
         }
     }
   }
-  P->chunk_floats = chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
-  info[0] = P->has_neg | (P->kc << 1);  // scoring variant (hbx_kde_logpdf / hbx_kde_acquire)
+  // continuous product on the f16 matrix cores (hi/lo split) when it has >= 16 dims and the
+  // categorical part is one-hot (or absent); otherwise the exact f32 MFMA product
+  const char* hm_env = getenv("HBX_HMODE");
+  const bool hm_ok = (P->du == 0 || P->kc > 0) && dcp >= 16;
+  P->hmode = (hm_ok && !(hm_env && hm_env[0] == '0')) ? 1 : 0;
+  P->nsc = nsc_of(dcp);
+  if (P->hmode)
+    P->chunk_floats = h_chunk_floats(dcp, P->kc, P->has_neg);
+  else
+    P->chunk_floats = chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
+  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4);  // scoring variant (hbx_kde_logpdf / _acquire)
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
