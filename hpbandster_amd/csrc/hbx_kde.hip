@@ -29,6 +29,7 @@
 #define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
 #define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
 #define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
+#define H_ROW_TILES 2  // hmode: 16-candidate row tiles per wave (32 candidates)
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -65,10 +66,12 @@ __host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 
 // hmode (all-f16) chunk: [64 f32: C_j] [64 obs x KTP halves: hi/lo continuous + one-hot] [signed:
 // 64 obs x KPP halves parity]; continuous slot k = 4c + pt of dim c holds (pt even ? Xh_c : Xl_c) so
 // the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl).
-// Rows are padded by 8 halves (16 B) so the 16 observation rows a wave reads are spread over banks.
+// Rows are padded by 16 halves (32 B) so the 16 observation rows a wave reads are spread over banks.
 __host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) / 32; }
-__host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 8; }
-__host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 8; }
+// row strides are 8*odd dwords: the 16 rows a ds_read_b128 lane group touches then cover all 64
+// banks exactly once (conflict-free)
+__host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 16; }
+__host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 16; }
 __host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
   return OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0);
 }
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   }
   if (hm && slot) {
     for (int k = 4 * dcp; k < 32 * P->nsc; ++k) hrow[k] = (_Float16)0.f;
-    for (int k = KTP - 8; k < KTP; ++k) hrow[k] = (_Float16)0.f;
+    for (int k = 32 * (P->nsc + P->kc); k < KTP; ++k) hrow[k] = (_Float16)0.f;
   }
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
@@ -663,28 +666,33 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
                                                                       const KdeParams* __restrict__ P,
                                                                       const float* __restrict__ table,
                                                                       KdeEst* __restrict__ out) {
-  constexpr int NSH = NSC + KC;           // f16 K-steps of 32
-  constexpr int KTP = 32 * NSH + 8;       // halves per observation row (padded)
-  constexpr int KPP = 32 * KC + 8;
+  constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
+  constexpr int NSH = NSC + KC;             // f16 K-steps of 32
+  constexpr int KTP = h_ktp(NSC * 8, KC);   // halves per observation row (padded); nsc_of(8 NSC) = NSC
+  constexpr int KPP = h_kpp(KC);
   constexpr int CHF = OBS_CHUNK + OBS_CHUNK * KTP / 2 + (SIGNED ? OBS_CHUNK * KPP / 2 : 0);
   __shared__ __align__(16) float lds[2 * CHF];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;
+  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16 * RT;
   const int n = P->n, dc = P->dc;
   const int ia = lane & 15, kq = lane >> 4;
 
-  f16x8 ah[NSH];
-  float ci_a = 0.f, bnd_a = 0.f;
-  {
-    int64_t ii = cbase + ia;
+  f16x8 ah[RT][NSH];
+  float ci_a[RT], bnd_a[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    int64_t ii = cbase + 16 * r + ia;
     if (ii >= Nc) ii = Nc - 1;
     const double* x = cand + ii * (int64_t)D;
+    float ci = 0.f, bnd = 0.f;
     for (int k = 0; k < dc; ++k) {
       const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-      ci_a = fmaf(-v, v, ci_a);
-      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
+      ci = fmaf(-v, v, ci);
+      bnd = fmaf(2.f * fabsf(v), P->xmax[k], bnd);
     }
+    ci_a[r] = ci;
+    bnd_a[r] = bnd;
 #pragma unroll
     for (int s = 0; s < NSC; ++s) {
 #pragma unroll
@@ -698,7 +706,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
           const float hi = (float)(_Float16)xc;
           v = (pt < 2) ? hi : (xc - hi);
         }
-        ah[s][j] = (_Float16)v;
+        ah[r][s][j] = (_Float16)v;
       }
     }
     const int tot = P->oh_total;
@@ -709,25 +717,22 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         const int t = (32 * s + 8 * kq + j) >> 1;
         float v = 0.f;
         if (t < tot && x[P->cat_dim[P->oh_dim[t]]] == (double)P->oh_level[t]) v = 1.f;
-        ah[NSC + s][j] = (_Float16)v;
+        ah[r][NSC + s][j] = (_Float16)v;
       }
     }
   }
-  bool nanc[4];
-  float ciq[4];
+  // accumulator rows of this lane: candidates cbase + 16 r + 4 kq + q
+  float ciq[RT][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    int64_t ii = cbase + 4 * kq + q;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-    bool nn = P->nan_all != 0;
-    for (int c = 0; c < P->nconst; ++c)
-      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
-    nanc[q] = nn;
-    ciq[q] = __shfl(ci_a, 4 * kq + q);
-  }
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ciq[r][q] = __shfl(ci_a[r], 4 * kq + q);
 
-  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
+  float S[RT][4], Sn[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[r][q] = Sn[r][q] = 0.f;
   const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
   constexpr int NT = 64 * MFMA_WAVES;
   constexpr int NV4 = CHF / 4;
@@ -743,35 +748,38 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   }
   __syncthreads();
 
-  auto tile = [&](const float* buf, int jt, f32x4& acc, f32x4& accp) {
+  // MFMAs of one 16-observation column tile for every row tile
+  auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
     const int jo = jt * 16 + ia;
     const float Cj = buf[jo];
     const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
-    acc = f32x4{ciq[0] + Cj, ciq[1] + Cj, ciq[2] + Cj, ciq[3] + Cj};
+    f16x8 b[NSH];
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r] = f32x4{ciq[r][0] + Cj, ciq[r][1] + Cj, ciq[r][2] + Cj, ciq[r][3] + Cj};
 #pragma unroll
     for (int s = 0; s < NSH; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], *(const f16x8*)(hb + 32 * s), acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
     if (SIGNED) {
       const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
-      accp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KC; ++s)
-        accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[NSC + s], *(const f16x8*)(pb + 32 * s), accp, 0, 0, 0);
-    }
-  };
-  auto epilogue = [&](const f32x4& acc, const f32x4& accp, float* Sb, float* Snb) {
+      for (int r = 0; r < RT; ++r) accp[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float e = __builtin_amdgcn_exp2f(acc[q]);
-      Sb[q] += e;
-      if (SIGNED) Snb[q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * accp[q]), e, Snb[q]);
+      for (int s = 0; s < KC; ++s) {
+        const f16x8 bp = *(const f16x8*)(pb + 32 * s);
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp, accp[r], 0, 0, 0);
+      }
     }
   };
 
   for (int c = 0; c < nchunks; ++c) {
     float* buf = lds + (c & 1) * CHF;
     const bool more = c + 1 < nchunks;
-    if (more) {
+    if (more) {  // next chunk -> registers, lands during this chunk's math
       const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
@@ -779,25 +787,39 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         if (v < NV4) pre[q] = src[v];
       }
     }
-    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
-    f32x4 acc0, acc1, ap0, ap1;
-    tile(buf, 0, acc0, ap0);
-    tile(buf, 1, acc1, ap1);
+    float Sb[RT][4], Snb[RT][4];
 #pragma unroll
-    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
-      const f32x4 n0 = acc0, n1 = acc1, m0 = ap0, m1 = ap1;
-      if (p + 1 < OBS_CHUNK / 32) {
-        tile(buf, 2 * p + 2, acc0, ap0);
-        tile(buf, 2 * p + 3, acc1, ap1);
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
+    // software pipeline: MFMAs of tile jt+1 are issued before the exp2/sum epilogue of tile jt
+    f32x4 acc[RT], accp[RT];
+    tile(buf, 0, acc, accp);
+#pragma unroll
+    for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
+      f32x4 cur[RT], curp[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        cur[r] = acc[r];
+        curp[r] = accp[r];
       }
-      epilogue(n0, m0, Sb, Snb);
-      epilogue(n1, m1, Sb, Snb);
+      if (jt + 1 < OBS_CHUNK / 16) tile(buf, jt + 1, acc, accp);
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
+          Sb[r][q] += e;
+          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, Snb[r][q]);
+        }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      S[q] += Sb[q];
-      if (SIGNED) Sn[q] += Snb[q];
-    }
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        S[r][q] += Sb[r][q];
+        if (SIGNED) Sn[r][q] += Snb[r][q];
+      }
     if (more) {
       float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
 #pragma unroll
@@ -809,30 +831,37 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
     __syncthreads();
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int r = 0; r < RT; ++r)
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      S[q] += __shfl_xor(S[q], o);
-      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
-    }
-  }
-  const int src_lane = (4 * kq + (ia & 3)) & 15;
-  const float ci_q = __shfl(ci_a, src_lane);
-  const float bnd_q = __shfl(bnd_a, src_lane);
-  if (ia < 4) {
-    const int q = ia;
-    const int64_t ii = cbase + 4 * kq + q;
-    float Sq = S[0], Snq = Sn[0];
-    bool nq = nanc[0];
-    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
-    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
-    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
-    if (ii < Nc) {
-      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
-      // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
-      if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
-      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
-      out[ii] = o;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        S[r][q] += __shfl_xor(S[r][q], o);
+        if (SIGNED) Sn[r][q] += __shfl_xor(Sn[r][q], o);
+      }
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int src_lane = (4 * kq + (ia & 3)) & 15;
+    const float ci_q = __shfl(ci_a[r], src_lane);
+    const float bnd_q = __shfl(bnd_a[r], src_lane);
+    if (ia < 4) {
+      const int q = ia;
+      const int64_t ii = cbase + 16 * r + 4 * kq + q;
+      float Sq = S[r][0], Snq = Sn[r][0];
+      if (q == 1) { Sq = S[r][1]; Snq = Sn[r][1]; }
+      if (q == 2) { Sq = S[r][2]; Snq = Sn[r][2]; }
+      if (q == 3) { Sq = S[r][3]; Snq = Sn[r][3]; }
+      if (ii < Nc) {
+        const double* x = cand + ii * (int64_t)D;
+        bool nq = P->nan_all != 0;
+        for (int cc = 0; cc < P->nconst; ++cc)
+          if (x[P->const_dim[cc]] != P->const_level[cc]) nq = true;
+        KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+        // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
+        if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
+        if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
+        out[ii] = o;
+      }
     }
   }
 }
@@ -1197,6 +1226,7 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 struct ScoreFns {
   logpdf_fn main, rescue;
+  int cands_per_block;
 };
 
 // variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
@@ -1217,17 +1247,17 @@ template <int DCP, int DUP, bool SG>
 static ScoreFns pick_kc(int kc, bool hm) {
   const logpdf_fn r = kde_rescue_kernel<DCP, SG>;
   if (hm) {
-    if constexpr (DCP >= 16) return {pick_h<nsc_of(DCP), SG>(kc), r};
-    return {nullptr, nullptr};
+    if constexpr (DCP >= 16) return {pick_h<nsc_of(DCP), SG>(kc), r, 16 * MFMA_WAVES * H_ROW_TILES};
+    return {nullptr, nullptr, 0};
   }
   switch (kc) {
-    case 0: return {kde_logpdf_kernel<DCP, DUP, SG>, r};
-    case 1: return {kde_logpdf_oh_kernel<DCP, 1, SG>, r};
-    case 2: return {kde_logpdf_oh_kernel<DCP, 2, SG>, r};
-    case 3: return {kde_logpdf_oh_kernel<DCP, 3, SG>, r};
-    case 4: return {kde_logpdf_oh_kernel<DCP, 4, SG>, r};
+    case 0: return {kde_logpdf_kernel<DCP, DUP, SG>, r, 16 * MFMA_WAVES};
+    case 1: return {kde_logpdf_oh_kernel<DCP, 1, SG>, r, 16 * MFMA_WAVES};
+    case 2: return {kde_logpdf_oh_kernel<DCP, 2, SG>, r, 16 * MFMA_WAVES};
+    case 3: return {kde_logpdf_oh_kernel<DCP, 3, SG>, r, 16 * MFMA_WAVES};
+    case 4: return {kde_logpdf_oh_kernel<DCP, 4, SG>, r, 16 * MFMA_WAVES};
   }
-  return {nullptr, nullptr};
+  return {nullptr, nullptr, 0};
 }
 
 template <int DCP, int DUP>
@@ -1259,13 +1289,13 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
     case 32: return pick_du<32>(du_pad, variant);
     case 64: return pick_du<64>(du_pad, variant);
   }
-  return {nullptr, nullptr};
+  return {nullptr, nullptr, 0};
 }
 
 // launch main + rescue scoring for one KDE
 static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
                         KdeEst* est, hipStream_t s) {
-  const unsigned gm = (unsigned)((Nc + 16 * MFMA_WAVES - 1) / (16 * MFMA_WAVES));
+  const unsigned gm = (unsigned)((Nc + f.cands_per_block - 1) / f.cands_per_block);
   hipLaunchKernelGGL(f.main, dim3(gm), dim3(64 * MFMA_WAVES), 0, s, cand, Nc, D, (const KdeParams*)params, table,
                      est);
   HBX_LAUNCH_CHECK();
