@@ -1,0 +1,122 @@
+"""SuccessiveHalving / SuccessiveResampling -- drop-ins for hpbandster/HB_iteration.py.
+
+Same state machine (QUEUED -> RUNNING -> REVIEW | CRASHED -> QUEUED/TERMINATED) and API
+(``get_next_run``, ``register_result``, ``process_results``, ``add_configuration``); the ranking step
+of ``process_results`` (``argsort(argsort(losses)) < k``, HB_iteration.py:179-182 and 239-242) runs
+as the GPU segmented top-k of libhbx.so (``promote.advance_mask``).
+"""
+
+import numpy as np
+
+from . import promote
+
+
+class SuccessiveHalving(object):
+    """One Hyperband bracket (reference HB_iteration.py:7-198)."""
+
+    def __init__(self, iter_number, num_configs, budgets, config_sampler, device=None):
+        self.data = {}
+        self.is_finished = False
+        self.HB_iter = iter_number
+        self.SH_iter = 0
+        self.budgets = budgets
+        self.num_configs = num_configs
+        self.actual_num_configs = [0] * len(num_configs)
+        self.config_sampler = config_sampler
+        self.num_running = 0
+        self.device = device
+
+    def add_configuration(self, config=None, config_info={}):
+        if config is None:
+            config, config_info = self.config_sampler(self.budgets[self.SH_iter])
+        if self.is_finished:
+            raise RuntimeError("This HB iteration is finished, you can't  add more results!")
+        if self.actual_num_configs[self.SH_iter] == self.num_configs[self.SH_iter]:
+            raise RuntimeError("Can't add another configuration to SH_iteration %i in HB_iteration %i."
+                               % (self.SH_iter, self.HB_iter))
+        config_id = (self.HB_iter, self.SH_iter, self.actual_num_configs[self.SH_iter])
+        self.data[config_id] = {
+            'config': config, 'config_info': config_info, 'results': {}, 'time_stamps': {},
+            'exceptions': {}, 'status': 'QUEUED', 'budget': self.budgets[self.SH_iter],
+        }
+        self.actual_num_configs[self.SH_iter] += 1
+        return config_id
+
+    def register_result(self, job):
+        if self.is_finished:
+            raise RuntimeError("This HB iteration is finished, you can't register more results!")
+        config_id = job.id
+        config = job.kwargs['config']
+        budget = job.kwargs['budget']
+        d = self.data[config_id]
+        assert d['config'] == config, 'Configurations differ!'
+        assert d['status'] == 'RUNNING', "Configuration wasn't scheduled for a run."
+        assert d['budget'] == budget, 'Budgets differ (%f != %f)!' % (d['budget'], budget)
+        d['time_stamps'][budget] = job.timestamps
+        d['results'][budget] = job.result
+        if (job.result is not None) and np.isfinite(job.result['loss']):
+            d['status'] = 'REVIEW'
+        else:
+            d['status'] = 'CRASHED'
+            d['exceptions'][budget] = {job.exception}
+        self.num_running -= 1
+
+    def get_next_run(self):
+        if self.is_finished:
+            return None
+        for k, v in self.data.items():
+            if v['status'] == 'QUEUED':
+                assert v['budget'] == self.budgets[self.SH_iter], \
+                    'Configuration budget does not align with current SH iteration!'
+                v['status'] = 'RUNNING'
+                self.num_running += 1
+                return (k, v['config'], v['budget'])
+        if self.actual_num_configs[self.SH_iter] < self.num_configs[self.SH_iter]:
+            self.add_configuration()
+            return self.get_next_run()
+        if self.num_running == 0:
+            self.process_results()
+            return self.get_next_run()
+        return None
+
+    def _advance_threshold(self):
+        """k of the top-k: configurations ranked below it advance."""
+        return self.num_configs[self.SH_iter]
+
+    def process_results(self):
+        self.SH_iter += 1
+        config_ids = [cid for cid in self.data.keys() if self.data[cid]['status'] == 'REVIEW']
+        if self.SH_iter >= len(self.num_configs):
+            self.cleanup()
+            return
+        if len(config_ids) > 0:
+            budgets = [self.data[cid]['budget'] for cid in config_ids]
+            if len(set(budgets)) > 1:
+                raise RuntimeError('Not all configurations have the same budget!')
+            budget = budgets[0]
+            losses = np.array([self.data[cid]['results'][budget]['loss'] for cid in config_ids], dtype=np.float64)
+            advance = promote.advance_mask(losses, self._advance_threshold(), device=self.device)
+            for i, cid in enumerate(config_ids):
+                if advance[i]:
+                    self.data[cid]['status'] = 'QUEUED'
+                    self.data[cid]['budget'] = self.budgets[self.SH_iter]
+                    self.actual_num_configs[self.SH_iter] += 1
+                else:
+                    self.data[cid]['status'] = 'TERMINATED'
+
+    def cleanup(self):
+        self.is_finished = True
+        for k, v in self.data.items():
+            assert v['status'] in ['TERMINATED', 'REVIEW', 'CRASHED'], 'Configuration has not finshed yet!'
+            del v['status']
+            del v['budget']
+
+
+class SuccessiveResampling(SuccessiveHalving):
+    """Advance the best half of the next stage's size, refill the rest with new samples
+    (reference HB_iteration.py:203-250)."""
+    resampling_rate = 0.5
+    min_samples_advance = 1
+
+    def _advance_threshold(self):
+        return max(self.min_samples_advance, self.num_configs[self.SH_iter] * (1 - self.resampling_rate))

@@ -1,0 +1,139 @@
+"""BOHB -- drop-in for hpbandster/config_generators/bohb.py with the KDE work on the MI355X.
+
+Same constructor kwargs, same ``get_config`` / ``new_result`` behaviour and the same consumption of
+the global numpy RNG (``np.random.rand`` / ``randint`` and ``scipy.stats.truncnorm.rvs``, in the
+reference's order), so a seeded run proposes the same configurations.  What moved to the GPU:
+
+* ``new_result``: the per-budget refit (argsort of the losses, good/bad split, normal-reference
+  bandwidths, observed level counts -- bohb.py:220-246) runs in libhbx.so (``kde.fit_pair``);
+* ``get_config``: the ``num_samples`` candidates are scored against l (good) and g (bad) and the
+  first index of min max(1e-8, g)/max(l, 1e-8) is selected exactly (bohb.py:124-161) by
+  ``KDEPair.acquire`` -- fp32 matrix-core scoring of every candidate, fp64 re-score of the ones that
+  can still be the minimum.
+
+``kde_models[budget]`` holds a ``KDEPair`` whose ``['good']`` / ``['bad']`` expose ``.data``,
+``.bw`` and ``.pdf`` like the statsmodels objects of the reference.
+"""
+
+import traceback
+
+import numpy as np
+import scipy.stats as sps
+
+from .. import _native
+from ..kde import fit_pair
+from .base import base_config_generator
+from ._cs import ConfigSpace
+
+
+class BOHB(base_config_generator):
+    def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
+                 random_fraction=1 / 3, bandwidth_factor=3, device=None, **kwargs):
+        super().__init__(**kwargs)
+        self.top_n_percent = top_n_percent
+        self.configspace = configspace
+        self.bw_factor = bandwidth_factor
+        self.min_points_in_model = min_points_in_model
+        if min_points_in_model is None:
+            self.min_points_in_model = len(self.configspace.get_hyperparameters()) + 1
+        self.num_samples = num_samples
+        self.random_fraction = random_fraction
+        self.device = device
+
+        hps = self.configspace.get_hyperparameters()
+        self.kde_vartypes = ""
+        self.vartypes = []
+        for h in hps:  # bohb.py:69-75
+            if hasattr(h, 'choices'):
+                self.kde_vartypes += 'u'
+                self.vartypes += [len(h.choices)]
+            else:
+                self.kde_vartypes += 'c'
+                self.vartypes += [0]
+        self.vartypes = np.array(self.vartypes, dtype=int)
+
+        self.cat_probs = []
+        self.configs = dict()
+        self.losses = dict()
+        self.good_config_rankings = dict()
+        self.kde_models = dict()
+
+    # -- candidates ---------------------------------------------------------------------------
+    def sample_candidates(self, kde_good, num_samples):
+        """bohb.py:133-147: around a random good observation, truncnorm per continuous dim (bounds
+        from bw, scale bandwidth_factor * bw), keep-or-resample per categorical dim.  Global RNG."""
+        D = len(self.vartypes)
+        cands = np.empty((num_samples, D), dtype=np.float64)
+        data = kde_good.data
+        bws = kde_good.bw
+        for i in range(num_samples):
+            idx = np.random.randint(0, len(data))
+            for d, (m, bw, t) in enumerate(zip(data[idx], bws, self.vartypes)):
+                if t == 0:
+                    cands[i, d] = sps.truncnorm.rvs(-m / bw, (1 - m) / bw, loc=m, scale=self.bw_factor * bw)
+                else:
+                    if np.random.rand() < (1 - bw):
+                        cands[i, d] = m
+                    else:
+                        cands[i, d] = np.random.randint(t)
+        return cands
+
+    def get_config(self, budget):
+        sample = None
+        info_dict = {}
+        if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
+            sample = self.configspace.sample_configuration().get_dictionary()
+            info_dict['model_based_pick'] = False
+
+        if sample is None:
+            try:
+                budget = max(self.kde_models.keys())  # always the largest-budget model (bohb.py:124)
+                pair = self.kde_models[budget]        # immutable snapshot (new_result swaps entries)
+                cands = self.sample_candidates(pair['good'], self.num_samples)
+                res = pair.acquire(cands)
+                if res.index < 0:
+                    self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
+                                      % self.num_samples)
+                    sample = self.configspace.sample_configuration().get_dictionary()
+                    info_dict['model_based_pick'] = False
+                else:
+                    best_vector = cands[res.index]
+                    self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
+                    sample = ConfigSpace.Configuration(self.configspace, vector=best_vector).get_dictionary()
+                    info_dict['model_based_pick'] = True
+            except _native.HbxError:
+                raise  # the engine failed: never hide it behind a random configuration
+            except Exception:
+                self.logger.warning("Sampling based optimization with %i samples failed\n %s \nUsing random configuration"
+                                    % (self.num_samples, traceback.format_exc()))
+                sample = self.configspace.sample_configuration().get_dictionary()
+                info_dict['model_based_pick'] = False
+        return sample, info_dict
+
+    # -- observations ---------------------------------------------------------------------------
+    def new_result(self, job):
+        super().new_result(job)
+        if job.result is None:
+            loss = np.inf  # crashed runs count as bad configurations (bohb.py:189-192)
+        else:
+            loss = job.result["loss"]
+        budget = job.kwargs["budget"]
+        if budget not in self.configs.keys():
+            self.configs[budget] = []
+            self.losses[budget] = []
+        if max(list(self.kde_models.keys()) + [-np.inf]) > budget:  # bohb.py:204-205
+            return
+        conf = ConfigSpace.Configuration(self.configspace, job.kwargs["config"])
+        self.configs[budget].append(conf.get_array())
+        self.losses[budget].append(loss)
+        if len(self.configs[budget]) <= self.min_points_in_model + 1:
+            return
+        train_configs = np.array(self.configs[budget])
+        train_losses = np.array(self.losses[budget])
+        pair = fit_pair(train_configs, train_losses, self.kde_vartypes, self.min_points_in_model,
+                        self.top_n_percent, device=self.device)
+        if pair is None:  # bohb.py:234-237: too few rows for a KDE
+            return
+        self.kde_models[budget] = pair
+        self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
+                          'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs, np.min(train_losses)))

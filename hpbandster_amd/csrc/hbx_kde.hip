@@ -72,8 +72,10 @@ __host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) 
 // banks exactly once (conflict-free)
 __host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 16; }
 __host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 16; }
+// padded to a multiple of 8 KB: every wave of the scoring block moves the same number of 1-KB
+// LDS-DMA pieces per chunk (the counted vmcnt of the pipeline depends on it)
 __host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
-  return OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0);
+  return (OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0) + 2047) & ~2047;
 }
 static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }  // floats per chunk
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
@@ -670,8 +672,13 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   constexpr int NSH = NSC + KC;             // f16 K-steps of 32
   constexpr int KTP = h_ktp(NSC * 8, KC);   // halves per observation row (padded); nsc_of(8 NSC) = NSC
   constexpr int KPP = h_kpp(KC);
-  constexpr int CHF = OBS_CHUNK + OBS_CHUNK * KTP / 2 + (SIGNED ? OBS_CHUNK * KPP / 2 : 0);
-  __shared__ __align__(16) float lds[2 * CHF];
+  constexpr int CHF = h_chunk_floats(NSC * 8, KC, SIGNED ? 1 : 0);
+  // LDS ring: 3 buffers (chunk c+2 in flight while c is used) when they fit in the 160 KB, else 2
+  constexpr int NBUF = (3 * CHF * 4 <= 160 * 1024) ? 3 : 2;
+  static_assert(NBUF * CHF * 4 <= 160 * 1024, "observation chunk too large for LDS");
+  constexpr int G = CHF * 4 / (1024 * MFMA_WAVES);         // 1-KB LDS-DMA pieces per wave per chunk
+  static_assert(G * 1024 * MFMA_WAVES == CHF * 4, "chunk must be a multiple of 8 KB");
+  __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16 * RT;
@@ -734,19 +741,26 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
 #pragma unroll
     for (int q = 0; q < 4; ++q) S[r][q] = Sn[r][q] = 0.f;
   const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
-  constexpr int NT = 64 * MFMA_WAVES;
-  constexpr int NV4 = CHF / 4;
-  constexpr int PER = (NV4 + NT - 1) / NT;
-  float4 pre[PER];
-  {
-    const float4* __restrict__ src = (const float4*)table;
+  // LDS-DMA (global_load_lds_dwordx4): each wave copies its G 1-KB pieces of a chunk straight into
+  // the ring; completion is tracked by a counted vmcnt + one raw barrier per chunk
+  auto issue = [&](int c) {
+    const float* src = table + (int64_t)c * CHF;
+    float* dst = lds + (c % NBUF) * CHF;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int v = threadIdx.x + q * NT;
-      if (v < NV4) ((float4*)lds)[v] = src[v];
+    for (int g = 0; g < G; ++g) {
+      const int piece = wave + g * MFMA_WAVES;
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
     }
+  };
+  issue(0);
+  if (NBUF == 3 && nchunks > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
+  __builtin_amdgcn_s_barrier();
 
   // MFMAs of one 16-observation column tile for every row tile
   auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
@@ -777,16 +791,8 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   };
 
   for (int c = 0; c < nchunks; ++c) {
-    float* buf = lds + (c & 1) * CHF;
-    const bool more = c + 1 < nchunks;
-    if (more) {  // next chunk -> registers, lands during this chunk's math
-      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) pre[q] = src[v];
-      }
-    }
+    const float* buf = lds + (c % NBUF) * CHF;
+    if (c + NBUF - 1 < nchunks) issue(c + NBUF - 1);  // its buffer was last read in iteration c-1
     float Sb[RT][4], Snb[RT][4];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -820,15 +826,13 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         S[r][q] += Sb[r][q];
         if (SIGNED) Sn[r][q] += Snb[r][q];
       }
-    if (more) {
-      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) dst[v] = pre[q];
-      }
-    }
-    __syncthreads();
+    // chunk c+1 complete for this wave (chunk c+2 may stay in flight), this wave's reads of buffer c
+    // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
+    if (NBUF == 3 && c + 2 < nchunks)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 #pragma unroll
   for (int r = 0; r < RT; ++r)

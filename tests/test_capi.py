@@ -39,7 +39,8 @@ def test_host_side_helpers():
     a, b, s = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
     assert L.hbx_kde_bucket(24, 8, a.ctypes.data, b.ctypes.data, s.ctypes.data) == 0
     assert (a[0], b[0]) == (24, 8) and s[0] == 28 * 80 + 64 * 8
-    assert L.hbx_kde_table_floats(100, 24, 8) == 2 * (28 * 80 + 64 * 4 * 16 * 2)
+    tf = L.hbx_kde_table_floats(100, 24, 8)  # capacity: largest layout prepare may pick, 2 chunks
+    assert tf % 2 == 0 and tf // 2 >= 28 * 80 + 64 * 4 * 16 * 2
     assert L.hbx_kde_bucket(100, 0, a.ctypes.data, b.ctypes.data, s.ctypes.data) == -3
     assert b"continuous" in L.hbx_last_error()
     assert L.hbx_kde_workspace_bytes(1000, 100) > 1000 * 16
