@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU-box round check: gpu tests, smoke, bench, rocprofv3 kernel-trace stats (run via gpurun).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-check}
+mkdir -p $OUT
+cd $R
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; cat $OUT/smoke.log; exit 2; }
+cat $OUT/smoke.log
+timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 3; }
+cat $OUT/bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $OUT/trace.log 2>&1 || { echo rocprof failed; tail -20 $OUT/trace.log; exit 4; }
+find $OUT/trace -name '*stats*' | head -5
+echo check done
