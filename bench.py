@@ -157,6 +157,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    last = kde.AcqResult.from_bytes(ws[int(pair.result_offset()):int(pair.result_offset()) + kde.RESULT_BYTES]
+                                    .cpu().numpy().tobytes())
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -175,7 +177,7 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,
                    "parallelism": "candidate-sharded x%d, RCCL all_gather of local winners" % world,
-                   "winner": winner[0]},
+                   "winner": winner[0], "shortlist": last.shortlist},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
                      "kernel": "kde_logpdf_kernel<24,8,false> (l and g launches)",

@@ -24,7 +24,7 @@
 #define HBX_LN2f 0.69314718055994531f
 #define HBX_LN_CLAMP (-18.420680743952367)   // ln(1e-8), bohb.py:129
 #define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
-#define EXACT_GRID 128
+#define EXACT_GRID 2048  // blocks of the exact re-score (grid-stride over its work items)
 #define SUM_BLOCK 32
 #define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
 #define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
@@ -110,14 +110,23 @@ __global__ __launch_bounds__(256) void kde_maxcode_kernel(const double* __restri
   if (threadIdx.x == 0) P->cat_maxcode[u] = red[0] >= 100000 ? -1 : red[0];
 }
 
-// Per continuous slot: mean of the KDE's data column (centre of the scaled coordinates).
-__global__ void kde_center_kernel(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
-                                  KdeParams* __restrict__ P) {
-  for (int k = threadIdx.x; k < P->dc; k += blockDim.x) {
-    const int d = P->cont_dim[k];
-    double acc = 0.0;
-    for (int j = 0; j < P->n; ++j) acc += X[rows[j] * (int64_t)D + d];
-    const double m = acc / (double)P->n;
+// Per continuous slot (one block each): mean of the KDE's data column, the centre of the scaled
+// coordinates.  Any finite centre is correct (table and candidates use the same one); it only keeps
+// the fp32 expansion well conditioned, so the summation order is free.
+__global__ __launch_bounds__(256) void kde_center_kernel(const double* __restrict__ X, int32_t D,
+                                                         const int64_t* __restrict__ rows,
+                                                         KdeParams* __restrict__ P) {
+  __shared__ double red[4];
+  const int k = blockIdx.x;
+  const int d = P->cont_dim[k];
+  const int n = P->n;
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < n; j += 256) acc += X[rows[j] * (int64_t)D + d];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double m = ((red[0] + red[1]) + (red[2] + red[3])) / (double)n;
     P->center[k] = (m == m && m - m == 0.0) ? m : 0.0;
   }
 }
@@ -685,6 +694,11 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   const int n = P->n, dc = P->dc;
   const int ia = lane & 15, kq = lane >> 4;
 
+  // A operands (candidate side).  Every lane walks all dims with wave-uniform (scalar) parameter
+  // indices -- independent loads of its candidate's row, no lane-varying parameter lookups -- and
+  // keeps the f16 slots its lane group kq owns: continuous dim c -> step c/8, lanes kq = (c%8)/2,
+  // halves 4(c%2)+{0,1} = hi, +{2,3} = lo; one-hot slot t -> step NSC + t/16, kq = (t%16)/4,
+  // halves 2(t%4)+{0,1}.
   f16x8 ah[RT][NSH];
   float ci_a[RT], bnd_a[RT];
 #pragma unroll
@@ -693,38 +707,37 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
     if (ii >= Nc) ii = Nc - 1;
     const double* x = cand + ii * (int64_t)D;
     float ci = 0.f, bnd = 0.f;
-    for (int k = 0; k < dc; ++k) {
-      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-      ci = fmaf(-v, v, ci);
-      bnd = fmaf(2.f * fabsf(v), P->xmax[k], bnd);
+#pragma unroll
+    for (int s = 0; s < NSH; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ah[r][s][j] = (_Float16)0.f;
+#pragma unroll
+    for (int c = 0; c < 8 * NSC; ++c) {
+      if (c < dc) {
+        const float v = (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
+        ci = fmaf(-v, v, ci);
+        bnd = fmaf(2.f * fabsf(v), P->xmax[c], bnd);
+        const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
+        const _Float16 hi = (_Float16)xc;
+        const _Float16 lo = (_Float16)(xc - (float)hi);
+        const bool mine = kq == ((c & 7) >> 1);
+        const int j0 = 4 * (c & 1);
+        ah[r][c >> 3][j0 + 0] = mine ? hi : ah[r][c >> 3][j0 + 0];
+        ah[r][c >> 3][j0 + 1] = mine ? hi : ah[r][c >> 3][j0 + 1];
+        ah[r][c >> 3][j0 + 2] = mine ? lo : ah[r][c >> 3][j0 + 2];
+        ah[r][c >> 3][j0 + 3] = mine ? lo : ah[r][c >> 3][j0 + 3];
+      }
     }
     ci_a[r] = ci;
     bnd_a[r] = bnd;
-#pragma unroll
-    for (int s = 0; s < NSC; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * s + 8 * kq + j;
-        const int c = k >> 2, pt = k & 3;
-        float v = 0.f;
-        if (c < dc) {
-          const float xx = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
-          const float xc = fminf(fmaxf(xx, -60000.f), 60000.f);
-          const float hi = (float)(_Float16)xc;
-          v = (pt < 2) ? hi : (xc - hi);
-        }
-        ah[r][s][j] = (_Float16)v;
-      }
-    }
     const int tot = P->oh_total;
 #pragma unroll
-    for (int s = 0; s < KC; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = (32 * s + 8 * kq + j) >> 1;
-        float v = 0.f;
-        if (t < tot && x[P->cat_dim[P->oh_dim[t]]] == (double)P->oh_level[t]) v = 1.f;
-        ah[r][NSC + s][j] = (_Float16)v;
+    for (int t = 0; t < 16 * KC; ++t) {
+      if (t < tot) {
+        const bool hit = (kq == ((t & 15) >> 2)) && x[P->oh_col[t]] == P->oh_val[t];
+        const int s = NSC + (t >> 4), j0 = 2 * (t & 3);
+        ah[r][s][j0 + 0] = hit ? (_Float16)1.f : ah[r][s][j0 + 0];
+        ah[r][s][j0 + 1] = hit ? (_Float16)1.f : ah[r][s][j0 + 1];
       }
     }
   }
@@ -1042,139 +1055,240 @@ __global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restr
   }
 }
 
-// numpy's pairwise summation (umath loops: n < 8 plain, <= 128 eight accumulators, else split).
-// dens.sum(axis=0) (SM:_kernel_base.py:516) runs it over the ufunc buffer chunks of 8192 elements,
-// accumulated left to right from 0.0 -- see np_sum below.
-__device__ double np_pairwise_sum(const double* a, int64_t n) {
-  // explicit stack instead of recursion: (offset, len, state)
-  struct Fr { int64_t off, len; double left; int st; };
-  Fr stk[48];
-  int sp = 0;
-  stk[0] = {0, n, 0.0, 0};
-  double ret = 0.0;
-  while (sp >= 0) {
-    Fr& f = stk[sp];
-    if (f.len <= 128) {
-      double res;
-      const double* p = a + f.off;
-      if (f.len < 8) {
-        res = 0.0;
-        for (int64_t i = 0; i < f.len; ++i) res += p[i];
-      } else {
-        double r0 = p[0], r1 = p[1], r2 = p[2], r3 = p[3], r4 = p[4], r5 = p[5], r6 = p[6], r7 = p[7];
-        int64_t i;
-        for (i = 8; i < f.len - (f.len % 8); i += 8) {
-          r0 += p[i + 0]; r1 += p[i + 1]; r2 += p[i + 2]; r3 += p[i + 3];
-          r4 += p[i + 4]; r5 += p[i + 5]; r6 += p[i + 6]; r7 += p[i + 7];
-        }
-        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-        for (; i < f.len; ++i) res += p[i];
-      }
-      ret = res;
-      --sp;
-      // propagate into parent frames
-      while (sp >= 0) {
-        Fr& pf = stk[sp];
-        if (pf.st == 1) {  // left child finished -> start right child
-          pf.left = ret;
-          pf.st = 2;
-          int64_t n2 = pf.len / 2;
-          n2 -= n2 % 8;
-          stk[++sp] = {pf.off + n2, pf.len - n2, 0.0, 0};
-          break;
-        } else {  // st == 2: right child finished
-          ret = pf.left + ret;
-          --sp;
-        }
-      }
-    } else {
-      int64_t n2 = f.len / 2;
-      n2 -= n2 % 8;
-      f.st = 1;
-      const int64_t off = f.off;
-      stk[++sp] = {off, n2, 0.0, 0};
-    }
+// numpy's pairwise summation (umath loops: n < 8 plain, <= 128 eight accumulators, else split at
+// n/2 rounded down to a multiple of 8).  dens.sum(axis=0) (SM:_kernel_base.py:516) runs it over the
+// ufunc buffer chunks of 8192 elements, accumulated left to right from 0.0 -- see exact_pdf.
+__device__ double pw_leaf_sum(const double* p, int len) {
+  if (len < 8) {
+    double res = 0.0;
+    for (int i = 0; i < len; ++i) res += p[i];
+    return res;
   }
-  return ret;
+  double r0 = p[0], r1 = p[1], r2 = p[2], r3 = p[3], r4 = p[4], r5 = p[5], r6 = p[6], r7 = p[7];
+  int i;
+  for (i = 8; i < len - (len % 8); i += 8) {
+    r0 += p[i + 0]; r1 += p[i + 1]; r2 += p[i + 2]; r3 += p[i + 3];
+    r4 += p[i + 4]; r5 += p[i + 5]; r6 += p[i + 6]; r7 += p[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < len; ++i) res += p[i];
+  return res;
 }
 
-// exact fp64 pdf of one KDE at x (reference arithmetic); dens = scratch[n]; called by a whole block
-__device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
-                            const KdeParams* __restrict__ P, const double* __restrict__ x,
-                            double* __restrict__ dens, double* __restrict__ sh) {
-  const int n = P->n;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const double* xr = X + rows[j] * (int64_t)D;
+#define PW_BUF 8192    // numpy ufunc buffer (elements)
+#define PW_CUT 3       // a buffer's split tree is cut at depth 3 into <= 8 independent units
+#define PW_UNITS 8
+#define PW_UNIT_MAX 1040  // longest depth-3 node of any m <= 8192 is 1031 elements
+#define PW_LEVELS 8    // a unit's own split tree has depth <= 7
+#define EXACT_THREADS 256
+#define EXACT_SPLIT_CAP 2048  // shortlists up to this size spread every (candidate, KDE) over units
+
+// Node (lev, t) of the split tree of an m-element buffer: walk t's bits from the root.  Returns
+// false when the node does not exist (an ancestor is already a leaf).
+__device__ __forceinline__ bool pw_node(int m, int lev, int t, int* off, int* len) {
+  int o = 0, l = m;
+  for (int b = lev - 1; b >= 0; --b) {
+    if (l <= 128) return false;
+    int n2 = l / 2;
+    n2 -= n2 % 8;
+    if ((t >> b) & 1) {
+      o += n2;
+      l -= n2;
+    } else {
+      l = n2;
+    }
+  }
+  *off = o;
+  *len = l;
+  return true;
+}
+
+// Unit u (0..7) of a buffer: the depth-3 node at position u, or the shallower leaf whose leftmost
+// depth-3 position is u.  Returns false for positions covered by another unit.
+__device__ __forceinline__ bool pw_unit(int m, int u, int* off, int* len) {
+  for (int lev = 0; lev <= PW_CUT; ++lev) {
+    const int sh = PW_CUT - lev;
+    if (!pw_node(m, lev, u >> sh, off, len)) return false;
+    if (lev == PW_CUT || *len <= 128) return (u & ((1 << sh) - 1)) == 0;
+  }
+  return false;
+}
+
+// Top of the tree (depth <= 3) from the unit sums, numpy's order; one thread.
+__device__ double pw_combine_units(int m, const double* us) {
+  double v[PW_CUT + 1][PW_UNITS];
+  for (int lev = PW_CUT; lev >= 0; --lev)
+    for (int t = 0; t < (1 << lev); ++t) {
+      int off, len;
+      if (!pw_node(m, lev, t, &off, &len)) continue;
+      v[lev][t] = (lev == PW_CUT || len <= 128) ? us[t << (PW_CUT - lev)] : v[lev + 1][2 * t] + v[lev + 1][2 * t + 1];
+    }
+  return v[0][0];
+}
+
+struct ExactShared {
+  double dens[PW_UNIT_MAX];
+  double nsum[PW_LEVELS][128];
+  double usum[PW_UNITS];
+  // per-dim constants of the reference kernels (SM:kernels.py:62-64,125): continuous -> (h*h)*2 in
+  // c0, categorical -> 1-h in c0 and h/(c-1) in c1; the point's coordinates in xd
+  double c0[HBX_MAX_D], c1[HBX_MAX_D], xd[HBX_MAX_D];
+  int32_t cont[HBX_MAX_D];
+};
+
+// Pairwise sum of a[0:m] (m <= 1040, in LDS) in numpy's order, whole block, level-synchronous:
+// a leaf (len <= 128) is summed by one thread, an inner node adds its two children of the level
+// below.  Same additions, same order, as the recursive reference loop.
+__device__ double np_pairwise_block(const double* a, int m, double (*nsum)[128]) {
+  for (int lev = PW_LEVELS - 1; lev >= 0; --lev) {
+    for (int t = threadIdx.x; t < (1 << lev); t += blockDim.x) {
+      int off, len;
+      if (pw_node(m, lev, t, &off, &len))
+        nsum[lev][t] = (len <= 128) ? pw_leaf_sum(a + off, len) : nsum[lev + 1][2 * t] + nsum[lev + 1][2 * t + 1];
+    }
+    __syncthreads();
+  }
+  return nsum[0][0];
+}
+
+// Per-dim constants + the point's coordinates into LDS (whole block).
+__device__ void exact_setup(const KdeParams* __restrict__ P, int32_t D, const double* __restrict__ x,
+                            ExactShared* sh) {
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const double h = P->bw[d];
+    const bool c = P->vartype[d] == 0;
+    sh->cont[d] = c;
+    sh->c0[d] = c ? (h * h) * 2. : 1. - h;
+    sh->c1[d] = c ? 0. : h / (double)(P->nlev[d] - 1);
+    sh->xd[d] = x[d];
+  }
+  __syncthreads();
+}
+
+// Sum of the per-observation terms Kval.prod(1) / prod(bw_c) (SM:_kernel_base.py:509-516) over
+// the observations [first, first+len) -- one unit of one buffer, pairwise order; whole block.
+__device__ double exact_unit(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
+                             const KdeParams* __restrict__ P, int first, int len, ExactShared* sh) {
+  const double pbc = P->prod_bw_c;
+  for (int j = threadIdx.x; j < len; j += blockDim.x) {
+    const double* xr = X + rows[first + j] * (int64_t)D;
     double p = 1.0;
+#pragma unroll 8
     for (int d = 0; d < D; ++d) {
-      const double h = P->bw[d];
+      const double v = xr[d], xv = sh->xd[d];
       double k;
-      if (P->vartype[d] == 0) {
-        const double diff = xr[d] - x[d];
-        k = HBX_INV_SQRT_2PI * exp(-(diff * diff) / ((h * h) * 2.));
+      if (sh->cont[d]) {
+        const double diff = v - xv;
+        k = HBX_INV_SQRT_2PI * exp(-(diff * diff) / sh->c0[d]);
       } else {
-        k = (xr[d] == x[d]) ? (1. - h) : (h / (double)(P->nlev[d] - 1));
+        k = (v == xv) ? sh->c0[d] : sh->c1[d];
       }
       p = (d == 0) ? k : p * k;
     }
-    dens[j] = p / P->prod_bw_c;
+    sh->dens[j] = p / pbc;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double acc = 0.0;  // np.add.reduce: identity 0.0, then one pairwise sum per 8192-element buffer
-    for (int64_t c = 0; c < n; c += 8192) acc = acc + np_pairwise_sum(dens + c, (n - c) < 8192 ? (n - c) : 8192);
-    *sh = acc / (double)n;
-  }
-  __syncthreads();
-  const double r = *sh;
-  __syncthreads();
-  return r;
+  return np_pairwise_block(sh->dens, len, sh->nsum);
 }
 
-__global__ __launch_bounds__(256) void kde_exact_kernel(
-    const double* __restrict__ cand, int32_t D, int64_t index_base,
+// exact fp64 pdf of one KDE at the point staged by exact_setup, one block, all units in turn
+__device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
+                            const KdeParams* __restrict__ P, ExactShared* sh) {
+  const int n = P->n;
+  double acc = 0.0;  // np.add.reduce: identity 0.0, then one pairwise sum per 8192-element buffer
+  for (int c = 0; c < n; c += PW_BUF) {
+    const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
+    for (int u = 0; u < PW_UNITS; ++u) {
+      int off, len;
+      if (!pw_unit(m, u, &off, &len)) continue;
+      const double v = exact_unit(X, D, rows, P, c + off, len, sh);
+      if (threadIdx.x == 0) sh->usum[u] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) acc = acc + pw_combine_units(m, sh->usum);
+  }
+  return acc / (double)n;  // valid in thread 0
+}
+
+// Exact re-score of the shortlist.  Small shortlists (<= EXACT_SPLIT_CAP): one work item per
+// (candidate, KDE, 8192-buffer, unit) so one candidate spreads over many CUs; the unit sums go to
+// `part` and kde_final combines them.  Larger: one item per (candidate, KDE), all units in turn.
+__global__ __launch_bounds__(EXACT_THREADS) void kde_exact_kernel(
+    const double* __restrict__ cand, int32_t D,
     const KdeParams* __restrict__ Pg, const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
     const KdeParams* __restrict__ Pb, const double* __restrict__ Xb, const int64_t* __restrict__ rows_b,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ count, double* __restrict__ exact,
-    double* __restrict__ exact_l, double* __restrict__ exact_g, double* __restrict__ scratch, int64_t nmax) {
-  __shared__ double sh;
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
+    double* __restrict__ exact_l, double* __restrict__ exact_g) {
+  __shared__ ExactShared sh;
   const int cnt = *count;
-  double* dens = scratch + (int64_t)blockIdx.x * nmax;
-  for (int p = blockIdx.x; p < cnt; p += gridDim.x) {
-    const double* x = cand + (int64_t)list[p] * D;
-    const double g = exact_pdf(Xb, D, rows_b, Pb, x, dens, &sh);
-    const double l = exact_pdf(Xg, D, rows_g, Pg, x, dens, &sh);
-    if (threadIdx.x == 0) {
-      // bohb.py:129 with Python max(): max(1e-8, g) keeps 1e-8 unless g > 1e-8 (NaN -> 1e-8);
-      // max(l, 1e-8) keeps l unless 1e-8 > l (NaN -> NaN)
-      const double G = (g > 1e-8) ? g : 1e-8;
-      const double L = (1e-8 > l) ? 1e-8 : l;
-      exact[p] = G / L;
-      exact_l[p] = l;
-      exact_g[p] = g;
+  const bool split = cnt <= EXACT_SPLIT_CAP;
+  const int per = split ? nbuf * PW_UNITS : 1;  // items per (candidate, KDE)
+  const int64_t items = (int64_t)cnt * 2 * per;
+  for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+    const int64_t pk = item / per;  // (candidate, KDE)
+    const int p = (int)(pk >> 1);
+    const bool isl = pk & 1;
+    const KdeParams* P = isl ? Pg : Pb;
+    const double* X = isl ? Xg : Xb;
+    const int64_t* rows = isl ? rows_g : rows_b;
+    if (split) {
+      const int r = (int)(item % per), b = r / PW_UNITS, u = r % PW_UNITS;
+      const int n = P->n, c = b * PW_BUF;
+      if (c >= n) continue;
+      const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
+      int off, len;
+      if (!pw_unit(m, u, &off, &len)) continue;
+      exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
+      const double v = exact_unit(X, D, rows, P, c + off, len, &sh);
+      if (threadIdx.x == 0) part[pk * per + r] = v;
+    } else {
+      exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
+      const double v = exact_pdf(X, D, rows, P, &sh);
+      if (threadIdx.x == 0) (isl ? exact_l : exact_g)[p] = v;
     }
+    __syncthreads();
   }
 }
 
+// split mode: pdf of every (shortlisted candidate, KDE) from its unit sums; one thread each
+__global__ __launch_bounds__(256) void kde_exact_combine_kernel(const KdeParams* __restrict__ Pg,
+                                                                const KdeParams* __restrict__ Pb,
+                                                                const int32_t* __restrict__ count, int32_t nbuf,
+                                                                const double* __restrict__ part,
+                                                                double* __restrict__ exact_l,
+                                                                double* __restrict__ exact_g) {
+  const int cnt = *count;
+  if (cnt > EXACT_SPLIT_CAP) return;
+  const int64_t pk = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pk >= 2 * (int64_t)cnt) return;
+  const bool isl = pk & 1;
+  const int n = (isl ? Pg : Pb)->n;
+  const double* us = part + pk * nbuf * PW_UNITS;
+  double acc = 0.0;
+  for (int c = 0, b = 0; c < n; c += PW_BUF, ++b) {
+    const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
+    acc = acc + pw_combine_units(m, us + b * PW_UNITS);
+  }
+  (isl ? exact_l : exact_g)[pk >> 1] = acc / (double)n;
+}
 
 // exact fp64 pdf of one KDE at every row of pts (grid-stride over points, one block per point)
-__global__ __launch_bounds__(256) void kde_pdf_exact_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
-                                                            const KdeParams* __restrict__ P,
-                                                            const double* __restrict__ X,
-                                                            const int64_t* __restrict__ rows,
-                                                            double* __restrict__ out, double* __restrict__ scratch,
-                                                            int64_t nmax) {
-  __shared__ double sh;
-  double* dens = scratch + (int64_t)blockIdx.x * nmax;
+__global__ __launch_bounds__(EXACT_THREADS) void kde_pdf_exact_kernel(const double* __restrict__ pts, int64_t Np,
+                                                                      int32_t D, const KdeParams* __restrict__ P,
+                                                                      const double* __restrict__ X,
+                                                                      const int64_t* __restrict__ rows,
+                                                                      double* __restrict__ out) {
+  __shared__ ExactShared sh;
   for (int64_t p = blockIdx.x; p < Np; p += gridDim.x) {
-    const double v = exact_pdf(X, D, rows, P, pts + p * D, dens, &sh);
+    exact_setup(P, D, pts + p * D, &sh);
+    const double v = exact_pdf(X, D, rows, P, &sh);
     if (threadIdx.x == 0) out[p] = v;
+    __syncthreads();
   }
 }
 
 __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ count,
-                                                        const double* __restrict__ exact,
                                                         const double* __restrict__ exact_l,
                                                         const double* __restrict__ exact_g,
                                                         const int32_t* __restrict__ flags, int64_t index_base,
@@ -1187,7 +1301,10 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
   int64_t bidx = INT64_MAX;
   int32_t bpos = -1;
   for (int p = threadIdx.x; p < cnt; p += 256) {
-    const double s = exact[p];
+    // bohb.py:129 with Python max(): max(1e-8, g) keeps 1e-8 unless g > 1e-8 (NaN -> 1e-8);
+    // max(l, 1e-8) keeps l unless 1e-8 > l (NaN -> NaN)
+    const double g = exact_g[p], l = exact_l[p];
+    const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
     const int64_t idx = list[p];
     // valid iff s < +inf (bohb.py:150 'val < best' with best = inf); strict '<', first index wins
     if (s < INFINITY && (s < best || (s == best && idx < bidx))) {
@@ -1311,7 +1428,7 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 
 // workspace layout (bytes), shared by hbx_kde_workspace_bytes and hbx_kde_acquire
 struct WsLayout {
-  size_t U, count, flags, res, est_l, est_g, lo, hi, list, exact, exact_l, exact_g, scratch, total;
+  size_t U, count, flags, res, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
 };
 
 static WsLayout ws_layout(int64_t Nc, int64_t nmax) {
@@ -1331,10 +1448,9 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax) {
   w.lo = take(4 * Nc);
   w.hi = take(4 * Nc);
   w.list = take(4 * Nc);
-  w.exact = take(8 * Nc);
   w.exact_l = take(8 * Nc);
   w.exact_g = take(8 * Nc);
-  w.scratch = take(8 * (size_t)EXACT_GRID * nmax);
+  w.part = take(8 * (size_t)2 * EXACT_SPLIT_CAP * PW_UNITS * ((nmax + PW_BUF - 1) / PW_BUF));
   w.total = o;
   return w;
 }
@@ -1475,6 +1591,8 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
         for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
           P->oh_dim[t] = u;
           P->oh_level[t] = l;
+          P->oh_col[t] = P->cat_dim[u];
+          P->oh_val[t] = (double)l;
           ++t;
         }
     }
@@ -1499,10 +1617,13 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   info[7] = P->du_pad;
   e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  const int dc_n = P->dc;
   free(P);
   if (e != hipSuccess) return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
-  hipLaunchKernelGGL(kde_center_kernel, dim3(1), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
-  HBX_LAUNCH_CHECK();
+  if (dc_n > 0) {
+    hipLaunchKernelGGL(kde_center_kernel, dim3(dc_n), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
+    HBX_LAUNCH_CHECK();
+  }
   const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
   hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
                      (KdeParams*)params, table);
@@ -1552,10 +1673,9 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   float* lo = (float*)(ws + w.lo);
   float* hi = (float*)(ws + w.hi);
   int32_t* list = (int32_t*)(ws + w.list);
-  double* exact = (double*)(ws + w.exact);
   double* exact_l = (double*)(ws + w.exact_l);
   double* exact_g = (double*)(ws + w.exact_g);
-  double* scratch = (double*)(ws + w.scratch);
+  double* part = (double*)(ws + w.part);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, res);
   HBX_LAUNCH_CHECK();
@@ -1574,19 +1694,26 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
     HBX_LAUNCH_CHECK();
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, U, flags, list, count);
     HBX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(256), 0, s, cand, D, index_base,
+    const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
+    hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_THREADS), 0, s, cand, D,
                        (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
-                       rows_bad, list, count, exact, exact_l, exact_g, scratch, nmax);
+                       rows_bad, list, count, nbuf, part, exact_l, exact_g);
+    HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 255) / 256), dim3(256), 0, s,
+                       (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,
+                       exact_g);
     HBX_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact, exact_l, exact_g, flags,
+  hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
                      index_base, res);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
 
 
-int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax) { return (int64_t)(8 * (size_t)EXACT_GRID * nmax); }
+// the exact pdf stages its per-observation terms in LDS: no global scratch is needed any more (the
+// entry point keeps its scratch argument; 256 bytes keep callers' allocations non-empty)
+int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax) { return 256; }
 
 // Exact fp64 pdf (reference arithmetic and operation order) of one prepared KDE at Np points
 // (device fp64 [Np][D]) -> out (device fp64 [Np]).  KDEMultivariate.pdf as a batched GPU call.
@@ -1597,8 +1724,8 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
   if (scratch_bytes < hbx_kde_pdf_scratch_bytes(n)) return hbx_fail(HBX_ERR_ARG, "pdf scratch too small");
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
-  hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, pts, Np, D,
-                     (const KdeParams*)params, X, rows, out, (double*)scratch, n);
+  hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(EXACT_THREADS), 0, (hipStream_t)stream, pts, Np, D,
+                     (const KdeParams*)params, X, rows, out);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }

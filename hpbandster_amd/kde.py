@@ -165,6 +165,10 @@ class KDEPair(object):
     def keys(self):
         return ["good", "bad"]
 
+    def result_offset(self):
+        """Byte offset of the AcqResult record inside an acquisition workspace."""
+        return int(N.lib().hbx_kde_result_ptr(4096)) - 4096
+
     def workspace_bytes(self, Nc):
         return int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
 

@@ -160,3 +160,29 @@ def test_rescue_path_far_candidates(device):
     l = O.pdf_many(pair.good.data, pair.good.bw, "cc", C)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, "cc", C)
     assert res.index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("n_obs", [10000, 20000])
+def test_exact_split_units_match_whole_sum(device, n_obs):
+    """The acquisition's exact re-score spreads one candidate's observations over tree units (one
+    block each) and recombines them; DeviceKDE.pdf sums every unit in one block.  Same additions in
+    the same order -> bit-identical pdfs; and both within 1e-13 of the reference's numpy sum (numpy
+    sums over 8192-element buffers: n=20000 has three)."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(n_obs, 24, 8, 4)
+    L = S.make_losses(n_obs)
+    vt = S.var_type_string(24, 8)
+    pair = kde.fit_pair(X, L, vt, 33, device=device)
+    C = S.make_candidates(64, 24, 8, 4)
+    res = pair.acquire(C)
+    assert res.index >= 0
+    w = C[res.index:res.index + 1]
+    assert np.asarray(pair.good.pdf(w)).item() == res.pdf_l
+    assert np.asarray(pair.bad.pdf(w)).item() == res.pdf_g
+    ref_l = O.pdf_many(pair.good.data, pair.good.bw, vt, w)[0]
+    ref_g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, w)[0]
+    np.testing.assert_allclose([res.pdf_l, res.pdf_g], [ref_l, ref_g], rtol=1e-13)
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
+    assert res.index == O.select(l, g)[0]
