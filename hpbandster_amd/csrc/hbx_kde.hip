@@ -20,16 +20,7 @@
 #include <vector>
 
 #include "hbx_common.h"
-
-#define HBX_LN2f 0.69314718055994531f
-#define HBX_LN_CLAMP (-18.420680743952367)   // ln(1e-8), bohb.py:129
-#define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
-#define EXACT_GRID 2048  // blocks of the exact re-score (grid-stride over its work items)
-#define SUM_BLOCK 32
-#define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
-#define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
-#define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
-#define H_ROW_TILES 2  // hmode: 16-candidate row tiles per wave (32 candidates)
+#include "hbx_kde_impl.h"
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -45,38 +36,6 @@ static void bucket_dims(int dc, int du, int* dc_pad, int* du_pad) {
     if (du <= b) { *du_pad = b; break; }
 }
 
-// Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
-//   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0
-//   [64][du_pad]        categorical codes (float), observation-major
-// KP = dc_pad + 2 rounded up to a multiple of 4 (MFMA 16x16x4 K step).  Observations past n in the
-// last chunk are padding with C_j = -1e30 (their terms are exactly 0).
-//
-// Categorical part when kc >= 1 (one-hot mode): 64 observations x kc*32 f16, observation-major,
-// slot k = 2*t + p of one-hot position t = (dim u, level) holds delta_u's f16 hi (p=0) / lo (p=1)
-// part when the observation has that level, else 0; for signed KDEs a second block of the same
-// shape holds 1 in the hi slot of matches in dims with negative match weight (parity count).
-#define OH_MAX_KC 4  // one-hot mode up to 4 f16 MFMA K-steps: sum over dims of levels <= 64
-__host__ __device__ constexpr int kp_of(int dc_pad) { return (dc_pad + 2 + 3) & ~3; }
-__host__ __device__ constexpr int cat_floats(int du_pad, int kc, int sgn) {
-  return kc == 0 ? OBS_CHUNK * du_pad : OBS_CHUNK * kc * 16 * (sgn ? 2 : 1);
-}
-__host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 0, int sgn = 0) {
-  return kp_of(dc_pad) * KROW + cat_floats(du_pad, kc, sgn);
-}
-// hmode (all-f16) chunk: [64 f32: C_j] [64 obs x KTP halves: hi/lo continuous + one-hot] [signed:
-// 64 obs x KPP halves parity]; continuous slot k = 4c + pt of dim c holds (pt even ? Xh_c : Xl_c) so
-// the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl).
-// Rows are padded by 16 halves (32 B) so the 16 observation rows a wave reads are spread over banks.
-__host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) / 32; }
-// row strides are 8*odd dwords: the 16 rows a ds_read_b128 lane group touches then cover all 64
-// banks exactly once (conflict-free)
-__host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 16; }
-__host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 16; }
-// padded to a multiple of 8 KB: every wave of the scoring block moves the same number of 1-KB
-// LDS-DMA pieces per chunk (the counted vmcnt of the pipeline depends on it)
-__host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
-  return (OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0) + 2047) & ~2047;
-}
 static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }  // floats per chunk
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 // capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket
@@ -227,660 +186,6 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)&P->cmax, __float_as_uint(a));
   if (j == 0)
     for (int q = 0; q < P->nconst; ++q) P->const_level[q] = x[P->const_dim[q]];
-}
-
-// ------------------------------------------------------------------------------------------
-// fp32 log-domain scoring
-//
-// Per (candidate i, observation j), in log2 units and minus the static bound M0:
-//   t_ij = C_j + c_i + sum_c x''_ic X'_jc + sum_u delta_u [x_iu == X_ju]
-// with X' = s (X - mu), x'' = 2 s (x - mu), c_i = -|x'_i|^2, C_j = -|X'_j|^2 + lb_sum - M0
-// (the expansion of -|x' - X'|^2).  The first three terms are one GEMM-shaped product
-// [candidates x K] . [K x observations] with K = 2 + Dc: they run on the f32 matrix cores
-// (v_mfma_f32_16x16x4_f32, an exact fp32 FMA chain in k order).  The categorical match,
-// exp2 and the sums run on the VALU beside them.  The categorical match is m = clamp(1 - d*d) on
-// the integer codes (d = x - X), which stays in the VALU (no VCC round trip).
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float cat_match(float a, float b) {
-  const float d = a - b;
-  return __builtin_amdgcn_fmed3f(fmaf(-d, d, 1.f), 0.f, 1.f);
-}
-
-__device__ __forceinline__ float cand_code(double xv) {
-  // codes are integers; anything else (incl. NaN) never equals an observed code
-  return (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
-}
-
-// Per-candidate epilogue: ln S+, ln S-, error bound (or the rescue marker err = -1)
-__device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, float S, float Sn, float off,
-                                             bool nan_c, float ci, float bnd, bool SIGNED, int chunk) {
-  KdeEst o;
-  o.pad = 0.f;
-  if (nan_c || S != S) {
-    o.lpos = NAN;
-    o.lneg = -INFINITY;
-    o.err = 0.f;
-    return o;
-  }
-  const float lnorm = (float)P->log_norm;
-  const float Sp = SIGNED ? (S - Sn) : S;
-  o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off) * HBX_LN2f + lnorm : -INFINITY;
-  o.lneg = (SIGNED && Sn > 0.f) ? (__log2f(Sn) + off) * HBX_LN2f + lnorm : -INFINITY;
-  const float u = 0x1p-24f;
-  const float Mabs = fabsf(ci) + P->cmax + bnd + P->sum_abs_delta;
-  const float dt = 3.f * (float)(P->dc + P->du + 4) * u * Mabs;  // |error of t|, log2 units
-  const float es = ((float)chunk + (float)P->n / (float)chunk + 24.f) * u * (SIGNED ? 3.f : 1.f);
-  o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
-  return o;
-}
-
-template <int DCP, int DUP, bool SIGNED>
-__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_kernel(const double* __restrict__ cand, int64_t Nc,
-                                                                    int32_t D, const KdeParams* __restrict__ P,
-                                                                    const float* __restrict__ table,
-                                                                    KdeEst* __restrict__ out) {
-  constexpr int KP = kp_of(DCP);
-  constexpr int NS = KP / 4;
-  constexpr int CHF = chunk_floats(DCP, DUP);
-  constexpr int NU = DUP > 0 ? DUP : 1;
-  __shared__ __align__(16) float lds[2 * CHF];  // double-buffered observation chunks
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;  // this wave's 16 candidates
-  const int n = P->n, dc = P->dc, du = P->du;
-  const int ia = lane & 15, kq = lane >> 4;
-
-  // A fragments: lane holds A[i = ia][k = 4s + kq]; A[i][0] = 1 (x C_j), A[i][1] = c_i, A[i][2+c] = x''_ic
-  float a[NS];
-  float ci_a = 0.f, bnd_a = 0.f;
-  {
-    int64_t ii = cbase + ia;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-    for (int k = 0; k < dc; ++k) {
-      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-      ci_a = fmaf(-v, v, ci_a);
-      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int k = 4 * s + kq;
-      float v = 0.f;
-      if (k == 0) {
-        v = 1.f;
-      } else if (k == 1) {
-        v = ci_a;
-      } else if (k - 2 < dc) {
-        const int c = k - 2;
-        v = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
-      }
-      a[s] = v;
-    }
-  }
-  // epilogue rows: the accumulator of lane holds candidates 4*kq + q (q = 0..3), observation ia
-  float xu[4][NU];
-  bool nanc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    int64_t ii = cbase + 4 * kq + q;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-#pragma unroll
-    for (int u = 0; u < DUP; ++u) xu[q][u] = (u < du) ? cand_code(x[P->cat_dim[u]]) : -1.f;
-    bool nn = P->nan_all != 0;
-    for (int c = 0; c < P->nconst; ++c)
-      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
-    nanc[q] = nn;
-  }
-  float dl[NU], ng[NU];
-#pragma unroll
-  for (int u = 0; u < DUP; ++u) {
-    dl[u] = (u < du) ? P->cat_delta[u] : 0.f;
-    ng[u] = (u < du) ? P->cat_negf[u] : 0.f;
-  }
-
-  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
-  constexpr int NT = 64 * MFMA_WAVES;                 // threads per block
-  constexpr int NV4 = CHF / 4;                        // float4 per chunk
-  constexpr int PER = (NV4 + NT - 1) / NT;            // float4 per thread per chunk
-  float4 pre[PER];
-  // stage chunk 0; later chunks are prefetched into registers during the previous chunk's math
-  {
-    const float4* __restrict__ src = (const float4*)table;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int v = threadIdx.x + q * NT;
-      if (v < NV4) ((float4*)lds)[v] = src[v];
-    }
-  }
-  __syncthreads();
-
-  // one 16x16 tile: B fragments and categorical codes of observation column jt*16 + ia
-  auto load_tile = [&](const float* buf, int jt, float* b, float* xo) {
-#pragma unroll
-    for (int s2 = 0; s2 < NS; ++s2) b[s2] = buf[(4 * s2 + kq) * KROW + jt * 16 + ia];
-#pragma unroll
-    for (int u = 0; u < DUP; ++u) xo[u] = buf[KP * KROW + (jt * 16 + ia) * DUP + u];
-  };
-  auto epilogue = [&](const f32x4& acc, const float* xo, float* Sb, float* Snb) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float t = acc[q];
-      float par = 0.f;
-#pragma unroll
-      for (int u = 0; u < DUP; ++u) {
-        const float m = cat_match(xu[q][u], xo[u]);
-        t = fmaf(dl[u], m, t);
-        if (SIGNED) par = fmaf(m, ng[u], -fabsf(par));
-      }
-      const float e = __builtin_amdgcn_exp2f(t);
-      Sb[q] += e;
-      if (SIGNED) Snb[q] = fmaf(fabsf(par), e, Snb[q]);
-    }
-  };
-
-  for (int c = 0; c < nchunks; ++c) {
-    float* buf = lds + (c & 1) * CHF;
-    const bool more = c + 1 < nchunks;
-    if (more) {  // prefetch the next chunk into registers (lands during this chunk's math)
-      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) pre[q] = src[v];
-      }
-    }
-    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
-    // software pipeline over tile pairs: MFMAs of pair p+1 are issued before the VALU epilogue of p
-    float b0[NS], b1[NS], xo0[NU], xo1[NU];
-    f32x4 acc0, acc1;
-    load_tile(buf, 0, b0, xo0);
-    load_tile(buf, 1, b1, xo1);
-    acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < NS; ++s2) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b0[s2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b1[s2], acc1, 0, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
-      f32x4 n0 = acc0, n1 = acc1;
-      float c0[NU], c1[NU];
-#pragma unroll
-      for (int u = 0; u < DUP; ++u) {
-        c0[u] = xo0[u];
-        c1[u] = xo1[u];
-      }
-      if (p + 1 < OBS_CHUNK / 32) {
-        load_tile(buf, 2 * p + 2, b0, xo0);
-        load_tile(buf, 2 * p + 3, b1, xo1);
-        acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < NS; ++s2) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b0[s2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b1[s2], acc1, 0, 0, 0);
-        }
-      }
-      epilogue(n0, c0, Sb, Snb);
-      epilogue(n1, c1, Sb, Snb);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      S[q] += Sb[q];
-      if (SIGNED) Sn[q] += Snb[q];
-    }
-    if (more) {  // publish the prefetched chunk into the other buffer
-      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) dst[v] = pre[q];
-      }
-    }
-    __syncthreads();
-  }
-  // reduce over the 16 lanes (observation columns) that share kq
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      S[q] += __shfl_xor(S[q], o);
-      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
-    }
-  }
-  // lane ia = q of group kq writes candidate 4*kq + q; c_i / bound of that candidate live in lane
-  // (4*kq + q) & 15 + 16*anything of the A layout -> fetch with a shuffle
-  const int src_lane = (4 * kq + (ia & 3)) & 15;
-  const float ci_q = __shfl(ci_a, src_lane);
-  const float bnd_q = __shfl(bnd_a, src_lane);
-  if (ia < 4) {
-    const int q = ia;
-    const int64_t ii = cbase + 4 * kq + q;
-    float Sq = S[0], Snq = Sn[0];
-    bool nq = nanc[0];
-    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
-    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
-    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
-    if (ii < Nc) {
-      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
-      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;  // rescue marker (kde_rescue_kernel)
-      out[ii] = o;
-    }
-  }
-}
-
-// One-hot mode: the categorical sum  sum_u delta_u [x_u == X_u]  is a second matrix product,
-// (candidate one-hot) x (delta-weighted observation one-hot), on the f16 matrix cores: operands are
-// 0/1 and the f16 hi+lo parts of delta_u, so every product is exact and only the fp32 accumulation
-// rounds.  It continues the same accumulator as the f32 continuous product, leaving the VALU only
-// exp2 and the running sums.  Signed KDEs add one more f16 product that counts matches in dims with
-// a negative match weight (the sign of the term is (-1)^count).
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-template <int DCP, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_oh_kernel(const double* __restrict__ cand,
-                                                                       int64_t Nc, int32_t D,
-                                                                       const KdeParams* __restrict__ P,
-                                                                       const float* __restrict__ table,
-                                                                       KdeEst* __restrict__ out) {
-  constexpr int KP = kp_of(DCP);
-  constexpr int NS = KP / 4;
-  constexpr int W = KC * 32;  // one-hot halves per observation
-  constexpr int CHF = chunk_floats(DCP, 0, KC, SIGNED ? 1 : 0);
-  __shared__ __align__(16) float lds[2 * CHF];
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16;
-  const int n = P->n, dc = P->dc;
-  const int ia = lane & 15, kq = lane >> 4;
-
-  float a[NS];
-  f16x8 ah[KC];
-  float ci_a = 0.f, bnd_a = 0.f;
-  {
-    int64_t ii = cbase + ia;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-    for (int k = 0; k < dc; ++k) {
-      const float v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
-      ci_a = fmaf(-v, v, ci_a);
-      bnd_a = fmaf(2.f * fabsf(v), P->xmax[k], bnd_a);
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int k = 4 * s + kq;
-      float v = 0.f;
-      if (k == 0) {
-        v = 1.f;
-      } else if (k == 1) {
-        v = ci_a;
-      } else if (k - 2 < dc) {
-        const int c = k - 2;
-        v = 2.f * (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
-      }
-      a[s] = v;
-    }
-    // candidate one-hot: lane holds A[row ia][k = 32 s + 8 kq + j]
-    const int tot = P->oh_total;
-#pragma unroll
-    for (int s = 0; s < KC; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = (32 * s + 8 * kq + j) >> 1;
-        float v = 0.f;
-        if (t < tot && x[P->cat_dim[P->oh_dim[t]]] == (double)P->oh_level[t]) v = 1.f;
-        ah[s][j] = (_Float16)v;
-      }
-    }
-  }
-  bool nanc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    int64_t ii = cbase + 4 * kq + q;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-    bool nn = P->nan_all != 0;
-    for (int c = 0; c < P->nconst; ++c)
-      if (x[P->const_dim[c]] != P->const_level[c]) nn = true;
-    nanc[q] = nn;
-  }
-
-  float S[4] = {0.f, 0.f, 0.f, 0.f}, Sn[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
-  constexpr int NT = 64 * MFMA_WAVES;
-  constexpr int NV4 = CHF / 4;
-  constexpr int PER = (NV4 + NT - 1) / NT;
-  float4 pre[PER];
-  {
-    const float4* __restrict__ src = (const float4*)table;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int v = threadIdx.x + q * NT;
-      if (v < NV4) ((float4*)lds)[v] = src[v];
-    }
-  }
-  __syncthreads();
-
-  // accumulate one 16x16 tile: f32 continuous product, then the f16 one-hot product
-  auto tile = [&](const float* buf, int jt, f32x4& acc, f32x4& accp) {
-    const _Float16* ohb = (const _Float16*)(buf + KP * KROW);
-    acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], buf[(4 * s + kq) * KROW + jt * 16 + ia], acc, 0, 0, 0);
-#pragma unroll
-    for (int s = 0; s < KC; ++s) {
-      const f16x8 b = *(const f16x8*)(ohb + (jt * 16 + ia) * W + 32 * s + 8 * kq);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], b, acc, 0, 0, 0);
-    }
-    if (SIGNED) {
-      accp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KC; ++s) {
-        const f16x8 b = *(const f16x8*)(ohb + OBS_CHUNK * W + (jt * 16 + ia) * W + 32 * s + 8 * kq);
-        accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[s], b, accp, 0, 0, 0);
-      }
-    }
-  };
-  auto epilogue = [&](const f32x4& acc, const f32x4& accp, float* Sb, float* Snb) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float e = __builtin_amdgcn_exp2f(acc[q]);
-      Sb[q] += e;
-      if (SIGNED) {
-        const float odd = 2.f * __builtin_amdgcn_fractf(0.5f * accp[q]);  // count mod 2
-        Snb[q] = fmaf(odd, e, Snb[q]);
-      }
-    }
-  };
-
-  for (int c = 0; c < nchunks; ++c) {
-    float* buf = lds + (c & 1) * CHF;
-    const bool more = c + 1 < nchunks;
-    if (more) {
-      const float4* __restrict__ src = (const float4*)(table + (int64_t)(c + 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) pre[q] = src[v];
-      }
-    }
-    float Sb[4] = {0.f, 0.f, 0.f, 0.f}, Snb[4] = {0.f, 0.f, 0.f, 0.f};
-    f32x4 acc0, acc1, ap0, ap1;
-    tile(buf, 0, acc0, ap0);
-    tile(buf, 1, acc1, ap1);
-#pragma unroll
-    for (int p = 0; p < OBS_CHUNK / 32; ++p) {
-      const f32x4 n0 = acc0, n1 = acc1, m0 = ap0, m1 = ap1;
-      if (p + 1 < OBS_CHUNK / 32) {
-        tile(buf, 2 * p + 2, acc0, ap0);
-        tile(buf, 2 * p + 3, acc1, ap1);
-      }
-      epilogue(n0, m0, Sb, Snb);
-      epilogue(n1, m1, Sb, Snb);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      S[q] += Sb[q];
-      if (SIGNED) Sn[q] += Snb[q];
-    }
-    if (more) {
-      float4* dst = (float4*)(lds + ((c + 1) & 1) * CHF);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int v = threadIdx.x + q * NT;
-        if (v < NV4) dst[v] = pre[q];
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      S[q] += __shfl_xor(S[q], o);
-      if (SIGNED) Sn[q] += __shfl_xor(Sn[q], o);
-    }
-  }
-  const int src_lane = (4 * kq + (ia & 3)) & 15;
-  const float ci_q = __shfl(ci_a, src_lane);
-  const float bnd_q = __shfl(bnd_a, src_lane);
-  if (ia < 4) {
-    const int q = ia;
-    const int64_t ii = cbase + 4 * kq + q;
-    float Sq = S[0], Snq = Sn[0];
-    bool nq = nanc[0];
-    if (q == 1) { Sq = S[1]; Snq = Sn[1]; nq = nanc[1]; }
-    if (q == 2) { Sq = S[2]; Snq = Sn[2]; nq = nanc[2]; }
-    if (q == 3) { Sq = S[3]; Snq = Sn[3]; nq = nanc[3]; }
-    if (ii < Nc) {
-      KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
-      if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
-      out[ii] = o;
-    }
-  }
-}
-
-// hmode: the whole exponent is one f16 matrix product.  Continuous coordinates are split into f16
-// hi + lo parts and all four cross products are summed (every f16 x f16 product is exact in fp32, so
-// the only extra error is the 2^-22 representation error of each coordinate -- accounted in the
-// bound); the one-hot categorical product follows in the same K loop.  C_j + c_i seed the
-// accumulator.  VALU work per pair: one add, exp2, one add.
-template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const double* __restrict__ cand,
-                                                                      int64_t Nc, int32_t D,
-                                                                      const KdeParams* __restrict__ P,
-                                                                      const float* __restrict__ table,
-                                                                      KdeEst* __restrict__ out) {
-  constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
-  constexpr int NSH = NSC + KC;             // f16 K-steps of 32
-  constexpr int KTP = h_ktp(NSC * 8, KC);   // halves per observation row (padded); nsc_of(8 NSC) = NSC
-  constexpr int KPP = h_kpp(KC);
-  constexpr int CHF = h_chunk_floats(NSC * 8, KC, SIGNED ? 1 : 0);
-  // LDS ring: 3 buffers (chunk c+2 in flight while c is used) when they fit in the 160 KB, else 2
-  constexpr int NBUF = (3 * CHF * 4 <= 160 * 1024) ? 3 : 2;
-  static_assert(NBUF * CHF * 4 <= 160 * 1024, "observation chunk too large for LDS");
-  constexpr int G = CHF * 4 / (1024 * MFMA_WAVES);         // 1-KB LDS-DMA pieces per wave per chunk
-  static_assert(G * 1024 * MFMA_WAVES == CHF * 4, "chunk must be a multiple of 8 KB");
-  __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16 * RT;
-  const int n = P->n, dc = P->dc;
-  const int ia = lane & 15, kq = lane >> 4;
-
-  // A operands (candidate side).  Every lane walks all dims with wave-uniform (scalar) parameter
-  // indices -- independent loads of its candidate's row, no lane-varying parameter lookups -- and
-  // keeps the f16 slots its lane group kq owns: continuous dim c -> step c/8, lanes kq = (c%8)/2,
-  // halves 4(c%2)+{0,1} = hi, +{2,3} = lo; one-hot slot t -> step NSC + t/16, kq = (t%16)/4,
-  // halves 2(t%4)+{0,1}.
-  f16x8 ah[RT][NSH];
-  float ci_a[RT], bnd_a[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    int64_t ii = cbase + 16 * r + ia;
-    if (ii >= Nc) ii = Nc - 1;
-    const double* x = cand + ii * (int64_t)D;
-    float ci = 0.f, bnd = 0.f;
-#pragma unroll
-    for (int s = 0; s < NSH; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ah[r][s][j] = (_Float16)0.f;
-#pragma unroll
-    for (int c = 0; c < 8 * NSC; ++c) {
-      if (c < dc) {
-        const float v = (float)(P->cont_scale[c] * (x[P->cont_dim[c]] - P->center[c]));
-        ci = fmaf(-v, v, ci);
-        bnd = fmaf(2.f * fabsf(v), P->xmax[c], bnd);
-        const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
-        const _Float16 hi = (_Float16)xc;
-        const _Float16 lo = (_Float16)(xc - (float)hi);
-        const bool mine = kq == ((c & 7) >> 1);
-        const int j0 = 4 * (c & 1);
-        ah[r][c >> 3][j0 + 0] = mine ? hi : ah[r][c >> 3][j0 + 0];
-        ah[r][c >> 3][j0 + 1] = mine ? hi : ah[r][c >> 3][j0 + 1];
-        ah[r][c >> 3][j0 + 2] = mine ? lo : ah[r][c >> 3][j0 + 2];
-        ah[r][c >> 3][j0 + 3] = mine ? lo : ah[r][c >> 3][j0 + 3];
-      }
-    }
-    ci_a[r] = ci;
-    bnd_a[r] = bnd;
-    const int tot = P->oh_total;
-#pragma unroll
-    for (int t = 0; t < 16 * KC; ++t) {
-      if (t < tot) {
-        const bool hit = (kq == ((t & 15) >> 2)) && x[P->oh_col[t]] == P->oh_val[t];
-        const int s = NSC + (t >> 4), j0 = 2 * (t & 3);
-        ah[r][s][j0 + 0] = hit ? (_Float16)1.f : ah[r][s][j0 + 0];
-        ah[r][s][j0 + 1] = hit ? (_Float16)1.f : ah[r][s][j0 + 1];
-      }
-    }
-  }
-  // accumulator rows of this lane: candidates cbase + 16 r + 4 kq + q
-  float ciq[RT][4];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ciq[r][q] = __shfl(ci_a[r], 4 * kq + q);
-
-  float S[RT][4], Sn[RT][4];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) S[r][q] = Sn[r][q] = 0.f;
-  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
-  // LDS-DMA (global_load_lds_dwordx4): each wave copies its G 1-KB pieces of a chunk straight into
-  // the ring; completion is tracked by a counted vmcnt + one raw barrier per chunk
-  auto issue = [&](int c) {
-    const float* src = table + (int64_t)c * CHF;
-    float* dst = lds + (c % NBUF) * CHF;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int piece = wave + g * MFMA_WAVES;
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
-    }
-  };
-  issue(0);
-  if (NBUF == 3 && nchunks > 1) {
-    issue(1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  // MFMAs of one 16-observation column tile for every row tile
-  auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
-    const int jo = jt * 16 + ia;
-    const float Cj = buf[jo];
-    const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
-    f16x8 b[NSH];
-#pragma unroll
-    for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r] = f32x4{ciq[r][0] + Cj, ciq[r][1] + Cj, ciq[r][2] + Cj, ciq[r][3] + Cj};
-#pragma unroll
-    for (int s = 0; s < NSH; ++s)
-#pragma unroll
-      for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
-    if (SIGNED) {
-      const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
-#pragma unroll
-      for (int r = 0; r < RT; ++r) accp[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KC; ++s) {
-        const f16x8 bp = *(const f16x8*)(pb + 32 * s);
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp, accp[r], 0, 0, 0);
-      }
-    }
-  };
-
-  for (int c = 0; c < nchunks; ++c) {
-    const float* buf = lds + (c % NBUF) * CHF;
-    if (c + NBUF - 1 < nchunks) issue(c + NBUF - 1);  // its buffer was last read in iteration c-1
-    float Sb[RT][4], Snb[RT][4];
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
-    // software pipeline: MFMAs of tile jt+1 are issued before the exp2/sum epilogue of tile jt
-    f32x4 acc[RT], accp[RT];
-    tile(buf, 0, acc, accp);
-#pragma unroll
-    for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
-      f32x4 cur[RT], curp[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        cur[r] = acc[r];
-        curp[r] = accp[r];
-      }
-      if (jt + 1 < OBS_CHUNK / 16) tile(buf, jt + 1, acc, accp);
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
-          Sb[r][q] += e;
-          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, Snb[r][q]);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        S[r][q] += Sb[r][q];
-        if (SIGNED) Sn[r][q] += Snb[r][q];
-      }
-    // chunk c+1 complete for this wave (chunk c+2 may stay in flight), this wave's reads of buffer c
-    // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
-    if (NBUF == 3 && c + 2 < nchunks)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        S[r][q] += __shfl_xor(S[r][q], o);
-        if (SIGNED) Sn[r][q] += __shfl_xor(Sn[r][q], o);
-      }
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    const int src_lane = (4 * kq + (ia & 3)) & 15;
-    const float ci_q = __shfl(ci_a[r], src_lane);
-    const float bnd_q = __shfl(bnd_a[r], src_lane);
-    if (ia < 4) {
-      const int q = ia;
-      const int64_t ii = cbase + 16 * r + 4 * kq + q;
-      float Sq = S[r][0], Snq = Sn[r][0];
-      if (q == 1) { Sq = S[r][1]; Snq = Sn[r][1]; }
-      if (q == 2) { Sq = S[r][2]; Snq = Sn[r][2]; }
-      if (q == 3) { Sq = S[r][3]; Snq = Sn[r][3]; }
-      if (ii < Nc) {
-        const double* x = cand + ii * (int64_t)D;
-        bool nq = P->nan_all != 0;
-        for (int cc = 0; cc < P->nconst; ++cc)
-          if (x[P->const_dim[cc]] != P->const_level[cc]) nq = true;
-        KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
-        // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
-        if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
-        if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
-        out[ii] = o;
-      }
-    }
-  }
 }
 
 // Rescue (rare): candidates whose every term sits far below the static bound M0 are recomputed
@@ -1344,73 +649,41 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
 // ------------------------------------------------------------------------------------------
 // launch-side dispatch over the (dc_pad, du_pad, signed) template buckets
 
-typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 struct ScoreFns {
   logpdf_fn main, rescue;
   int cands_per_block;
 };
 
-// variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
-// bit 4 = hmode (whole exponent on the f16 matrix cores)
-template <int NSC, bool SG>
-static logpdf_fn pick_h(int kc) {
-  switch (kc) {
-    case 0: return kde_logpdf_h_kernel<NSC, 0, SG>;
-    case 1: return kde_logpdf_h_kernel<NSC, 1, SG>;
-    case 2: return kde_logpdf_h_kernel<NSC, 2, SG>;
-    case 3: return kde_logpdf_h_kernel<NSC, 3, SG>;
-    case 4: return kde_logpdf_h_kernel<NSC, 4, SG>;
+template <bool SG>
+static logpdf_fn pick_rescue(int dc_pad) {
+  switch (dc_pad) {
+    case 0: return kde_rescue_kernel<0, SG>;
+    case 4: return kde_rescue_kernel<4, SG>;
+    case 8: return kde_rescue_kernel<8, SG>;
+    case 16: return kde_rescue_kernel<16, SG>;
+    case 24: return kde_rescue_kernel<24, SG>;
+    case 32: return kde_rescue_kernel<32, SG>;
+    case 64: return kde_rescue_kernel<64, SG>;
   }
   return nullptr;
 }
 
-template <int DCP, int DUP, bool SG>
-static ScoreFns pick_kc(int kc, bool hm) {
-  const logpdf_fn r = kde_rescue_kernel<DCP, SG>;
-  if (hm) {
-    if constexpr (DCP >= 16) return {pick_h<nsc_of(DCP), SG>(kc), r, 16 * MFMA_WAVES * H_ROW_TILES};
-    return {nullptr, nullptr, 0};
-  }
-  switch (kc) {
-    case 0: return {kde_logpdf_kernel<DCP, DUP, SG>, r, 16 * MFMA_WAVES};
-    case 1: return {kde_logpdf_oh_kernel<DCP, 1, SG>, r, 16 * MFMA_WAVES};
-    case 2: return {kde_logpdf_oh_kernel<DCP, 2, SG>, r, 16 * MFMA_WAVES};
-    case 3: return {kde_logpdf_oh_kernel<DCP, 3, SG>, r, 16 * MFMA_WAVES};
-    case 4: return {kde_logpdf_oh_kernel<DCP, 4, SG>, r, 16 * MFMA_WAVES};
-  }
-  return {nullptr, nullptr, 0};
-}
-
-template <int DCP, int DUP>
-static ScoreFns pick_signed(int variant) {
-  const int kc = (variant >> 1) & 7;
-  const bool hm = (variant >> 4) & 1;
-  return (variant & 1) ? pick_kc<DCP, DUP, true>(kc, hm) : pick_kc<DCP, DUP, false>(kc, hm);
-}
-
-template <int DCP>
-static ScoreFns pick_du(int du_pad, int variant) {
-  switch (du_pad) {
-    case 0: return pick_signed<DCP, 0>(variant & 0x11);  // no categorical dims: kc irrelevant
-    case 4: return pick_signed<DCP, 4>(variant);
-    case 8: return pick_signed<DCP, 8>(variant);
-    case 16: return pick_signed<DCP, 16>(variant);
-    case 32: return pick_signed<DCP, 32>(variant);
-  }
-  return {nullptr, nullptr};
-}
-
+// variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
+// bit 4 = hmode (whole exponent on the f16 matrix cores)
 static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
-  switch (dc_pad) {
-    case 0: return pick_du<0>(du_pad, variant);
-    case 4: return pick_du<4>(du_pad, variant);
-    case 8: return pick_du<8>(du_pad, variant);
-    case 16: return pick_du<16>(du_pad, variant);
-    case 24: return pick_du<24>(du_pad, variant);
-    case 32: return pick_du<32>(du_pad, variant);
-    case 64: return pick_du<64>(du_pad, variant);
+  const bool sg = variant & 1;
+  const int kc = du_pad == 0 ? 0 : (variant >> 1) & 7;  // no categorical dims: kc irrelevant
+  const bool hm = (variant >> 4) & 1;
+  int dcp, dup;
+  bucket_dims(dc_pad, du_pad, &dcp, &dup);
+  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0};  // not a bucket
+  const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
+  if (hm) {
+    if (dc_pad < 16) return {nullptr, nullptr, 0};
+    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * MFMA_WAVES * H_ROW_TILES};
   }
-  return {nullptr, nullptr, 0};
+  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES};
+  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES};
 }
 
 // launch main + rescue scoring for one KDE
@@ -1576,6 +849,10 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   }
   P->kc = 0;
   P->oh_total = 0;
+  for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
+    P->oh_col[t] = 0;
+    P->oh_val[t] = NAN;
+  }
   if (P->du > 0) {
     int tot = 0;
     bool ok = true;

@@ -1,0 +1,108 @@
+// hbx_kde_impl.h -- definitions shared by the KDE scoring translation units (device code +
+// chunk-layout helpers).  Split across files only so the template buckets compile in parallel.
+#pragma once
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "hbx_common.h"
+
+#define HBX_LN2f 0.69314718055994531f
+#define HBX_LN_CLAMP (-18.420680743952367)   // ln(1e-8), bohb.py:129
+#define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
+#define EXACT_GRID 2048  // blocks of the exact re-score (grid-stride over its work items)
+#define SUM_BLOCK 32
+#define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
+#define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
+#define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
+#define H_ROW_TILES 2  // hmode: 16-candidate row tiles per wave (32 candidates)
+
+// Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
+//   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0
+//   [64][du_pad]        categorical codes (float), observation-major
+// KP = dc_pad + 2 rounded up to a multiple of 4 (MFMA 16x16x4 K step).  Observations past n in the
+// last chunk are padding with C_j = -1e30 (their terms are exactly 0).
+//
+// Categorical part when kc >= 1 (one-hot mode): 64 observations x kc*32 f16, observation-major,
+// slot k = 2*t + p of one-hot position t = (dim u, level) holds delta_u's f16 hi (p=0) / lo (p=1)
+// part when the observation has that level, else 0; for signed KDEs a second block of the same
+// shape holds 1 in the hi slot of matches in dims with negative match weight (parity count).
+#define OH_MAX_KC 4  // one-hot mode up to 4 f16 MFMA K-steps: sum over dims of levels <= 64
+__host__ __device__ constexpr int kp_of(int dc_pad) { return (dc_pad + 2 + 3) & ~3; }
+__host__ __device__ constexpr int cat_floats(int du_pad, int kc, int sgn) {
+  return kc == 0 ? OBS_CHUNK * du_pad : OBS_CHUNK * kc * 16 * (sgn ? 2 : 1);
+}
+__host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 0, int sgn = 0) {
+  return kp_of(dc_pad) * KROW + cat_floats(du_pad, kc, sgn);
+}
+// hmode (all-f16) chunk: [64 f32: C_j] [64 obs x KTP halves: hi/lo continuous + one-hot] [signed:
+// 64 obs x KPP halves parity]; continuous slot k = 4c + pt of dim c holds (pt even ? Xh_c : Xl_c) so
+// the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl).
+// Rows are padded by 16 halves (32 B) so the 16 observation rows a wave reads are spread over banks.
+__host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) / 32; }
+// row strides are 8*odd dwords: the 16 rows a ds_read_b128 lane group touches then cover all 64
+// banks exactly once (conflict-free)
+__host__ __device__ constexpr int h_ktp(int dc_pad, int kc) { return 32 * (nsc_of(dc_pad) + kc) + 16; }
+__host__ __device__ constexpr int h_kpp(int kc) { return 32 * kc + 16; }
+// padded to a multiple of 8 KB: every wave of the scoring block moves the same number of 1-KB
+// LDS-DMA pieces per chunk (the counted vmcnt of the pipeline depends on it)
+__host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
+  return (OBS_CHUNK + OBS_CHUNK * h_ktp(dc_pad, kc) / 2 + (sgn ? OBS_CHUNK * h_kpp(kc) / 2 : 0) + 2047) & ~2047;
+}
+// ------------------------------------------------------------------------------------------
+// fp32 log-domain scoring
+//
+// Per (candidate i, observation j), in log2 units and minus the static bound M0:
+//   t_ij = C_j + c_i + sum_c x''_ic X'_jc + sum_u delta_u [x_iu == X_ju]
+// with X' = s (X - mu), x'' = 2 s (x - mu), c_i = -|x'_i|^2, C_j = -|X'_j|^2 + lb_sum - M0
+// (the expansion of -|x' - X'|^2).  The first three terms are one GEMM-shaped product
+// [candidates x K] . [K x observations] with K = 2 + Dc: they run on the f32 matrix cores
+// (v_mfma_f32_16x16x4_f32, an exact fp32 FMA chain in k order).  The categorical match,
+// exp2 and the sums run on the VALU beside them.  The categorical match is m = clamp(1 - d*d) on
+// the integer codes (d = x - X), which stays in the VALU (no VCC round trip).
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float cat_match(float a, float b) {
+  const float d = a - b;
+  return __builtin_amdgcn_fmed3f(fmaf(-d, d, 1.f), 0.f, 1.f);
+}
+
+__device__ __forceinline__ float cand_code(double xv) {
+  // codes are integers; anything else (incl. NaN) never equals an observed code
+  return (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
+}
+
+// Per-candidate epilogue: ln S+, ln S-, error bound (or the rescue marker err = -1)
+__device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, float S, float Sn, float off,
+                                             bool nan_c, float ci, float bnd, bool SIGNED, int chunk) {
+  KdeEst o;
+  o.pad = 0.f;
+  if (nan_c || S != S) {
+    o.lpos = NAN;
+    o.lneg = -INFINITY;
+    o.err = 0.f;
+    return o;
+  }
+  const float lnorm = (float)P->log_norm;
+  const float Sp = SIGNED ? (S - Sn) : S;
+  o.lpos = (Sp > 0.f) ? (__log2f(Sp) + off) * HBX_LN2f + lnorm : -INFINITY;
+  o.lneg = (SIGNED && Sn > 0.f) ? (__log2f(Sn) + off) * HBX_LN2f + lnorm : -INFINITY;
+  const float u = 0x1p-24f;
+  const float Mabs = fabsf(ci) + P->cmax + bnd + P->sum_abs_delta;
+  const float dt = 3.f * (float)(P->dc + P->du + 4) * u * Mabs;  // |error of t|, log2 units
+  const float es = ((float)chunk + (float)P->n / (float)chunk + 24.f) * u * (SIGNED ? 3.f : 1.f);
+  o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
+  return o;
+}
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
+
+// host-side pickers of the scoring kernel instances (nullptr when the bucket has none)
+logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
+logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
+logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip

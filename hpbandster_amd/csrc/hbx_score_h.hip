@@ -1,0 +1,281 @@
+// hbx_score_h.hip -- scoring kernel, whole exponent on the f16 matrix cores (hmode).
+#include "hbx_common.h"
+#include "hbx_kde_impl.h"
+
+// hmode: the whole exponent is one f16 matrix product.  Continuous coordinates are split into f16
+// hi + lo parts and all four cross products are summed (every f16 x f16 product is exact in fp32, so
+// the only extra error is the 2^-22 representation error of each coordinate -- accounted in the
+// bound); the one-hot categorical product follows in the same K loop.  C_j + c_i seed the
+// accumulator.  VALU work per pair: one add, exp2, one add.
+template <int NSC, int KC, bool SIGNED>
+__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const double* __restrict__ cand,
+                                                                      int64_t Nc, int32_t D,
+                                                                      const KdeParams* __restrict__ P,
+                                                                      const float* __restrict__ table,
+                                                                      KdeEst* __restrict__ out) {
+  constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
+  constexpr int NSH = NSC + KC;             // f16 K-steps of 32
+  constexpr int KTP = h_ktp(NSC * 8, KC);   // halves per observation row (padded); nsc_of(8 NSC) = NSC
+  constexpr int KPP = h_kpp(KC);
+  constexpr int CHF = h_chunk_floats(NSC * 8, KC, SIGNED ? 1 : 0);
+  // LDS ring: 3 buffers (chunk c+2 in flight while c is used) when they fit in the 160 KB, else 2
+  constexpr int NBUF = (3 * CHF * 4 <= 160 * 1024) ? 3 : 2;
+  static_assert(NBUF * CHF * 4 <= 160 * 1024, "observation chunk too large for LDS");
+  constexpr int G = CHF * 4 / (1024 * MFMA_WAVES);         // 1-KB LDS-DMA pieces per wave per chunk
+  static_assert(G * 1024 * MFMA_WAVES == CHF * 4, "chunk must be a multiple of 8 KB");
+  __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16 * RT;
+  const int n = P->n, dc = P->dc;
+  const int ia = lane & 15, kq = lane >> 4;
+
+  // A operands (candidate side).  Lane group kq owns, per K-step s, continuous dims
+  // c = 8s + 2kq + {0,1} (halves 4e+{0,1} = hi, 4e+{2,3} = lo of x''_c) and one-hot slots
+  // t = 16(s-NSC) + 4kq + q (halves 2q+{0,1}).  The per-dim parameters and the wave's candidate
+  // rows (contiguous in HBM: one coalesced copy) are staged in LDS first, so every lane touches only
+  // its own dims.  c_i = -|x'_i|^2 and the bound term are summed over the four lane groups with a
+  // butterfly (bitwise identical in all four).  Rows fall back to global reads when the rows of all
+  // waves do not fit in the (not yet used) LDS ring (large D).
+  struct ContPrm { double scale, center; float xmax; int32_t col; };
+  struct OhPrm { double val; int32_t col, pad; };
+  __shared__ ContPrm cprm[8 * NSC];
+  __shared__ OhPrm oprm[16 * (KC > 0 ? KC : 1)];
+  const int tid = threadIdx.x;
+  if (tid < 8 * NSC) {
+    const bool act = tid < dc;  // padding: never read unmasked
+    cprm[tid] = ContPrm{act ? P->cont_scale[tid] : 0.0, act ? P->center[tid] : 0.0, act ? P->xmax[tid] : 0.f,
+                        act ? P->cont_dim[tid] : 0};
+  }
+  if (tid < 16 * KC) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
+  const bool staged = (int64_t)MFMA_WAVES * 16 * RT * D * 8 <= (int64_t)NBUF * CHF * 4 && cbase < Nc;
+  const int64_t nv = (Nc - cbase) < 16 * RT ? (Nc - cbase) : 16 * RT;  // valid rows of this wave
+  double* xs = (double*)lds + (int64_t)wave * 16 * RT * D;
+  if (staged) {
+    const int tot = (int)(nv * D);
+    const double* src = cand + cbase * (int64_t)D;
+    for (int e = lane; e < tot; e += 64) xs[e] = src[e];
+  }
+  __syncthreads();
+  f16x8 ah[RT][NSH];
+  float ci_a[RT], bnd_a[RT];
+  // row tile r of the A operands from candidate row x (LDS or global; inlined once for each)
+  auto build = [&](int r, const double* x) {
+    float ci = 0.f, bnd = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSC; ++s) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int c = 8 * s + 2 * kq + e;
+        const ContPrm q = cprm[c];
+        const float v0 = (float)(q.scale * (x[q.col] - q.center));
+        const float v = c < dc ? v0 : 0.f;
+        ci = fmaf(-v, v, ci);
+        bnd = fmaf(2.f * fabsf(v), q.xmax, bnd);
+        const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
+        const _Float16 hi = (_Float16)xc;
+        const _Float16 lo = (_Float16)(xc - (float)hi);
+        ah[r][s][4 * e + 0] = hi;
+        ah[r][s][4 * e + 1] = hi;
+        ah[r][s][4 * e + 2] = lo;
+        ah[r][s][4 * e + 3] = lo;
+      }
+    }
+    ci += __shfl_xor(ci, 16);
+    ci += __shfl_xor(ci, 32);
+    bnd += __shfl_xor(bnd, 16);
+    bnd += __shfl_xor(bnd, 32);
+    ci_a[r] = ci;
+    bnd_a[r] = bnd;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const OhPrm o = oprm[16 * s + 4 * kq + q];
+        const _Float16 h = (x[o.col] == o.val) ? (_Float16)1.f : (_Float16)0.f;
+        ah[r][NSC + s][2 * q + 0] = h;
+        ah[r][NSC + s][2 * q + 1] = h;
+      }
+    }
+  };
+  if (staged) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int loc = (16 * r + ia) < nv ? (16 * r + ia) : (int)nv - 1;
+      build(r, xs + loc * D);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      int64_t ii = cbase + 16 * r + ia;
+      if (ii >= Nc) ii = Nc - 1;
+      build(r, cand + ii * (int64_t)D);
+    }
+  }
+  // accumulator rows of this lane: candidates cbase + 16 r + 4 kq + q
+  float ciq[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ciq[r][q] = __shfl(ci_a[r], 4 * kq + q);
+
+  float S[RT][4], Sn[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[r][q] = Sn[r][q] = 0.f;
+  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
+  // LDS-DMA (global_load_lds_dwordx4): each wave copies its G 1-KB pieces of a chunk straight into
+  // the ring; completion is tracked by a counted vmcnt + one raw barrier per chunk
+  auto issue = [&](int c) {
+    const float* src = table + (int64_t)c * CHF;
+    float* dst = lds + (c % NBUF) * CHF;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int piece = wave + g * MFMA_WAVES;
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
+    }
+  };
+  __syncthreads();  // every wave has read its staged rows: the ring may be overwritten
+  issue(0);
+  if (NBUF == 3 && nchunks > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  // MFMAs of one 16-observation column tile for every row tile
+  auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
+    const int jo = jt * 16 + ia;
+    const float Cj = buf[jo];
+    const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
+    f16x8 b[NSH];
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r] = f32x4{ciq[r][0] + Cj, ciq[r][1] + Cj, ciq[r][2] + Cj, ciq[r][3] + Cj};
+#pragma unroll
+    for (int s = 0; s < NSH; ++s)
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
+    if (SIGNED) {
+      const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) accp[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+        const f16x8 bp = *(const f16x8*)(pb + 32 * s);
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp, accp[r], 0, 0, 0);
+      }
+    }
+  };
+
+  for (int c = 0; c < nchunks; ++c) {
+    const float* buf = lds + (c % NBUF) * CHF;
+    if (c + NBUF - 1 < nchunks) issue(c + NBUF - 1);  // its buffer was last read in iteration c-1
+    float Sb[RT][4], Snb[RT][4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
+    // software pipeline: MFMAs of tile jt+1 are issued before the exp2/sum epilogue of tile jt
+    f32x4 acc[RT], accp[RT];
+    tile(buf, 0, acc, accp);
+#pragma unroll
+    for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
+      f32x4 cur[RT], curp[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        cur[r] = acc[r];
+        curp[r] = accp[r];
+      }
+      if (jt + 1 < OBS_CHUNK / 16) tile(buf, jt + 1, acc, accp);
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
+          Sb[r][q] += e;
+          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, Snb[r][q]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        S[r][q] += Sb[r][q];
+        if (SIGNED) Sn[r][q] += Snb[r][q];
+      }
+    // chunk c+1 complete for this wave (chunk c+2 may stay in flight), this wave's reads of buffer c
+    // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
+    if (NBUF == 3 && c + 2 < nchunks)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        S[r][q] += __shfl_xor(S[r][q], o);
+        if (SIGNED) Sn[r][q] += __shfl_xor(Sn[r][q], o);
+      }
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int src_lane = (4 * kq + (ia & 3)) & 15;
+    const float ci_q = __shfl(ci_a[r], src_lane);
+    const float bnd_q = __shfl(bnd_a[r], src_lane);
+    if (ia < 4) {
+      const int q = ia;
+      const int64_t ii = cbase + 16 * r + 4 * kq + q;
+      float Sq = S[r][0], Snq = Sn[r][0];
+      if (q == 1) { Sq = S[r][1]; Snq = Sn[r][1]; }
+      if (q == 2) { Sq = S[r][2]; Snq = Sn[r][2]; }
+      if (q == 3) { Sq = S[r][3]; Snq = Sn[r][3]; }
+      if (ii < Nc) {
+        const double* x = cand + ii * (int64_t)D;
+        bool nq = P->nan_all != 0;
+        for (int cc = 0; cc < P->nconst; ++cc)
+          if (x[P->const_dim[cc]] != P->const_level[cc]) nq = true;
+        KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+        // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
+        if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
+        if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
+        out[ii] = o;
+      }
+    }
+  }
+}
+
+template <int NSC, bool SG>
+static logpdf_fn pick_kc(int kc) {
+  switch (kc) {
+    case 0: return kde_logpdf_h_kernel<NSC, 0, SG>;
+    case 1: return kde_logpdf_h_kernel<NSC, 1, SG>;
+    case 2: return kde_logpdf_h_kernel<NSC, 2, SG>;
+    case 3: return kde_logpdf_h_kernel<NSC, 3, SG>;
+    case 4: return kde_logpdf_h_kernel<NSC, 4, SG>;
+  }
+  return nullptr;
+}
+
+template <bool SG>
+static logpdf_fn pick_nsc(int nsc, int kc) {
+  switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {16, 24, 32, 64}
+    case 2: return pick_kc<2, SG>(kc);
+    case 3: return pick_kc<3, SG>(kc);
+    case 4: return pick_kc<4, SG>(kc);
+    case 8: return pick_kc<8, SG>(kc);
+  }
+  return nullptr;
+}
+
+logpdf_fn hbx_pick_h(int nsc, int kc, bool sg) { return sg ? pick_nsc<true>(nsc, kc) : pick_nsc<false>(nsc, kc); }
