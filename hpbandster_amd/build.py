@@ -40,6 +40,12 @@ def _flags():
             "-ffp-contract=off"]
 
 
+# per-file extra flags: the scoring loops interleave MFMAs with scalar f32 adds; SLP packing them into
+# v_pk_add_f32 costs more issue cycles beside MFMAs than the plain adds (MI355X_MICROARCH.md)
+EXTRA_FLAGS = {"hbx_score_h.hip": ["-fno-slp-vectorize"], "hbx_score_oh.hip": ["-fno-slp-vectorize"],
+               "hbx_score_f32.hip": ["-fno-slp-vectorize"]}
+
+
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
@@ -53,7 +59,7 @@ def _compile(src, force):
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
         return obj, False
-    cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj]
+    cmd = [hipcc()] + _flags() + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s" % (src, r.stdout))

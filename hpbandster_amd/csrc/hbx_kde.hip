@@ -174,6 +174,16 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   if (slot) {
     if (hm) {
       ch[jj] = Cf;
+      // C_j as three f16 pieces in the lo.lo slots 4c+3 of dims c = 0, 1, 2 (A side = 1 there);
+      // padding rows get -60000, so their terms underflow to 0 (c_i <= 0, the rest of the row is 0)
+      const float cv = ok ? fmaxf(Cf, -H_CMAX) : -H_CMAX;
+      const _Float16 c0 = (_Float16)cv;
+      const float r1 = cv - (float)c0;
+      const _Float16 c1 = (_Float16)r1;
+      const _Float16 c2 = (_Float16)(r1 - (float)c1);
+      hrow[3] = c0;
+      hrow[7] = c1;
+      hrow[11] = c2;
     } else {
       ch[0 * KROW + jj] = Cf;
       ch[1 * KROW + jj] = 1.f;
@@ -895,6 +905,9 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   const int dc_n = P->dc;
+  const bool hmode = P->hmode != 0;
+  static thread_local KdeParams Ph;  // host copy for a possible f32-MFMA rebuild (below)
+  Ph = *P;
   free(P);
   if (e != hipSuccess) return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
   if (dc_n > 0) {
@@ -905,6 +918,26 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
   hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
                      (KdeParams*)params, table);
   HBX_LAUNCH_CHECK();
+  if (hmode) {
+    // the f16 C_j pieces need |C_j| <= H_CMAX; otherwise rebuild for the f32-MFMA kernels
+    float cm = 0.f;
+    HBX_HIP(hipMemcpyAsync(&cm, &((KdeParams*)params)->cmax, sizeof(float), hipMemcpyDeviceToHost, s));
+    HBX_HIP(hipStreamSynchronize(s));
+    if (!(cm <= H_CMAX)) {
+      Ph.hmode = 0;
+      Ph.chunk_floats = chunk_floats(dcp, dup, Ph.kc, Ph.kc ? Ph.has_neg : 0);
+      info[0] = Ph.has_neg | (Ph.kc << 1);
+      HBX_HIP(hipMemcpyAsync(params, &Ph, sizeof(KdeParams), hipMemcpyHostToDevice, s));
+      if (dc_n > 0) {
+        hipLaunchKernelGGL(kde_center_kernel, dim3(dc_n), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
+        HBX_LAUNCH_CHECK();
+      }
+      hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
+                         (KdeParams*)params, table);
+      HBX_LAUNCH_CHECK();
+      HBX_HIP(hipStreamSynchronize(s));
+    }
+  }
   return HBX_OK;
 }
 

@@ -39,8 +39,13 @@ __host__ __device__ constexpr int chunk_floats(int dc_pad, int du_pad, int kc = 
 }
 // hmode (all-f16) chunk: [64 f32: C_j] [64 obs x KTP halves: hi/lo continuous + one-hot] [signed:
 // 64 obs x KPP halves parity]; continuous slot k = 4c + pt of dim c holds (pt even ? Xh_c : Xl_c) so
-// the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl).
-// Rows are padded by 16 halves (32 B) so the 16 observation rows a wave reads are spread over banks.
+// the four products xh.Xh + xh.Xl + xl.Xh + xl.Xl reassemble x''.X' (A side: pt < 2 ? xh : xl) --
+// except for dims c = 0, 1, 2, whose lo.lo slot 4c+3 carries one of the three exact f16 pieces of
+// C_j against A = 1 (the dropped lo.lo products, <= 2^-22 |x''_c||X'_c| each, are in the bound), so
+// C_j enters the product on the matrix cores; c_i enters as the accumulator input.  Needs
+// |C_j| <= H_CMAX (f16 range) and dc >= 3: hbx_kde_prepare falls back to the f32-MFMA kernels
+// otherwise.  Rows are padded by 16 halves (32 B) so the 16 rows a wave reads spread over banks.
+#define H_CMAX 60000.f  // |C_j| limit of the three-piece f16 split
 __host__ __device__ constexpr int nsc_of(int dc_pad) { return (4 * dc_pad + 31) / 32; }
 // row strides are 8*odd dwords: the 16 rows a ds_read_b128 lane group touches then cover all 64
 // banks exactly once (conflict-free)

@@ -3,10 +3,11 @@
 #include "hbx_kde_impl.h"
 
 // hmode: the whole exponent is one f16 matrix product.  Continuous coordinates are split into f16
-// hi + lo parts and all four cross products are summed (every f16 x f16 product is exact in fp32, so
-// the only extra error is the 2^-22 representation error of each coordinate -- accounted in the
-// bound); the one-hot categorical product follows in the same K loop.  C_j + c_i seed the
-// accumulator.  VALU work per pair: one add, exp2, one add.
+// hi + lo parts and the cross products are summed (every f16 x f16 product is exact in fp32; the
+// representation error of each coordinate, 2^-22 relative, and the three lo.lo products given up to
+// the C_j pieces are in the bound); C_j rides along as three exact f16 pieces against A = 1 and the
+// one-hot categorical product follows in the same K loop.  c_i is the accumulator input of the first
+// MFMA.  VALU work per pair: exp2 and one add.
 template <int NSC, int KC, bool SIGNED>
 __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const double* __restrict__ cand,
                                                                       int64_t Nc, int32_t D,
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         ah[r][s][4 * e + 0] = hi;
         ah[r][s][4 * e + 1] = hi;
         ah[r][s][4 * e + 2] = lo;
-        ah[r][s][4 * e + 3] = lo;
+        ah[r][s][4 * e + 3] = c < 3 ? (_Float16)1.f : lo;  // dims 0-2: against a C_j piece
       }
     }
     ci += __shfl_xor(ci, 16);
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
     }
   }
   // accumulator rows of this lane: candidates cbase + 16 r + 4 kq + q
-  float ciq[RT][4];
+  f32x4 ciq[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -150,15 +151,14 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   // MFMAs of one 16-observation column tile for every row tile
   auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
     const int jo = jt * 16 + ia;
-    const float Cj = buf[jo];
     const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
     f16x8 b[NSH];
 #pragma unroll
     for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r] = f32x4{ciq[r][0] + Cj, ciq[r][1] + Cj, ciq[r][2] + Cj, ciq[r][3] + Cj};
+    for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][0], b[0], ciq[r], 0, 0, 0);
 #pragma unroll
-    for (int s = 0; s < NSH; ++s)
+    for (int s = 1; s < NSH; ++s)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
     if (SIGNED) {
@@ -246,8 +246,9 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         for (int cc = 0; cc < P->nconst; ++cc)
           if (x[P->const_dim[cc]] != P->const_level[cc]) nq = true;
         KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
-        // f16 hi/lo representation error of the continuous coordinates: 2 * 2^-22 * sum|x''X'|
-        if (o.err > 0.f) o.err += 4.f * 0x1p-22f * bnd_q * HBX_LN2f;
+        // f16 hi/lo representation error of both coordinates and the three lo.lo products given up
+        // to the C_j pieces (each <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
+        if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-20f) * HBX_LN2f;
         if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
         out[ii] = o;
       }

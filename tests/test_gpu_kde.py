@@ -186,3 +186,37 @@ def test_exact_split_units_match_whole_sum(device, n_obs):
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
     assert res.index == O.select(l, g)[0]
+
+
+def test_hmode_falls_back_when_cj_exceeds_f16_range(device):
+    """A far outlier among tightly clustered observations makes |C_j| = |X'_j|^2 + ... exceed the
+    f16 range of the C_j pieces: that KDE is prepared for the f32-MFMA kernel instead, the other one
+    stays on the f16 kernel, and the acquisition still matches the reference."""
+    from hpbandster_amd import kde
+    rs = np.random.RandomState(11)
+    n, D = 8500, 16
+    X = 0.5 + 1e-3 * rs.rand(n, D)
+    X[17] = 0.0  # the outlier
+    L = rs.rand(n)
+    L[17] = np.sort(L)[n // 2]  # mid loss: lands in the bad KDE only
+    vt = "c" * D
+    pair = kde.fit_pair(X, L, vt, D + 1, device=device)
+    assert 17 in set(pair.bad.rows_dev.cpu().numpy()) and 17 not in set(pair.good.rows_dev.cpu().numpy())
+    assert (pair.good.variant >> 4) & 1 == 1  # f16 matrix-core kernel
+    assert (pair.bad.variant >> 4) & 1 == 0   # fallback: f32 MFMA
+    C = np.vstack([0.5 + 1e-3 * rs.rand(200, D), 0.02 * rs.rand(56, D)])
+    res, logl, logg = pair.acquire(C, logs=True)
+    for est, k in ((logl, pair.good), (logg, pair.bad)):
+        lref = O.log_pdf_many(k.data, k.bw, vt, C)
+        fin = np.isfinite(lref)
+        assert np.array_equal(np.isfinite(est), fin)
+        err = np.abs(est[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        # candidates inside the cluster: the north-star tolerance
+        assert err[:fin[:200].sum()].max() <= 1e-5
+        # candidates ~100 bandwidths from the KDE centre next to the outlier: the fp32 expansion
+        # -|x'|^2 - |X'|^2 + 2x'.X' cancels terms of ~1e5 (documented in DESIGN.md); the estimate is
+        # still within its rigorous bound, which is what keeps the selection exact
+        assert err.max() <= 5e-2
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
+    assert res.index == O.select(l, g)[0]
