@@ -8,8 +8,24 @@
 // the C_j pieces are in the bound); C_j rides along as three exact f16 pieces against A = 1 and the
 // one-hot categorical product follows in the same K loop.  c_i is the accumulator input of the first
 // MFMA.  VALU work per pair: exp2 and one add.
+// sched_group_barrier pattern: NM times {1 MFMA, then a share of NV VALU ops}, the remainder spread
+// over the first MFMAs (LLVM SchedGroupMask: MFMA = 0x8, VALU = 0x2)
+template <int I, int NM, int NV>
+struct SgbAlternate {
+  static __device__ __forceinline__ void run() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    constexpr int n = NV / NM + (I < NV % NM ? 1 : 0);
+    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x002, n, 0);
+    SgbAlternate<I + 1, NM, NV>::run();
+  }
+};
+template <int NM, int NV>
+struct SgbAlternate<NM, NM, NV> {
+  static __device__ __forceinline__ void run() {}
+};
+
 template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const double* __restrict__ cand,
+__global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(const double* __restrict__ cand,
                                                                       int64_t Nc, int32_t D,
                                                                       const KdeParams* __restrict__ P,
                                                                       const float* __restrict__ table,
@@ -38,10 +54,16 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   // its own dims.  c_i = -|x'_i|^2 and the bound term are summed over the four lane groups with a
   // butterfly (bitwise identical in all four).  Rows fall back to global reads when the rows of all
   // waves do not fit in the (not yet used) LDS ring (large D).
+  // All of it lives in the one LDS array (a second __shared__ object beside the LDS-DMA ring makes
+  // hipcc wait vmcnt(0) before every ds_read of the main loop): staged rows first, parameters after.
   struct ContPrm { double scale, center; float xmax; int32_t col; };
   struct OhPrm { double val; int32_t col, pad; };
-  __shared__ ContPrm cprm[8 * NSC];
-  __shared__ OhPrm oprm[16 * (KC > 0 ? KC : 1)];
+  constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 16 * (KC > 0 ? KC : 1) * (int)sizeof(OhPrm);
+  static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
+  const int64_t rows_bytes = (int64_t)MFMA_WAVES * 16 * RT * D * 8;
+  const bool rows_fit = rows_bytes + PRM_BYTES <= (int64_t)NBUF * CHF * 4;
+  ContPrm* cprm = (ContPrm*)((char*)lds + (rows_fit ? rows_bytes : 0));
+  OhPrm* oprm = (OhPrm*)(cprm + 8 * NSC);
   const int tid = threadIdx.x;
   if (tid < 8 * NSC) {
     const bool act = tid < dc;  // padding: never read unmasked
@@ -49,7 +71,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
                         act ? P->cont_dim[tid] : 0};
   }
   if (tid < 16 * KC) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
-  const bool staged = (int64_t)MFMA_WAVES * 16 * RT * D * 8 <= (int64_t)NBUF * CHF * 4 && cbase < Nc;
+  const bool staged = rows_fit && cbase < Nc;
   const int64_t nv = (Nc - cbase) < 16 * RT ? (Nc - cbase) : 16 * RT;  // valid rows of this wave
   double* xs = (double*)lds + (int64_t)wave * 16 * RT * D;
   if (staged) {
@@ -128,9 +150,9 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
   const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
   // LDS-DMA (global_load_lds_dwordx4): each wave copies its G 1-KB pieces of a chunk straight into
   // the ring; completion is tracked by a counted vmcnt + one raw barrier per chunk
-  auto issue = [&](int c) {
-    const float* src = table + (int64_t)c * CHF;
-    float* dst = lds + (c % NBUF) * CHF;
+  auto issue = [&](int c, int slot) {
+    const float* src = table + (int64_t)(c < nchunks ? c : nchunks - 1) * CHF;
+    float* dst = lds + slot * CHF;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int piece = wave + g * MFMA_WAVES;
@@ -138,14 +160,14 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
                                        (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
     }
   };
+  // The loads of every iteration are unconditional (past the last chunk the last chunk is re-loaded
+  // into the free buffer and never read), so the counted vmcnt is the same in every iteration and the
+  // loop body is one basic block the scheduler can interleave.
+  constexpr int PD = NBUF - 1;  // chunks in flight ahead of the one being read
   __syncthreads();  // every wave has read its staged rows: the ring may be overwritten
-  issue(0);
-  if (NBUF == 3 && nchunks > 1) {
-    issue(1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+#pragma unroll
+  for (int i = 0; i < PD; ++i) issue(i, i);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (PD - 1)) : "memory");  // chunk 0 landed
   __builtin_amdgcn_s_barrier();
 
   // MFMAs of one 16-observation column tile for every row tile
@@ -177,7 +199,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
 
   for (int c = 0; c < nchunks; ++c) {
     const float* buf = lds + (c % NBUF) * CHF;
-    if (c + NBUF - 1 < nchunks) issue(c + NBUF - 1);  // its buffer was last read in iteration c-1
+    issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
     float Sb[RT][4], Snb[RT][4];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -200,9 +222,20 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float e = __builtin_amdgcn_exp2f(cur[r][q]);
-          Sb[r][q] += e;
-          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, Snb[r][q]);
+          Sb[r][q] = jt == 0 ? e : Sb[r][q] + e;
+          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, jt == 0 ? 0.f : Snb[r][q]);
         }
+      if (!SIGNED && jt + 1 < OBS_CHUNK / 16) {
+        // interleave the exp2/sum epilogue of tile jt with the MFMAs of tile jt+1 (hipcc otherwise
+        // emits all MFMAs of the chunk back to back and the VALU work after them): the B-fragment
+        // reads first, a few exps while they land, then one MFMA / one or two VALU ops alternating
+        __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);  // DS_READ: B fragments of tile jt+1
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);    // VALU
+        if (jt == 0)
+          SgbAlternate<0, NSH * RT, 4 * RT - 2>::run();  // exp2 only (no running sum yet)
+        else
+          SgbAlternate<0, NSH * RT, 8 * RT - 2>::run();  // exp2 + add
+      }
     }
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -211,14 +244,12 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) void kde_logpdf_h_kernel(const dou
         S[r][q] += Sb[r][q];
         if (SIGNED) Sn[r][q] += Snb[r][q];
       }
-    // chunk c+1 complete for this wave (chunk c+2 may stay in flight), this wave's reads of buffer c
+    // chunk c+1 complete for this wave (PD-1 chunks stay in flight), this wave's reads of buffer c
     // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
-    if (NBUF == 3 && c + 2 < nchunks)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G * (PD - 1)) : "memory");
     __builtin_amdgcn_s_barrier();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
