@@ -9,7 +9,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libhbx.so")
+# HBX_LIB_PATH: load another build of the same library (diagnostic ablation builds, tools/ablate.sh)
+LIB_PATH = os.environ.get("HBX_LIB_PATH") or os.path.join(_HERE, "_lib", "libhbx.so")
 
 _lock = threading.Lock()
 _lib = None

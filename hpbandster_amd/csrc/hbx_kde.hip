@@ -864,17 +864,26 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
     P->oh_val[t] = NAN;
   }
   if (P->du > 0) {
+    // one-hot positions, every dim's block starting at an even position (a padding position, level
+    // -1, never matches): the sparse matrix-core kernel relies on adjacent pairs never spanning dims
     int tot = 0;
     bool ok = true;
     for (int u = 0; u < P->du; ++u) {
       if (P->cat_maxcode[u] < 0) ok = false;
-      else tot += P->cat_maxcode[u] + 1;
+      else tot = ((tot + 1) & ~1) + P->cat_maxcode[u] + 1;
     }
     if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
       P->kc = (2 * tot + 31) / 32;
       P->oh_total = tot;
       int t = 0;
-      for (int u = 0; u < P->du; ++u)
+      for (int u = 0; u < P->du; ++u) {
+        if (t & 1) {
+          P->oh_dim[t] = u;
+          P->oh_level[t] = -1;
+          P->oh_col[t] = 0;
+          P->oh_val[t] = NAN;
+          ++t;
+        }
         for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
           P->oh_dim[t] = u;
           P->oh_level[t] = l;
@@ -882,6 +891,7 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
           P->oh_val[t] = (double)l;
           ++t;
         }
+      }
     }
   }
   // continuous product on the f16 matrix cores (hi/lo split) when it has >= 16 dims and the

@@ -104,6 +104,7 @@ __device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, fl
 }
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x16 __attribute__((ext_vector_type(16)));
 
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 

@@ -8,6 +8,15 @@
 // the C_j pieces are in the bound); C_j rides along as three exact f16 pieces against A = 1 and the
 // one-hot categorical product follows in the same K loop.  c_i is the accumulator input of the first
 // MFMA.  VALU work per pair: exp2 and one add.
+// Diagnostic ablations (tools/ablate.sh builds them into separate libraries; never the shipped
+// default): 1 = no exp2, 2 = first K-step MFMA only, 3 = no per-chunk LDS-DMA/wait/barrier,
+// 4 = no running-sum adds, 5 = neither exp2 nor adds, 6 = 2 + 5.  Dropped values are kept alive with
+// empty asm statements (no dead-code elimination of the MFMAs); the rescue marker is disabled.
+// Results are wrong in every ablated build; only timing is read.
+#ifndef HBX_H_ABLATE
+#define HBX_H_ABLATE 0
+#endif
+
 // sched_group_barrier pattern: NM times {1 MFMA, then a share of NV VALU ops}, the remainder spread
 // over the first MFMAs (LLVM SchedGroupMask: MFMA = 0x8, VALU = 0x2)
 template <int I, int NM, int NV>
@@ -32,6 +41,12 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
                                                                       KdeEst* __restrict__ out) {
   constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
   constexpr int NSH = NSC + KC;             // f16 K-steps of 32
+  // one-hot product on the sparse matrix cores (v_smfmac_f32_16x16x64_f16, 2:4 structured sparsity:
+  // the candidate side has at most one match per pair of adjacent one-hot positions) -- one sparse
+  // 64-wide step replaces two dense 32-wide steps
+  constexpr bool SP = !SIGNED && KC > 0 && (KC % 2 == 0);
+  constexpr int KS = SP ? KC / 2 : 1;       // sparse 64-wide steps
+  constexpr int NMT = SP ? NSC + KC / 2 : NSH;  // matrix instructions per row tile and 16-obs tile
   constexpr int KTP = h_ktp(NSC * 8, KC);   // halves per observation row (padded); nsc_of(8 NSC) = NSC
   constexpr int KPP = h_kpp(KC);
   constexpr int CHF = h_chunk_floats(NSC * 8, KC, SIGNED ? 1 : 0);
@@ -81,6 +96,8 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   }
   __syncthreads();
   f16x8 ah[RT][NSH];
+  f16x8 asp[RT][KS];  // SP: compressed one-hot A (two nonzeros per group of four K slots)
+  int aidx[RT][KS];   // SP: their positions, one nibble per group (first | second << 2)
   float ci_a[RT], bnd_a[RT];
   // row tile r of the A operands from candidate row x (LDS or global; inlined once for each)
   auto build = [&](int r, const double* x) {
@@ -110,14 +127,34 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     bnd += __shfl_xor(bnd, 32);
     ci_a[r] = ci;
     bnd_a[r] = bnd;
+    if constexpr (SP) {
+      // lane group kq covers dense K [16kq, 16kq+16) of each 64-wide step: one-hot positions
+      // t0 = 32 s + 8 kq + 2q and t0+1 (slots 2t, 2t+1 each); prepare pads every dim's positions to
+      // start even, so the two never belong to different dims and at most one of them matches
 #pragma unroll
-    for (int s = 0; s < KC; ++s) {
+      for (int s = 0; s < KS; ++s) {
+        int idx = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const OhPrm o = oprm[16 * s + 4 * kq + q];
-        const _Float16 h = (x[o.col] == o.val) ? (_Float16)1.f : (_Float16)0.f;
-        ah[r][NSC + s][2 * q + 0] = h;
-        ah[r][NSC + s][2 * q + 1] = h;
+        for (int q = 0; q < 4; ++q) {
+          const OhPrm o0 = oprm[32 * s + 8 * kq + 2 * q], o1 = oprm[32 * s + 8 * kq + 2 * q + 1];
+          const bool m0 = x[o0.col] == o0.val, m1 = x[o1.col] == o1.val;
+          const _Float16 h = (m0 || m1) ? (_Float16)1.f : (_Float16)0.f;
+          asp[r][s][2 * q + 0] = h;
+          asp[r][s][2 * q + 1] = h;
+          idx |= (m1 ? 0xE : 0x4) << (4 * q);  // slots (2,3) of the group if t0+1 matches, else (0,1)
+        }
+        aidx[r][s] = idx;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const OhPrm o = oprm[16 * s + 4 * kq + q];
+          const _Float16 h = (x[o.col] == o.val) ? (_Float16)1.f : (_Float16)0.f;
+          ah[r][NSC + s][2 * q + 0] = h;
+          ah[r][NSC + s][2 * q + 1] = h;
+        }
       }
     }
   };
@@ -179,10 +216,24 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
 #pragma unroll
     for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][0], b[0], ciq[r], 0, 0, 0);
+    constexpr int NDENSE = (HBX_H_ABLATE == 2 || HBX_H_ABLATE == 6) ? 1 : (SP ? NSC : NSH);
 #pragma unroll
-    for (int s = 1; s < NSH; ++s)
+    for (int s = 1; s < NDENSE; ++s)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
+    if constexpr (SP && HBX_H_ABLATE != 2 && HBX_H_ABLATE != 6) {
+      // B of the sparse step: lane group g holds K = 8g .. 8g+7 and 32 + 8g .. 32 + 8g + 7 of the
+      // 64-wide step, i.e. the two dense fragments already read
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const f16x8 lo = b[NSC + 2 * s], hi = b[NSC + 2 * s + 1];
+        const f16x16 b16 = {lo[0], lo[1], lo[2], lo[3], lo[4], lo[5], lo[6], lo[7],
+                            hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          acc[r] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(asp[r][s], b16, acc[r], aidx[r][s], 0, 0);
+      }
+    }
     if (SIGNED) {
       const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
 #pragma unroll
@@ -198,8 +249,8 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   };
 
   for (int c = 0; c < nchunks; ++c) {
-    const float* buf = lds + (c % NBUF) * CHF;
-    issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
+    const float* buf = lds + (HBX_H_ABLATE == 3 ? 0 : (c % NBUF)) * CHF;
+    if (HBX_H_ABLATE != 3) issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
     float Sb[RT][4], Snb[RT][4];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -221,8 +272,11 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
-          Sb[r][q] = jt == 0 ? e : Sb[r][q] + e;
+          constexpr bool NOEXP = HBX_H_ABLATE == 1 || HBX_H_ABLATE == 5 || HBX_H_ABLATE == 6;
+          constexpr bool NOADD = HBX_H_ABLATE == 4 || HBX_H_ABLATE == 5 || HBX_H_ABLATE == 6;
+          const float e = NOEXP ? cur[r][q] : __builtin_amdgcn_exp2f(cur[r][q]);
+          if (NOADD) asm volatile("" ::"v"(e));
+          Sb[r][q] = (jt == 0 || NOADD) ? e : Sb[r][q] + e;
           if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, jt == 0 ? 0.f : Snb[r][q]);
         }
       if (!SIGNED && jt + 1 < OBS_CHUNK / 16) {
@@ -232,9 +286,9 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
         __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);  // DS_READ: B fragments of tile jt+1
         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);    // VALU
         if (jt == 0)
-          SgbAlternate<0, NSH * RT, 4 * RT - 2>::run();  // exp2 only (no running sum yet)
+          SgbAlternate<0, NMT * RT, 4 * RT - 2>::run();  // exp2 only (no running sum yet)
         else
-          SgbAlternate<0, NSH * RT, 8 * RT - 2>::run();  // exp2 + add
+          SgbAlternate<0, NMT * RT, 8 * RT - 2>::run();  // exp2 + add
       }
     }
 #pragma unroll
@@ -246,8 +300,10 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
       }
     // chunk c+1 complete for this wave (PD-1 chunks stay in flight), this wave's reads of buffer c
     // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G * (PD - 1)) : "memory");
-    __builtin_amdgcn_s_barrier();
+    if (HBX_H_ABLATE != 3) {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G * (PD - 1)) : "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 #pragma unroll
@@ -280,7 +336,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
         // f16 hi/lo representation error of both coordinates and the three lo.lo products given up
         // to the C_j pieces (each <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
         if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-20f) * HBX_LN2f;
-        if (!nq && Sq == Sq && Sq < 0x1p-64f) o.err = -1.f;
+        if (!nq && Sq == Sq && Sq < 0x1p-64f && HBX_H_ABLATE == 0) o.err = -1.f;
         out[ii] = o;
       }
     }

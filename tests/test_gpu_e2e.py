@@ -1,0 +1,114 @@
+"""End to end (BASELINE config #1 semantics): HpBandSter.run + BOHB on the toy function, with the KDE
+refits and acquisitions on the GPU, against the run the reference itself produced
+(tests/golden/gen_golden.py gen_e2e: the reference's HB_master.py + bohb.py on statsmodels 0.12.2,
+driven by a synchronous in-process dispatcher so the RNG streams are deterministic).
+
+Same seeds, same toy function (loss = mean of x + noise/budget over int(budget) draws, 20 % simulated
+crashes), same eta=2 ladder 1..64, 4 Hyperband iterations.  Every get_config call must take the same
+branch (model-based or random) and propose the same x; every run must have the same id, budget and
+loss; the incumbent must match.  scipy's truncnorm (candidate draws) differs between the fixture's
+scipy 1.7 and this interpreter by a few ulp, hence the 1e-12 tolerances on x and the losses.
+"""
+import time
+
+import numpy as np
+import pytest
+
+from tests import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+
+class _Job(object):
+    def __init__(self, id, **kwargs):
+        self.id, self.kwargs, self.timestamps = id, kwargs, {}
+        self.result, self.exception, self.worker_name = None, None, None
+
+    def time_it(self, which):
+        self.timestamps[which] = time.time()
+
+
+class _SyncDispatcher(object):
+    """The fixture generator's dispatcher: run each job at submission, call back synchronously."""
+
+    def __init__(self, compute):
+        self.compute = compute
+        self.new_result_callback = None
+
+    def run(self):
+        return
+
+    def number_of_workers(self):
+        return 1
+
+    def shutdown(self, shutdown_workers=False):
+        return
+
+    def submit_job(self, id, **kwargs):
+        job = _Job(id, **kwargs)
+        job.time_it("submitted")
+        job.time_it("started")
+        res = self.compute(kwargs["config"], kwargs["budget"])
+        job.time_it("finished")
+        if res is None:
+            job.exception = "RuntimeError: simulated failure"
+        else:
+            job.result = res
+        self.new_result_callback(job)
+        return job
+
+
+def test_toy_function_run_matches_reference(device, tmp_path):
+    from hpbandster_amd import configspace as CS
+    from hpbandster_amd.HB_master import HpBandSter
+    from hpbandster_amd.config_generators import BOHB
+
+    records, ref = G.load_e2e()
+    space = CS.ConfigurationSpace(seed=5)
+    space.add_hyperparameter(CS.UniformFloatHyperparameter("x", lower=0, upper=1))
+    noise = np.random.RandomState(17)
+
+    def compute(config, budget):
+        if noise.rand() < 0.2:
+            return None
+        res = [config["x"] + noise.randn() / budget for _ in range(int(budget))]
+        return {"loss": float(np.mean(res)), "info": res}
+
+    np.random.seed(123)
+    cg = BOHB(space, device=device)
+    calls = []
+    orig = cg.get_config
+
+    def get_config(budget):
+        cfg, info = orig(budget)
+        calls.append((budget, cfg["x"], bool(info["model_based_pick"])))
+        return cfg, info
+
+    cg.get_config = get_config
+    hb = HpBandSter(run_id="0", config_generator=cg, working_directory=str(tmp_path), eta=2, min_budget=1,
+                    max_budget=64, dispatcher=_SyncDispatcher(compute))
+    res = hb.run(4)
+    hb.shutdown()
+
+    assert len(calls) == len(records)
+    assert sum(bool(r["model_based"]) for r in records) > 0  # the KDE path is exercised
+    for (b, x, mb), r in zip(calls, records):
+        assert b == float(r["budget"])
+        assert mb == bool(r["model_based"])
+        np.testing.assert_allclose(x, float(r["x"]), rtol=0, atol=1e-12)
+
+    runs = []
+    for cid, d in res.data.items():
+        for b, rr in d["results"].items():
+            runs.append([list(cid), float(b), None if rr is None else rr["loss"], d["config"]["x"]])
+    runs.sort(key=lambda r: (r[0], r[1]))
+    want = sorted(ref["runs"], key=lambda r: (r[0], r[1]))
+    assert len(runs) == len(want)
+    for got, w in zip(runs, want):
+        assert got[0] == w[0] and got[1] == w[1]
+        assert (got[2] is None) == (w[2] is None)
+        if w[2] is not None:
+            np.testing.assert_allclose(got[2], w[2], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(got[3], w[3], rtol=0, atol=1e-12)
+    inc = res.get_incumbent_id()
+    assert (None if inc is None else list(inc)) == ref["incumbent"]

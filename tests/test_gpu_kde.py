@@ -220,3 +220,37 @@ def test_hmode_falls_back_when_cj_exceeds_f16_range(device):
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
     assert res.index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("dc,levels", [
+    (20, [3, 5, 2, 3, 4, 3]),   # odd level counts: one-hot positions padded per dim, sparse (2:4) product
+    (24, [4, 4, 4]),            # 12 positions -> one dense f16 one-hot step (kc = 1)
+    (30, [4] * 16),             # 64 positions -> kc = 4, two sparse steps
+    (17, []),                   # continuous only on the f16 kernel
+])
+def test_hmode_categorical_layouts_match_oracle(device, dc, levels):
+    """The f16 matrix-core kernel over one-hot layouts the bench shape does not use."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    du = len(levels)
+    n = 2000
+    X = S.make_observations(n, dc, du, levels if du else 2, seed=21)
+    L = S.make_losses(n, seed=22)
+    vt = S.var_type_string(dc, du)
+    pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    assert (pair.good.variant >> 4) & 1 == 1 and (pair.bad.variant >> 4) & 1 == 1
+    C = S.make_candidates(384, dc, du, levels if du else 2, seed=23)
+    res, logl, logg = pair.acquire(C, logs=True)
+    for est, k in ((logl, pair.good), (logg, pair.bad)):
+        lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        fin = np.isfinite(lref)
+        assert np.array_equal(np.isfinite(est), fin)
+        err = np.abs(est[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        # the north-star tolerance (1e-5) is stated at D <= 32; beyond it the fp32 expansion
+        # -|x'|^2 - |X'|^2 + 2x'.X' cancels larger terms (error ~ 2^-24 sum|terms|), still inside
+        # the rigorous per-candidate bound that keeps the selection exact
+        assert err.max() <= (1e-5 if dc + du <= 32 else 3e-5), err.max()
+        assert np.median(err) <= 1e-6
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+    assert res.index == O.select(l, g)[0]
