@@ -75,7 +75,9 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   struct OhPrm { double val; int32_t col, pad; };
   constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 16 * (KC > 0 ? KC : 1) * (int)sizeof(OhPrm);
   static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
-  const int64_t rows_bytes = (int64_t)MFMA_WAVES * 16 * RT * D * 8;
+  // staged rows are DS = D|1 doubles apart (odd): the 16 rows a lane group reads hit distinct banks
+  const int DS = D | 1;
+  const int64_t rows_bytes = (int64_t)MFMA_WAVES * 16 * RT * DS * 8;
   const bool rows_fit = rows_bytes + PRM_BYTES <= (int64_t)NBUF * CHF * 4;
   ContPrm* cprm = (ContPrm*)((char*)lds + (rows_fit ? rows_bytes : 0));
   OhPrm* oprm = (OhPrm*)(cprm + 8 * NSC);
@@ -88,11 +90,17 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   if (tid < 16 * KC) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
   const bool staged = rows_fit && cbase < Nc;
   const int64_t nv = (Nc - cbase) < 16 * RT ? (Nc - cbase) : 16 * RT;  // valid rows of this wave
-  double* xs = (double*)lds + (int64_t)wave * 16 * RT * D;
+  double* xs = (double*)lds + (int64_t)wave * 16 * RT * DS;
   if (staged) {
-    const int tot = (int)(nv * D);
     const double* src = cand + cbase * (int64_t)D;
-    for (int e = lane; e < tot; e += 64) xs[e] = src[e];
+    if (D <= 64) {  // 64 / D rows per pass, coalesced
+      const int rpi = 64 / D, lr = lane / D, lc = lane - lr * D;
+      if (lr < rpi)
+        for (int row = lr; row < nv; row += rpi) xs[row * DS + lc] = src[row * D + lc];
+    } else {
+      for (int row = 0; row < nv; ++row)
+        for (int c = lane; c < D; c += 64) xs[row * DS + c] = src[row * D + c];
+    }
   }
   __syncthreads();
   f16x8 ah[RT][NSH];
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const int loc = (16 * r + ia) < nv ? (16 * r + ia) : (int)nv - 1;
-      build(r, xs + loc * D);
+      build(r, xs + loc * DS);
     }
   } else {
 #pragma unroll
@@ -323,10 +331,12 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     if (ia < 4) {
       const int q = ia;
       const int64_t ii = cbase + 16 * r + 4 * kq + q;
-      float Sq = S[r][0], Snq = Sn[r][0];
-      if (q == 1) { Sq = S[r][1]; Snq = Sn[r][1]; }
-      if (q == 2) { Sq = S[r][2]; Snq = Sn[r][2]; }
-      if (q == 3) { Sq = S[r][3]; Snq = Sn[r][3]; }
+      // select tree on named values (a runtime index into S would put S in scratch memory)
+      const bool b0 = (ia & 1) != 0, b1 = (ia & 2) != 0;
+      const float s0 = S[r][0], s1 = S[r][1], s2 = S[r][2], s3 = S[r][3];
+      const float n0 = Sn[r][0], n1 = Sn[r][1], n2 = Sn[r][2], n3 = Sn[r][3];
+      const float Sq = b1 ? (b0 ? s3 : s2) : (b0 ? s1 : s0);
+      const float Snq = b1 ? (b0 ? n3 : n2) : (b0 ? n1 : n0);
       if (ii < Nc) {
         const double* x = cand + ii * (int64_t)D;
         bool nq = P->nan_all != 0;
