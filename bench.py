@@ -76,6 +76,7 @@ def parse():
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-config5", action="store_true", help="skip the secondary SH-promotion line")
     return ap.parse_args()
 
 
@@ -101,6 +102,72 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": "%d of the %d candidates x %d observations (D=%d), fp64 C oracle, %.1f s"
                       % (n, cands.shape[0], Xg.shape[0] + Xb.shape[0], X.shape[1], dt)}
+
+
+def config5(device, B=10_000, n=1_000, reps=10):
+    """Secondary line: BASELINE config #5, batched successive-halving promotion (eta=3 -> k=333) over
+    B brackets x n configs (fp64 losses resident in HBM) plus one batched KDE refit of every bracket
+    (D=8 continuous).  Algorithmic HBM bytes per promoted config: 8 (loss) + 8 (order) + 1 (mask)."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    L = N.lib()
+    losses = torch.from_numpy(S.make_bracket_losses(B, n).reshape(-1)).to(device)
+    seg = torch.arange(B + 1, dtype=torch.int64, device=device) * n
+    k = torch.full((B,), float(n // 3), dtype=torch.float64, device=device)
+    order = torch.empty(B * n, dtype=torch.int64, device=device)
+    adv = torch.empty(B * n, dtype=torch.uint8, device=device)
+    nadv = torch.empty(B, dtype=torch.int64, device=device)
+    sb = int(L.hbx_sort_scratch_bytes(B * n))
+    scr = torch.empty(sb, dtype=torch.uint8, device=device)
+    sh = N.stream_handle()
+
+    def promote():
+        N.check(L.hbx_sh_promote(N.ptr(losses), N.ptr(seg), B, n, B * n, N.ptr(k), N.ptr(order), N.ptr(adv),
+                                 N.ptr(nadv), N.ptr(scr), sb, sh))
+    promote()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        promote()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    ok = bool((nadv == n // 3).all().item())
+    # batched refit of every bracket's KDE pair (argsort + normal-reference bandwidths), D = 8
+    D = 8
+    X = torch.from_numpy(np.random.RandomState(4).rand(B * n, D)).to(device)
+    ng, nb = kde.bohb_split_sizes(n, D + 1)
+    ngd = torch.full((B,), ng, dtype=torch.int64, device=device)
+    nbd = torch.full((B,), nb, dtype=torch.int64, device=device)
+    fg = torch.full((B,), kde.bandwidth_factor(ng, D), dtype=torch.float64, device=device)
+    fb = torch.full((B,), kde.bandwidth_factor(nb, D), dtype=torch.float64, device=device)
+    vt = torch.zeros(D, dtype=torch.int32, device=device)
+    bwg = torch.empty((B, D), dtype=torch.float64, device=device)
+    bwb = torch.empty((B, D), dtype=torch.float64, device=device)
+    nlg = torch.empty((B, D), dtype=torch.int32, device=device)
+    nlb = torch.empty((B, D), dtype=torch.int32, device=device)
+
+    def refit():
+        N.check(L.hbx_seg_argsort(N.ptr(losses), N.ptr(seg), B, n, B * n, N.ptr(order), N.ptr(scr), sb, sh))
+        N.check(L.hbx_kde_fit(N.ptr(X), D, N.ptr(seg), B, N.ptr(order), N.ptr(ngd), N.ptr(nbd), N.ptr(fg), N.ptr(fb),
+                              N.ptr(vt), N.ptr(bwg), N.ptr(bwb), N.ptr(nlg), N.ptr(nlb), sh))
+    refit()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        refit()
+    e1.record()
+    torch.cuda.synchronize()
+    ms_fit = e0.elapsed_time(e1) / reps
+    gbs = B * n * 17 / (ms * 1e-3) / 1e9
+    return {"workload": "sh_promotion_B%d_n%d_eta3" % (B, n), "configs_per_s": B * n / (ms * 1e-3),
+            "ms_per_launch": ms, "masks_ok": ok,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
+                         "bytes_per_config": 17},
+            "refit_all_brackets_ms": ms_fit, "refit_dims": D}
 
 
 def load_traffic(workload):
@@ -227,6 +294,11 @@ def main():
                      "mfma_util": mfma_util, "issue_bound": issue_bound},
         "cpu_baseline": None,
     }
+    if rank == 0 and not a.no_config5:
+        try:
+            out["config5"] = config5(device)
+        except Exception as e:  # a side measurement; report why it is missing
+            out["config5"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),

@@ -54,8 +54,29 @@ __device__ double np_pairwise_gather(const double* X, int32_t D, int32_t d, cons
 __device__ double np_sum_column(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
                                 double mean, bool sq) {
   if (D > 1) {  // axis-0 reduction of an (n, D) C-array: sequential down the column
+    // the additions stay strictly in row order; only the (independent) gathers are batched, so 16
+    // loads are in flight per round trip instead of one
+    constexpr int U = 16;
     double acc = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
+    int64_t i = 0;
+    for (; i + U <= n; i += U) {
+      int64_t rr[U];
+      double v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) rr[k] = rows[i + k];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = X[rr[k] * (int64_t)D + d];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (sq) {
+          const double t = v[k] - mean;
+          acc = acc + t * t;
+        } else {
+          acc = acc + v[k];
+        }
+      }
+    }
+    for (; i < n; ++i) {
       const double x = X[rows[i] * (int64_t)D + d];
       if (sq) {
         const double t = x - mean;
@@ -124,20 +145,104 @@ __global__ __launch_bounds__(128) void kde_fit_stats_kernel(
   uint32_t* bm = bits[threadIdx.x];
   for (int w = 0; w < 32; ++w) bm[w] = 0u;
   int32_t cnt = 0;
-  for (int64_t i = 0; i < ns; ++i) {
-    const double x = Xs[ord[i] * (int64_t)D + d];
-    const int v = (int)x;
-    if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
-      cnt = -1;  // categorical codes must be integers in [0, 1024)
-      break;
-    }
-    const uint32_t m = 1u << (v & 31);
-    if (!(bm[v >> 5] & m)) {
-      bm[v >> 5] |= m;
-      ++cnt;
+  constexpr int U = 16;  // gathers batched U at a time (the count is order-independent anyway)
+  for (int64_t i0 = 0; i0 < ns && cnt >= 0; i0 += U) {
+    double xv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) xv[k] = (i0 + k < ns) ? Xs[ord[i0 + k] * (int64_t)D + d] : 0.0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (i0 + k >= ns) break;  // past the set (the gather above loaded a dummy 0.0)
+      const double x = xv[k];
+      const int v = (int)x;
+      if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
+        cnt = -1;  // categorical codes must be integers in [0, 1024)
+        break;
+      }
+      const uint32_t m = 1u << (v & 31);
+      if (!(bm[v >> 5] & m)) {
+        bm[v >> 5] |= m;
+        ++cnt;
+      }
     }
   }
   *nlo = cnt;
+}
+
+// One workgroup per (segment, set, dim) -- used when there are too few columns to fill the GPU with
+// one thread each (a single BOHB refit: 2 x D columns).  The gathers of a column are staged in LDS by
+// the whole block; thread 0 then adds them strictly in row order (np.std's axis-0 reduction order,
+// D > 1), so the result is bit-identical to the thread-per-column kernel.  Level counts come from a
+// block-wide bitmap (order-independent).
+#define FIT_TILE 4096
+__global__ __launch_bounds__(256) void kde_fit_col_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off,
+    const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
+    const double* __restrict__ fac_good, const double* __restrict__ fac_bad, const int32_t* __restrict__ vartype,
+    double* __restrict__ bw_good, double* __restrict__ bw_bad, int32_t* __restrict__ nlev_good,
+    int32_t* __restrict__ nlev_bad) {
+  __shared__ double v[FIT_TILE];
+  __shared__ uint32_t bits[32];
+  __shared__ double red;
+  __shared__ int bad_code;
+  const int64_t t = blockIdx.x;
+  const int32_t d = (int32_t)(t % D);
+  const int64_t bs = t / D;
+  const int64_t b = bs >> 1;
+  const bool good = (bs & 1) == 0;
+  const int64_t ns = good ? n_good[b] : n_bad[b];
+  const int64_t s0 = seg_off[b], len = seg_off[b + 1] - s0;
+  double* bwo = (good ? bw_good : bw_bad) + b * D + d;
+  int32_t* nlo = (good ? nlev_good : nlev_bad) + b * D + d;
+  if (ns <= 0 || ns > len) {
+    if (threadIdx.x == 0) {
+      *bwo = NAN;
+      *nlo = 0;
+    }
+    return;
+  }
+  const int64_t* ord = order + s0 + (good ? 0 : (len - ns));
+  const double* Xs = X + s0 * (int64_t)D;
+  if (threadIdx.x < 32) bits[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) bad_code = 0;
+  double mean = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {
+    double acc = 0.0;  // thread 0
+    for (int64_t c = 0; c < ns; c += FIT_TILE) {
+      const int m = (int)((ns - c) < FIT_TILE ? (ns - c) : FIT_TILE);
+      __syncthreads();
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const double x = Xs[ord[c + i] * (int64_t)D + d];
+        if (pass == 0) {
+          v[i] = x;
+          if (vartype[d] != 0) {
+            const int iv = (int)x;
+            if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) bad_code = 1;
+            else atomicOr(&bits[iv >> 5], 1u << (iv & 31));
+          }
+        } else {
+          const double q = x - mean;
+          v[i] = q * q;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int i = 0; i < m; ++i) acc = acc + v[i];
+    }
+    if (threadIdx.x == 0) red = acc;
+    __syncthreads();
+    if (pass == 0) mean = red / (double)ns;
+  }
+  if (threadIdx.x == 0) {
+    const double var = red / (double)ns;
+    *bwo = (1.06 * sqrt(var)) * (good ? fac_good[b] : fac_bad[b]);
+    int cnt = 0;
+    if (vartype[d] != 0) {
+      for (int w = 0; w < 32; ++w) cnt += __popc(bits[w]);
+      if (bad_code) cnt = -1;
+    }
+    *nlo = cnt;
+  }
 }
 
 extern "C" {
@@ -184,9 +289,14 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
   if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
   if (B <= 0) return HBX_OK;
   const int64_t total = B * 2 * D;
-  hipLaunchKernelGGL(kde_fit_stats_kernel, dim3((unsigned)((total + 127) / 128)), dim3(128), 0,
-                     (hipStream_t)stream, X, D, seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype,
-                     bw_good, bw_bad, nlev_good, nlev_bad);
+  if (D > 1 && total < 16384) {  // few columns: one workgroup each (LDS-staged gathers)
+    hipLaunchKernelGGL(kde_fit_col_kernel, dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, X, D, seg_off,
+                       order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad);
+  } else {
+    hipLaunchKernelGGL(kde_fit_stats_kernel, dim3((unsigned)((total + 127) / 128)), dim3(128), 0,
+                       (hipStream_t)stream, X, D, seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype,
+                       bw_good, bw_bad, nlev_good, nlev_bad);
+  }
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
