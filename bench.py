@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the secondary SH-promotion line")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="winner exchange: nccl (= RCCL over xGMI) or gloo (CPU, multi-process rehearsal)")
+    ap.add_argument("--share-gpu", action="store_true", help="ranks share the visible GPUs (rehearsal only)")
     return ap.parse_args()
 
 
@@ -194,10 +197,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one process per GPU; --share-gpu maps every rank onto the visible devices round-robin (rehearsal
+    # of the multi-process path on a 1-GPU box, with --backend gloo: RCCL refuses two ranks per GPU)
+    ndev = torch.cuda.device_count()
+    dev_idx = local % ndev if a.share_gpu else local
+    torch.cuda.set_device(dev_idx)
+    device = torch.device("cuda", dev_idx)
+    comm_dev = device if a.backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(a.backend)
 
     D = a.dc + a.du
     var_type = S.var_type_string(a.dc, a.du)
@@ -217,6 +228,7 @@ def main():
         rv = pair.acquire(c_dev, index_base=base, workspace=ws, sync=False, events=ev)
         loc = torch.stack([rv[8:16].view(torch.float64)[0], rv[0:8].view(torch.int64)[0].to(torch.float64)])
         if world > 1:
+            loc = loc.to(comm_dev)
             allr = [torch.empty_like(loc) for _ in range(world)]
             dist.all_gather(allr, loc)
             allr = torch.stack(allr)
@@ -253,7 +265,7 @@ def main():
     last = kde.AcqResult.from_bytes(ws[int(pair.result_offset()):int(pair.result_offset()) + kde.RESULT_BYTES]
                                     .cpu().numpy().tobytes())
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
+        t = torch.tensor([el], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     pairs_step = world * Nc * (Ng + Nb)
@@ -282,7 +294,7 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": workload, "candidates_per_gpu": Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,
-                   "parallelism": "candidate-sharded x%d, RCCL all_gather of local winners" % world,
+                   "parallelism": "candidate-sharded x%d, %s all_gather of local winners" % (world, "RCCL" if a.backend == "nccl" else "gloo"),
                    "winner": winner[0], "shortlist": last.shortlist},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
