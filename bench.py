@@ -173,6 +173,47 @@ def config5(device, B=10_000, n=1_000, reps=10):
             "refit_all_brackets_ms": ms_fit, "refit_dims": D}
 
 
+def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
+    """Side measurement: one SH stage's get_config calls at the reference's real size
+    (bohb.py:23 num_samples=64; 81 = the first stage of an eta=3 bracket) against config #3's model:
+    81 sequential acquisitions of 64 candidates vs one batched pass; wall time per call, winners
+    reaching the host in both cases (what BOHB needs)."""
+    import torch
+    from hpbandster_amd import synthetic as S
+    C = torch.from_numpy(S.make_candidates(calls * per_call, dc, du, levels, seed=S.SEED_CAND + 7)).to(device)
+    ws1 = torch.empty(pair.workspace_bytes(per_call), dtype=torch.uint8, device=device)
+    wsb = torch.empty(pair.batch_workspace_bytes(calls * per_call, per_call), dtype=torch.uint8, device=device)
+    rb = torch.empty(calls * kde_result_bytes(), dtype=torch.uint8, device=device)
+
+    def seq():
+        outs = [pair.acquire(C[i * per_call:(i + 1) * per_call], workspace=ws1, sync=False).clone()
+                for i in range(calls)]
+        return torch.stack(outs).cpu()
+
+    def bat():
+        return pair.acquire_batch(C, per_call, workspace=wsb, results=rb, sync=False).cpu()
+
+    a, b = seq(), bat()
+    same = bool(torch.equal(a.reshape(-1), b.reshape(-1)))
+    res = {}
+    for name, fn in (("sequential", seq), ("batched", bat)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = (time.perf_counter() - t0) / reps
+    return {"workload": "sh_stage_%dx%d_get_config" % (calls, per_call), "calls": calls,
+            "candidates_per_call": per_call, "records_identical": same,
+            "ms_sequential": res["sequential"] * 1e3, "ms_batched": res["batched"] * 1e3,
+            "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
+
+
+def kde_result_bytes():
+    from hpbandster_amd import kde
+    return kde.RESULT_BYTES
+
+
 def load_traffic(workload):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -311,6 +352,11 @@ def main():
             out["config5"] = config5(device)
         except Exception as e:  # a side measurement; report why it is missing
             out["config5"] = {"error": repr(e)}
+    if rank == 0 and not a.no_config5:
+        try:
+            out["batched_acquisition"] = batched(pair, device, a.dc, a.du, a.levels)
+        except Exception as e:
+            out["batched_acquisition"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),

@@ -38,6 +38,11 @@ SIGNATURES = {
                                 c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
                                 c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_batch_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
+    "hbx_kde_acquire_batch": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i64,
+                                      c_vp, c_vp, c_vp, c_vp, c_i32,
+                                      c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
+                                      c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hbx_event_create": (c_i32, [c_vp]),
     "hbx_event_destroy": (c_i32, [c_vp]),
     "hbx_event_elapsed_ms": (c_i32, [c_vp, c_vp, c_vp]),

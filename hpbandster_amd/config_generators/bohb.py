@@ -110,6 +110,46 @@ class BOHB(base_config_generator):
                 info_dict['model_based_pick'] = False
         return sample, info_dict
 
+    def get_config_batch(self, budget, k):
+        """``[self.get_config(budget) for _ in range(k)]`` with one GPU pass for all model-based calls.
+
+        Valid while no result arrives in between (the model is fixed): an SH stage's first
+        ``num_configs[0]`` samples (HB_iteration.py:136-138).  The global numpy RNG is consumed in the
+        same order as k sequential calls (the draws of a call do not depend on earlier calls' scores)
+        and the configspace RNG is consumed in call order, so the returned list is identical to the
+        sequential one.
+        """
+        plan = []  # per call: None (random pick) or the row offset of its candidates
+        blocks = []
+        pair = None
+        for _ in range(int(k)):
+            if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
+                plan.append(None)
+                continue
+            if pair is None:
+                pair = self.kde_models[max(self.kde_models.keys())]  # bohb.py:124
+            plan.append(len(blocks) * self.num_samples)
+            blocks.append(self.sample_candidates(pair['good'], self.num_samples))
+        results = []
+        if blocks:
+            cands = np.concatenate(blocks, axis=0)
+            results = pair.acquire_batch(cands, self.num_samples)
+        out = []
+        for off in plan:
+            if off is None:
+                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
+                continue
+            res = results[off // self.num_samples]
+            if res.index < 0:
+                self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
+                                  % self.num_samples)
+                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
+            else:
+                vec = cands[off + res.index]
+                out.append((ConfigSpace.Configuration(self.configspace, vector=vec).get_dictionary(),
+                            {'model_based_pick': True}))
+        return out
+
     # -- observations ---------------------------------------------------------------------------
     def new_result(self, job):
         super().new_result(job)

@@ -288,6 +288,21 @@ __global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, Acq
   }
 }
 
+// batched acquisition: per-segment bound, flags, shortlist count, best score and (index, position) key
+__global__ void acq_init_batch_kernel(int64_t B, uint32_t* __restrict__ U, int32_t* __restrict__ flags,
+                                      int32_t* __restrict__ segcnt, uint64_t* __restrict__ best,
+                                      uint64_t* __restrict__ key, int32_t* __restrict__ count) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0) *count = 0;
+  if (b < B) {
+    U[b] = hbx_f2ord(INFINITY);
+    flags[b] = 0;
+    segcnt[b] = 0;
+    best[b] = ~0ull;
+    key[b] = ~0ull;
+  }
+}
+
 // ln-pdf interval [lo, hi] and point estimate from (ln S+, ln S-, relative bound); -inf means pdf <= 0
 __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* hi, float* pt) {
   const float m = fmaxf(e.lpos, e.lneg);
@@ -302,13 +317,16 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
   *lo = (S - E) > 0.f ? m + __logf(S - E) - 1e-6f * fabsf(m) - 1e-5f : -INFINITY;
 }
 
+// Candidates [b*seg, (b+1)*seg) form acquisition b (seg = Nc: one acquisition).  U[b] = min over the
+// segment of the upper score bound, flags[b] bit 0 = overflow risk (re-score the whole segment).
 __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
-                                                          const KdeEst* __restrict__ eg, int64_t Nc,
+                                                          const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo, float* __restrict__ hi,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   float h = INFINITY;
+  const uint32_t sg = (uint32_t)(i < Nc ? i : Nc - 1) / seg;
   if (i < Nc) {
     const KdeEst a = el[i], b = eg[i];
     const float C = (float)HBX_LN_CLAMP;
@@ -341,32 +359,34 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
     if (logg) logg[i] = gpt;
     lo[i] = slo;
     hi[i] = shi;
-    if (of) atomicOr(flags, 1);
+    if (of) atomicOr(flags + sg, 1);
   }
-  // block min of hi
-  __shared__ float red[4];
-  for (int o = 32; o > 0; o >>= 1) h = fminf(h, __shfl_xor(h, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float m = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
-    if (m < INFINITY) atomicMin(U, hbx_f2ord(m));
+  // min of hi per segment: wave reduction when the wave lies in one segment, else per lane
+  const uint32_t s0 = __shfl(sg, 0), s63 = __shfl(sg, 63);
+  if (s0 == s63) {
+    for (int o = 32; o > 0; o >>= 1) h = fminf(h, __shfl_xor(h, o));
+    if ((threadIdx.x & 63) == 0 && h < INFINITY) atomicMin(U + sg, hbx_f2ord(h));
+  } else if (h < INFINITY) {
+    atomicMin(U + sg, hbx_f2ord(h));
   }
 }
 
-__global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restrict__ lo, int64_t Nc,
+__global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restrict__ lo, int64_t Nc, uint32_t seg,
                                                             const uint32_t* __restrict__ U,
                                                             const int32_t* __restrict__ flags,
                                                             int32_t* __restrict__ list,
-                                                            int32_t* __restrict__ count) {
+                                                            int32_t* __restrict__ count,
+                                                            int32_t* __restrict__ segcnt) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= Nc) return;
-  const float u = hbx_ord2f(*U);
-  const bool all = (*flags & 1) != 0;
+  const uint32_t sg = (uint32_t)i / seg;
+  const float u = hbx_ord2f(U[sg]);
+  const bool all = (flags[sg] & 1) != 0;
   const float l = lo[i];
   if (l == l && (all || l <= u)) {
     const int pos = atomicAdd(count, 1);
     list[pos] = (int32_t)i;
+    if (segcnt) atomicAdd(segcnt + sg, 1);
   }
 }
 
@@ -656,6 +676,68 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
   }
 }
 
+// Batched argmin, three passes over the shortlist: (1) per-segment minimum of the exact score,
+// (2) among the entries reaching it the smallest index (strict '<', first index -- bohb.py:149-152),
+// (3) one thread per segment writes its record.  Scores are > 0 or NaN (both factors are clamped
+// to >= 1e-8), so the bits of a finite score order like the score.
+__device__ __forceinline__ double bohb_score(double g, double l) {
+  return ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);  // Python max() semantics, see kde_final
+}
+
+__global__ __launch_bounds__(256) void kde_batch_min_kernel(const int32_t* __restrict__ list,
+                                                            const int32_t* __restrict__ count, uint32_t seg,
+                                                            const double* __restrict__ exact_l,
+                                                            const double* __restrict__ exact_g,
+                                                            uint64_t* __restrict__ best) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *count) return;
+  const double s = bohb_score(exact_g[p], exact_l[p]);
+  if (s < INFINITY) atomicMin((unsigned long long*)best + (uint32_t)list[p] / seg,
+                              (unsigned long long)__double_as_longlong(s));
+}
+
+__global__ __launch_bounds__(256) void kde_batch_key_kernel(const int32_t* __restrict__ list,
+                                                            const int32_t* __restrict__ count, uint32_t seg,
+                                                            const double* __restrict__ exact_l,
+                                                            const double* __restrict__ exact_g,
+                                                            const uint64_t* __restrict__ best,
+                                                            uint64_t* __restrict__ key) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *count) return;
+  const double s = bohb_score(exact_g[p], exact_l[p]);
+  const uint32_t i = (uint32_t)list[p], sg = i / seg;
+  if (s < INFINITY && (uint64_t)__double_as_longlong(s) == best[sg])
+    atomicMin((unsigned long long*)key + sg, ((unsigned long long)(i - sg * seg) << 32) | (uint32_t)p);
+}
+
+__global__ __launch_bounds__(256) void kde_batch_final_kernel(int64_t B, const uint64_t* __restrict__ key,
+                                                              const int32_t* __restrict__ segcnt,
+                                                              const int32_t* __restrict__ flags,
+                                                              const double* __restrict__ exact_l,
+                                                              const double* __restrict__ exact_g,
+                                                              int64_t index_base, AcqResult* __restrict__ res) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  AcqResult r;
+  r.shortlist = segcnt[b];
+  r.flags = flags[b];
+  r.pad = 0;
+  const uint64_t k = key[b];
+  if (k == ~0ull) {
+    r.index = -1;
+    r.score = NAN;
+    r.pdf_l = NAN;
+    r.pdf_g = NAN;
+  } else {
+    const int p = (int)(uint32_t)k;
+    r.index = (int64_t)(k >> 32) + index_base;
+    r.pdf_l = exact_l[p];
+    r.pdf_g = exact_g[p];
+    r.score = bohb_score(r.pdf_g, r.pdf_l);
+  }
+  res[b] = r;
+}
+
 // ------------------------------------------------------------------------------------------
 // launch-side dispatch over the (dc_pad, du_pad, signed) template buckets
 
@@ -709,12 +791,14 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
   return HBX_OK;
 }
 
-// workspace layout (bytes), shared by hbx_kde_workspace_bytes and hbx_kde_acquire
+// workspace layout (bytes), shared by the *_workspace_bytes helpers and the acquisitions; B = number
+// of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
+// comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t U, count, flags, res, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
+  size_t res, U, count, flags, segcnt, best, key, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
 };
 
-static WsLayout ws_layout(int64_t Nc, int64_t nmax) {
+static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   WsLayout w;
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -722,10 +806,13 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax) {
     o += (bytes + 255) & ~(size_t)255;
     return r;
   };
-  w.U = take(4);
-  w.count = take(4);
-  w.flags = take(4);
   w.res = take(sizeof(AcqResult));
+  w.count = take(4);
+  w.U = take(4 * B);
+  w.flags = take(4 * B);
+  w.segcnt = take(4 * B);
+  w.best = take(8 * B);
+  w.key = take(8 * B);
   w.est_l = take(sizeof(KdeEst) * Nc);
   w.est_g = take(sizeof(KdeEst) * Nc);
   w.lo = take(4 * Nc);
@@ -962,21 +1049,24 @@ int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params
   return launch_score(f, cand, Nc, D, params, table, (KdeEst*)est_out, (hipStream_t)stream);
 }
 
-// One acquisition: score every candidate against l (good) and g (bad), shortlist, exact re-score,
-// argmin.  index_base offsets the reported index (candidate sharding across GPUs).  The result
-// (AcqResult) stays in the workspace; hbx_kde_result_ptr() gives its device address.
-int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
-                    const void* params_good, const float* table_good, const double* X_good,
-                    const int64_t* rows_good, int32_t variant_good,
-                    const void* params_bad, const float* table_bad, const double* X_bad,
-                    const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
-                    int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
-                    void* events, void* stream) {
+}  // extern "C"
+
+// Shared body of hbx_kde_acquire (batch_res == nullptr: one acquisition over all Nc candidates, the
+// record stays in the workspace) and hbx_kde_acquire_batch (B = ceil(Nc/seg) acquisitions over
+// consecutive segments of seg candidates, one record each into batch_res).
+static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t seg, int32_t D, int64_t index_base,
+                        const void* params_good, const float* table_good, const double* X_good,
+                        const int64_t* rows_good, int32_t variant_good, const void* params_bad,
+                        const float* table_bad, const double* X_bad, const int64_t* rows_bad, int32_t variant_bad,
+                        int32_t dc_pad, int32_t du_pad, int64_t nmax, float* logl_out, float* logg_out,
+                        AcqResult* batch_res, void* workspace, int64_t ws_bytes, void* events, void* stream) {
   if ((!cand && Nc > 0) || !params_good || !table_good || !X_good || !rows_good || !params_bad || !table_bad ||
       !X_bad || !rows_bad || !workspace)
-    return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire: null pointer");
+    return hbx_fail(HBX_ERR_ARG, "%s: null pointer", who);
   if (Nc < 0 || Nc > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "Nc=%lld out of range", (long long)Nc);
-  const WsLayout w = ws_layout(Nc, nmax);
+  if (seg < 1) return hbx_fail(HBX_ERR_ARG, "%s: segment length %lld", who, (long long)seg);
+  const int64_t B = batch_res ? (Nc + seg - 1) / seg : 1;
+  const WsLayout w = ws_layout(Nc, nmax, B);
   if ((size_t)ws_bytes < w.total)
     return hbx_fail(HBX_ERR_ARG, "workspace too small: %lld < %lld bytes", (long long)ws_bytes,
                     (long long)w.total);
@@ -987,6 +1077,9 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   uint32_t* U = (uint32_t*)(ws + w.U);
   int32_t* count = (int32_t*)(ws + w.count);
   int32_t* flags = (int32_t*)(ws + w.flags);
+  int32_t* segcnt = (int32_t*)(ws + w.segcnt);
+  uint64_t* best = (uint64_t*)(ws + w.best);
+  uint64_t* key = (uint64_t*)(ws + w.key);
   AcqResult* res = (AcqResult*)(ws + w.res);
   KdeEst* el = (KdeEst*)(ws + w.est_l);
   KdeEst* eg = (KdeEst*)(ws + w.est_g);
@@ -997,10 +1090,16 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
   double* exact_g = (double*)(ws + w.exact_g);
   double* part = (double*)(ws + w.part);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, res);
+  const uint32_t sg = (uint32_t)(batch_res ? seg : (Nc > 0 ? Nc : 1));
+  if (B == 0) return HBX_OK;  // batched call without candidates: no records
+  if (batch_res)
+    hipLaunchKernelGGL(acq_init_batch_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, U, flags,
+                       segcnt, best, key, count);
+  else
+    hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, res);
   HBX_LAUNCH_CHECK();
+  const dim3 grid((unsigned)((Nc + 255) / 256));
   if (Nc > 0) {
-    const dim3 grid((unsigned)((Nc + 255) / 256));
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     if (ev) HBX_HIP(hipEventRecord(ev[0], s));
     int rc = launch_score(fg, cand, Nc, D, params_good, table_good, el, s);
@@ -1009,10 +1108,11 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
     rc = launch_score(fb, cand, Nc, D, params_bad, table_bad, eg, s);
     if (rc) return rc;
     if (ev) HBX_HIP(hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, logl_out, logg_out, lo, hi, U,
+    hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
                        flags);
     HBX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, U, flags, list, count);
+    hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
+                       batch_res ? segcnt : (int32_t*)nullptr);
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
     hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_THREADS), 0, s, cand, D,
@@ -1024,12 +1124,61 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
                        exact_g);
     HBX_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
-                     index_base, res);
-  HBX_LAUNCH_CHECK();
+  if (!batch_res) {
+    hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
+                       index_base, res);
+    HBX_LAUNCH_CHECK();
+    return HBX_OK;
+  }
+  if (Nc > 0) {
+    hipLaunchKernelGGL(kde_batch_min_kernel, grid, dim3(256), 0, s, list, count, sg, exact_l, exact_g, best);
+    HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kde_batch_key_kernel, grid, dim3(256), 0, s, list, count, sg, exact_l, exact_g, best, key);
+    HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kde_batch_final_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, key, segcnt,
+                       flags, exact_l, exact_g, index_base, batch_res);
+    HBX_LAUNCH_CHECK();
+  }
   return HBX_OK;
 }
 
+extern "C" {
+
+// One acquisition: score every candidate against l (good) and g (bad), shortlist, exact re-score,
+// argmin.  index_base offsets the reported index (candidate sharding across GPUs).  The result
+// (AcqResult) stays in the workspace; hbx_kde_result_ptr() gives its device address.
+int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
+                    const void* params_good, const float* table_good, const double* X_good,
+                    const int64_t* rows_good, int32_t variant_good,
+                    const void* params_bad, const float* table_bad, const double* X_bad,
+                    const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
+                    int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
+                    void* events, void* stream) {
+  return acquire_impl("hbx_kde_acquire", cand, Nc, Nc > 0 ? Nc : 1, D, index_base, params_good, table_good, X_good,
+                      rows_good, variant_good, params_bad, table_bad, X_bad, rows_bad, variant_bad, dc_pad, du_pad,
+                      nmax, logl_out, logg_out, nullptr, workspace, ws_bytes, events, stream);
+}
+
+int64_t hbx_kde_batch_workspace_bytes(int64_t Nc, int64_t seg, int64_t nmax) {
+  if (seg < 1) return -1;
+  return (int64_t)ws_layout(Nc, nmax, (Nc + seg - 1) / seg).total;
+}
+
+// Batched acquisition: candidates [b*seg, min((b+1)*seg, Nc)) are the num_samples candidates of
+// get_config call b; every segment gets its own exact argmin (index relative to the segment start,
+// plus index_base) in results[b].  Same kernels as hbx_kde_acquire, one pass for all segments.
+int hbx_kde_acquire_batch(const double* cand, int64_t Nc, int64_t seg, int32_t D, int64_t index_base,
+                          const void* params_good, const float* table_good, const double* X_good,
+                          const int64_t* rows_good, int32_t variant_good,
+                          const void* params_bad, const float* table_bad, const double* X_bad,
+                          const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
+                          int64_t nmax, float* logl_out, float* logg_out, void* results, void* workspace,
+                          int64_t ws_bytes, void* stream) {
+  if (!results) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_batch: null results");
+  return acquire_impl("hbx_kde_acquire_batch", cand, Nc, seg, D, index_base, params_good, table_good, X_good,
+                      rows_good, variant_good, params_bad, table_bad, X_bad, rows_bad, variant_bad, dc_pad, du_pad,
+                      nmax, logl_out, logg_out, (AcqResult*)results, workspace, ws_bytes, nullptr, stream);
+}
 
 // the exact pdf stages its per-observation terms in LDS: no global scratch is needed any more (the
 // entry point keeps its scratch argument; 256 bytes keep callers' allocations non-empty)

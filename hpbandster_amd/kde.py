@@ -214,6 +214,47 @@ class KDEPair(object):
             return res, logl.cpu().numpy(), logg.cpu().numpy()
         return res
 
+    def batch_workspace_bytes(self, Nc, seg):
+        return int(N.lib().hbx_kde_batch_workspace_bytes(int(Nc), int(seg), self.nmax))
+
+    def acquire_batch(self, cands, seg, stream=None, workspace=None, results=None, sync=True):
+        """B = ceil(Nc/seg) acquisitions in one pass: candidates [b*seg, (b+1)*seg) are the candidates
+        of get_config call b.  Returns a list of B AcqResult (index relative to the segment start).
+        With ``sync=False`` returns the device tensor of the B raw records instead."""
+        torch = _torch()
+        L = N.lib()
+        dev = self.good.device
+        if isinstance(cands, np.ndarray):
+            c_dev = torch.from_numpy(np.ascontiguousarray(cands, dtype=np.float64)).to(dev)
+        else:
+            c_dev = cands
+            if c_dev.dtype != torch.float64 or not c_dev.is_contiguous():
+                raise N.HbxError("candidate tensor must be contiguous float64 [Nc, D]")
+        Nc, seg = int(c_dev.shape[0]), int(seg)
+        D = self.good.k_vars
+        if seg < 1:
+            raise N.HbxError("segment length must be >= 1")
+        if Nc > 0 and (c_dev.dim() != 2 or int(c_dev.shape[1]) != D):
+            raise N.HbxError("candidates must be [Nc, %d], got %s" % (D, tuple(c_dev.shape)))
+        B = (Nc + seg - 1) // seg
+        wsb = self.batch_workspace_bytes(Nc, seg)
+        ws = workspace if workspace is not None else torch.empty(wsb, dtype=torch.uint8, device=dev)
+        if ws.numel() < wsb:
+            raise N.HbxError("workspace too small")
+        out = results if results is not None else torch.empty(max(B, 1) * RESULT_BYTES, dtype=torch.uint8, device=dev)
+        if out.numel() < B * RESULT_BYTES:
+            raise N.HbxError("result buffer too small")
+        g, b = self.good, self.bad
+        N.check(L.hbx_kde_acquire_batch(N.ptr(c_dev), Nc, seg, D, 0,
+                                        N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.variant,
+                                        N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.variant,
+                                        g.dc_pad, g.du_pad, self.nmax, None, None, N.ptr(out), N.ptr(ws), ws.numel(),
+                                        N.stream_handle(stream)))
+        if not sync:
+            return out[:B * RESULT_BYTES]
+        raw = out[:B * RESULT_BYTES].cpu().numpy().tobytes()
+        return [AcqResult.from_bytes(raw[i * RESULT_BYTES:(i + 1) * RESULT_BYTES]) for i in range(B)]
+
 
 class ScoreEvents(object):
     """Three hipEvents bracketing the two scoring launches of one acquisition (bench timing)."""

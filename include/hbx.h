@@ -104,6 +104,21 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
                     void* events, void* stream);
 
+/* Batched acquisition: B = ceil(Nc / seg) independent get_config calls against the same model in one
+ * pass (replaces B sequential runs of the bohb.py:124-169 loop, as an SH stage issues
+ * them back to back, HB_iteration.py:136-138).  Candidates [b*seg, min((b+1)*seg, Nc)) belong to call b;
+ * results: device buffer of B * hbx_acq_result_bytes() records, record b = call b's exact argmin with
+ * the index relative to its segment start (+ index_base), -1 when the segment has no finite score.
+ * Workspace: hbx_kde_batch_workspace_bytes(Nc, seg, nmax). */
+int64_t hbx_kde_batch_workspace_bytes(int64_t Nc, int64_t seg, int64_t nmax);
+int hbx_kde_acquire_batch(const double* cand, int64_t Nc, int64_t seg, int32_t D, int64_t index_base,
+                          const void* params_good, const float* table_good, const double* X_good,
+                          const int64_t* rows_good, int32_t variant_good,
+                          const void* params_bad, const float* table_bad, const double* X_bad,
+                          const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
+                          int64_t nmax, float* logl_out, float* logg_out, void* results, void* workspace,
+                          int64_t ws_bytes, void* stream);
+
 /* Optional timing: `events` of hbx_kde_acquire is NULL or an array of three hipEvent_t recorded on
  * `stream` before the l scoring launch, between l and g, and after g. */
 int hbx_event_create(void** ev);

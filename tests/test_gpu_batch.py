@@ -1,0 +1,120 @@
+"""GPU parity of the batched acquisition: B get_config calls in one pass.
+
+Each segment of ``seg`` candidates is one call of the reference's num_samples loop
+(bohb.py:124-169); its winner must be the first index of the minimum of the reference's own scores
+over that segment (golden fixtures: scores computed by statsmodels in the reference run), and
+bit-identical to a separate ``acquire`` on the segment.  ``get_config_batch`` must return exactly
+what k sequential ``get_config`` calls return from the same RNG states.
+"""
+import numpy as np
+import pytest
+
+from oracle import kde_oracle as O
+from tests import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair_from_fixture(c):
+    from hpbandster_amd import kde
+    return kde.fit_pair_from_rows(c["X"], c["good_idx"], c["bad_idx"], c["var_type"], c["bw_good"], c["bw_bad"],
+                                  c["nlev_good"], c["nlev_bad"])
+
+
+@pytest.mark.parametrize("name", G.kde_case_names())
+@pytest.mark.parametrize("seg", [1, 7, 64])
+def test_batch_matches_reference_per_segment(device, name, seg):
+    c = G.load_kde_case(name)
+    pair = _pair_from_fixture(c)
+    C, S = c["cands"], c["scores"]
+    res = pair.acquire_batch(C, seg)
+    assert len(res) == (len(C) + seg - 1) // seg
+    for b, r in enumerate(res):
+        a, e = b * seg, min((b + 1) * seg, len(C))
+        assert r.index == O.py_argmin(S[a:e]), (name, seg, b)
+        if r.index >= 0:
+            np.testing.assert_allclose(r.score, S[a + r.index], rtol=1e-13)
+        if b % 5 == 0:  # the same call on the segment alone: bit-identical record
+            one = pair.acquire(C[a:e])
+            assert (one.index, one.shortlist, one.flags) == (r.index, r.shortlist, r.flags)
+            if one.index >= 0:
+                assert (one.score, one.pdf_l, one.pdf_g) == (r.score, r.pdf_l, r.pdf_g)
+
+
+def test_batch_edge_segments(device):
+    """NaN-only segment -> -1 for that call only; duplicates -> first index; ragged tail; empty."""
+    c = G.load_kde_case("mixed8")
+    pair = _pair_from_fixture(c)
+    C = c["cands"][:40].copy()
+    C[10:20] = np.nan                     # segment 1 (seg 10): no finite score
+    C[25] = C[22]                         # segment 2: duplicate of an earlier candidate
+    res = pair.acquire_batch(C[:37], 10)  # 4 segments, the last has 7
+    assert len(res) == 4
+    assert res[1].index == -1
+    S = np.array([O.py_score(l, g) for l, g in zip(
+        O.pdf_many(pair.good.data, pair.good.bw, c["var_type"], C[:37], pair.good.nlev),
+        O.pdf_many(pair.bad.data, pair.bad.bw, c["var_type"], C[:37], pair.bad.nlev))])
+    for b, r in enumerate(res):
+        a, e = b * 10, min(b * 10 + 10, 37)
+        assert r.index == O.py_argmin(S[a:e])
+    assert pair.acquire_batch(np.zeros((0, C.shape[1])), 8) == []
+
+
+def test_batch_at_bench_dims(device):
+    """100 calls x 64 candidates against 1e4 observations at D=32 (24c + 8u): every call's record
+    equals the separate acquisition of its segment."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(10000, 24, 8, 4)
+    L = S.make_losses(10000)
+    pair = kde.fit_pair(X, L, S.var_type_string(24, 8), 33, device=device)
+    C = S.make_candidates(6400, 24, 8, 4)
+    res = pair.acquire_batch(C, 64)
+    assert len(res) == 100
+    for b in range(0, 100, 3):
+        one = pair.acquire(C[64 * b:64 * b + 64])
+        r = res[b]
+        assert (one.index, one.score, one.pdf_l, one.pdf_g, one.shortlist) == \
+            (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist)
+
+
+def _fitted_bohb(device, seed):
+    from hpbandster_amd import configspace as CS
+    from hpbandster_amd.config_generators import BOHB
+    space = CS.ConfigurationSpace(seed=seed)
+    for i in range(3):
+        space.add_hyperparameter(CS.UniformFloatHyperparameter("x%d" % i, lower=-2, upper=3))
+    space.add_hyperparameter(CS.CategoricalHyperparameter("c", ["a", "b", "c", "d"]))
+    cg = BOHB(space, device=device, random_fraction=0.25, num_samples=32)
+
+    class Job(object):
+        pass
+
+    rs = np.random.RandomState(seed)
+    for k in range(40):
+        cfg = space.sample_configuration().get_dictionary()
+        j = Job()
+        j.id, j.kwargs, j.exception, j.timestamps = (0, 0, k), {"config": cfg, "budget": 1.0}, None, {}
+        j.result = {"loss": float(rs.rand()), "info": None}
+        cg.new_result(j)
+    assert len(cg.kde_models) == 1
+    return cg, space
+
+
+def test_get_config_batch_equals_sequential(device):
+    seq_cg, seq_space = _fitted_bohb(device, 11)
+    np.random.seed(7)
+    seq_space.seed(99)
+    seq = [seq_cg.get_config(1.0) for _ in range(30)]
+    after_seq = np.random.get_state()[1].copy(), np.random.get_state()[2]
+    bat_cg, bat_space = _fitted_bohb(device, 11)
+    np.random.seed(7)
+    bat_space.seed(99)
+    bat = bat_cg.get_config_batch(1.0, 30)
+    np.testing.assert_array_equal(np.random.get_state()[1], after_seq[0])  # same global RNG consumption
+    assert np.random.get_state()[2] == after_seq[1]
+    assert sum(i["model_based_pick"] for _, i in seq) >= 10
+    assert len(seq) == len(bat)
+    for (c1, i1), (c2, i2) in zip(seq, bat):
+        assert i1 == i2
+        assert c1 == c2

@@ -12,6 +12,6 @@ cat $OUT/smoke.log
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 3; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $OUT/trace.log 2>&1 || { echo rocprof failed; tail -20 $OUT/trace.log; exit 4; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-config5 > $OUT/trace.log 2>&1 || { echo rocprof failed; tail -20 $OUT/trace.log; exit 4; }
 find $OUT/trace -name '*stats*' | head -5
 echo check done
