@@ -209,6 +209,40 @@ def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
             "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
 
 
+def sampler_line(pair, device, dc, du, levels, Nc, ws, reps=10):
+    """Side measurement: BOHB's candidate rule for Nc candidates drawn on the GPU
+    (Philox + truncnorm inversion), alone and followed by the acquisition -- a whole model-based
+    get_config at Nc candidates.  HBM roofline of the sampler: 8 B written per (candidate, dim)."""
+    import torch
+    from hpbandster_amd import kde
+    lv = np.array([0] * dc + [levels] * du)
+    D = dc + du
+
+    def samp(k):
+        return pair.good.sample(lv, 3.0, Nc, seed=1234, counter_base=k * Nc)[0]
+
+    samp(0)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(reps):
+        samp(k + 1)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    t0 = time.perf_counter()
+    for k in range(reps):
+        r = pair.acquire(samp(k + 100), workspace=ws)
+    torch.cuda.synchronize()
+    ms_e2e = (time.perf_counter() - t0) / reps * 1e3
+    gbs = Nc * D * 8 / (ms * 1e-3) / 1e9
+    return {"workload": "gpu_sampler_cand%d_d%d" % (Nc, D), "ms_per_launch": ms,
+            "candidates_per_s": Nc / (ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
+                         "bytes_per_element": 8},
+            "ms_sample_plus_acquire": ms_e2e, "last_winner": r.index}
+
+
 def kde_result_bytes():
     from hpbandster_amd import kde
     return kde.RESULT_BYTES
@@ -357,6 +391,10 @@ def main():
             out["batched_acquisition"] = batched(pair, device, a.dc, a.du, a.levels)
         except Exception as e:
             out["batched_acquisition"] = {"error": repr(e)}
+        try:
+            out["gpu_sampler"] = sampler_line(pair, device, a.dc, a.du, a.levels, Nc, ws)
+        except Exception as e:
+            out["gpu_sampler"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),

@@ -28,8 +28,19 @@ from ._cs import ConfigSpace
 
 class BOHB(base_config_generator):
     def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
-                 random_fraction=1 / 3, bandwidth_factor=3, device=None, **kwargs):
+                 random_fraction=1 / 3, bandwidth_factor=3, device=None, sampler="host", sampler_seed=None,
+                 **kwargs):
         super().__init__(**kwargs)
+        # sampler 'host': the reference's draws from the global numpy RNG (seeded runs reproduce the
+        # reference's proposals); 'gpu': the same rule drawn on the GPU from a Philox stream
+        # (distributional parity; for large num_samples, where host sampling dominates)
+        if sampler not in ("host", "gpu"):
+            raise ValueError("sampler must be 'host' or 'gpu'")
+        self.sampler = sampler
+        if sampler_seed is None and sampler == "gpu":
+            sampler_seed = int.from_bytes(np.random.bytes(8), "little")
+        self.sampler_seed = sampler_seed
+        self._sample_counter = 0
         self.top_n_percent = top_n_percent
         self.configspace = configspace
         self.bw_factor = bandwidth_factor
@@ -78,6 +89,16 @@ class BOHB(base_config_generator):
                         cands[i, d] = np.random.randint(t)
         return cands
 
+    def draw_candidates(self, pair, num_samples):
+        """Candidates of one get_config call (or of several back to back): host numpy array, or with
+        the GPU sampler a device tensor plus its per-candidate domain-error flags."""
+        if self.sampler == "host":
+            return self.sample_candidates(pair['good'], num_samples), None
+        cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, num_samples, self.sampler_seed,
+                                            self._sample_counter)
+        self._sample_counter += num_samples
+        return cands, err
+
     def get_config(self, budget):
         sample = None
         info_dict = {}
@@ -89,8 +110,10 @@ class BOHB(base_config_generator):
             try:
                 budget = max(self.kde_models.keys())  # always the largest-budget model (bohb.py:124)
                 pair = self.kde_models[budget]        # immutable snapshot (new_result swaps entries)
-                cands = self.sample_candidates(pair['good'], self.num_samples)
+                cands, err = self.draw_candidates(pair, self.num_samples)
                 res = pair.acquire(cands)
+                if err is not None and bool(err.any()):
+                    raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
                 if res.index < 0:
                     self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
                                       % self.num_samples)
@@ -98,6 +121,8 @@ class BOHB(base_config_generator):
                     info_dict['model_based_pick'] = False
                 else:
                     best_vector = cands[res.index]
+                    if err is not None:
+                        best_vector = best_vector.cpu().numpy()
                     self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
                     sample = ConfigSpace.Configuration(self.configspace, vector=best_vector).get_dictionary()
                     info_dict['model_based_pick'] = True
@@ -129,10 +154,14 @@ class BOHB(base_config_generator):
             if pair is None:
                 pair = self.kde_models[max(self.kde_models.keys())]  # bohb.py:124
             plan.append(len(blocks) * self.num_samples)
-            blocks.append(self.sample_candidates(pair['good'], self.num_samples))
-        results = []
+            blocks.append(None if self.sampler == "gpu" else self.sample_candidates(pair['good'], self.num_samples))
+        results, bad = [], None
         if blocks:
-            cands = np.concatenate(blocks, axis=0)
+            if self.sampler == "gpu":  # one draw for all calls: same Philox counters as call by call
+                cands, err = self.draw_candidates(pair, len(blocks) * self.num_samples)
+                bad = err.view(len(blocks), self.num_samples).any(dim=1).cpu().numpy()
+            else:
+                cands = np.concatenate(blocks, axis=0)
             results = pair.acquire_batch(cands, self.num_samples)
         out = []
         for off in plan:
@@ -140,12 +169,18 @@ class BOHB(base_config_generator):
                 out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
                 continue
             res = results[off // self.num_samples]
-            if res.index < 0:
+            if bad is not None and bad[off // self.num_samples]:
+                self.logger.warning("Sampling based optimization with %i samples failed (truncnorm domain error)"
+                                    "\nUsing random configuration" % self.num_samples)
+                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
+            elif res.index < 0:
                 self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
                                   % self.num_samples)
                 out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
             else:
                 vec = cands[off + res.index]
+                if bad is not None:
+                    vec = vec.cpu().numpy()
                 out.append((ConfigSpace.Configuration(self.configspace, vector=vec).get_dictionary(),
                             {'model_based_pick': True}))
         return out

@@ -273,9 +273,10 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
 // ------------------------------------------------------------------------------------------
 // score intervals, shortlist, exact re-score, final argmin
 
-__global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, AcqResult* res) {
+__global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1, AcqResult* res) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     *U = hbx_f2ord(INFINITY);
+    *first1 = INT32_MAX;
     *count = 0;
     *flags = 0;
     res->index = -1;
@@ -291,13 +292,15 @@ __global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, Acq
 // batched acquisition: per-segment bound, flags, shortlist count, best score and (index, position) key
 __global__ void acq_init_batch_kernel(int64_t B, uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                       int32_t* __restrict__ segcnt, uint64_t* __restrict__ best,
-                                      uint64_t* __restrict__ key, int32_t* __restrict__ count) {
+                                      uint64_t* __restrict__ key, int32_t* __restrict__ first1,
+                                      int32_t* __restrict__ count) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) *count = 0;
   if (b < B) {
     U[b] = hbx_f2ord(INFINITY);
     flags[b] = 0;
     segcnt[b] = 0;
+    first1[b] = INT32_MAX;
     best[b] = ~0ull;
     key[b] = ~0ull;
   }
@@ -319,13 +322,18 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 
 // Candidates [b*seg, (b+1)*seg) form acquisition b (seg = Nc: one acquisition).  U[b] = min over the
 // segment of the upper score bound, flags[b] bit 0 = overflow risk (re-score the whole segment).
+// Candidates whose l and g are both certainly below 1e-8 score exactly 1e-8/1e-8 = 1 (bohb.py:129):
+// they tie, so only the first of them per segment (first1[b]) can win and needs the exact re-score
+// (BOHB's own sampler puts most candidates there at D = 32: the truncnorm scale is 3 bw).
 __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
                                                           const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo, float* __restrict__ hi,
-                                                          uint32_t* __restrict__ U, int32_t* __restrict__ flags) {
+                                                          uint32_t* __restrict__ U, int32_t* __restrict__ flags,
+                                                          int32_t* __restrict__ first1) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   float h = INFINITY;
+  bool one = false;
   const uint32_t sg = (uint32_t)(i < Nc ? i : Nc - 1) / seg;
   if (i < Nc) {
     const KdeEst a = el[i], b = eg[i];
@@ -354,6 +362,12 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
       slo = Glo - fmaxf(lhi, C);
       shi = Ghi - fmaxf(llo, C);
       h = shi;
+      const float C1 = C - 1e-4f;  // margin for the rounding of ln(1e-8) to float
+      if (lhi < C1 && (b.lpos != b.lpos || ghi < C1)) {  // both clamped: score exactly 1 (ln 0)
+        one = true;
+        slo = NAN;  // excluded from the shortlist unless it is the segment's first exact tie
+        shi = h = 0.f;
+      }
     }
     if (logl) logl[i] = lpt;
     if (logg) logg[i] = gpt;
@@ -361,13 +375,45 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
     hi[i] = shi;
     if (of) atomicOr(flags + sg, 1);
   }
-  // min of hi per segment: wave reduction when the wave lies in one segment, else per lane
+  // min of hi and first exact tie per segment.  Same-address atomics serialise in L2 (~10 ns each),
+  // so: block reduction when the block lies in one segment (the common case), one wave-level atomic
+  // when the wave does, per lane otherwise; and an atomic only when it can still lower the value.
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t blk0 = (int64_t)blockIdx.x * 256;
+  const int64_t blk1 = (blk0 + 255 < Nc ? blk0 + 255 : Nc - 1);
+  auto lower_u = [&](uint32_t sgi, float hv) {
+    const uint32_t o = hbx_f2ord(hv);
+    if (hv < INFINITY && o < __hip_atomic_load(U + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(U + sgi, o);
+  };
+  auto lower_first = [&](uint32_t sgi, int32_t iv) {
+    if (iv < __hip_atomic_load(first1 + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(first1 + sgi, iv);
+  };
   const uint32_t s0 = __shfl(sg, 0), s63 = __shfl(sg, 63);
   if (s0 == s63) {
     for (int o = 32; o > 0; o >>= 1) h = fminf(h, __shfl_xor(h, o));
-    if ((threadIdx.x & 63) == 0 && h < INFINITY) atomicMin(U + sg, hbx_f2ord(h));
-  } else if (h < INFINITY) {
-    atomicMin(U + sg, hbx_f2ord(h));
+    const uint64_t ones = __ballot(one);
+    const int32_t f1 = ones ? (int32_t)(blk0 + 64 * wv + __ffsll((long long)ones) - 1) : INT32_MAX;
+    if ((uint32_t)(blk0 / seg) == (uint32_t)(blk1 / seg)) {
+      __shared__ float rh[4];
+      __shared__ int32_t rf[4];
+      if (lane == 0) {
+        rh[wv] = h;
+        rf[wv] = f1;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float hb = fminf(fminf(rh[0], rh[1]), fminf(rh[2], rh[3]));
+        const int32_t fb = min(min(rf[0], rf[1]), min(rf[2], rf[3]));
+        lower_u(sg, hb);
+        if (fb != INT32_MAX) lower_first(sg, fb);
+      }
+    } else if (lane == 0) {
+      lower_u(sg, h);
+      if (f1 != INT32_MAX) lower_first(sg, f1);
+    }
+  } else {
+    lower_u(sg, h);
+    if (one) lower_first(sg, (int32_t)i);
   }
 }
 
@@ -376,14 +422,15 @@ __global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restr
                                                             const int32_t* __restrict__ flags,
                                                             int32_t* __restrict__ list,
                                                             int32_t* __restrict__ count,
-                                                            int32_t* __restrict__ segcnt) {
+                                                            int32_t* __restrict__ segcnt,
+                                                            const int32_t* __restrict__ first1) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= Nc) return;
   const uint32_t sg = (uint32_t)i / seg;
   const float u = hbx_ord2f(U[sg]);
   const bool all = (flags[sg] & 1) != 0;
   const float l = lo[i];
-  if (l == l && (all || l <= u)) {
+  if ((l == l && (all || l <= u)) || (int32_t)i == first1[sg]) {
     const int pos = atomicAdd(count, 1);
     list[pos] = (int32_t)i;
     if (segcnt) atomicAdd(segcnt + sg, 1);
@@ -795,7 +842,7 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 // of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
 // comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t res, U, count, flags, segcnt, best, key, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
+  size_t res, U, count, flags, segcnt, best, key, first1, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
 };
 
 static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
@@ -813,6 +860,7 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.segcnt = take(4 * B);
   w.best = take(8 * B);
   w.key = take(8 * B);
+  w.first1 = take(4 * B);
   w.est_l = take(sizeof(KdeEst) * Nc);
   w.est_g = take(sizeof(KdeEst) * Nc);
   w.lo = take(4 * Nc);
@@ -1080,6 +1128,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   int32_t* segcnt = (int32_t*)(ws + w.segcnt);
   uint64_t* best = (uint64_t*)(ws + w.best);
   uint64_t* key = (uint64_t*)(ws + w.key);
+  int32_t* first1 = (int32_t*)(ws + w.first1);
   AcqResult* res = (AcqResult*)(ws + w.res);
   KdeEst* el = (KdeEst*)(ws + w.est_l);
   KdeEst* eg = (KdeEst*)(ws + w.est_g);
@@ -1094,9 +1143,9 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   if (B == 0) return HBX_OK;  // batched call without candidates: no records
   if (batch_res)
     hipLaunchKernelGGL(acq_init_batch_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, U, flags,
-                       segcnt, best, key, count);
+                       segcnt, best, key, first1, count);
   else
-    hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, res);
+    hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res);
   HBX_LAUNCH_CHECK();
   const dim3 grid((unsigned)((Nc + 255) / 256));
   if (Nc > 0) {
@@ -1109,10 +1158,10 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     if (rc) return rc;
     if (ev) HBX_HIP(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
-                       flags);
+                       flags, first1);
     HBX_LAUNCH_CHECK();
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
-                       batch_res ? segcnt : (int32_t*)nullptr);
+                       batch_res ? segcnt : (int32_t*)nullptr, first1);
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
     hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_THREADS), 0, s, cand, D,

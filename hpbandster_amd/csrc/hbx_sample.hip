@@ -1,0 +1,230 @@
+// hbx_sample.hip -- BOHB's candidate sampler on the GPU (bohb.py:133-147).
+//
+// Per candidate i: a good observation idx ~ U{0..n-1} (bohb.py:135), then per dim d of its row m:
+//   continuous (levels[d] == 0): truncnorm.rvs(a=-m/bw, b=(1-m)/bw, loc=m, scale=bw_factor*bw)
+//     (bohb.py:141).  The bounds are in units of bw while the scale is bw_factor*bw, so the sample
+//     lies in [m - bw_factor*m, m + bw_factor*(1-m)] -- the reference's quirk, kept as is;
+//   categorical (levels[d] = t): keep m with probability 1 - bw, else U{0..t-1} (bohb.py:143-146).
+// The truncated normal is drawn by inversion, z = Phi^-1(Phi(a) + u (Phi(b) - Phi(a))), evaluated on
+// the lower side (a > 0 is mirrored) so the tail probabilities keep their relative precision.
+// Random numbers: Philox4x32-10 keyed by the seed; counter = (candidate index, dim, stream) -- the
+// reference draws from numpy's global RNG, so parity is distributional (tests/test_gpu_sample.py).
+//
+// One thread per (candidate, dim) element: the writes of a wave are contiguous (8 B per element).
+// The datum draws of a block's candidates go through LDS; Phi at the bounds comes from a per-model
+// table when many candidates are drawn (hbx_kde_sample_table), so a draw costs one Philox block and
+// one normcdfinv.
+#include <math.h>
+
+#include "hbx_common.h"
+#include "hbx_philox.h"
+
+#define SAMPLE_BLOCK 256
+#define HBX_INV_SQRT_2PI_D 0.3989422804014327
+// diagnostic ablations (tools/ablate_sample.sh; never the shipped default): 1 = no normcdfinv,
+// 2 = no per-element Philox, 3 = both.  Timing only.
+#ifndef HBX_S_ABLATE
+#define HBX_S_ABLATE 0
+#endif
+#define DATUM_WORD 0xFFFFFFFFu  // counter word of the per-candidate datum draw (dims use 0..D-1)
+
+__device__ __forceinline__ HbxU32x4 draw(uint64_t seed, uint64_t i, uint32_t word, uint32_t stream) {
+  HbxU32x4 c;
+  c.x[0] = (uint32_t)i;
+  c.x[1] = (uint32_t)(i >> 32);
+  c.x[2] = word;
+  c.x[3] = stream;
+  return hbx_philox4x32_10_impl(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// Standardised bounds of a continuous dim around datum m, mirrored so that lo <= 0 side is used
+// (a > 0 -> sample -z from [-b, -a]); false when scipy's a < b check fails.
+__device__ __forceinline__ bool tn_bounds(double m, double h, double* lo, double* hi, bool* flip) {
+  const double a = -m / h, b = (1.0 - m) / h;
+  if (!(a < b)) return false;
+  *flip = a > 0.0;
+  *lo = *flip ? -b : a;
+  *hi = *flip ? -a : b;
+  return true;
+}
+
+// Phi^-1(p), p in (0, 1), in double precision at a fraction of ocml's normcdfinv (which dominated
+// the sampler: 1.15 of 1.38 ms at 1e6 x 32): solve on the lower side Phi(w) = q = min(p, 1-p) from
+// the fp32 normcdfinvf guess (relative error ~1e-7; an Abramowitz-Stegun 26.2.23 guess below fp32
+// range, refined by an extra step), then one Halley step in double (cubic: the guess error cubed is
+// below double rounding).
+__device__ __forceinline__ double norm_ppf(double p) {
+  const bool up = p > 0.5;
+  const double q = up ? 1.0 - p : p;  // exact for p >= 0.5 (Sterbenz)
+  double w;
+  if (q > 1e-37) {
+    w = (double)normcdfinvf((float)q);
+  } else {
+    const double t = sqrt(-2.0 * log(q));
+    w = -(t - (2.515517 + t * (0.802853 + t * 0.010328)) / (1.0 + t * (1.432788 + t * (0.189269 + t * 0.001308))));
+    const double d0 = (normcdf(w) - q) / (HBX_INV_SQRT_2PI_D * exp(-0.5 * w * w));  // |error| < 4.5e-4: one
+    w -= d0 / (1.0 + 0.5 * w * d0);                                                   // more Halley step
+  }
+  const double f = normcdf(w) - q;
+  const double d = f / (HBX_INV_SQRT_2PI_D * exp(-0.5 * w * w));
+  w -= d / (1.0 + 0.5 * w * d);
+  return up ? -w : w;
+}
+
+// z = Phi^-1(Phi(lo) + u (Phi(hi) - Phi(lo))) clamped to [lo, hi]
+__device__ __forceinline__ double tn_invert(double plo, double phi, double lo, double hi, double u) {
+  const double z = norm_ppf(fma(u, phi - plo, plo));
+  return fmin(fmax(z, lo), hi);
+}
+
+__global__ void norm_ppf_kernel(const double* __restrict__ p, int64_t n, double* __restrict__ z) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) z[i] = norm_ppf(p[i]);
+}
+
+// Per (datum j, dim d) constants of the continuous dims: {Phi(lo), Phi(hi)} (NaN pair: domain error;
+// the sign of Phi(hi) - Phi(lo) is unused).  A property of the good KDE, computed once per model when
+// many candidates are drawn from it (the two normcdf calls dominate a draw otherwise).
+__global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_table_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
+    const double* __restrict__ bw, const int32_t* __restrict__ levels, double2* __restrict__ tab) {
+  const int64_t total = n * (int64_t)D;
+  for (int64_t e = (int64_t)blockIdx.x * SAMPLE_BLOCK + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * SAMPLE_BLOCK) {
+    const int64_t j = e / D;
+    const int d = (int)(e - j * D);
+    double2 r = make_double2(0.0, 0.0);
+    if (levels[d] == 0) {
+      double lo, hi;
+      bool flip;
+      if (tn_bounds(X[rows[j] * (int64_t)D + d], bw[d], &lo, &hi, &flip))
+        r = make_double2(normcdf(lo), normcdf(hi));
+      else
+        r = make_double2(NAN, NAN);
+    }
+    tab[e] = r;
+  }
+}
+
+// One thread per (candidate, dim) element; a block covers SAMPLE_BLOCK consecutive elements and first
+// draws the datum of each candidate they touch into LDS (one Philox call per candidate, not per
+// element).  IDX is uint32_t when Nc * D < 2^32 (cheap index division) else uint64_t.
+template <typename IDX>
+__global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
+    const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
+    double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
+    double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
+  __shared__ int32_t sdat[SAMPLE_BLOCK + 1];
+  const IDX total = (IDX)(Nc * (int64_t)D), Dd = (IDX)D;
+  for (IDX base = (IDX)blockIdx.x * SAMPLE_BLOCK; base < total; base += (IDX)gridDim.x * SAMPLE_BLOCK) {
+    const IDX c0 = base / Dd;
+    const IDX last = (base + SAMPLE_BLOCK < total ? base + SAMPLE_BLOCK : total) - 1;
+    const int nc = (int)(last / Dd - c0) + 1;
+    for (int t = threadIdx.x; t < nc; t += SAMPLE_BLOCK) {
+      const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)(c0 + t), DATUM_WORD, stream_id), 0);
+      const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
+      sdat[t] = idx;
+      if (datum) datum[c0 + t] = idx;
+    }
+    __syncthreads();
+    const IDX e = base + threadIdx.x;
+    if (e < total) {
+      const IDX i = e / Dd;
+      const int d = (int)(e - i * Dd);
+      const int32_t idx = sdat[i - c0];
+      const double m = X[rows[idx] * (int64_t)D + d];
+      const double h = bw[d];
+      const int t = levels[d];
+      HbxU32x4 r;
+      if (HBX_S_ABLATE & 2) {
+        r.x[0] = (uint32_t)e * 0x9E3779B9u; r.x[1] = (uint32_t)e ^ 0x85EBCA6Bu;
+        r.x[2] = r.x[0] ^ 0xC2B2AE35u; r.x[3] = r.x[1] * 3u;
+      } else {
+        r = draw(seed, counter_base + (uint64_t)i, (uint32_t)d, stream_id);
+      }
+      const double u = hbx_u01_open(hbx_bits64(r, 0));
+      double v;
+      if (t == 0) {
+        double lo, hi;
+        bool flip;
+        if (!tn_bounds(m, h, &lo, &hi, &flip)) {  // scipy's argcheck fails: the reference call raises
+          v = NAN;
+          if (domain_err) domain_err[i] = 1;
+        } else {
+          double plo, phi;
+          if (tab) {
+            const double2 p = tab[(int64_t)idx * D + d];
+            plo = p.x;
+            phi = p.y;
+          } else {
+            plo = normcdf(lo);
+            phi = normcdf(hi);
+          }
+          const double z = (HBX_S_ABLATE & 1) ? fma(u, hi - lo, lo) + 0.0 * (plo + phi) : tn_invert(plo, phi, lo, hi, u);
+          v = fma(bw_factor * h, flip ? -z : z, m);
+        }
+      } else {
+        v = (u < 1.0 - h) ? m : (double)(int64_t)__umul64hi(hbx_bits64(r, 1), (uint64_t)t);
+      }
+      cands[e] = v;
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" {
+
+int hbx_philox4x32_10(const uint32_t* counter, const uint32_t* key, uint32_t* out) {
+  if (!counter || !key || !out) return hbx_fail(HBX_ERR_ARG, "hbx_philox4x32_10: null pointer");
+  HbxU32x4 c;
+  for (int k = 0; k < 4; ++k) c.x[k] = counter[k];
+  const HbxU32x4 r = hbx_philox4x32_10_impl(c, key[0], key[1]);
+  for (int k = 0; k < 4; ++k) out[k] = r.x[k];
+  return HBX_OK;
+}
+
+int hbx_norm_ppf(const double* p, int64_t n, double* z, void* stream) {
+  if (n < 0 || (n > 0 && (!p || !z))) return hbx_fail(HBX_ERR_ARG, "hbx_norm_ppf: bad arguments");
+  if (n == 0) return HBX_OK;
+  hipLaunchKernelGGL(norm_ppf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p, n, z);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+int64_t hbx_kde_sample_table_bytes(int64_t n, int32_t D) { return n * (int64_t)D * 16; }
+
+int hbx_kde_sample_table(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
+                         const int32_t* levels, double* tab, void* stream) {
+  if (n < 1 || D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample_table: n=%lld D=%d", (long long)n, D);
+  if (!X || !rows || !bw || !levels || !tab) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample_table: null pointer");
+  const int64_t blocks = (n * (int64_t)D + SAMPLE_BLOCK - 1) / SAMPLE_BLOCK;
+  hipLaunchKernelGGL(kde_sample_table_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(SAMPLE_BLOCK),
+                     0, (hipStream_t)stream, X, D, rows, n, bw, levels, (double2*)tab);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
+                   const int32_t* levels, const double* tab, double bw_factor, uint64_t seed, uint64_t counter_base,
+                   uint32_t stream_id, int64_t Nc, double* cands, int64_t* datum, uint8_t* domain_err, void* stream) {
+  if (Nc < 0 || D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld D=%d", (long long)Nc, D);
+  if (Nc == 0) return HBX_OK;
+  if (!X || !rows || !bw || !levels || !cands) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: null pointer");
+  if (n < 1 || n > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: n=%lld observations", (long long)n);
+  hipStream_t s = (hipStream_t)stream;
+  if (domain_err) HBX_HIP(hipMemsetAsync(domain_err, 0, (size_t)Nc, s));
+  const int64_t total = Nc * (int64_t)D;
+  const int64_t blocks = (total + SAMPLE_BLOCK - 1) / SAMPLE_BLOCK;
+  const unsigned grid = (unsigned)(blocks < 65536 ? blocks : 65536);
+  if (total + SAMPLE_BLOCK < (int64_t)UINT32_MAX)
+    hipLaunchKernelGGL(kde_sample_kernel<uint32_t>, dim3(grid), dim3(SAMPLE_BLOCK), 0, s, X, D, rows, n, bw, levels,
+                       (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
+  else
+    hipLaunchKernelGGL(kde_sample_kernel<uint64_t>, dim3(grid), dim3(SAMPLE_BLOCK), 0, s, X, D, rows, n, bw, levels,
+                       (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+}  // extern "C"

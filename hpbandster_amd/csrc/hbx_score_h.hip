@@ -256,6 +256,40 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     }
   };
 
+  // Per-candidate shift: the exponent's maximum over chunk 0 (a lower bound of the maximum over all
+  // observations) is moved to 0 through the accumulator input.  Without it candidates far from every
+  // observation -- most of what BOHB's own sampler proposes at D = 32, where the truncnorm scale is
+  // 3 bw -- would underflow fp32 against the static bound M0 and need the slow rescue pass.  Terms of
+  // later chunks can exceed the probe's maximum; a sum that leaves [2^-64, 2^100] still takes the
+  // rescue.  Costs one chunk of MFMAs (no exp2) per block.
+  float dl[RT][4];
+  {
+    f32x4 acc[RT], accp[RT];
+    float mx[RT][4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx[r][q] = -INFINITY;
+#pragma unroll
+    for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
+      tile(lds, jt, acc, accp);
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mx[r][q] = fmaxf(mx[r][q], acc[r][q]);
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) mx[r][q] = fmaxf(mx[r][q], __shfl_xor(mx[r][q], o));
+        const float d = rintf(-mx[r][q]);
+        dl[r][q] = (HBX_H_ABLATE == 0 && d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
+        ciq[r][q] += dl[r][q];
+      }
+  }
+
   for (int c = 0; c < nchunks; ++c) {
     const float* buf = lds + (HBX_H_ABLATE == 3 ? 0 : (c % NBUF)) * CHF;
     if (HBX_H_ABLATE != 3) issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
@@ -336,17 +370,19 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
       const float s0 = S[r][0], s1 = S[r][1], s2 = S[r][2], s3 = S[r][3];
       const float n0 = Sn[r][0], n1 = Sn[r][1], n2 = Sn[r][2], n3 = Sn[r][3];
       const float Sq = b1 ? (b0 ? s3 : s2) : (b0 ? s1 : s0);
+      const float dq = b1 ? (b0 ? dl[r][3] : dl[r][2]) : (b0 ? dl[r][1] : dl[r][0]);
       const float Snq = b1 ? (b0 ? n3 : n2) : (b0 ? n1 : n0);
       if (ii < Nc) {
         const double* x = cand + ii * (int64_t)D;
         bool nq = P->nan_all != 0;
         for (int cc = 0; cc < P->nconst; ++cc)
           if (x[P->const_dim[cc]] != P->const_level[cc]) nq = true;
-        KdeEst o = finish_est(P, Sq, Snq, 0.f, nq, ci_q, bnd_q, SIGNED, OBS_CHUNK / 16);
+        // S carries the factor 2^dq; |c_i| + dq bounds the rounding of the shifted accumulator input
+        KdeEst o = finish_est(P, Sq, Snq, -dq, nq, ci_q - dq, bnd_q, SIGNED, OBS_CHUNK / 16);
         // f16 hi/lo representation error of both coordinates and the three lo.lo products given up
         // to the C_j pieces (each <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
         if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-20f) * HBX_LN2f;
-        if (!nq && Sq == Sq && Sq < 0x1p-64f && HBX_H_ABLATE == 0) o.err = -1.f;
+        if (!nq && Sq == Sq && (Sq < 0x1p-64f || Sq > 0x1p100f) && HBX_H_ABLATE == 0) o.err = -1.f;
         out[ii] = o;
       }
     }

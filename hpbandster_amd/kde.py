@@ -129,6 +129,45 @@ class DeviceKDE(object):
                                     N.stream_handle(stream)))
         return np.squeeze(out.cpu().numpy())
 
+    def sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id=0, stream=None, table=None):
+        """BOHB's candidate rule around this (good) KDE's observations, on the GPU (bohb.py:133-147).
+
+        ``levels``: per dim 0 (continuous) or the number of choices.  Candidate i draws from the
+        Philox stream (seed, counter_base + i, stream_id).  Returns (cands [Nc, D] f64, datum [Nc] i64,
+        domain_err [Nc] u8) device tensors."""
+        torch = _torch()
+        L = N.lib()
+        D = self.k_vars
+        if getattr(self, "_bw_dev", None) is None:
+            self._bw_dev = torch.from_numpy(np.ascontiguousarray(self.bw, dtype=np.float64)).to(self.device)
+        lv = np.ascontiguousarray(np.asarray(levels, dtype=np.int32))
+        if lv.shape != (D,):
+            raise N.HbxError("levels must have %d entries" % D)
+        key = lv.tobytes()
+        if getattr(self, "_lv_key", None) != key:
+            self._lv_dev, self._lv_key = torch.from_numpy(lv).to(self.device), key
+            self._tab = None
+        Nc = int(Nc)
+        if table is None:
+            table = Nc >= 4 * self.nobs  # the Phi table pays off when draws outnumber (row, dim) pairs
+        tab = None
+        if table:
+            if getattr(self, "_tab", None) is None:
+                self._tab = torch.empty(int(L.hbx_kde_sample_table_bytes(self.nobs, D)) // 8, dtype=torch.float64,
+                                        device=self.device)
+                N.check(L.hbx_kde_sample_table(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs,
+                                               N.ptr(self._bw_dev), N.ptr(self._lv_dev), N.ptr(self._tab),
+                                               N.stream_handle(stream)))
+            tab = self._tab
+        cands = torch.empty((Nc, D), dtype=torch.float64, device=self.device)
+        datum = torch.empty(Nc, dtype=torch.int64, device=self.device)
+        err = torch.empty(Nc, dtype=torch.uint8, device=self.device)
+        N.check(L.hbx_kde_sample(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs, N.ptr(self._bw_dev),
+                                 N.ptr(self._lv_dev), N.ptr(tab), float(bw_factor), int(seed) & (2 ** 64 - 1),
+                                 int(counter_base) & (2 ** 64 - 1), int(stream_id) & 0xFFFFFFFF, Nc, N.ptr(cands),
+                                 N.ptr(datum), N.ptr(err), N.stream_handle(stream)))
+        return cands, datum, err
+
     def logpdf_est(self, cand_dev, stream=None):
         """fp32 log-domain estimate per candidate -> (lpos, lneg, err) numpy arrays."""
         torch = _torch()

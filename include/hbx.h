@@ -136,6 +136,32 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
                       const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
                       void* stream);
 
+/* ---- candidate sampler (bohb.py:133-147, on the GPU) --------------------------------------- */
+/* Philox4x32-10 block function (host): out[4] = philox(counter[4], key[2]).  Exposed for the
+ * known-answer tests of the generator the sampler uses. */
+int hbx_philox4x32_10(const uint32_t* counter, const uint32_t* key, uint32_t* out);
+
+/* Nc candidates around the good KDE's observations, BOHB's rule: datum = rows[U{0..n-1}], then per
+ * dim truncnorm(-m/bw, (1-m)/bw, loc=m, scale=bw_factor*bw) (levels[d] == 0) or keep-with-prob-(1-bw)
+ * / U{0..t-1} (levels[d] = t).  X: device f64[*][D]; rows: device i64[n] (the good KDE's rows);
+ * bw: device f64[D]; levels: device i32[D].  Candidate i uses Philox counter (counter_base + i, dim,
+ * stream_id) under key = seed, so consecutive calls with advancing counter_base equal one call over
+ * the union.  cands: device f64[Nc][D]; datum: nullable device i64[Nc] (drawn row positions);
+ * domain_err: nullable device u8[Nc], 1 where a continuous dim's bounds fail scipy's a < b check
+ * (the reference's call raises and falls back to a random configuration). */
+int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
+                   const int32_t* levels, const double* tab, double bw_factor, uint64_t seed, uint64_t counter_base,
+                   uint32_t stream_id, int64_t Nc, double* cands, int64_t* datum, uint8_t* domain_err, void* stream);
+/* Standard normal quantile Phi^-1 (device f64[n] -> device f64[n]), the sampler's inversion
+ * routine (scipy.special.ndtri semantics on (0, 1)). */
+int hbx_norm_ppf(const double* p, int64_t n, double* z, void* stream);
+/* Optional per-model table for hbx_kde_sample (`tab`, nullable): Phi at the standardised truncnorm
+ * bounds of every (good row, continuous dim), device f64[hbx_kde_sample_table_bytes(n, D) / 8].  Same
+ * draws with or without it; it saves two normcdf per draw when Nc >> n. */
+int64_t hbx_kde_sample_table_bytes(int64_t n, int32_t D);
+int hbx_kde_sample_table(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
+                         const int32_t* levels, double* tab, void* stream);
+
 /* ---- successive-halving promotion -------------------------------------------------------- */
 /* advance[i] = rank_i < k[b] among the finite losses of bracket b (non-finite = CRASHED, never
  * advance).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B]; order: device

@@ -54,3 +54,21 @@ def test_errors_are_reported_not_swallowed():
     assert rc == -1
     with pytest.raises(N.HbxError):
         N.check(rc)
+
+
+# Philox4x32-10 known-answer vectors (Random123 kat_vectors: counter, key -> output)
+PHILOX_KAT = [
+    ([0, 0, 0, 0], [0, 0], [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]),
+    ([0xffffffff] * 4, [0xffffffff] * 2, [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]),
+    ([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0],
+     [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]),
+]
+
+
+@pytest.mark.parametrize("ctr,key,want", PHILOX_KAT)
+def test_philox_known_answers(ctr, key, want):
+    """The sampler's generator (hbx_philox.h, host build of the same function the kernel uses)."""
+    from hpbandster_amd import _native as N
+    c, k, o = np.array(ctr, np.uint32), np.array(key, np.uint32), np.zeros(4, np.uint32)
+    N.check(N.lib().hbx_philox4x32_10(N.ptr(c), N.ptr(k), N.ptr(o)))
+    assert [int(v) for v in o] == want

@@ -254,3 +254,32 @@ def test_hmode_categorical_layouts_match_oracle(device, dc, levels):
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
     assert res.index == O.select(l, g)[0]
+
+
+def test_clamped_ties_score_one_first_index(device):
+    """Candidates whose l and g are both below 1e-8 score exactly max(1e-8,g)/max(l,1e-8) = 1
+    (bohb.py:129) and tie; the first of them wins unless some candidate scores below 1.  Only the
+    first tie needs the exact re-score, so the shortlist stays small (BOHB's sampler at D=32 puts
+    most candidates there)."""
+    from hpbandster_amd import kde
+    rs = np.random.RandomState(8)
+    D = 12
+    X = rs.rand(400, D)
+    L = rs.rand(400)
+    pair = kde.fit_pair(X, L, "c" * D, D + 1, device=device)
+    far = 5.0 + rs.rand(3000, D)  # pdf underflows for both KDEs
+    res = pair.acquire(far)
+    assert res.index == 0 and res.score == 1.0
+    assert res.shortlist <= 2
+    near = pair.good.data[:3] + 1e-3
+    C = np.vstack([far[:1000], near, far[1000:]])
+    l = O.pdf_many(pair.good.data, pair.good.bw, "c" * D, C)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, "c" * D, C)
+    want, scores = O.select(l, g)
+    res = pair.acquire(C)
+    assert res.index == want
+    assert res.shortlist <= 10
+    # batched: a far-only segment and a mixed one
+    rb = pair.acquire_batch(np.vstack([far[:500], C[800:1300]]), 500)
+    assert rb[0].index == 0 and rb[0].score == 1.0
+    assert rb[1].index == O.py_argmin(scores[800:1300])
