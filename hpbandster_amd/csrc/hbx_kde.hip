@@ -791,6 +791,7 @@ __global__ __launch_bounds__(256) void kde_batch_final_kernel(int64_t B, const u
 struct ScoreFns {
   logpdf_fn main, rescue;
   int cands_per_block;
+  int threads;
 };
 
 template <bool SG>
@@ -815,22 +816,29 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const bool hm = (variant >> 4) & 1;
   int dcp, dup;
   bucket_dims(dc_pad, du_pad, &dcp, &dup);
-  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0};  // not a bucket
+  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm) {
-    if (dc_pad < 16) return {nullptr, nullptr, 0};
-    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * MFMA_WAVES * H_ROW_TILES};
+    if (dc_pad < 16) return {nullptr, nullptr, 0, 0};
+    // the 16x16-tile kernel; HBX_SCORE_TILE=32 selects the 32x32-tile variant for unsigned sums (an
+    // experiment: fewer issue cycles per pair on paper, slower as measured -- DESIGN.md section 4)
+    const char* tenv = getenv("HBX_SCORE_TILE");  // read per call (tests switch it in-process)
+    const bool t32 = tenv && atoi(tenv) == 32;
+    if (!sg && t32) {
+      const logpdf_fn f = hbx_pick_h32(nsc_of(dc_pad), kc);
+      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES};
+    }
+    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * MFMA_WAVES * H_ROW_TILES, 64 * MFMA_WAVES};
   }
-  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES};
-  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES};
+  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};
+  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};
 }
 
 // launch main + rescue scoring for one KDE
 static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
                         KdeEst* est, hipStream_t s) {
   const unsigned gm = (unsigned)((Nc + f.cands_per_block - 1) / f.cands_per_block);
-  hipLaunchKernelGGL(f.main, dim3(gm), dim3(64 * MFMA_WAVES), 0, s, cand, Nc, D, (const KdeParams*)params, table,
-                     est);
+  hipLaunchKernelGGL(f.main, dim3(gm), dim3(f.threads), 0, s, cand, Nc, D, (const KdeParams*)params, table, est);
   HBX_LAUNCH_CHECK();
   hipLaunchKernelGGL(f.rescue, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D,
                      (const KdeParams*)params, table, est);

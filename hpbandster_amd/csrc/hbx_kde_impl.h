@@ -80,9 +80,11 @@ __device__ __forceinline__ float cand_code(double xv) {
   return (xv == rint(xv) && fabs(xv) < 1e6) ? (float)xv : -1e9f;
 }
 
-// Per-candidate epilogue: ln S+, ln S-, error bound (or the rescue marker err = -1)
-__device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, float S, float Sn, float off,
-                                             bool nan_c, float ci, float bnd, bool SIGNED, int chunk) {
+// Per-candidate epilogue: ln S+, ln S-, error bound (or the rescue marker err = -1).  sum_terms bounds
+// the relative rounding error of the fp32 sums in units of 2^-24 (sequential additions along the
+// longest accumulation path).
+__device__ __forceinline__ KdeEst finish_est_terms(const KdeParams* __restrict__ P, float S, float Sn, float off,
+                                                   bool nan_c, float ci, float bnd, bool SIGNED, float sum_terms) {
   KdeEst o;
   o.pad = 0.f;
   if (nan_c || S != S) {
@@ -98,9 +100,15 @@ __device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, fl
   const float u = 0x1p-24f;
   const float Mabs = fabsf(ci) + P->cmax + bnd + P->sum_abs_delta;
   const float dt = 3.f * (float)(P->dc + P->du + 4) * u * Mabs;  // |error of t|, log2 units
-  const float es = ((float)chunk + (float)P->n / (float)chunk + 24.f) * u * (SIGNED ? 3.f : 1.f);
+  const float es = sum_terms * u * (SIGNED ? 3.f : 1.f);
   o.err = 2.f * (dt * HBX_LN2f + es) + 16.f * u;
   return o;
+}
+
+__device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, float S, float Sn, float off,
+                                             bool nan_c, float ci, float bnd, bool SIGNED, int chunk) {
+  return finish_est_terms(P, S, Sn, off, nan_c, ci, bnd, SIGNED,
+                          (float)chunk + (float)P->n / (float)chunk + 24.f);
 }
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -112,3 +120,5 @@ typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, con
 logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
 logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
 logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
+logpdf_fn hbx_pick_h32(int nsc, int kc);                     // hbx_score_h32.hip (unsigned sums only)
+#define H32_WAVES 8  // waves per block of the 32x32 hmode kernel (32 candidates each)
