@@ -828,7 +828,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
       const logpdf_fn f = hbx_pick_h32(nsc_of(dc_pad), kc);
       if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES};
     }
-    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * MFMA_WAVES * H_ROW_TILES, 64 * MFMA_WAVES};
+    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES};
   }
   if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};
   return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};

@@ -18,6 +18,10 @@
 #define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
 #define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
 #define H_ROW_TILES 2  // hmode: 16-candidate row tiles per wave (32 candidates)
+// hmode (16x16 tiles): waves per block, two blocks per CU.  (A 16-wave block with a 6-deep ring --
+// half the LDS-DMA instructions per pair -- ended in a GPU memory fault on its first launch; cause not
+// found, so it is not offered.)
+#define H16_WAVES 8
 
 // Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
 //   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0

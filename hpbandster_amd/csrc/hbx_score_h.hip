@@ -34,7 +34,7 @@ struct SgbAlternate<NM, NM, NV> {
 };
 
 template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(const double* __restrict__ cand,
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(const double* __restrict__ cand,
                                                                       int64_t Nc, int32_t D,
                                                                       const KdeParams* __restrict__ P,
                                                                       const float* __restrict__ table,
@@ -51,14 +51,24 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   constexpr int KPP = h_kpp(KC);
   constexpr int CHF = h_chunk_floats(NSC * 8, KC, SIGNED ? 1 : 0);
   // LDS ring: 3 buffers (chunk c+2 in flight while c is used) when they fit in the 160 KB, else 2
-  constexpr int NBUF = (3 * CHF * 4 <= 160 * 1024) ? 3 : 2;
-  static_assert(NBUF * CHF * 4 <= 160 * 1024, "observation chunk too large for LDS");
-  constexpr int G = CHF * 4 / (1024 * MFMA_WAVES);         // 1-KB LDS-DMA pieces per wave per chunk
-  static_assert(G * 1024 * MFMA_WAVES == CHF * 4, "chunk must be a multiple of 8 KB");
+  constexpr int HW = H16_WAVES;             // waves per block (16 candidates x RT each)
+  static_assert(HW == 8, "only the 8-wave block is validated");
+  // LDS ring: with 8-wave blocks (two per CU) 3 buffers when they fit, else 2; with 16-wave blocks (one
+  // per CU) as many as fit, at most 6 (the staged candidate rows of 16 waves need the room)
+  constexpr int NMAX = 160 * 1024 / (CHF * 4);
+  constexpr int NBUF = HW > 8 ? (NMAX < 6 ? NMAX : 6) : (NMAX >= 3 ? 3 : 2);
+  static_assert(NBUF >= 2 && NBUF * CHF * 4 <= 160 * 1024, "observation chunk too large for LDS");
+  // 1-KB LDS-DMA pieces per chunk: GL per wave, one more for the first NX waves.  The issue cost of an
+  // LDS-DMA instruction (~60-100 cycles) is per instruction, so larger blocks (more candidates sharing
+  // one chunk load) issue fewer of them per pair.
+  constexpr int GP = CHF * 4 / 1024;
+  constexpr int GL = GP / HW, NX = GP % HW;
+  static_assert(GP * 1024 == CHF * 4, "chunk must be a multiple of 1 KB");
   __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * MFMA_WAVES + wave) * 16 * RT;
+  const int64_t cbase = ((int64_t)blockIdx.x * HW + wave) * 16 * RT;
+  const bool xpiece = wave < NX;  // this wave issues GL + 1 pieces per chunk
   const int n = P->n, dc = P->dc;
   const int ia = lane & 15, kq = lane >> 4;
 
@@ -77,7 +87,7 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
   // staged rows are DS = D|1 doubles apart (odd): the 16 rows a lane group reads hit distinct banks
   const int DS = D | 1;
-  const int64_t rows_bytes = (int64_t)MFMA_WAVES * 16 * RT * DS * 8;
+  const int64_t rows_bytes = (int64_t)HW * 16 * RT * DS * 8;
   const bool rows_fit = rows_bytes + PRM_BYTES <= (int64_t)NBUF * CHF * 4;
   ContPrm* cprm = (ContPrm*)((char*)lds + (rows_fit ? rows_bytes : 0));
   OhPrm* oprm = (OhPrm*)(cprm + 8 * NSC);
@@ -199,10 +209,11 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     const float* src = table + (int64_t)(c < nchunks ? c : nchunks - 1) * CHF;
     float* dst = lds + slot * CHF;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int piece = wave + g * MFMA_WAVES;
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
+    for (int g = 0; g < GL + (NX ? 1 : 0); ++g) {
+      const int piece = wave + g * HW;
+      if (g < GL || xpiece)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
     }
   };
   // The loads of every iteration are unconditional (past the last chunk the last chunk is re-loaded
@@ -212,7 +223,11 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
   __syncthreads();  // every wave has read its staged rows: the ring may be overwritten
 #pragma unroll
   for (int i = 0; i < PD; ++i) issue(i, i);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (PD - 1)) : "memory");  // chunk 0 landed
+  // chunk 0 landed (the waves' piece counts differ: GL or GL + 1 per chunk)
+  if (NX && xpiece)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((GL + 1) * (PD - 1)) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (PD - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
 
   // MFMAs of one 16-observation column tile for every row tile
@@ -343,7 +358,10 @@ __global__ __launch_bounds__(64 * MFMA_WAVES) __attribute__((amdgpu_waves_per_eu
     // chunk c+1 complete for this wave (PD-1 chunks stay in flight), this wave's reads of buffer c
     // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
     if (HBX_H_ABLATE != 3) {
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G * (PD - 1)) : "memory");
+      if (NX && xpiece)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((GL + 1) * (PD - 1)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
       __builtin_amdgcn_s_barrier();
     }
   }
