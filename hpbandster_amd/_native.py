@@ -49,6 +49,8 @@ SIGNATURES = {
     "hbx_norm_ppf": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_sample_table_bytes": (c_i64, [c_i64, c_i32]),
     "hbx_kde_sample_table": (c_i32, [c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "hbx_kde_cv_terms": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp]),
     "hbx_event_create": (c_i32, [c_vp]),
     "hbx_event_destroy": (c_i32, [c_vp]),
     "hbx_event_elapsed_ms": (c_i32, [c_vp, c_vp, c_vp]),

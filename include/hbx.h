@@ -162,6 +162,21 @@ int64_t hbx_kde_sample_table_bytes(int64_t n, int32_t D);
 int hbx_kde_sample_table(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
                          const int32_t* levels, double* tab, void* stream);
 
+/* ---- cross-validation bandwidth objectives (KDEMultivariate bw='cv_ls' / 'cv_ml') ------------ */
+/* Per-observation sums of the CV objectives at bandwidths bw (SM:kernel_density.py:126-160,246-332;
+ * the reference's caller: kde.py:145-147):
+ *   F[i] = sum_j prod_d kbar_d(X_j, X_i) / bwprod     (convolution kernels; imse's first term)
+ *   L[i] = sum_{j != i} prod_d k_d(X_j, X_i) / bwprod (leave-one-out kernels)
+ * imse = sum_i F[i] / n^2 - 2 sum_i L[i] / (n (n-1)); loo log-likelihood = -sum_i log L[i] (host sums,
+ * in order).  X: device f64[n][D]; vartype: device i32[D] (0 = 'c', 1 = 'u'); bw: device f64[D];
+ * lev/lev_off: device, per categorical dim d the ascending unique values of -X[:, d] in
+ * lev[lev_off[d] .. lev_off[d+1]) (continuous dims: empty); loo_levels: device i32[n][D], the level
+ * count of column d without row i; c4 = 1/sqrt(4 pi), c2 = 1/sqrt(2 pi), bwprod = prod of the
+ * continuous bandwidths in dim order (host).  F or L may be NULL (not computed). */
+int hbx_kde_cv_terms(const double* X, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
+                     const double* lev, const int32_t* lev_off, const int32_t* loo_levels, double c4, double c2,
+                     double bwprod, double* F, double* L, void* stream);
+
 /* ---- successive-halving promotion -------------------------------------------------------- */
 /* advance[i] = rank_i < k[b] among the finite losses of bracket b (non-finite = CRASHED, never
  * advance).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B]; order: device

@@ -216,3 +216,121 @@ def hb_bracket(it, eta, max_SH_iter):
     n0 = int(np.floor((max_SH_iter) / (s + 1)) * eta ** s)
     ns = [max(int(n0 * (eta ** (-i))), 1) for i in range(s + 1)]
     return s, ns
+
+
+# --------------------------------------------------------------------------------------
+# cross-validation bandwidth objectives (KDEMultivariate bw='cv_ls' / 'cv_ml'; kde.py:145-147)
+
+
+def _gaussian_convolution(h, Xi, x):
+    """SM:kernels.py gaussian_convolution: (1/sqrt(4 pi)) exp(-(Xi - x)^2 / (h^2 4))."""
+    return (1. / np.sqrt(4 * np.pi)) * np.exp(-(Xi - x) ** 2 / (h ** 2 * 4.))
+
+
+def _aitchison_aitken_convolution(h, Xi, Xj):
+    """SM:kernels.py:166-174: sum over the column's levels (np.unique order) of the two AA kernels."""
+    vals = np.unique(Xi)
+    c = vals.size
+    out = np.zeros(Xi.size)
+    for x in vals:
+        out += _aitchison_aitken(h, Xi, x, np.asarray(c)) * _aitchison_aitken(h, np.asarray(Xj).reshape(1), x, np.asarray(c))
+    return out
+
+
+def _loo_rows(n, i):
+    m = np.ones(n, dtype=bool)
+    m[i] = False
+    return m
+
+
+def cv_terms(data, bw, var_type, rows=None):
+    """Per-observation sums of the two CV objectives, reference operation order.
+
+    F[i] = convolution-kernel sum over all j (SM:kernel_density.py:300-311, imse's first loop),
+    L[i] = leave-one-out kernel sum over j != i (SM:kernel_density.py:313-322 == the gpke call of
+    loo_likelihood, SM:kernel_density.py:153-158); both divided by the continuous bandwidth product
+    (a sequential np.prod) before numpy's contiguous sum.  ``rows``: only these i (others NaN).
+    """
+    data = np.asarray(data, dtype=np.float64)
+    bw = np.asarray(bw, dtype=np.float64)
+    n, D = data.shape
+    neg = -data
+    iscont = np.array([t == "c" for t in var_type])
+    bwprod = bw[iscont].prod()
+    F = np.full(n, np.nan)
+    L = np.full(n, np.nan)
+    rows = range(n) if rows is None else rows
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        K = np.empty((n, D))
+        for i in rows:
+            for d, t in enumerate(var_type):
+                if t == "c":
+                    K[:, d] = _gaussian_convolution(bw[d], neg[:, d], neg[i, d])
+                else:
+                    K[:, d] = _aitchison_aitken_convolution(bw[d], neg[:, d], neg[i, d])
+            F[i] = (K.prod(axis=1) / bwprod).sum(axis=0)
+        K = np.empty((n - 1, D))
+        for i in rows:
+            Xn = -data[_loo_rows(n, i)]
+            for d, t in enumerate(var_type):
+                if t == "c":
+                    K[:, d] = _gaussian(bw[d], Xn[:, d], neg[i, d])
+                else:
+                    K[:, d] = _aitchison_aitken(bw[d], Xn[:, d], neg[i, d], np.asarray(np.unique(Xn[:, d]).size))
+            L[i] = (K.prod(axis=1) / bwprod).sum(axis=0)
+    return F, L
+
+
+def imse_from_terms(F, L, n):
+    """SM:kernel_density.py:300-326: F and L accumulated from int 0 in row order, then the CV formula."""
+    Fs, Ls = 0, 0
+    for v in F:
+        Fs += v
+    for v in L:
+        Ls += v
+    return Fs / n ** 2 - 2 * Ls / (n * (n - 1))
+
+
+def loo_from_terms(L):
+    """SM:kernel_density.py:153-160 with func=np.log: -(sum_i log L_i), accumulated from int 0."""
+    s = 0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for v in L:
+            s += np.log(v)
+    return -s
+
+
+def imse(data, bw, var_type):
+    F, L = cv_terms(data, bw, var_type)
+    return imse_from_terms(F, L, np.asarray(data).shape[0])
+
+
+def loo_likelihood(data, bw, var_type):
+    _, L = cv_terms(data, bw, var_type)
+    return loo_from_terms(L)
+
+
+def set_bw_bounds(bw, var_type):
+    """SM:_kernel_base.py:267-277: negative -> 1e-10, categorical capped at 1."""
+    bw = np.array(bw, dtype=np.float64)
+    bw[bw < 0] = 1e-10
+    cat = np.array([t != "c" for t in var_type])
+    bw[cat] = np.minimum(bw[cat], 1.)
+    return bw
+
+
+def cv_bandwidth(data, var_type, method="cv_ls"):
+    """SM:_kernel_base.py:279-332: scipy.optimize.fmin (Nelder-Mead) from the normal-reference rule."""
+    from scipy import optimize
+    data = np.asarray(data, dtype=np.float64)
+    h0 = normal_reference_bw(data)
+    if method == "cv_ls":
+        obj = lambda b: imse(data, b, var_type)  # noqa: E731
+    elif method == "cv_ml":
+        obj = lambda b: loo_likelihood(data, b, var_type)  # noqa: E731
+    else:
+        raise ValueError(method)
+    bw = optimize.fmin(obj, x0=h0, maxiter=1e3, maxfun=1e3, disp=0, xtol=1e-3)
+    return set_bw_bounds(bw, var_type)
