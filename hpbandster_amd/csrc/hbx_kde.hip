@@ -708,7 +708,15 @@ struct ScoreFns {
   logpdf_fn main, rescue;
   int cands_per_block;
   int threads;
+  logpdf_pair_fn pair;  // the same kernel over both KDEs in one grid (hmode 16x16 only), or nullptr
 };
+
+// l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
+// HBX_SCORE_PAIR=0 keeps two launches (read per call: tests switch it in-process)
+static bool pair_enabled() {
+  const char* e = getenv("HBX_SCORE_PAIR");
+  return !(e && atoi(e) == 0);
+}
 
 template <bool SG>
 static logpdf_fn pick_rescue(int dc_pad) {
@@ -732,22 +740,23 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const bool hm = (variant >> 4) & 1;
   int dcp, dup;
   bucket_dims(dc_pad, du_pad, &dcp, &dup);
-  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0};  // not a bucket
+  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm) {
-    if (dc_pad < 16) return {nullptr, nullptr, 0, 0};
+    if (dc_pad < 16) return {nullptr, nullptr, 0, 0, nullptr};
     // the 16x16-tile kernel; HBX_SCORE_TILE=32 selects the 32x32-tile variant for unsigned sums (an
     // experiment: fewer issue cycles per pair on paper, slower as measured -- DESIGN.md section 4)
     const char* tenv = getenv("HBX_SCORE_TILE");  // read per call (tests switch it in-process)
     const bool t32 = tenv && atoi(tenv) == 32;
     if (!sg && t32) {
       const logpdf_fn f = hbx_pick_h32(nsc_of(dc_pad), kc);
-      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES};
+      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES, nullptr};
     }
-    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES};
+    return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES,
+            hbx_pick_h_pair(nsc_of(dc_pad), kc, sg)};
   }
-  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};
-  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES};
+  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr};
+  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr};
 }
 
 // launch main + rescue scoring for one KDE
@@ -759,6 +768,40 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
   hipLaunchKernelGGL(f.rescue, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D,
                      (const KdeParams*)params, table, est);
   HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// launch main + rescue scoring for both KDEs of an acquisition: one pair launch when both run the
+// same hmode instance (KDE 1 -- the bad one, normally the larger -- first), else two single launches.
+// Events (optional): [0] before, [1] after KDE 0's launches, [2] after KDE 1's; a pair launch
+// records [1] and [2] together after everything.
+static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
+                         const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
+                         int32_t D, hipEvent_t* ev, hipStream_t s) {
+  if (ev) HBX_HIP(hipEventRecord(ev[0], s));
+  if (f0.pair && f0.main == f1.main && pair_enabled()) {
+    const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
+    if ((uint64_t)gm * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm};
+    hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
+    HBX_LAUNCH_CHECK();
+    for (int k = 0; k < 2; ++k) {
+      hipLaunchKernelGGL(f0.rescue, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D,
+                         (const KdeParams*)(k ? params1 : params0), k ? table1 : table0, k ? est1 : est0);
+      HBX_LAUNCH_CHECK();
+    }
+    if (ev) {
+      HBX_HIP(hipEventRecord(ev[1], s));
+      HBX_HIP(hipEventRecord(ev[2], s));
+    }
+    return HBX_OK;
+  }
+  int rc = launch_score(f0, cand, Nc, D, params0, table0, est0, s);
+  if (rc) return rc;
+  if (ev) HBX_HIP(hipEventRecord(ev[1], s));
+  rc = launch_score(f1, cand, Nc, D, params1, table1, est1, s);
+  if (rc) return rc;
+  if (ev) HBX_HIP(hipEventRecord(ev[2], s));
   return HBX_OK;
 }
 
@@ -1074,13 +1117,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   const dim3 grid((unsigned)((Nc + 255) / 256));
   if (Nc > 0) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
-    if (ev) HBX_HIP(hipEventRecord(ev[0], s));
-    int rc = launch_score(fg, cand, Nc, D, params_good, table_good, el, s);
+    const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
     if (rc) return rc;
-    if (ev) HBX_HIP(hipEventRecord(ev[1], s));
-    rc = launch_score(fb, cand, Nc, D, params_bad, table_bad, eg, s);
-    if (rc) return rc;
-    if (ev) HBX_HIP(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
                        flags, first1);
     HBX_LAUNCH_CHECK();

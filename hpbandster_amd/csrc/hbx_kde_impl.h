@@ -120,9 +120,22 @@ typedef _Float16 f16x16 __attribute__((ext_vector_type(16)));
 
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 
+// kernel arguments of the two-KDE (l and g in one grid) hmode launch
+struct KdePairArgs {
+  const KdeParams* P0;
+  const KdeParams* P1;
+  const float* table0;
+  const float* table1;
+  KdeEst* out0;
+  KdeEst* out1;
+  unsigned nblk0;
+};
+typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
+
 // host-side pickers of the scoring kernel instances (nullptr when the bucket has none)
 logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
 logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
 logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
+logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
 logpdf_fn hbx_pick_h32(int nsc, int kc);                     // hbx_score_h32.hip (unsigned sums only)
 #define H32_WAVES 8  // waves per block of the 32x32 hmode kernel (32 candidates each)

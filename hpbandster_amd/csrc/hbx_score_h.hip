@@ -33,12 +33,13 @@ struct SgbAlternate<NM, NM, NV> {
   static __device__ __forceinline__ void run() {}
 };
 
+// The kernel body, for block `blk` of one KDE's grid (the single-KDE kernel and the l+g pair kernel
+// below both run it).
 template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(const double* __restrict__ cand,
-                                                                      int64_t Nc, int32_t D,
-                                                                      const KdeParams* __restrict__ P,
-                                                                      const float* __restrict__ table,
-                                                                      KdeEst* __restrict__ out) {
+__device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                  const KdeParams* __restrict__ P,
+                                                  const float* __restrict__ table, KdeEst* __restrict__ out,
+                                                  const unsigned blk) {
   constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
   constexpr int NSH = NSC + KC;             // f16 K-steps of 32
   // one-hot product on the sparse matrix cores (v_smfmac_f32_16x16x64_f16, 2:4 structured sparsity:
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
   __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cbase = ((int64_t)blockIdx.x * HW + wave) * 16 * RT;
+  const int64_t cbase = ((int64_t)blk * HW + wave) * 16 * RT;
   const bool xpiece = wave < NX;  // this wave issues GL + 1 pieces per chunk
   const int n = P->n, dc = P->dc;
   const int ia = lane & 15, kq = lane >> 4;
@@ -405,6 +406,51 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
       }
     }
   }
+}
+
+template <int NSC, int KC, bool SIGNED>
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
+    const float* __restrict__ table, KdeEst* __restrict__ out) {
+  kde_logpdf_h_body<NSC, KC, SIGNED>(cand, Nc, D, P, table, out, blockIdx.x);
+}
+
+// Both KDEs of an acquisition in one launch: blocks [0, nblk0) score KDE 0, the rest KDE 1 over the
+// same candidates.  The launcher puts the larger KDE first, so the short KDE's blocks fill the tail
+// of the long one's last wave of blocks (and one launch gap goes away).
+template <int NSC, int KC, bool SIGNED>
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_pair_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+  const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
+  kde_logpdf_h_body<NSC, KC, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                     second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+}
+
+template <int NSC, bool SG>
+static logpdf_pair_fn pick_pair_kc(int kc) {
+  switch (kc) {
+    case 0: return kde_logpdf_h_pair_kernel<NSC, 0, SG>;
+    case 1: return kde_logpdf_h_pair_kernel<NSC, 1, SG>;
+    case 2: return kde_logpdf_h_pair_kernel<NSC, 2, SG>;
+    case 3: return kde_logpdf_h_pair_kernel<NSC, 3, SG>;
+    case 4: return kde_logpdf_h_pair_kernel<NSC, 4, SG>;
+  }
+  return nullptr;
+}
+
+template <bool SG>
+static logpdf_pair_fn pick_pair_nsc(int nsc, int kc) {
+  switch (nsc) {
+    case 2: return pick_pair_kc<2, SG>(kc);
+    case 3: return pick_pair_kc<3, SG>(kc);
+    case 4: return pick_pair_kc<4, SG>(kc);
+    case 8: return pick_pair_kc<8, SG>(kc);
+  }
+  return nullptr;
+}
+
+logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg) {
+  return sg ? pick_pair_nsc<true>(nsc, kc) : pick_pair_nsc<false>(nsc, kc);
 }
 
 template <int NSC, bool SG>

@@ -299,3 +299,29 @@ def test_tile32_variant_matches_oracle(device, name, monkeypatch):
         fin = np.isfinite(lref)
         err = np.abs(est[fin] - lref[fin]) / np.maximum(1, np.abs(lref[fin]))
         assert err.max() <= 3e-5, (name, err.max())
+
+
+@pytest.mark.parametrize("shape", [(24, 8, 4, 3000, 20011), (32, 0, 0, 1000, 777), (16, 8, 3, 400, 65)])
+def test_pair_launch_identical_to_two_launches(device, shape, monkeypatch):
+    """l and g scored by one pair launch (the default) against two single launches
+    (HBX_SCORE_PAIR=0): the same kernel body per block, so the ln-pdf estimates and the acquisition
+    record are bit-identical; the chosen index is the oracle's."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lev, n_obs, n_cand = shape
+    X = S.make_observations(n_obs, dc, du, lev)
+    L = S.make_losses(n_obs)
+    vt = S.var_type_string(dc, du)
+    pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    C = S.make_candidates(n_cand, dc, du, lev)
+    monkeypatch.setenv("HBX_SCORE_PAIR", "1")
+    r1, l1, g1 = pair.acquire(C, logs=True)
+    monkeypatch.setenv("HBX_SCORE_PAIR", "0")
+    r0, l0, g0 = pair.acquire(C, logs=True)
+    assert np.array_equal(l1.view(np.uint32), l0.view(np.uint32))
+    assert np.array_equal(g1.view(np.uint32), g0.view(np.uint32))
+    assert (r1.index, r1.pdf_l, r1.pdf_g, r1.shortlist) == (r0.index, r0.pdf_l, r0.pdf_g, r0.shortlist)
+    if n_cand <= 1000:
+        l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
+        g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
+        assert r1.index == O.select(l, g)[0]
