@@ -13,7 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("--traffic-out")
 ap.add_argument("--workload")
-ap.add_argument("--kernel", default="kde_logpdf_h_kernel")
+ap.add_argument("--kernel", default="kde_logpdf_h_pair_kernel")
 a = ap.parse_args()
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
@@ -40,7 +40,8 @@ if a.traffic_out:
     write = sum(out[k].get("WRITE_SIZE", 0) * out[k]["dispatches"] for k in ks) / sum(out[k]["dispatches"] for k in ks)
     rec = {"workload": a.workload, "kernel": a.kernel, "fetch_size_kb_raw": fetch, "write_size_kb": write,
            "bytes_per_launch": 2 * fetch * 1024 + write * 1024,
-           "note": "HBM-side bytes per launch (mean over the l and g launches) = 2 x FETCH_SIZE + WRITE_SIZE "
-                   "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md); from tools/profile_pmc.sh"}
+           "note": "HBM-side bytes per launch (%s) = 2 x FETCH_SIZE + WRITE_SIZE "
+                   "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md); from tools/profile_pmc.sh"
+                   % ("l and g in one launch" if "pair" in a.kernel else "mean over the l and g launches")}
     json.dump(rec, open(a.traffic_out, "w"), indent=1)
     print(json.dumps(rec))
