@@ -209,6 +209,31 @@ def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
             "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
 
 
+def cv_line(device, n=4096, D=8, reps=5):
+    """Side measurement: the cv_ls objective of KernelDensityEstimator's fit
+    (KDEMultivariate.imse, fp64 in the reference's operation order) at n observations: 2 n^2 pair
+    terms (convolution F and leave-one-out L) per evaluation, one hbx_kde_cv_terms launch; plus a whole
+    Nelder-Mead bandwidth selection.  Synthetic U[0,1) data, D continuous dims."""
+    import torch
+    from hpbandster_amd.cv import CVObjective
+    X = np.random.RandomState(5).rand(n, D)
+    obj = CVObjective(X, "c" * D, device=device)
+    h0 = obj.normal_reference()
+    obj.imse(h0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(reps):
+        obj.imse(h0 * (1 + 0.01 * k))
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    e0 = obj.evals
+    t0 = time.perf_counter()
+    obj.select("cv_ls")
+    sel = time.perf_counter() - t0
+    return {"workload": "cv_ls_imse_obs%d_d%d" % (n, D), "ms_per_eval": ms,
+            "pair_terms_per_s": 2 * n * n / (ms * 1e-3), "select_s": sel, "select_evals": obj.evals - e0,
+            "dtype": "f64"}
+
+
 def sampler_line(pair, device, dc, du, levels, Nc, ws, reps=10):
     """Side measurement: BOHB's candidate rule for Nc candidates drawn on the GPU
     (Philox + truncnorm inversion), alone and followed by the acquisition -- a whole model-based
@@ -402,6 +427,10 @@ def main():
             out["gpu_sampler"] = sampler_line(pair, device, a.dc, a.du, a.levels, Nc, ws)
         except Exception as e:
             out["gpu_sampler"] = {"error": repr(e)}
+        try:
+            out["cv_objective"] = cv_line(device)
+        except Exception as e:
+            out["cv_objective"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),

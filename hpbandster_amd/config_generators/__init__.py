@@ -1,4 +1,5 @@
-"""Config generators: the get_config/new_result drop-ins (BOHB and KDEEI run their KDE work on GPU)."""
+"""Config generators: the get_config/new_result drop-ins (BOHB, KDEEI and KernelDensityEstimator run their
+KDE work on the GPU)."""
 from .base import base_config_generator  # noqa: F401
 from .random_sampling import RandomSampling  # noqa: F401
 
@@ -10,4 +11,7 @@ def __getattr__(name):  # BOHB / KDEEI import scipy; load them lazily
     if name == "KDEEI":
         from .kde_ei import KDEEI
         return KDEEI
+    if name == "KernelDensityEstimator":
+        from .kde import KernelDensityEstimator
+        return KernelDensityEstimator
     raise AttributeError(name)
