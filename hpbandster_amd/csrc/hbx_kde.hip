@@ -743,7 +743,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm) {
-    if (dc_pad < 16) return {nullptr, nullptr, 0, 0, nullptr};
+    if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr};
     // the 16x16-tile kernel; HBX_SCORE_TILE=32 selects the 32x32-tile variant for unsigned sums (an
     // experiment: fewer issue cycles per pair on paper, slower as measured -- DESIGN.md section 4)
     const char* tenv = getenv("HBX_SCORE_TILE");  // read per call (tests switch it in-process)
@@ -996,10 +996,11 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
       }
     }
   }
-  // continuous product on the f16 matrix cores (hi/lo split) when it has >= 16 dims and the
-  // categorical part is one-hot (or absent); otherwise the exact f32 MFMA product
+  // continuous product on the f16 matrix cores (hi/lo split) when it has >= 8 dims (one full
+  // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
+  // otherwise the exact f32 MFMA product
   const char* hm_env = getenv("HBX_HMODE");
-  const bool hm_ok = (P->du == 0 || P->kc > 0) && dcp >= 16;
+  const bool hm_ok = (P->du == 0 || P->kc > 0) && dcp >= 8;
   P->hmode = (hm_ok && !(hm_env && hm_env[0] == '0')) ? 1 : 0;
   P->nsc = nsc_of(dcp);
   if (P->hmode)

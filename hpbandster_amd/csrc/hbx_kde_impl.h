@@ -17,7 +17,17 @@
 #define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
 #define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
 #define MFMA_WAVES 8   // waves per scoring block; each wave owns 16 candidates
+#ifndef H_ROW_TILES
 #define H_ROW_TILES 2  // hmode: 16-candidate row tiles per wave (32 candidates)
+#endif
+// hmode: minimum waves per SIMD the register allocation must allow (128 VGPRs at 4)
+#ifndef H_WAVES_PER_EU
+#if H_ROW_TILES <= 2
+#define H_WAVES_PER_EU 4
+#else
+#define H_WAVES_PER_EU 2
+#endif
+#endif
 // hmode (16x16 tiles): waves per block, two blocks per CU.  (A 16-wave block with a 6-deep ring --
 // half the LDS-DMA instructions per pair -- ended in a GPU memory fault on its first launch; cause not
 // found, so it is not offered.)

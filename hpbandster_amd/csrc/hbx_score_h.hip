@@ -409,7 +409,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
 }
 
 template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_kernel(
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(H_WAVES_PER_EU))) void kde_logpdf_h_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
   kde_logpdf_h_body<NSC, KC, SIGNED>(cand, Nc, D, P, table, out, blockIdx.x);
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
 // same candidates.  The launcher puts the larger KDE first, so the short KDE's blocks fill the tail
 // of the long one's last wave of blocks (and one launch gap goes away).
 template <int NSC, int KC, bool SIGNED>
-__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h_pair_kernel(
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(H_WAVES_PER_EU))) void kde_logpdf_h_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   kde_logpdf_h_body<NSC, KC, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
@@ -441,6 +441,7 @@ static logpdf_pair_fn pick_pair_kc(int kc) {
 template <bool SG>
 static logpdf_pair_fn pick_pair_nsc(int nsc, int kc) {
   switch (nsc) {
+    case 1: return pick_pair_kc<1, SG>(kc);
     case 2: return pick_pair_kc<2, SG>(kc);
     case 3: return pick_pair_kc<3, SG>(kc);
     case 4: return pick_pair_kc<4, SG>(kc);
@@ -467,7 +468,8 @@ static logpdf_fn pick_kc(int kc) {
 
 template <bool SG>
 static logpdf_fn pick_nsc(int nsc, int kc) {
-  switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {16, 24, 32, 64}
+  switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {8, 16, 24, 32, 64}
+    case 1: return pick_kc<1, SG>(kc);
     case 2: return pick_kc<2, SG>(kc);
     case 3: return pick_kc<3, SG>(kc);
     case 4: return pick_kc<4, SG>(kc);

@@ -47,8 +47,12 @@ def test_fit_bit_exact(device, name):
     np.testing.assert_array_equal(pair.bad.nlev, c["nlev_bad"])
 
 
+@pytest.mark.parametrize("hmode", ["1", "0"])
 @pytest.mark.parametrize("name", G.kde_case_names())
-def test_logpdf_fp32_within_tolerance(device, name):
+def test_logpdf_fp32_within_tolerance(device, name, hmode, monkeypatch):
+    """hmode "1": the default kernel choice (f16 matrix-core exponent where the shape allows it);
+    "0" (HBX_HMODE=0, read when the KDE is prepared): the f32-MFMA fallback kernels everywhere."""
+    monkeypatch.setenv("HBX_HMODE", hmode)
     c = G.load_kde_case(name)
     pair = _pair_from_fixture(c)
     C = c["cands"]
@@ -81,8 +85,10 @@ def test_exact_pdf_matches_reference(device, name):
     np.testing.assert_allclose(g, c["pdf_g"][:len(C)], rtol=1e-13, atol=0, equal_nan=True)
 
 
+@pytest.mark.parametrize("hmode", ["1", "0"])
 @pytest.mark.parametrize("name", G.kde_case_names())
-def test_acquire_chosen_index_bit_exact(device, name):
+def test_acquire_chosen_index_bit_exact(device, name, hmode, monkeypatch):
+    monkeypatch.setenv("HBX_HMODE", hmode)
     c = G.load_kde_case(name)
     pair = _pair_from_fixture(c)
     res = pair.acquire(c["cands"])
