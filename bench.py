@@ -346,19 +346,24 @@ def main():
     base = rank * Nc
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     ev = kde.ScoreEvents()
+    # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
+    # KDEs, not switched off, not the opt-in 32x32 tile
+    fused = (kernel_model(pair.bad, a.dc, a.du)["model"] is not None and pair.good.variant == pair.bad.variant
+             and os.environ.get("HBX_SCORE_PAIR", "1") != "0" and os.environ.get("HBX_SCORE_TILE", "") != "32")
     log("rank %d/%d: %d candidates x (%d + %d) observations, D=%d" % (rank, world, Nc, Ng, Nb, D))
 
     def step():
         rv = pair.acquire(c_dev, index_base=base, workspace=ws, sync=False, events=ev)
-        loc = torch.stack([rv[8:16].view(torch.float64)[0], rv[0:8].view(torch.int64)[0].to(torch.float64)])
+        loc = rv[0:16]  # the record's (int64 index, f64 score), exchanged as raw bytes: no conversion kernels
         if world > 1:
             loc = loc.to(comm_dev)
-            allr = [torch.empty_like(loc) for _ in range(world)]
-            dist.all_gather(allr, loc)
-            allr = torch.stack(allr)
+            allr = torch.empty(world * 16, dtype=torch.uint8, device=comm_dev)
+            dist.all_gather_into_tensor(allr, loc)
         else:
-            allr = loc[None]
-        h = allr.cpu().numpy()  # the winner reaches the host (what BOHB needs)
+            allr = loc
+        raw = allr.cpu().numpy()  # the winner reaches the host (what BOHB needs)
+        rec = raw.view(np.dtype([("i", "<i8"), ("s", "<f8")]))
+        h = np.stack([rec["s"], rec["i"].astype(np.float64)], axis=1)
         ok = (h[:, 1] >= 0) & (h[:, 0] < np.inf)
         if not ok.any():
             return -1, np.nan
@@ -378,7 +383,7 @@ def main():
     winner = None
     for s in range(a.steps):
         winner = step()
-        ml, mg = ev.elapsed_ms()  # step() synchronised on the result: events are complete
+        ml, mg = ev.elapsed_ms(fused)  # step() synchronised on the result: events are complete
         t_l += ml
         t_g += mg
     torch.cuda.synchronize()
@@ -401,10 +406,6 @@ def main():
     workload = "kde_acquisition_d%d_%dc%du_obs%d_cand%d" % (D, a.dc, a.du, a.obs, Nc)
     traffic = load_traffic(workload)
     km = kernel_model(pair.bad, a.dc, a.du)
-    # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
-    # KDEs, not switched off, not the opt-in 32x32 tile
-    fused = (km["model"] is not None and pair.good.variant == pair.bad.variant
-             and os.environ.get("HBX_SCORE_PAIR", "1") != "0" and os.environ.get("HBX_SCORE_TILE", "") != "32")
     if fused:
         km["kernel"] = km["kernel"].replace("kde_logpdf_h_kernel", "kde_logpdf_h_pair_kernel")
     mfma_util = issue_bound = None

@@ -202,12 +202,11 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
 // with a true maximum (two passes over the observations), one candidate per thread on the VALU.
 // Continuous coordinates come from the table's f32 part, categorical codes straight from the data.
 template <int DCP, bool SIGNED>
-__global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
-                                                         const KdeParams* __restrict__ P,
-                                                         const float* __restrict__ table,
-                                                         KdeEst* __restrict__ out) {
+__device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                const KdeParams* __restrict__ P, const float* __restrict__ table,
+                                                KdeEst* __restrict__ out, const unsigned blk) {
   constexpr int NC = DCP > 0 ? DCP : 1;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
   const bool need = i < Nc && out[i].err == -1.f;
   if (!__any(need)) return;
   if (!need) return;
@@ -268,6 +267,23 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
     mx = 0.f;
   }
   out[i] = finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);
+}
+
+template <int DCP, bool SIGNED>
+__global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                         const KdeParams* __restrict__ P,
+                                                         const float* __restrict__ table,
+                                                         KdeEst* __restrict__ out) {
+  kde_rescue_body<DCP, SIGNED>(cand, Nc, D, P, table, out, blockIdx.x);
+}
+
+// both KDEs' rescue passes in one launch (blocks [0, nblk0) KDE 0, the rest KDE 1)
+template <int DCP, bool SIGNED>
+__global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                              KdePairArgs a) {
+  const bool second = blockIdx.x >= a.nblk0;
+  kde_rescue_body<DCP, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                               second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -709,6 +725,7 @@ struct ScoreFns {
   int cands_per_block;
   int threads;
   logpdf_pair_fn pair;  // the same kernel over both KDEs in one grid (hmode 16x16 only), or nullptr
+  logpdf_pair_fn rescue_pair;
 };
 
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
@@ -716,6 +733,20 @@ struct ScoreFns {
 static bool pair_enabled() {
   const char* e = getenv("HBX_SCORE_PAIR");
   return !(e && atoi(e) == 0);
+}
+
+template <bool SG>
+static logpdf_pair_fn pick_rescue_pair(int dc_pad) {
+  switch (dc_pad) {
+    case 0: return kde_rescue_pair_kernel<0, SG>;
+    case 4: return kde_rescue_pair_kernel<4, SG>;
+    case 8: return kde_rescue_pair_kernel<8, SG>;
+    case 16: return kde_rescue_pair_kernel<16, SG>;
+    case 24: return kde_rescue_pair_kernel<24, SG>;
+    case 32: return kde_rescue_pair_kernel<32, SG>;
+    case 64: return kde_rescue_pair_kernel<64, SG>;
+  }
+  return nullptr;
 }
 
 template <bool SG>
@@ -740,23 +771,23 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const bool hm = (variant >> 4) & 1;
   int dcp, dup;
   bucket_dims(dc_pad, du_pad, &dcp, &dup);
-  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr};  // not a bucket
+  if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr, nullptr};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm) {
-    if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr};
+    if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
     // the 16x16-tile kernel; HBX_SCORE_TILE=32 selects the 32x32-tile variant for unsigned sums (an
     // experiment: fewer issue cycles per pair on paper, slower as measured -- DESIGN.md section 4)
     const char* tenv = getenv("HBX_SCORE_TILE");  // read per call (tests switch it in-process)
     const bool t32 = tenv && atoi(tenv) == 32;
     if (!sg && t32) {
       const logpdf_fn f = hbx_pick_h32(nsc_of(dc_pad), kc);
-      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES, nullptr};
+      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES, nullptr, nullptr};
     }
     return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES,
-            hbx_pick_h_pair(nsc_of(dc_pad), kc, sg)};
+            hbx_pick_h_pair(nsc_of(dc_pad), kc, sg), sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }
-  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr};
-  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr};
+  if (kc == 0) return {hbx_pick_f32(dc_pad, du_pad, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr, nullptr};
+  return {hbx_pick_oh(dc_pad, kc, sg), r, 16 * MFMA_WAVES, 64 * MFMA_WAVES, nullptr, nullptr};
 }
 
 // launch main + rescue scoring for one KDE
@@ -774,26 +805,22 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 // launch main + rescue scoring for both KDEs of an acquisition: one pair launch when both run the
 // same hmode instance (KDE 1 -- the bad one, normally the larger -- first), else two single launches.
 // Events (optional): [0] before, [1] after KDE 0's launches, [2] after KDE 1's; a pair launch
-// records [1] and [2] together after everything.
+// records [0] and [1] only ([1] after everything).
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
                          int32_t D, hipEvent_t* ev, hipStream_t s) {
   if (ev) HBX_HIP(hipEventRecord(ev[0], s));
-  if (f0.pair && f0.main == f1.main && pair_enabled()) {
+  if (f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled()) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
-    if ((uint64_t)gm * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
+    const unsigned gr = (unsigned)((Nc + 255) / 256);
+    if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
     KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm};
     hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
-    for (int k = 0; k < 2; ++k) {
-      hipLaunchKernelGGL(f0.rescue, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D,
-                         (const KdeParams*)(k ? params1 : params0), k ? table1 : table0, k ? est1 : est0);
-      HBX_LAUNCH_CHECK();
-    }
-    if (ev) {
-      HBX_HIP(hipEventRecord(ev[1], s));
-      HBX_HIP(hipEventRecord(ev[2], s));
-    }
+    a.nblk0 = gr;
+    hipLaunchKernelGGL(f0.rescue_pair, dim3(2 * gr), dim3(256), 0, s, cand, Nc, D, a);
+    HBX_LAUNCH_CHECK();
+    if (ev) HBX_HIP(hipEventRecord(ev[1], s));
     return HBX_OK;
   }
   int rc = launch_score(f0, cand, Nc, D, params0, table0, est0, s);

@@ -308,12 +308,15 @@ class ScoreEvents(object):
             self._ev[i] = h.value
         self.address = ctypes.addressof(self._ev)
 
-    def elapsed_ms(self):
-        """(l launch ms, g launch ms) of the last recorded acquisition (events must be complete)."""
+    def elapsed_ms(self, fused=False):
+        """(l launch ms, g launch ms) of the last recorded acquisition (events must be complete).
+        ``fused``: l and g ran as one pair launch, which records only events 0 and 1 -> (l+g, 0)."""
         import ctypes
         L = N.lib()
         a, b = ctypes.c_float(), ctypes.c_float()
         N.check(L.hbx_event_elapsed_ms(self._ev[0], self._ev[1], ctypes.addressof(a)))
+        if fused:
+            return a.value, 0.0
         N.check(L.hbx_event_elapsed_ms(self._ev[1], self._ev[2], ctypes.addressof(b)))
         return a.value, b.value
 

@@ -120,7 +120,9 @@ int hbx_kde_acquire_batch(const double* cand, int64_t Nc, int64_t seg, int32_t D
                           int64_t ws_bytes, void* stream);
 
 /* Optional timing: `events` of hbx_kde_acquire is NULL or an array of three hipEvent_t recorded on
- * `stream` before the l scoring launch, between l and g, and after g. */
+ * `stream` before the l scoring launch, between l and g, and after g -- or, when l and g are scored by
+ * one pair launch (both KDEs on the same hmode kernel, HBX_SCORE_PAIR not 0), only [0] before and [1]
+ * after it. */
 int hbx_event_create(void** ev);
 int hbx_event_destroy(void* ev);
 int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
