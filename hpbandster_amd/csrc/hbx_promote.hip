@@ -9,6 +9,7 @@
 // numpy's argsort is unstable, so on tied losses the reference's choice is platform dependent.
 #include "hbx_common.h"
 #include "hbx_sort.h"
+#include <stdlib.h>
 
 __global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restrict__ loss,
                                                          const int64_t* __restrict__ seg_off,
@@ -40,6 +41,86 @@ __global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restric
   if (threadIdx.x == 0 && n_advance) n_advance[b] = cnt;
 }
 
+// Brackets of up to 1024 configurations (every SH bracket of a realistic ladder): one wave per
+// bracket, the bitonic network entirely in registers -- logical element i = 16 lane + r lives in
+// register r of lane `lane`; strides < 16 compare registers of one lane, strides >= 16 exchange with
+// lane ^ (stride / 16) through cross-lane shuffles.  No LDS, no barriers; same (key, position) order
+// as sh_promote_kernel, so order / advance / n_advance are identical.
+#define PW_PER_LANE 16
+__global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __restrict__ loss,
+                                                              const int64_t* __restrict__ seg_off, int64_t B,
+                                                              const double* __restrict__ k,
+                                                              int64_t* __restrict__ order,
+                                                              uint8_t* __restrict__ advance,
+                                                              int64_t* __restrict__ n_advance) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole wave
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  uint64_t key[PW_PER_LANE];
+  int32_t pos[PW_PER_LANE];
+#pragma unroll
+  for (int r = 0; r < PW_PER_LANE; ++r) {
+    const int i = lane * PW_PER_LANE + r;
+    key[r] = i < n ? key_promote(loss[s + i]) : ~0ull;
+    pos[r] = i < n ? i : 0x7fffffff;
+  }
+#pragma unroll
+  for (int size = 2; size <= 64 * PW_PER_LANE; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= PW_PER_LANE) {
+        const int lm = stride / PW_PER_LANE;
+        const bool lower = (lane & lm) == 0;
+#pragma unroll
+        for (int r = 0; r < PW_PER_LANE; ++r) {
+          const uint64_t ok = __shfl_xor(key[r], lm);
+          const int32_t op = __shfl_xor(pos[r], lm);
+          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
+          const bool other_less = kv_less(ok, op, key[r], pos[r]);
+          // ascending run: the lower index keeps the smaller element; descending: the larger
+          const bool take = (lower == up) ? other_less : !other_less;
+          if (take) {
+            key[r] = ok;
+            pos[r] = op;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < PW_PER_LANE; ++r) {
+          if (r & stride) continue;
+          const int q = r | stride;
+          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
+          const bool gt = kv_less(key[q], pos[q], key[r], pos[r]);
+          if (gt == up) {
+            const uint64_t tk = key[r];
+            key[r] = key[q];
+            key[q] = tk;
+            const int32_t tp = pos[r];
+            pos[r] = pos[q];
+            pos[q] = tp;
+          }
+        }
+      }
+    }
+  }
+  const double kb = k[b];
+  int mine = 0;
+#pragma unroll
+  for (int r = 0; r < PW_PER_LANE; ++r) {
+    const int rank = lane * PW_PER_LANE + r;
+    if (rank < n) {
+      order[s + rank] = pos[r];
+      const bool adv = key[r] != ~0ull && (double)rank < kb;  // finite loss (key_promote) and rank < k
+      advance[s + pos[r]] = adv ? 1 : 0;
+      mine += adv;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if (lane == 0 && n_advance) n_advance[b] = mine;
+}
+
 extern "C" {
 
 int64_t hbx_sort_scratch_bytes(int64_t N);
@@ -53,6 +134,13 @@ int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_
   if (!loss || !seg_off || !k || !order || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
+  const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-bracket kernel for every size
+  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0)) {
+    hipLaunchKernelGGL(sh_promote_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, loss,
+                       seg_off, B, k, order, advance, n_advance);
+    HBX_LAUNCH_CHECK();
+    return HBX_OK;
+  }
   int tile = 64;
   while (tile < max_seg && tile < 4096) tile <<= 1;
   char* sc = (char*)scratch;

@@ -85,3 +85,29 @@ def test_config5_shape_with_fit(device):
         good, bad = O.bohb_split(Xb, Lb, D + 1)
         np.testing.assert_array_equal(bwg[b], O.normal_reference_bw(Xb[good]))
         np.testing.assert_array_equal(bwb[b], O.normal_reference_bw(Xb[bad]))
+
+
+@pytest.mark.parametrize("B,n", [(300, 1024), (97, 200), (5, 1), (64, 3)])
+def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
+    """Brackets of <= 1024 configurations run the register-resident wave kernel; HBX_PROMOTE_WAVE=0
+    forces the LDS block kernel.  Same (loss, position) order: order, masks and counts identical,
+    masks equal to the oracle; empty brackets, ties and non-finite losses included."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(B + n)
+    lens = rs.randint(0, n + 1, size=B)
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = np.round(rs.rand(seg[-1]) * 50) / 50  # many ties
+    loss[rs.rand(seg[-1]) < 0.05] = np.inf
+    loss[rs.rand(seg[-1]) < 0.03] = np.nan
+    loss[rs.rand(seg[-1]) < 0.01] = -np.inf
+    k = np.maximum(lens * 0.34, 1.0)
+    monkeypatch.setenv("HBX_PROMOTE_WAVE", "1")
+    a1, o1, c1 = (t.cpu().numpy() for t in promote.promote_segments(loss, seg, k, device=device, return_order=True))
+    monkeypatch.setenv("HBX_PROMOTE_WAVE", "0")
+    a0, o0, c0 = (t.cpu().numpy() for t in promote.promote_segments(loss, seg, k, device=device, return_order=True))
+    np.testing.assert_array_equal(a1, a0)
+    np.testing.assert_array_equal(o1[:seg[-1]], o0[:seg[-1]])
+    np.testing.assert_array_equal(c1[:B], c0[:B])
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(a1[s:e].astype(bool), O.sh_advance(loss[s:e], k[b]))
