@@ -12,6 +12,7 @@
 // because the device pow() is not guaranteed to round the same way.
 #include "hbx_common.h"
 #include "hbx_sort.h"
+#include <stdlib.h>
 
 __device__ double np_pairwise_gather(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
                                      double mean, bool sq);
@@ -104,6 +105,25 @@ __global__ __launch_bounds__(256) void seg_argsort_kernel(const double* __restri
   const int64_t b = blockIdx.x;
   const int64_t s = seg_off[b], e = seg_off[b + 1];
   block_sort_segment<false>(loss + s, e - s, tile, lk, li, gk + s, gi + s, gk2 + s, gi2 + s, order + s);
+}
+
+// segments of up to 1024 losses: one wave each, sorted in registers (wave_sort_1024)
+__global__ __launch_bounds__(256) void seg_argsort_wave_kernel(const double* __restrict__ loss,
+                                                               const int64_t* __restrict__ seg_off, int64_t B,
+                                                               int64_t* __restrict__ order) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole wave
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  uint64_t key[PW_PER_LANE];
+  int32_t pos[PW_PER_LANE];
+  wave_sort_1024<false>(loss + s, n, lane, key, pos);
+#pragma unroll
+  for (int r = 0; r < PW_PER_LANE; ++r) {
+    const int rank = lane * PW_PER_LANE + r;
+    if (rank < n) order[s + rank] = pos[r];
+  }
 }
 
 // one thread per (segment, set in {good, bad}, dim): bandwidth and observed level count
@@ -263,6 +283,13 @@ int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64
   if (!loss || !seg_off || !order || (!scratch && N > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort: null");
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
+  const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-segment kernel for every size
+  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0)) {
+    hipLaunchKernelGGL(seg_argsort_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       loss, seg_off, B, order);
+    HBX_LAUNCH_CHECK();
+    return HBX_OK;
+  }
   const int tile = sort_tile(max_seg);
   char* sc = (char*)scratch;
   uint64_t* gk = (uint64_t*)sc;

@@ -42,11 +42,8 @@ __global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restric
 }
 
 // Brackets of up to 1024 configurations (every SH bracket of a realistic ladder): one wave per
-// bracket, the bitonic network entirely in registers -- logical element i = 16 lane + r lives in
-// register r of lane `lane`; strides < 16 compare registers of one lane, strides >= 16 exchange with
-// lane ^ (stride / 16) through cross-lane shuffles.  No LDS, no barriers; same (key, position) order
-// as sh_promote_kernel, so order / advance / n_advance are identical.
-#define PW_PER_LANE 16
+// bracket, sorted in registers (wave_sort_1024, hbx_sort.h).  Same (key, position) order as
+// sh_promote_kernel, so order / advance / n_advance are identical.
 __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __restrict__ loss,
                                                               const int64_t* __restrict__ seg_off, int64_t B,
                                                               const double* __restrict__ k,
@@ -60,51 +57,7 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
   const int n = (int)(seg_off[b + 1] - s);
   uint64_t key[PW_PER_LANE];
   int32_t pos[PW_PER_LANE];
-#pragma unroll
-  for (int r = 0; r < PW_PER_LANE; ++r) {
-    const int i = lane * PW_PER_LANE + r;
-    key[r] = i < n ? key_promote(loss[s + i]) : ~0ull;
-    pos[r] = i < n ? i : 0x7fffffff;
-  }
-#pragma unroll
-  for (int size = 2; size <= 64 * PW_PER_LANE; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride >= PW_PER_LANE) {
-        const int lm = stride / PW_PER_LANE;
-        const bool lower = (lane & lm) == 0;
-#pragma unroll
-        for (int r = 0; r < PW_PER_LANE; ++r) {
-          const uint64_t ok = __shfl_xor(key[r], lm);
-          const int32_t op = __shfl_xor(pos[r], lm);
-          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
-          const bool other_less = kv_less(ok, op, key[r], pos[r]);
-          // ascending run: the lower index keeps the smaller element; descending: the larger
-          const bool take = (lower == up) ? other_less : !other_less;
-          if (take) {
-            key[r] = ok;
-            pos[r] = op;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < PW_PER_LANE; ++r) {
-          if (r & stride) continue;
-          const int q = r | stride;
-          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
-          const bool gt = kv_less(key[q], pos[q], key[r], pos[r]);
-          if (gt == up) {
-            const uint64_t tk = key[r];
-            key[r] = key[q];
-            key[q] = tk;
-            const int32_t tp = pos[r];
-            pos[r] = pos[q];
-            pos[q] = tp;
-          }
-        }
-      }
-    }
-  }
+  wave_sort_1024<true>(loss + s, n, lane, key, pos);
   const double kb = k[b];
   int mine = 0;
 #pragma unroll

@@ -126,3 +126,60 @@ __device__ void block_sort_segment(const double* __restrict__ loss, int64_t n, i
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) order[i] = si[i];
   __syncthreads();
 }
+
+// Segments of up to 1024 elements, one wave: logical element i = 16 lane + r lives in register r of
+// lane `lane`; the bitonic network runs in registers -- strides < 16 compare registers of one lane,
+// strides >= 16 exchange with lane ^ (stride / 16) through cross-lane shuffles.  No LDS, no barriers.
+// On return register r of lane `lane` holds rank 16 lane + r: its key and position (padding past n:
+// key ~0, position 0x7fffffff, after every real element).  Same (key, position) order as
+// block_sort_segment.
+#define PW_PER_LANE 16
+template <bool PROMOTE>
+__device__ __forceinline__ void wave_sort_1024(const double* __restrict__ loss, int n, int lane,
+                                               uint64_t (&key)[PW_PER_LANE], int32_t (&pos)[PW_PER_LANE]) {
+#pragma unroll
+  for (int r = 0; r < PW_PER_LANE; ++r) {
+    const int i = lane * PW_PER_LANE + r;
+    key[r] = i < n ? (PROMOTE ? key_promote(loss[i]) : key_argsort(loss[i])) : ~0ull;
+    pos[r] = i < n ? i : 0x7fffffff;
+  }
+#pragma unroll
+  for (int size = 2; size <= 64 * PW_PER_LANE; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= PW_PER_LANE) {
+        const int lm = stride / PW_PER_LANE;
+        const bool lower = (lane & lm) == 0;
+#pragma unroll
+        for (int r = 0; r < PW_PER_LANE; ++r) {
+          const uint64_t ok = __shfl_xor(key[r], lm);
+          const int32_t op = __shfl_xor(pos[r], lm);
+          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
+          const bool other_less = kv_less(ok, op, key[r], pos[r]);
+          // ascending run: the lower index keeps the smaller element; descending: the larger
+          const bool take = (lower == up) ? other_less : !other_less;
+          if (take) {
+            key[r] = ok;
+            pos[r] = op;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < PW_PER_LANE; ++r) {
+          if (r & stride) continue;
+          const int q = r | stride;
+          const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
+          const bool gt = kv_less(key[q], pos[q], key[r], pos[r]);
+          if (gt == up) {
+            const uint64_t tk = key[r];
+            key[r] = key[q];
+            key[q] = tk;
+            const int32_t tp = pos[r];
+            pos[r] = pos[q];
+            pos[q] = tp;
+          }
+        }
+      }
+    }
+  }
+}

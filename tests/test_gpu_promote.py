@@ -111,3 +111,36 @@ def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
     for b in range(B):
         s, e = seg[b], seg[b + 1]
         np.testing.assert_array_equal(a1[s:e].astype(bool), O.sh_advance(loss[s:e], k[b]))
+
+
+@pytest.mark.parametrize("B,n", [(200, 1024), (33, 100), (1, 1000), (3, 1500)])
+def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
+    """hbx_seg_argsort (the refit's split, bohb.py:220): np.argsort order (-inf < finite < +inf < NaN),
+    ties by position, through the wave kernel (segments <= 1024) and the block kernel
+    (HBX_PROMOTE_WAVE=0, and every longer segment)."""
+    import torch
+    from hpbandster_amd import _native as N
+    rs = np.random.RandomState(B * 3 + n)
+    lens = rs.randint(0, n + 1, size=B)
+    lens[0] = n
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = np.round(rs.rand(seg[-1]) * 40) / 40
+    loss[rs.rand(seg[-1]) < 0.04] = np.inf
+    loss[rs.rand(seg[-1]) < 0.04] = np.nan
+    loss[rs.rand(seg[-1]) < 0.02] = -np.inf
+    L = N.lib()
+    ld = torch.from_numpy(loss).to(device)
+    segd = torch.from_numpy(seg).to(device)
+    sb = int(L.hbx_sort_scratch_bytes(int(seg[-1])))
+    scr = torch.empty(max(sb, 1), dtype=torch.uint8, device=device)
+    outs = []
+    for wave in ("1", "0"):
+        monkeypatch.setenv("HBX_PROMOTE_WAVE", wave)
+        order = torch.full((max(int(seg[-1]), 1),), -1, dtype=torch.int64, device=device)
+        N.call("hbx_seg_argsort", N.ptr(ld), N.ptr(segd), B, int(lens.max()), int(seg[-1]), N.ptr(order),
+               N.ptr(scr), sb, N.stream_handle())
+        outs.append(order.cpu().numpy()[:seg[-1]])
+    np.testing.assert_array_equal(outs[0], outs[1])
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(outs[0][s:e], np.argsort(loss[s:e], kind="stable"))
