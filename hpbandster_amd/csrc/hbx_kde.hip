@@ -527,7 +527,12 @@ __device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64
 // Exact re-score of the shortlist.  Small shortlists (<= EXACT_SPLIT_CAP): one work item per
 // (candidate, KDE, 8192-buffer, unit) so one candidate spreads over many CUs; the unit sums go to
 // `part` and kde_final combines them.  Larger: one item per (candidate, KDE), all units in turn.
-__global__ __launch_bounds__(EXACT_THREADS) void kde_exact_kernel(
+// threads per block of the acquisition's exact re-score: one unit (<= 1040 observations) per block, so
+// 1024 threads compute its terms in one pass (16 waves: 4 per SIMD hide the fp64 exp latency)
+#ifndef EXACT_ACQ_THREADS
+#define EXACT_ACQ_THREADS 1024
+#endif
+__global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
     const double* __restrict__ cand, int32_t D,
     const KdeParams* __restrict__ Pg, const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
     const KdeParams* __restrict__ Pb, const double* __restrict__ Xb, const int64_t* __restrict__ rows_b,
@@ -1154,7 +1159,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                        batch_res ? segcnt : (int32_t*)nullptr, first1);
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
-    hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_THREADS), 0, s, cand, D,
+    hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,
                        (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
                        rows_bad, list, count, nbuf, part, exact_l, exact_g);
     HBX_LAUNCH_CHECK();
