@@ -193,6 +193,14 @@ class KDEPair(object):
         if (good.dc_pad, good.du_pad) != (bad.dc_pad, bad.du_pad):
             raise N.HbxError("good/bad KDEs prepared for different kernel buckets")
         self.nmax = max(good.nobs, bad.nobs)
+        # per-call constants of acquire(): the prepared KDEs' device pointers and variant codes, the
+        # workspace size per candidate count, the result record's offset (host overhead of a
+        # get_config at the reference's 64 candidates is of the order of the GPU work)
+        self._kde_args = (N.ptr(good.params), N.ptr(good.table), N.ptr(good.X_dev), N.ptr(good.rows_dev),
+                          good.variant, N.ptr(bad.params), N.ptr(bad.table), N.ptr(bad.X_dev),
+                          N.ptr(bad.rows_dev), bad.variant, good.dc_pad, good.du_pad, self.nmax)
+        self._wsb = {}
+        self._roff = None
 
     def __getitem__(self, key):  # cg.kde_models[b]['good'] like the reference dict
         if key == "good":
@@ -209,7 +217,10 @@ class KDEPair(object):
         return int(N.lib().hbx_kde_result_ptr(4096)) - 4096
 
     def workspace_bytes(self, Nc):
-        return int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
+        wsb = self._wsb.get(Nc)
+        if wsb is None:
+            wsb = self._wsb[Nc] = int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
+        return wsb
 
     def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True, events=None):
         """Select the first index minimising max(1e-8, g)/max(l, 1e-8) over the candidates.
@@ -238,13 +249,13 @@ class KDEPair(object):
             raise N.HbxError("workspace too small")
         logl = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         logg = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
-        g, b = self.good, self.bad
-        N.check(L.hbx_kde_acquire(N.ptr(c_dev), Nc, D, int(index_base),
-                                  N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.variant,
-                                  N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.variant,
-                                  g.dc_pad, g.du_pad, self.nmax, N.ptr(logl), N.ptr(logg), N.ptr(ws), ws.numel(),
+        wsp = ws.data_ptr()
+        N.check(L.hbx_kde_acquire(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args,
+                                  N.ptr(logl), N.ptr(logg), wsp, ws.numel(),
                                   events.address if events is not None else None, N.stream_handle(stream)))
-        off = int(L.hbx_kde_result_ptr(N.ptr(ws))) - N.ptr(ws)
+        if self._roff is None:
+            self._roff = int(L.hbx_kde_result_ptr(wsp)) - wsp
+        off = self._roff
         rview = ws[off:off + RESULT_BYTES]
         if not sync:
             return rview
