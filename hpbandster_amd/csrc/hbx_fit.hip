@@ -126,6 +126,49 @@ __global__ __launch_bounds__(256) void seg_argsort_wave_kernel(const double* __r
   }
 }
 
+// Segments of 1024 < n <= RANK_MAX_SEG: stable rank by counting, spread over many workgroups.
+// rank(i) = #{j : (key_j, j) < (key_i, i)} -- a total order, so the ranks are a permutation and
+// order[rank(i)] = i is the stable argsort.  Grid (i blocks of 256, j chunks of RANK_J, segment):
+// each workgroup counts one j chunk (staged in LDS) for its 256 elements and adds the partial counts
+// into rank[] (zeroed first); a second kernel scatters order[rank(i)] = i.  O(n^2) compares on every
+// CU at once instead of one workgroup's merge passes.
+#define RANK_J 512
+#define RANK_MAX_SEG 65536
+__global__ __launch_bounds__(256) void seg_rank_count_kernel(const double* __restrict__ loss,
+                                                             const int64_t* __restrict__ seg_off,
+                                                             int32_t* __restrict__ rank) {
+  __shared__ uint64_t kt[RANK_J];
+  const int64_t b = blockIdx.z;
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  const int j0 = blockIdx.y * RANK_J;
+  if ((int)blockIdx.x * 256 >= n || j0 >= n) return;  // whole block
+  const int m = (n - j0) < RANK_J ? (n - j0) : RANK_J;
+  for (int t = threadIdx.x; t < m; t += 256) kt[t] = key_argsort(loss[s + j0 + t]);
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ki = key_argsort(loss[s + i]);
+  // j < i (j = j0 + t): equal keys count too; j >= i: only strictly smaller keys
+  const int split = i - j0 < 0 ? 0 : (i - j0 > m ? m : i - j0);
+  int c = 0;
+#pragma unroll 8
+  for (int t = 0; t < split; ++t) c += kt[t] <= ki;
+#pragma unroll 8
+  for (int t = split; t < m; ++t) c += kt[t] < ki;
+  if (c) atomicAdd(rank + s + i, c);
+}
+
+__global__ __launch_bounds__(256) void seg_rank_scatter_kernel(const int64_t* __restrict__ seg_off,
+                                                               const int32_t* __restrict__ rank,
+                                                               int64_t* __restrict__ order) {
+  const int64_t b = blockIdx.y;
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) order[s + rank[s + i]] = i;
+}
+
 // one thread per (segment, set in {good, bad}, dim): bandwidth and observed level count
 __global__ __launch_bounds__(128) void kde_fit_stats_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
@@ -284,9 +327,25 @@ int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
   const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-segment kernel for every size
-  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0)) {
+  const char* renv = getenv("HBX_SORT_RANK");     // 0: LDS tiles + merges for every segment > 1024
+  const bool rank_ok = max_seg <= RANK_MAX_SEG && B <= 65535 && !(renv && atoi(renv) == 0);
+  // many short segments: one wave each; a few (a single refit split): the counting rank spreads
+  // each segment over many workgroups
+  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0) && (B >= 64 || !rank_ok)) {
     hipLaunchKernelGGL(seg_argsort_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        loss, seg_off, B, order);
+    HBX_LAUNCH_CHECK();
+    return HBX_OK;
+  }
+  if (rank_ok) {
+    int32_t* rank = (int32_t*)scratch;  // N int32 of the (24 N + 64)-byte sort scratch
+    HBX_HIP(hipMemsetAsync(rank, 0, sizeof(int32_t) * (size_t)N, (hipStream_t)stream));
+    const unsigned gi = (unsigned)((max_seg + 255) / 256);
+    hipLaunchKernelGGL(seg_rank_count_kernel, dim3(gi, (unsigned)((max_seg + RANK_J - 1) / RANK_J), (unsigned)B),
+                       dim3(256), 0, (hipStream_t)stream, loss, seg_off, rank);
+    HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(seg_rank_scatter_kernel, dim3(gi, (unsigned)B), dim3(256), 0, (hipStream_t)stream, seg_off,
+                       rank, order);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }

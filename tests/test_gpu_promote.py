@@ -113,11 +113,11 @@ def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
         np.testing.assert_array_equal(a1[s:e].astype(bool), O.sh_advance(loss[s:e], k[b]))
 
 
-@pytest.mark.parametrize("B,n", [(200, 1024), (33, 100), (1, 1000), (3, 1500)])
+@pytest.mark.parametrize("B,n", [(200, 1024), (33, 100), (1, 1000), (3, 1500), (1, 10000), (4, 3000)])
 def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
     """hbx_seg_argsort (the refit's split, bohb.py:220): np.argsort order (-inf < finite < +inf < NaN),
-    ties by position, through the wave kernel (segments <= 1024) and the block kernel
-    (HBX_PROMOTE_WAVE=0, and every longer segment)."""
+    ties by position, through the wave kernel (segments <= 1024) or the counting-rank kernel
+    (1024 < segments <= 65536), and the block kernel (HBX_PROMOTE_WAVE=0 HBX_SORT_RANK=0)."""
     import torch
     from hpbandster_amd import _native as N
     rs = np.random.RandomState(B * 3 + n)
@@ -136,6 +136,7 @@ def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
     outs = []
     for wave in ("1", "0"):
         monkeypatch.setenv("HBX_PROMOTE_WAVE", wave)
+        monkeypatch.setenv("HBX_SORT_RANK", wave)
         order = torch.full((max(int(seg[-1]), 1),), -1, dtype=torch.int64, device=device)
         N.call("hbx_seg_argsort", N.ptr(ld), N.ptr(segd), B, int(lens.max()), int(seg[-1]), N.ptr(order),
                N.ptr(scr), sb, N.stream_handle())
