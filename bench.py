@@ -233,6 +233,34 @@ def config2_line(device, reps=50):
             "ms_per_step": el * 1e3, "winner": r.index, "variant": int(pair.bad.variant)}
 
 
+def refit_line(X, losses, var_type, device, reps=10):
+    """Side measurement: one BOHB refit at config #3's observation set as
+    new_result runs it (bohb.py:220-251) -- host arrays in, split + bandwidths + level counts + the
+    prepared scoring tables out (kde.fit_pair) -- beside the same arithmetic in host numpy
+    (argsort, row gathers, 1.06 std n^(-1/(4+D)), unique level counts)."""
+    import torch
+    from hpbandster_amd import kde
+    D = X.shape[1]
+    kde.fit_pair(X, losses, var_type, D + 1, device=device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        kde.fit_pair(X, losses, var_type, D + 1, device=device)
+    torch.cuda.synchronize()
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    ng, nb = kde.bohb_split_sizes(X.shape[0], D + 1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        idx = np.argsort(losses)
+        for rows, n in ((idx[:ng], ng), (idx[-nb:], nb)):
+            data = X[rows]
+            bw = 1.06 * np.std(data, axis=0) * n ** (-1. / (4 + D))
+            lev = [np.unique(data[:, d]).size for d in range(D) if var_type[d] == "u"]
+    host_ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"workload": "bohb_refit_obs%d_d%d" % X.shape, "ms_per_refit": gpu_ms,
+            "host_numpy_ms": host_ms, "note": "wall clock, host arrays in (H2D copies included)"}
+
+
 def cv_line(device, n=4096, D=8, reps=5):
     """Side measurement: the cv_ls objective of KernelDensityEstimator's fit
     (KDEMultivariate.imse, fp64 in the reference's operation order) at n observations: 2 n^2 pair
@@ -462,6 +490,10 @@ def main():
             out["config2"] = config2_line(device)
         except Exception as e:
             out["config2"] = {"error": repr(e)}
+        try:
+            out["refit"] = refit_line(X, losses, var_type, device)
+        except Exception as e:
+            out["refit"] = {"error": repr(e)}
         try:
             out["cv_objective"] = cv_line(device)
         except Exception as e:

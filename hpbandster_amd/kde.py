@@ -369,28 +369,31 @@ def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=Non
     # numpy slicing semantics: idx[:n_good] / idx[-n_bad:] clip at n
     n_good, n_bad = min(n_good, n), min(n_bad, n)
     vt = var_type_codes(var_type)
-    X_dev = torch.from_numpy(X).to(device)
-    loss_dev = torch.from_numpy(loss).to(device)
-    seg = torch.tensor([0, n], dtype=torch.int64, device=device)
+    # few, large copies (each host<->device copy of a small tensor costs a round trip): observations
+    # and losses in one f64 buffer, segment bounds and split sizes in one int64 tensor, the two
+    # bandwidth factors and the var types beside them
+    buf = torch.from_numpy(np.concatenate([X.reshape(-1), loss])).to(device)
+    X_dev = buf[:n * D].view(n, D)
+    loss_dev = buf[n * D:]
+    meta = torch.from_numpy(np.array([0, n, n_good, n_bad], dtype=np.int64)).to(device)
+    seg, ng, nb = meta[0:2], meta[2:3], meta[3:4]
+    facs = torch.from_numpy(np.array([bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D)])).to(device)
+    fg, fb = facs[0:1], facs[1:2]
     order = torch.empty(n, dtype=torch.int64, device=device)
     sb = int(L.hbx_sort_scratch_bytes(n))
     scratch = torch.empty(sb, dtype=torch.uint8, device=device)
     sh = N.stream_handle(stream)
     N.check(L.hbx_seg_argsort(N.ptr(loss_dev), N.ptr(seg), 1, n, n, N.ptr(order), N.ptr(scratch), sb, sh))
-    ng = torch.tensor([n_good], dtype=torch.int64, device=device)
-    nb = torch.tensor([n_bad], dtype=torch.int64, device=device)
-    fg = torch.tensor([bandwidth_factor(n_good, D)], dtype=torch.float64, device=device)
-    fb = torch.tensor([bandwidth_factor(n_bad, D)], dtype=torch.float64, device=device)
     vt_dev = torch.from_numpy(vt).to(device)
-    bw_g = torch.empty(D, dtype=torch.float64, device=device)
-    bw_b = torch.empty(D, dtype=torch.float64, device=device)
-    nl_g = torch.empty(D, dtype=torch.int32, device=device)
-    nl_b = torch.empty(D, dtype=torch.int32, device=device)
+    outb = torch.empty(24 * D, dtype=torch.uint8, device=device)  # bw_g, bw_b f64[D]; nl_g, nl_b i32[D]
+    bw_g, bw_b = outb[:8 * D].view(torch.float64), outb[8 * D:16 * D].view(torch.float64)
+    nl_g, nl_b = outb[16 * D:20 * D].view(torch.int32), outb[20 * D:].view(torch.int32)
     N.check(L.hbx_kde_fit(N.ptr(X_dev), D, N.ptr(seg), 1, N.ptr(order), N.ptr(ng), N.ptr(nb), N.ptr(fg), N.ptr(fb),
                           N.ptr(vt_dev), N.ptr(bw_g), N.ptr(bw_b), N.ptr(nl_g), N.ptr(nl_b), sh))
+    oh = outb.cpu().numpy()
+    bw_gh, bw_bh = oh[:8 * D].view(np.float64).copy(), oh[8 * D:16 * D].view(np.float64).copy()
+    nl_gh, nl_bh = oh[16 * D:20 * D].view(np.int32).copy(), oh[20 * D:].view(np.int32).copy()
     order_h = order.cpu().numpy()
-    bw_gh, bw_bh = bw_g.cpu().numpy(), bw_b.cpu().numpy()
-    nl_gh, nl_bh = nl_g.cpu().numpy(), nl_b.cpu().numpy()
     if (nl_gh < 0).any() or (nl_bh < 0).any():
         raise N.HbxError("categorical codes must be integers in [0, 1024)")
     rows_g = order[:n_good]
