@@ -289,8 +289,19 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
         }
       }
       __syncthreads();
-      if (threadIdx.x == 0)
-        for (int i = 0; i < m; ++i) acc = acc + v[i];
+      if (threadIdx.x == 0) {
+        // numpy's axis-0 order: one dependent add per row.  32 LDS reads are issued ahead of their
+        // adds so the read latency hides behind the add chain (same additions, same order).
+        int i = 0;
+        for (; i + 32 <= m; i += 32) {
+          double r[32];
+#pragma unroll
+          for (int k = 0; k < 32; ++k) r[k] = v[i + k];
+#pragma unroll
+          for (int k = 0; k < 32; ++k) acc = acc + r[k];
+        }
+        for (; i < m; ++i) acc = acc + v[i];
+      }
     }
     if (threadIdx.x == 0) red = acc;
     __syncthreads();
