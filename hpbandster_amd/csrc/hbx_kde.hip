@@ -92,6 +92,8 @@ __global__ __launch_bounds__(256) void kde_center_kernel(const double* __restric
 
 // Fill the chunked observation table (layout above).  X'_jc = s_c * (X_jc - mu_c),
 // C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per table slot j < nchunks*64.
+// one thread per observation row (a serial walk over its dims); launched as 64-thread blocks so a
+// 1e4-row table spreads over ~150 CUs instead of ~40
 __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict__ X, int32_t D,
                                                         const int64_t* __restrict__ rows,
                                                         KdeParams* __restrict__ P,
@@ -1060,7 +1062,7 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
     HBX_LAUNCH_CHECK();
   }
   const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
-  hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
+  hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 63) / 64), dim3(64), 0, s, X, D, rows,
                      (KdeParams*)params, table);
   HBX_LAUNCH_CHECK();
   if (hmode) {
@@ -1077,7 +1079,7 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
         hipLaunchKernelGGL(kde_center_kernel, dim3(dc_n), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
         HBX_LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 255) / 256), dim3(256), 0, s, X, D, rows,
+      hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 63) / 64), dim3(64), 0, s, X, D, rows,
                          (KdeParams*)params, table);
       HBX_LAUNCH_CHECK();
       HBX_HIP(hipStreamSynchronize(s));
