@@ -379,21 +379,24 @@ def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=Non
     seg, ng, nb = meta[0:2], meta[2:3], meta[3:4]
     facs = torch.from_numpy(np.array([bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D)])).to(device)
     fg, fb = facs[0:1], facs[1:2]
-    order = torch.empty(n, dtype=torch.int64, device=device)
+    # outputs in one buffer, read back with one copy: order i64[n], bw_g, bw_b f64[D], nl_g, nl_b i32[D]
+    outall = torch.empty(8 * n + 24 * D, dtype=torch.uint8, device=device)
+    order = outall[:8 * n].view(torch.int64)
+    outb = outall[8 * n:]
     sb = int(L.hbx_sort_scratch_bytes(n))
     scratch = torch.empty(sb, dtype=torch.uint8, device=device)
     sh = N.stream_handle(stream)
     N.check(L.hbx_seg_argsort(N.ptr(loss_dev), N.ptr(seg), 1, n, n, N.ptr(order), N.ptr(scratch), sb, sh))
     vt_dev = torch.from_numpy(vt).to(device)
-    outb = torch.empty(24 * D, dtype=torch.uint8, device=device)  # bw_g, bw_b f64[D]; nl_g, nl_b i32[D]
     bw_g, bw_b = outb[:8 * D].view(torch.float64), outb[8 * D:16 * D].view(torch.float64)
     nl_g, nl_b = outb[16 * D:20 * D].view(torch.int32), outb[20 * D:].view(torch.int32)
     N.check(L.hbx_kde_fit(N.ptr(X_dev), D, N.ptr(seg), 1, N.ptr(order), N.ptr(ng), N.ptr(nb), N.ptr(fg), N.ptr(fb),
                           N.ptr(vt_dev), N.ptr(bw_g), N.ptr(bw_b), N.ptr(nl_g), N.ptr(nl_b), sh))
-    oh = outb.cpu().numpy()
+    ah = outall.cpu().numpy()
+    order_h = ah[:8 * n].view(np.int64)
+    oh = ah[8 * n:]
     bw_gh, bw_bh = oh[:8 * D].view(np.float64).copy(), oh[8 * D:16 * D].view(np.float64).copy()
     nl_gh, nl_bh = oh[16 * D:20 * D].view(np.int32).copy(), oh[20 * D:].view(np.int32).copy()
-    order_h = order.cpu().numpy()
     if (nl_gh < 0).any() or (nl_bh < 0).any():
         raise N.HbxError("categorical codes must be integers in [0, 1024)")
     rows_g = order[:n_good]
