@@ -375,9 +375,9 @@ def main():
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     ev = kde.ScoreEvents()
     # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
-    # KDEs, not switched off, not the opt-in 32x32 tile
+    # KDEs, not switched off
     fused = (kernel_model(pair.bad, a.dc, a.du)["model"] is not None and pair.good.variant == pair.bad.variant
-             and os.environ.get("HBX_SCORE_PAIR", "1") != "0" and os.environ.get("HBX_SCORE_TILE", "") != "32")
+             and os.environ.get("HBX_SCORE_PAIR", "1") != "0")
     log("rank %d/%d: %d candidates x (%d + %d) observations, D=%d" % (rank, world, Nc, Ng, Nb, D))
 
     def step():

@@ -782,14 +782,6 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
-    // the 16x16-tile kernel; HBX_SCORE_TILE=32 selects the 32x32-tile variant for unsigned sums (an
-    // experiment: fewer issue cycles per pair on paper, slower as measured -- DESIGN.md section 4)
-    const char* tenv = getenv("HBX_SCORE_TILE");  // read per call (tests switch it in-process)
-    const bool t32 = tenv && atoi(tenv) == 32;
-    if (!sg && t32) {
-      const logpdf_fn f = hbx_pick_h32(nsc_of(dc_pad), kc);
-      if (f) return {f, r, 32 * H32_WAVES, 64 * H32_WAVES, nullptr, nullptr};
-    }
     return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES,
             hbx_pick_h_pair(nsc_of(dc_pad), kc, sg), sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }

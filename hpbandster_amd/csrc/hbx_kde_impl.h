@@ -147,5 +147,3 @@ logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
 logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
 logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
-logpdf_fn hbx_pick_h32(int nsc, int kc);                     // hbx_score_h32.hip (unsigned sums only)
-#define H32_WAVES 8  // waves per block of the 32x32 hmode kernel (32 candidates each)

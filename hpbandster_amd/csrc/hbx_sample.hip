@@ -21,11 +21,6 @@
 
 #define SAMPLE_BLOCK 256
 #define HBX_INV_SQRT_2PI_D 0.3989422804014327
-// diagnostic ablations (tools/ablate_sample.sh; never the shipped default): 1 = no normcdfinv,
-// 2 = no per-element Philox, 3 = both.  Timing only.
-#ifndef HBX_S_ABLATE
-#define HBX_S_ABLATE 0
-#endif
 #define DATUM_WORD 0xFFFFFFFFu  // counter word of the per-candidate datum draw (dims use 0..D-1)
 
 __device__ __forceinline__ HbxU32x4 draw(uint64_t seed, uint64_t i, uint32_t word, uint32_t stream) {
@@ -136,13 +131,7 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
       const double m = X[rows[idx] * (int64_t)D + d];
       const double h = bw[d];
       const int t = levels[d];
-      HbxU32x4 r;
-      if (HBX_S_ABLATE & 2) {
-        r.x[0] = (uint32_t)e * 0x9E3779B9u; r.x[1] = (uint32_t)e ^ 0x85EBCA6Bu;
-        r.x[2] = r.x[0] ^ 0xC2B2AE35u; r.x[3] = r.x[1] * 3u;
-      } else {
-        r = draw(seed, counter_base + (uint64_t)i, (uint32_t)d, stream_id);
-      }
+      const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)d, stream_id);
       const double u = hbx_u01_open(hbx_bits64(r, 0));
       double v;
       if (t == 0) {
@@ -161,7 +150,7 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
             plo = normcdf(lo);
             phi = normcdf(hi);
           }
-          const double z = (HBX_S_ABLATE & 1) ? fma(u, hi - lo, lo) + 0.0 * (plo + phi) : tn_invert(plo, phi, lo, hi, u);
+          const double z = tn_invert(plo, phi, lo, hi, u);
           v = fma(bw_factor * h, flip ? -z : z, m);
         }
       } else {

@@ -8,14 +8,6 @@
 // the C_j pieces are in the bound); C_j rides along as three exact f16 pieces against A = 1 and the
 // one-hot categorical product follows in the same K loop.  c_i is the accumulator input of the first
 // MFMA.  VALU work per pair: exp2 and one add.
-// Diagnostic ablations (tools/ablate.sh builds them into separate libraries; never the shipped
-// default): 1 = no exp2, 2 = first K-step MFMA only, 3 = no per-chunk LDS-DMA/wait/barrier,
-// 4 = no running-sum adds, 5 = neither exp2 nor adds, 6 = 2 + 5.  Dropped values are kept alive with
-// empty asm statements (no dead-code elimination of the MFMAs); the rescue marker is disabled.
-// Results are wrong in every ablated build; only timing is read.
-#ifndef HBX_H_ABLATE
-#define HBX_H_ABLATE 0
-#endif
 
 // sched_group_barrier pattern: NM times {1 MFMA, then a share of NV VALU ops}, the remainder spread
 // over the first MFMAs (LLVM SchedGroupMask: MFMA = 0x8, VALU = 0x2)
@@ -240,12 +232,12 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
     for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
 #pragma unroll
     for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][0], b[0], ciq[r], 0, 0, 0);
-    constexpr int NDENSE = (HBX_H_ABLATE == 2 || HBX_H_ABLATE == 6) ? 1 : (SP ? NSC : NSH);
+    constexpr int NDENSE = SP ? NSC : NSH;
 #pragma unroll
     for (int s = 1; s < NDENSE; ++s)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
-    if constexpr (SP && HBX_H_ABLATE != 2 && HBX_H_ABLATE != 6) {
+    if constexpr (SP) {
       // B of the sparse step: lane group g holds K = 8g .. 8g+7 and 32 + 8g .. 32 + 8g + 7 of the
       // 64-wide step, i.e. the two dense fragments already read
 #pragma unroll
@@ -301,14 +293,14 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) mx[r][q] = fmaxf(mx[r][q], __shfl_xor(mx[r][q], o));
         const float d = rintf(-mx[r][q]);
-        dl[r][q] = (HBX_H_ABLATE == 0 && d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
+        dl[r][q] = (d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
         ciq[r][q] += dl[r][q];
       }
   }
 
   for (int c = 0; c < nchunks; ++c) {
-    const float* buf = lds + (HBX_H_ABLATE == 3 ? 0 : (c % NBUF)) * CHF;
-    if (HBX_H_ABLATE != 3) issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
+    const float* buf = lds + (c % NBUF) * CHF;
+    issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
     float Sb[RT][4], Snb[RT][4];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -330,11 +322,8 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          constexpr bool NOEXP = HBX_H_ABLATE == 1 || HBX_H_ABLATE == 5 || HBX_H_ABLATE == 6;
-          constexpr bool NOADD = HBX_H_ABLATE == 4 || HBX_H_ABLATE == 5 || HBX_H_ABLATE == 6;
-          const float e = NOEXP ? cur[r][q] : __builtin_amdgcn_exp2f(cur[r][q]);
-          if (NOADD) asm volatile("" ::"v"(e));
-          Sb[r][q] = (jt == 0 || NOADD) ? e : Sb[r][q] + e;
+          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
+          Sb[r][q] = jt == 0 ? e : Sb[r][q] + e;
           if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, jt == 0 ? 0.f : Snb[r][q]);
         }
       if (!SIGNED && jt + 1 < OBS_CHUNK / 16) {
@@ -358,13 +347,11 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       }
     // chunk c+1 complete for this wave (PD-1 chunks stay in flight), this wave's reads of buffer c
     // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
-    if (HBX_H_ABLATE != 3) {
-      if (NX && xpiece)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((GL + 1) * (PD - 1)) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
-      __builtin_amdgcn_s_barrier();
-    }
+    if (NX && xpiece)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((GL + 1) * (PD - 1)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
+    __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 #pragma unroll
@@ -401,7 +388,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
         // f16 hi/lo representation error of both coordinates and the three lo.lo products given up
         // to the C_j pieces (each <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
         if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-20f) * HBX_LN2f;
-        if (!nq && Sq == Sq && (Sq < 0x1p-64f || Sq > 0x1p100f) && HBX_H_ABLATE == 0) o.err = -1.f;
+        if (!nq && Sq == Sq && (Sq < 0x1p-64f || Sq > 0x1p100f)) o.err = -1.f;
         out[ii] = o;
       }
     }

@@ -291,22 +291,6 @@ def test_clamped_ties_score_one_first_index(device):
     assert rb[1].index == O.py_argmin(scores[800:1300])
 
 
-@pytest.mark.parametrize("name", ["d32m", "mixed8", "hgt1", "catonly"])
-def test_tile32_variant_matches_oracle(device, name, monkeypatch):
-    """The 32x32-tile hmode variant (HBX_SCORE_TILE=32, unsigned sums) against the reference: same
-    chosen index, ln-pdfs within the fp32 tolerance."""
-    monkeypatch.setenv("HBX_SCORE_TILE", "32")
-    c = G.load_kde_case(name)
-    pair = _pair_from_fixture(c)
-    res, logl, logg = pair.acquire(c["cands"], logs=True)
-    assert res.index == c["chosen"]
-    for est, kde_ in ((logl, pair.good), (logg, pair.bad)):
-        lref = O.log_pdf_many(c["X"][kde_.rows_dev.cpu().numpy()], kde_.bw, c["var_type"], c["cands"], kde_.nlev)
-        fin = np.isfinite(lref)
-        err = np.abs(est[fin] - lref[fin]) / np.maximum(1, np.abs(lref[fin]))
-        assert err.max() <= 3e-5, (name, err.max())
-
-
 @pytest.mark.parametrize("shape", [(24, 8, 4, 3000, 20011), (32, 0, 0, 1000, 777), (16, 8, 3, 400, 65)])
 def test_pair_launch_identical_to_two_launches(device, shape, monkeypatch):
     """l and g scored by one pair launch (the default) against two single launches
