@@ -32,6 +32,10 @@ SIGNATURES = {
     "hbx_kde_bucket": (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp]),
     "hbx_kde_table_floats": (c_i64, [c_i32, c_i32, c_i32]),
     "hbx_kde_prepare": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_refit_out_bytes": (c_i64, [c_i64, c_i32]),
+    "hbx_kde_refit_scratch_bytes": (c_i64, [c_i64, c_i32]),
+    "hbx_kde_refit": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_double,
+                              ctypes.c_double, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "hbx_kde_logpdf": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "hbx_kde_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "hbx_kde_acquire": (c_i32, [c_vp, c_i64, c_i32, c_i64,
@@ -55,8 +59,17 @@ SIGNATURES = {
     "hbx_event_destroy": (c_i32, [c_vp]),
     "hbx_event_elapsed_ms": (c_i32, [c_vp, c_vp, c_vp]),
     "hbx_kde_result_ptr": (c_vp, [c_vp]),
+    "hbx_kde_ws_offsets": (c_i32, [c_i64, c_i64, c_i64, c_vp]),
+    "hbx_np_exp": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_pdf_scratch_bytes": (c_i64, [c_i64]),
     "hbx_kde_pdf_exact": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_rccl_unique_id_bytes": (c_i64, []),
+    "hbx_rccl_get_unique_id": (c_i32, [c_vp]),
+    "hbx_rccl_comm_init": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32]),
+    "hbx_rccl_comm_destroy": (c_i32, [c_vp]),
+    "hbx_argmax_gather_bytes": (c_i64, [c_i32]),
+    "hbx_argmax_allreduce": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "hbx_argmax_records": (c_i32, [c_vp, c_i32, c_vp, c_vp]),
     "hbx_sh_promote": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
 }
 
@@ -107,7 +120,31 @@ def ptr(t):
     return t.ctypes.data
 
 
-def stream_handle(stream=None):
+def stream_handle(stream=None, device=None):
+    """hipStream_t of ``stream``, else torch's current stream of ``device`` (not of the calling thread's
+    current device: a dispatcher thread's current device is 0 whatever device the model lives on)."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return s.cuda_stream
+
+
+class on_device(object):
+    """Context of one engine call: ``device`` current (so torch's copies and allocations land there) and,
+    with an explicit ``stream``, that stream current too -- the host<->device copies torch enqueues and
+    the kernels libhbx enqueues are then ordered on one stream."""
+
+    def __init__(self, device, stream=None):
+        import torch
+        self._ctx = [torch.cuda.device(device)]
+        if stream is not None:
+            self._ctx.append(torch.cuda.stream(stream))
+
+    def __enter__(self):
+        for c in self._ctx:
+            c.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        for c in reversed(self._ctx):
+            c.__exit__(*exc)
+        return False

@@ -76,7 +76,10 @@ def build(force=False, jobs=None, verbose=True):
     rebuilt = any(r for _, r in results)
     if rebuilt or force or not os.path.exists(LIB):
         tmp = LIB + ".tmp"
-        cmd = [hipcc(), "-shared", "-fPIC", "--offload-arch=%s" % ARCH, "-o", tmp] + objs
+        # RCCL for the multi-GPU winner exchange (hbx_dist.hip); at run time the SONAME librccl.so.1
+        # resolves to the copy torch has already loaded, so one RCCL runtime serves both
+        cmd = [hipcc(), "-shared", "-fPIC", "--offload-arch=%s" % ARCH, "-o", tmp] + objs + [
+            "-L/opt/rocm/lib", "-lrccl"]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s" % r.stdout)

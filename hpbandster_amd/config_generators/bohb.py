@@ -21,7 +21,7 @@ import numpy as np
 import scipy.stats as sps
 
 from .. import _native
-from ..kde import fit_pair
+from ..kde import ObservationStore
 from .base import base_config_generator
 from ._cs import ConfigSpace
 
@@ -68,6 +68,7 @@ class BOHB(base_config_generator):
         self.losses = dict()
         self.good_config_rankings = dict()
         self.kde_models = dict()
+        self._stores = dict()  # budget -> ObservationStore: the budget's rows resident in HBM
 
     # -- candidates ---------------------------------------------------------------------------
     def sample_candidates(self, kde_good, num_samples):
@@ -199,16 +200,21 @@ class BOHB(base_config_generator):
         if max(list(self.kde_models.keys()) + [-np.inf]) > budget:  # bohb.py:204-205
             return
         conf = ConfigSpace.Configuration(self.configspace, job.kwargs["config"])
-        self.configs[budget].append(conf.get_array())
+        vec = conf.get_array()
+        self.configs[budget].append(vec)
         self.losses[budget].append(loss)
+        store = self._stores.get(budget)
+        if store is None:
+            store = self._stores[budget] = ObservationStore(len(self.kde_vartypes), self.kde_vartypes,
+                                                            device=self.device)
+        store.add(vec, loss)
         if len(self.configs[budget]) <= self.min_points_in_model + 1:
             return
-        train_configs = np.array(self.configs[budget])
-        train_losses = np.array(self.losses[budget])
-        pair = fit_pair(train_configs, train_losses, self.kde_vartypes, self.min_points_in_model,
-                        self.top_n_percent, device=self.device)
+        # one refit call: the new row to the device, argsort, split, bandwidths, both KDEs prepared
+        pair = store.refit(self.min_points_in_model, self.top_n_percent)
         if pair is None:  # bohb.py:234-237: too few rows for a KDE
             return
-        self.kde_models[budget] = pair
+        self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
         self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
-                          'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs, np.min(train_losses)))
+                          'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,
+                                                       np.min(store.losses_host)))

@@ -12,7 +12,7 @@ import numpy as np
 import scipy.optimize as spo
 import scipy.stats as sps
 
-from ..kde import fit_pair
+from ..kde import ObservationStore
 from .base import base_config_generator
 from ._cs import ConfigSpace
 
@@ -35,6 +35,7 @@ class KDEEI(base_config_generator):
         self.configs = dict()
         self.losses = dict()
         self.kde_models = dict()
+        self._stores = dict()  # budget -> ObservationStore (rows resident in HBM)
 
     def get_config(self, budget):
         sample = None
@@ -82,13 +83,17 @@ class KDEEI(base_config_generator):
             self.configs[budget] = []
             self.losses[budget] = []
         conf = ConfigSpace.Configuration(self.configspace, job.kwargs['config'])
-        self.configs[budget].append(conf.get_array())
+        vec = conf.get_array()
+        self.configs[budget].append(vec)
         self.losses[budget].append(loss)
+        store = self._stores.get(budget)
+        if store is None:
+            store = self._stores[budget] = ObservationStore(len(self.var_type), self.var_type, device=self.device)
+        store.add(vec, loss)
         if len(self.configs[budget]) <= self.min_points_in_model:
             return
         if len(self.configs[budget]) % self.update_after_n_points == 0:
-            pair = fit_pair(np.array(self.configs[budget]), np.array(self.losses[budget]), self.var_type,
-                            self.min_points_in_model, self.top_n_percent, device=self.device, split_rule="kde_ei")
+            pair = store.refit(self.min_points_in_model, self.top_n_percent, split_rule="kde_ei")
             if pair is None:
                 return
             self.kde_models[budget] = pair

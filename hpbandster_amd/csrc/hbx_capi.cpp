@@ -20,7 +20,7 @@ const char* hbx_last_error(void) { return g_err; }
 
 const char* hbx_version(void) { return "hbx 0.1.0 gfx950"; }
 
-int64_t hbx_kde_param_bytes(void) { return (int64_t)sizeof(KdeParams); }
+int64_t hbx_kde_param_bytes(void) { return (int64_t)HBX_PARAM_BYTES; }
 
 int64_t hbx_kde_est_bytes(void) { return (int64_t)sizeof(KdeEst); }
 

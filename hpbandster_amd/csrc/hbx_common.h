@@ -54,6 +54,8 @@ struct KdeParams {
   double prod_bw_c;   // sequential product of continuous bandwidths (reference op order)
   float cmax;         // max_j |C_j| over the table (error bound)
   float sum_abs_delta;// sum |delta_u| over finite deltas (error bound)
+  float cmax2;        // max_j |C_j| of the f32-layout rebuild (hmode table out of the f16 range)
+  int32_t pad1;
   int32_t kc;         // categorical mode: 0 = VALU match on codes, k >= 1 = one-hot on f16 MFMA,
                       // k steps of K=32 (2 * oh_total <= 32 k)
   int32_t hmode;      // 1: continuous product on f16 matrix cores too (hi/lo split coordinates)
@@ -83,6 +85,11 @@ struct KdeParams {
   double bw[HBX_MAX_D];
 };
 
+// A parameter buffer (hbx_kde_param_bytes()) is the KdeParams block followed by a staging area for
+// hbx_kde_prepare's host inputs (bandwidths, level counts) and its info record.
+#define HBX_PARAM_STAGE ((sizeof(KdeParams) + 255) & ~(size_t)255)
+#define HBX_PARAM_BYTES (HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 64)
+
 // Per-candidate output of the fp32 log-domain scoring kernel, one per KDE.
 struct KdeEst {
   float lpos;   // ln(sum of positive terms) + log_norm   (NaN: structural NaN pdf)
@@ -91,16 +98,19 @@ struct KdeEst {
   float pad;
 };
 
-// Result of one acquisition on one device.
+// Result of one acquisition on one device.  The first 24 bytes (index, score, rel, flags) are what a
+// multi-GPU winner exchange needs.
 struct AcqResult {
   int64_t index;     // winning candidate (global index), -1 when no finite score exists
   double score;      // its exact fp64 score max(1e-8, g) / max(l, 1e-8)
+  float rel;         // bound of |score - score in numpy's arithmetic| / score (exp may differ by ulps)
+  int32_t flags;     // HBX_ACQ_* bits
+  int32_t shortlist; // candidates re-scored in fp64
+  int32_t near;      // candidates whose score is within the bounds of the winner's (1: certified)
   double pdf_l;      // exact fp64 l(x) of the winner
   double pdf_g;      // exact fp64 g(x) of the winner
-  int64_t shortlist; // candidates re-scored in fp64
-  int32_t flags;     // bit0: fp64 overflow risk -> every candidate re-scored
-  int32_t pad;
 };
+// flags: HBX_ACQ_OVERFLOW / HBX_ACQ_NEAR_TIE / HBX_ACQ_RESOLVED (include/hbx.h)
 
 // float <-> order-preserving uint32 (for atomicMin on floats of either sign)
 __device__ __forceinline__ uint32_t hbx_f2ord(float f) {
@@ -111,9 +121,11 @@ __device__ __forceinline__ float hbx_ord2f(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-// double -> order-preserving uint64 with every NaN mapped past +inf
+// double -> order-preserving uint64 with every NaN mapped past +inf; -0.0 and 0.0 map to one key
+// (numpy's comparison sorts treat them as equal: ties, ranked by position)
 __device__ __forceinline__ uint64_t hbx_d2ord(double d) {
   if (d != d) return ~0ull;
+  if (d == 0.0) d = 0.0;
   uint64_t u = (uint64_t)__double_as_longlong(d);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }

@@ -13,6 +13,7 @@
 #include <math.h>
 
 #include "hbx_common.h"
+#include "hbx_npexp.h"
 #include "hbx_pairwise.h"
 
 struct CvShared {
@@ -34,7 +35,7 @@ __device__ __forceinline__ double cv_conv_term(const double* __restrict__ xj, in
     double k;
     if (sh->cont[d]) {
       const double t = xj[d] - sh->xi[d];
-      k = c4 * exp(-(t * t) / sh->h4[d]);
+      k = c4 * hbx_npexp::exp(-(t * t) / sh->h4[d]);
     } else {
       // sum over the column's levels (ascending order of the negated values, np.unique of -data)
       const double vj = -xj[d], vi = -sh->xi[d];
@@ -58,7 +59,7 @@ __device__ __forceinline__ double cv_loo_term(const double* __restrict__ xj, int
     double k;
     if (sh->cont[d]) {
       const double t = xj[d] - sh->xi[d];
-      k = c2 * exp(-(t * t) / sh->h2[d]);
+      k = c2 * hbx_npexp::exp(-(t * t) / sh->h2[d]);
     } else {
       k = (xj[d] == sh->xi[d]) ? sh->a1[d] : sh->a0loo[d];
     }

@@ -322,7 +322,11 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
 extern "C" {
 
 // Scratch bytes hbx_kde_fit / hbx_sh_promote need for N total rows.
-int64_t hbx_sort_scratch_bytes(int64_t N) { return (int64_t)(2 * (sizeof(uint64_t) + sizeof(int32_t)) * N + 64); }
+// sort scratch: two (key, position) ping-pong arrays, then room for the promotion's sorted positions
+// when its caller passes no `order` buffer (hbx_sh_promote, brackets > 1024)
+int64_t hbx_sort_scratch_bytes(int64_t N) {
+  return (int64_t)((2 * (sizeof(uint64_t) + sizeof(int32_t)) + sizeof(int64_t)) * N + 64);
+}
 
 static int sort_tile(int64_t max_seg) {
   int tile = 64;

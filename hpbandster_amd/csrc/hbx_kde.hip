@@ -25,9 +25,9 @@
 // ------------------------------------------------------------------------------------------
 // model preparation
 
-static void bucket_dims(int dc, int du, int* dc_pad, int* du_pad) {
-  static const int dcb[] = {0, 4, 8, 16, 24, 32, 64};
-  static const int dub[] = {0, 4, 8, 16, 32};
+__host__ __device__ static void bucket_dims(int dc, int du, int* dc_pad, int* du_pad) {
+  const int dcb[] = {0, 4, 8, 16, 24, 32, 64};
+  const int dub[] = {0, 4, 8, 16, 32};
   *dc_pad = -1;
   *du_pad = -1;
   for (int b : dcb)
@@ -36,7 +36,7 @@ static void bucket_dims(int dc, int du, int* dc_pad, int* du_pad) {
     if (du <= b) { *du_pad = b; break; }
 }
 
-static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }  // floats per chunk
+__host__ __device__ static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 // capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
@@ -46,41 +46,190 @@ static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
   return n_chunks(n) * (int64_t)(a > c ? a : c);
 }
 
-// Per active categorical dim (one block each): max observed code, -1 if some code is not an
-// integer in [0, 1024) (then the one-hot mode is not used).
-__global__ __launch_bounds__(256) void kde_maxcode_kernel(const double* __restrict__ X, int32_t D,
-                                                          const int64_t* __restrict__ rows,
-                                                          KdeParams* __restrict__ P) {
-  __shared__ int red[256];
-  const int u = blockIdx.x;
-  const int d = P->cat_dim[u];
-  int m = -1, bad = 0;
-  for (int j = threadIdx.x; j < P->n; j += blockDim.x) {
-    const double v = X[rows[j] * (int64_t)D + d];
-    if (!(v >= 0.0 && v < 1024.0) || v != floor(v)) bad = 1;
-    else m = max(m, (int)v);
-  }
-  red[threadIdx.x] = bad ? 100000 : m;
+// Model preparation runs on the device from (data rows, bandwidths, level counts), so a refit needs
+// no host round trip until its single read-back (hbx_kde_refit).  One or two KDEs per launch
+// (PrepSet): block / block range k belongs to KDE k.
+struct PrepArgs {
+  const double* X;      // device f64[*][D]
+  const int64_t* rows;  // device i64[n]
+  const double* bw;     // device f64[D]
+  const int32_t* nlev;  // device i32[D]
+  KdeParams* P;
+  int32_t* info;        // device i32[8]
+  int32_t n, D;
+  int32_t hm_allowed;   // HBX_HMODE not 0
+  int32_t nblk_table;   // blocks of this KDE in the table launches
+  uint32_t vt[HBX_MAX_D / 32];  // bit d: dim d categorical ('u')
+};
+struct PrepSet {
+  PrepArgs k[2];
+  int32_t nk;
+};
+
+__device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
+
+// The parameter block of one KDE (one workgroup): per-dim scales and log-ratios (thread 0, serial in
+// dim order), the largest observed code of every active categorical dim (whole block), then the
+// one-hot layout and the kernel mode.
+__global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
+  const PrepArgs& A = blockIdx.x ? ps.k[1] : ps.k[0];  // (no dynamic index into the kernel arguments)
+  KdeParams* P = A.P;
+  const int D = A.D, n = A.n;
+  uint32_t* pz = (uint32_t*)P;
+  for (int i = threadIdx.x; i < (int)(sizeof(KdeParams) / 4); i += blockDim.x) pz[i] = 0u;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
+  __shared__ int s_du;
+  __shared__ int s_catdim[HBX_MAX_D];
+  __shared__ int red[256];
+  if (threadIdx.x == 0) {
+    const double LOG2E = 1.4426950408889634;
+    double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
+    float sad = 0.f;
+    int dc = 0, du = 0, nconst = 0, dc_tot = 0, du_tot = 0;
+    for (int d = 0; d < D; ++d) (prep_cat(A, d) ? du_tot : dc_tot)++;
+    int dcp, dup;
+    bucket_dims(dc_tot, du_tot, &dcp, &dup);
+    P->n = n;
+    P->D = D;
+    P->dc_pad = dcp;
+    P->du_pad = dup;
+    P->stride = table_stride(dcp, dup);
+    for (int d = 0; d < D; ++d) {
+      const double h = A.bw[d];
+      const bool cat = prep_cat(A, d);
+      P->vartype[d] = cat ? 1 : 0;
+      P->nlev[d] = A.nlev[d];
+      P->bw[d] = h;
+      if (!cat) {
+        const int k = dc++;
+        P->cont_dim[k] = d;
+        prod_bw_c *= h;  // np.prod(bw[iscontinuous]), sequential in dim order
+        if (!(h > 0.0)) {
+          P->nan_all = 1;  // exp(-0/0) * ... / 0 -> NaN for every candidate
+          P->cont_scale[k] = 0.0;
+        } else {
+          P->cont_scale[k] = sqrt(LOG2E / 2.0) / h;
+          sum_ln_h += log(h);
+        }
+      } else {
+        const int c = A.nlev[d];
+        if (c == 1 && h == 0.0) {  // single observed level: match -> 1, mismatch -> 0/0 = NaN
+          P->const_dim[nconst++] = d;
+          continue;
+        }
+        if (c < 2 || !(h > 0.0) || h != h) {  // includes c == -1: codes not integers in [0, 1024)
+          P->unsupported = 1;
+          continue;
+        }
+        const double a = 1.0 - h, b = h / (double)(c - 1);
+        const double lb = log2(b);
+        const double la = (a == 0.0) ? -INFINITY : log2(fabs(a));
+        const int u = du++;
+        P->cat_dim[u] = d;
+        s_catdim[u] = d;
+        m0 += (la > lb) ? la : lb;
+        lb_sum += lb;
+        if (a == 0.0) {
+          P->cat_delta[u] = -1e30f;
+        } else {
+          P->cat_delta[u] = (float)(la - lb);
+          sad += fabsf(P->cat_delta[u]);
+        }
+        P->cat_negf[u] = (a < 0.0) ? 1.f : 0.f;
+        if (a < 0.0) P->has_neg = 1;
+      }
+    }
+    P->dc = dc;
+    P->du = du;
+    P->nconst = nconst;
+    P->m0_log2 = m0;
+    P->lb_sum = lb_sum;
+    P->prod_bw_c = prod_bw_c;
+    P->sum_abs_delta = sad;
+    P->log_norm = -log((double)n) - sum_ln_h - 0.5 * (double)dc * log(2.0 * M_PI) + m0 * M_LN2;
+    P->X = A.X;
+    P->rows = A.rows;
+    s_du = du;
+  }
+  __syncthreads();
+  // largest observed code per active categorical dim; -1 if some code is not an integer in [0, 1024)
+  for (int u = 0; u < s_du; ++u) {
+    const int d = s_catdim[u];
+    int m = -1, bad = 0;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      const double v = A.X[A.rows[j] * (int64_t)D + d];
+      if (!(v >= 0.0 && v < 1024.0) || v != floor(v)) bad = 1;
+      else m = max(m, (int)v);
+    }
+    red[threadIdx.x] = bad ? 100000 : m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) P->cat_maxcode[u] = red[0] >= 100000 ? -1 : red[0];
     __syncthreads();
   }
-  if (threadIdx.x == 0) P->cat_maxcode[u] = red[0] >= 100000 ? -1 : red[0];
+  if (threadIdx.x != 0) return;
+  for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
+    P->oh_col[t] = 0;
+    P->oh_val[t] = NAN;
+  }
+  // categorical mode: one-hot on the f16 matrix cores when every active dim has integer codes in
+  // [0, 1024) and the one-hot width sum(max code + 1) fits OH_MAX_KC K-steps; else VALU matching.
+  // One-hot positions: every dim's block starts at an even position (a padding position, level -1,
+  // never matches) -- the sparse matrix-core kernel relies on adjacent pairs never spanning dims.
+  const int du = P->du, dcp = P->dc_pad, dup = P->du_pad;
+  if (du > 0) {
+    int tot = 0;
+    bool ok = true;
+    for (int u = 0; u < du; ++u) {
+      if (P->cat_maxcode[u] < 0) ok = false;
+      else tot = ((tot + 1) & ~1) + P->cat_maxcode[u] + 1;
+    }
+    if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
+      P->kc = (2 * tot + 31) / 32;
+      P->oh_total = tot;
+      int t = 0;
+      for (int u = 0; u < du; ++u) {
+        if (t & 1) {
+          P->oh_dim[t] = u;
+          P->oh_level[t] = -1;
+          ++t;
+        }
+        for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
+          P->oh_dim[t] = u;
+          P->oh_level[t] = l;
+          P->oh_col[t] = P->cat_dim[u];
+          P->oh_val[t] = (double)l;
+          ++t;
+        }
+      }
+    }
+  }
+  // continuous product on the f16 matrix cores (hi/lo split) when it has >= 8 dims (one full
+  // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
+  // otherwise the exact f32 MFMA product.  |C_j| beyond the f16 range is caught after the table.
+  const bool hm_ok = (du == 0 || P->kc > 0) && dcp >= 8;
+  P->hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
+  P->nsc = nsc_of(dcp);
+  P->chunk_floats = P->hmode ? h_chunk_floats(dcp, P->kc, P->has_neg)
+                             : chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
 }
 
-// Per continuous slot (one block each): mean of the KDE's data column, the centre of the scaled
-// coordinates.  Any finite centre is correct (table and candidates use the same one); it only keeps
-// the fp32 expansion well conditioned, so the summation order is free.
-__global__ __launch_bounds__(256) void kde_center_kernel(const double* __restrict__ X, int32_t D,
-                                                         const int64_t* __restrict__ rows,
-                                                         KdeParams* __restrict__ P) {
-  __shared__ double red[4];
-  const int k = blockIdx.x;
+// Per continuous slot: mean of the KDE's data column, the centre of the scaled coordinates.  Any
+// finite centre is correct (table and candidates use the same one); it only keeps the fp32 expansion
+// well conditioned, so the summation order is free.  Blocks [k*D, (k+1)*D) belong to KDE k.
+__global__ __launch_bounds__(256) void kde_center_kernel(PrepSet ps) {
+  const PrepArgs& A = (int)blockIdx.x >= ps.k[0].D ? ps.k[1] : ps.k[0];
+  const int k = blockIdx.x % ps.k[0].D;
+  KdeParams* P = A.P;
+  if (k >= P->dc) return;
   const int d = P->cont_dim[k];
-  const int n = P->n;
+  const int n = A.n;
+  __shared__ double red[4];
   double acc = 0.0;
-  for (int j = threadIdx.x; j < n; j += 256) acc += X[rows[j] * (int64_t)D + d];
+  for (int j = threadIdx.x; j < n; j += 256) acc += A.X[A.rows[j] * (int64_t)A.D + d];
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
@@ -90,15 +239,13 @@ __global__ __launch_bounds__(256) void kde_center_kernel(const double* __restric
   }
 }
 
-// Fill the chunked observation table (layout above).  X'_jc = s_c * (X_jc - mu_c),
-// C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per table slot j < nchunks*64.
-// one thread per observation row (a serial walk over its dims); launched as 64-thread blocks so a
-// 1e4-row table spreads over ~150 CUs instead of ~40
-__global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict__ X, int32_t D,
-                                                        const int64_t* __restrict__ rows,
-                                                        KdeParams* __restrict__ P,
-                                                        float* __restrict__ table) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
+// C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per observation row (a serial walk over
+// its dims), 64-thread blocks so a 1e4-row table spreads over ~150 CUs.  `hm` / `chunk_f` select the
+// layout; |C_j| and |X'| maxima go to *cmax_acc / P->xmax.
+__device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
+                                               KdeParams* __restrict__ P, float* __restrict__ table, int j, bool hm,
+                                               int chunk_f, float* cmax_acc) {
   const int n = P->n;
   const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
   const bool ok = j < n;
@@ -106,9 +253,8 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   const double* x = X + (ok ? rows[j] : rows[0]) * (int64_t)D;
   const int dc = P->dc, du = P->du, dcp = P->dc_pad, dup = P->du_pad;
   const int KP = kp_of(dcp);
-  float* ch = table + (int64_t)(j / OBS_CHUNK) * P->chunk_floats;
+  float* ch = table + (int64_t)(j / OBS_CHUNK) * chunk_f;
   const int jj = j % OBS_CHUNK;
-  const bool hm = P->hmode != 0;
   const int KTP = h_ktp(dcp, P->kc);
   _Float16* hrow = (_Float16*)(ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
@@ -195,9 +341,104 @@ __global__ __launch_bounds__(256) void kde_table_kernel(const double* __restrict
   }
   float a = ok ? fabsf(Cf) : 0.f;
   for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
-  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)&P->cmax, __float_as_uint(a));
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)cmax_acc, __float_as_uint(a));
   if (j == 0)
     for (int q = 0; q < P->nconst; ++q) P->const_level[q] = x[P->const_dim[q]];
+}
+
+// f32-MFMA layout of an hmode KDE whose C_j left the f16 range of the three-piece split
+__device__ __forceinline__ bool table_needs_rebuild(const KdeParams* P) { return P->hmode && !(P->cmax <= H_CMAX); }
+
+// pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
+// block of a KDE that needs none exits at once)
+__global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0, float* table1, int pass) {
+  const bool second = ps.nk > 1 && (int)blockIdx.x >= ps.k[0].nblk_table;
+  const PrepArgs& A = ps.k[second ? 1 : 0];
+  KdeParams* P = A.P;
+  const int j = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64 + threadIdx.x;
+  if (pass == 0) {
+    kde_table_body(A.X, A.D, A.rows, P, second ? table1 : table0, j, P->hmode != 0, P->chunk_floats, &P->cmax);
+  } else if (table_needs_rebuild(P)) {
+    kde_table_body(A.X, A.D, A.rows, P, second ? table1 : table0, j, false,
+                   chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0), &P->cmax2);
+  }
+}
+
+// Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
+// du_pad}; variant = has_neg | kc << 1 | hmode << 4 selects the scoring kernel.
+__global__ void kde_prep_finish_kernel(PrepSet ps) {
+  const int k = threadIdx.x;
+  if (k >= ps.nk) return;
+  const PrepArgs& A = k ? ps.k[1] : ps.k[0];
+  KdeParams* P = A.P;
+  if (table_needs_rebuild(P)) {
+    P->hmode = 0;
+    P->chunk_floats = chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0);
+    P->cmax = P->cmax2;
+  }
+  int32_t* info = A.info;
+  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4);
+  info[1] = P->nan_all;
+  info[2] = P->unsupported;
+  info[3] = P->dc;
+  info[4] = P->du;
+  info[5] = P->nconst;
+  info[6] = P->dc_pad;
+  info[7] = P->du_pad;
+}
+
+static int64_t prep_table_blocks(int64_t n) { return (((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK + 63) / 64; }
+
+// host: fill a PrepArgs (vartype from host memory), checking the table capacity
+static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* rows, int32_t n, const int32_t* vartype,
+                     const double* bw, const int32_t* nlev, void* params, int32_t* info, int64_t table_floats_) {
+  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
+  if (n < 1) return hbx_fail(HBX_ERR_ARG, "KDE with n=%d observations", n);
+  memset(A, 0, sizeof(*A));
+  int dc = 0, du = 0;
+  for (int d = 0; d < D; ++d) {
+    if (vartype[d] != 0) {
+      A->vt[d >> 5] |= 1u << (d & 31);
+      ++du;
+    } else {
+      ++dc;
+    }
+  }
+  int dcp, dup;
+  bucket_dims(dc, du, &dcp, &dup);
+  if (dcp < 0 || dup < 0)
+    return hbx_fail(HBX_ERR_UNSUPPORTED, "no scoring kernel for %d continuous / %d categorical dims", dc, du);
+  if (table_floats_ < table_floats(n, dcp, dup))
+    return hbx_fail(HBX_ERR_ARG, "table too small: %lld < %lld floats", (long long)table_floats_,
+                    (long long)table_floats(n, dcp, dup));
+  const char* hm_env = getenv("HBX_HMODE");  // 0: the f32-MFMA kernels everywhere (tests)
+  A->X = X;
+  A->rows = rows;
+  A->bw = bw;
+  A->nlev = nlev;
+  A->P = (KdeParams*)params;
+  A->info = info;
+  A->n = n;
+  A->D = D;
+  A->hm_allowed = !(hm_env && hm_env[0] == '0');
+  A->nblk_table = (int32_t)prep_table_blocks(n);
+  return HBX_OK;
+}
+
+// enqueue the preparation of ps.nk KDEs (no host synchronisation)
+static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s) {
+  hipLaunchKernelGGL(kde_params_kernel, dim3(ps.nk), dim3(256), 0, s, ps);
+  HBX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kde_center_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
+  HBX_LAUNCH_CHECK();
+  const unsigned tb = (unsigned)(ps.k[0].nblk_table + (ps.nk > 1 ? ps.k[1].nblk_table : 0));
+  hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 0);
+  HBX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 1);
+  HBX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kde_prep_finish_kernel, dim3(1), dim3(64), 0, s, ps);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
 }
 
 // Rescue (rare): candidates whose every term sits far below the static bound M0 are recomputed
@@ -303,7 +544,8 @@ __global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int
     res->pdf_g = NAN;
     res->shortlist = 0;
     res->flags = 0;
-    res->pad = 0;
+    res->near = 0;
+    res->rel = 0.f;
   }
 }
 
@@ -311,13 +553,14 @@ __global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int
 __global__ void acq_init_batch_kernel(int64_t B, uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                       int32_t* __restrict__ segcnt, uint64_t* __restrict__ best,
                                       uint64_t* __restrict__ key, int32_t* __restrict__ first1,
-                                      int32_t* __restrict__ count) {
+                                      int32_t* __restrict__ count, int32_t* __restrict__ segnear) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) *count = 0;
   if (b < B) {
     U[b] = hbx_f2ord(INFINITY);
     flags[b] = 0;
     segcnt[b] = 0;
+    segnear[b] = 0;
     first1[b] = INT32_MAX;
     best[b] = ~0ull;
     key[b] = ~0ull;
@@ -455,6 +698,7 @@ __global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restr
   }
 }
 
+#include "hbx_npexp.h"
 #include "hbx_pairwise.h"
 
 struct ExactShared {
@@ -495,7 +739,7 @@ __device__ double exact_unit(const double* __restrict__ X, int32_t D, const int6
       double k;
       if (sh->cont[d]) {
         const double diff = v - xv;
-        k = HBX_INV_SQRT_2PI * exp(-(diff * diff) / sh->c0[d]);
+        k = HBX_INV_SQRT_2PI * hbx_npexp::exp(-(diff * diff) / sh->c0[d]);  // numpy's exp, bit for bit
       } else {
         k = (v == xv) ? sh->c0[d] : sh->c1[d];
       }
@@ -608,19 +852,55 @@ __global__ __launch_bounds__(EXACT_THREADS) void kde_pdf_exact_kernel(const doub
   }
 }
 
+// Bound of |exact pdf here - pdf in numpy's arithmetic| / pdf for one KDE at one candidate.  Both run
+// the same IEEE operations in the same order (SM:_kernel_base.py:509-516: per-dim kernels, dim-ordered
+// product, / prod(bw_c), numpy's pairwise sum, / n) except exp, where ocml's and numpy's results may
+// differ by ulps: per term <= (6 D + 4) u, plus 2 u per level of the summation tree (<= 40 levels up
+// to 1e5 observations) -- (8 D + 160) 2^-52 leaves a margin over both.  Sums with negative terms
+// (categorical bandwidth > 1) scale by their condition number sum|t| / |sum t|, taken pessimistically
+// from the fp32 estimate (inf when its sign is not certain).
+__device__ __forceinline__ double exact_rel(const KdeParams* __restrict__ P, const KdeEst e) {
+  const double base = (8.0 * (double)P->D + 160.0) * 0x1p-52;
+  if (!P->has_neg) return base;
+  const float m = fmaxf(e.lpos, e.lneg);
+  if (!(m > -INFINITY)) return base;
+  const float a = __expf(e.lpos - m), b = __expf(e.lneg - m);
+  const float den = fabsf(a - b) - (e.err + 1e-6f) * (a + b);
+  if (!(den > 0.f)) return INFINITY;
+  return base * (double)((a + b) / den) * 1.01;
+}
+
+// relative bound of one candidate's score (bohb.py:129: g clamped, / l clamped): both pdfs' bounds
+// plus the division's rounding
+__device__ __forceinline__ double score_rel(const KdeParams* __restrict__ Pg, const KdeParams* __restrict__ Pb,
+                                            const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
+                                            int64_t i) {
+  return exact_rel(Pg, el[i]) + exact_rel(Pb, eg[i]) + 0x1p-51;
+}
+
+// p may beat the winner in numpy's arithmetic only if s_p (1 - R_p) <= s_best (1 + R_best)
+__device__ __forceinline__ bool near_best(double s, double rp, double best, double rb) {
+  return s < INFINITY && s <= best * (1.0 + 1.0001 * (rp + rb));
+}
+
 __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ count,
                                                         const double* __restrict__ exact_l,
                                                         const double* __restrict__ exact_g,
                                                         const int32_t* __restrict__ flags, int64_t index_base,
-                                                        AcqResult* __restrict__ res) {
+                                                        const KdeParams* __restrict__ Pg,
+                                                        const KdeParams* __restrict__ Pb,
+                                                        const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
+                                                        int32_t* __restrict__ near_list, AcqResult* __restrict__ res) {
   __shared__ double bs[256];
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
+  __shared__ int32_t nnear;
   const int cnt = *count;
   double best = INFINITY;
   int64_t bidx = INT64_MAX;
   int32_t bpos = -1;
+  if (threadIdx.x == 0) nnear = 0;
   for (int p = threadIdx.x; p < cnt; p += 256) {
     // bohb.py:129 with Python max(): max(1e-8, g) keeps 1e-8 unless g > 1e-8 (NaN -> 1e-8);
     // max(l, 1e-8) keeps l unless 1e-8 > l (NaN -> NaN)
@@ -650,14 +930,29 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
     }
     __syncthreads();
   }
+  // the near set: every re-scored candidate the winner cannot be told apart from by these bounds
+  const int32_t wp = bp[0];
+  double rb = 0.0;
+  if (wp >= 0) {
+    const double sb = bs[0];
+    rb = score_rel(Pg, Pb, el, eg, list[wp]);
+    for (int p = threadIdx.x; p < cnt; p += 256) {
+      const double g = exact_g[p], l = exact_l[p];
+      const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
+      if (p == wp || near_best(s, score_rel(Pg, Pb, el, eg, list[p]), sb, rb)) near_list[atomicAdd(&nnear, 1)] = list[p];
+    }
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     res->shortlist = cnt;
-    res->flags = *flags;
-    if (bp[0] >= 0) {
+    res->flags = *flags | (nnear > 1 ? HBX_ACQ_NEAR_TIE : 0);
+    res->near = nnear;
+    res->rel = (float)rb;
+    if (wp >= 0) {
       res->index = bi[0] + index_base;
       res->score = bs[0];
-      res->pdf_l = exact_l[bp[0]];
-      res->pdf_g = exact_g[bp[0]];
+      res->pdf_l = exact_l[wp];
+      res->pdf_g = exact_g[wp];
     }
   }
 }
@@ -696,18 +991,54 @@ __global__ __launch_bounds__(256) void kde_batch_key_kernel(const int32_t* __res
     atomicMin((unsigned long long*)key + sg, ((unsigned long long)(i - sg * seg) << 32) | (uint32_t)p);
 }
 
+// per shortlist entry: 1 in near_flag (and counted in segnear) when its segment's winner cannot be
+// told apart from it by the error bounds (kde_final_kernel's near set, per segment)
+__global__ __launch_bounds__(256) void kde_batch_near_kernel(const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ count, uint32_t seg,
+                                                             const double* __restrict__ exact_l,
+                                                             const double* __restrict__ exact_g,
+                                                             const uint64_t* __restrict__ key,
+                                                             const KdeParams* __restrict__ Pg,
+                                                             const KdeParams* __restrict__ Pb,
+                                                             const KdeEst* __restrict__ el,
+                                                             const KdeEst* __restrict__ eg,
+                                                             int32_t* __restrict__ near_flag,
+                                                             int32_t* __restrict__ segnear) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *count) return;
+  const uint32_t i = (uint32_t)list[p], sg = i / seg;
+  const uint64_t k = key[sg];
+  int f = 0;
+  if (k != ~0ull) {
+    const int wp = (int)(uint32_t)k;
+    const double sb = bohb_score(exact_g[wp], exact_l[wp]);
+    const double rb = score_rel(Pg, Pb, el, eg, list[wp]);
+    const double s = bohb_score(exact_g[p], exact_l[p]);
+    f = (p == wp || near_best(s, score_rel(Pg, Pb, el, eg, i), sb, rb)) ? 1 : 0;
+  }
+  near_flag[p] = f;
+  if (f) atomicAdd(segnear + sg, 1);
+}
+
 __global__ __launch_bounds__(256) void kde_batch_final_kernel(int64_t B, const uint64_t* __restrict__ key,
                                                               const int32_t* __restrict__ segcnt,
                                                               const int32_t* __restrict__ flags,
+                                                              const int32_t* __restrict__ segnear,
+                                                              const int32_t* __restrict__ list,
                                                               const double* __restrict__ exact_l,
                                                               const double* __restrict__ exact_g,
+                                                              const KdeParams* __restrict__ Pg,
+                                                              const KdeParams* __restrict__ Pb,
+                                                              const KdeEst* __restrict__ el,
+                                                              const KdeEst* __restrict__ eg,
                                                               int64_t index_base, AcqResult* __restrict__ res) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   AcqResult r;
   r.shortlist = segcnt[b];
-  r.flags = flags[b];
-  r.pad = 0;
+  r.near = segnear[b];
+  r.flags = flags[b] | (r.near > 1 ? HBX_ACQ_NEAR_TIE : 0);
+  r.rel = 0.f;
   const uint64_t k = key[b];
   if (k == ~0ull) {
     r.index = -1;
@@ -720,6 +1051,7 @@ __global__ __launch_bounds__(256) void kde_batch_final_kernel(int64_t B, const u
     r.pdf_l = exact_l[p];
     r.pdf_g = exact_g[p];
     r.score = bohb_score(r.pdf_g, r.pdf_l);
+    r.rel = (float)score_rel(Pg, Pb, el, eg, list[p]);
   }
   res[b] = r;
 }
@@ -835,7 +1167,8 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
 // of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
 // comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t res, U, count, flags, segcnt, best, key, first1, est_l, est_g, lo, hi, list, exact_l, exact_g, part, total;
+  size_t res, U, count, flags, segcnt, segnear, best, key, first1, est_l, est_g, lo, hi, list, near, exact_l, exact_g,
+      part, total;
 };
 
 static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
@@ -851,6 +1184,7 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.U = take(4 * B);
   w.flags = take(4 * B);
   w.segcnt = take(4 * B);
+  w.segnear = take(4 * B);
   w.best = take(8 * B);
   w.key = take(8 * B);
   w.first1 = take(4 * B);
@@ -859,6 +1193,7 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.lo = take(4 * Nc);
   w.hi = take(4 * Nc);
   w.list = take(4 * Nc);
+  w.near = take(4 * Nc);
   w.exact_l = take(8 * Nc);
   w.exact_g = take(8 * Nc);
   w.part = take(8 * (size_t)2 * EXACT_SPLIT_CAP * PW_UNITS * ((nmax + PW_BUF - 1) / PW_BUF));
@@ -887,198 +1222,161 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax) { return (int64_t)ws_l
 // Build one KDE (good or bad) for scoring.  Host arrays: vartype[D] (0='c', 1='u'), bw[D], nlev[D].
 // Device arrays: X[N][D] fp64 (rows of the whole budget), rows[n] int64 (this KDE's rows, in the
 // reference's order).  Outputs: params (device, hbx_kde_param_bytes()), table (device fp32,
-// hbx_kde_table_floats(n, dc_pad, du_pad) floats), info[8] (host): {has_neg, nan_all, unsupported, dc, du, nconst, dc_pad, du_pad}.
+// hbx_kde_table_floats(n, dc_pad, du_pad) floats), info[8] (host): {variant, nan_all, unsupported, dc, du,
+// nconst, dc_pad, du_pad}.  The host inputs go to the parameter buffer's staging area; the parameters
+// are derived on the device (kde_params_kernel); one synchronisation for the info record.
 int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, const int32_t* vartype,
                     const double* bw, const int32_t* nlev, void* params, float* table, int64_t table_floats_,
                     int32_t* info, void* stream) {
   if (!X || !rows || !vartype || !bw || !nlev || !params || !table || !info)
     return hbx_fail(HBX_ERR_ARG, "hbx_kde_prepare: null pointer");
-  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
-  if (n < 1) return hbx_fail(HBX_ERR_ARG, "hbx_kde_prepare: n=%d", n);
-  KdeParams* P = (KdeParams*)calloc(1, sizeof(KdeParams));
-  if (!P) return hbx_fail(HBX_ERR_ARG, "out of host memory");
-  P->n = n;
-  P->D = D;
-  int dc_tot = 0, du_tot = 0;
-  for (int d = 0; d < D; ++d) (vartype[d] == 0 ? dc_tot : du_tot)++;
-  int dcp, dup;
-  bucket_dims(dc_tot, du_tot, &dcp, &dup);
-  if (dcp < 0 || dup < 0) {
-    free(P);
-    return hbx_fail(HBX_ERR_UNSUPPORTED, "no scoring kernel for %d continuous / %d categorical dims", dc_tot,
-                    du_tot);
-  }
-  P->dc_pad = dcp;
-  P->du_pad = dup;
-  P->stride = table_stride(dcp, dup);
-  if (table_floats_ < table_floats(n, dcp, dup)) {
-    free(P);
-    return hbx_fail(HBX_ERR_ARG, "table too small: %lld < %lld floats", (long long)table_floats_,
-                    (long long)table_floats(n, dcp, dup));
-  }
-  const double LOG2E = 1.4426950408889634;
-  double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
-  float sad = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const double h = bw[d];
-    P->vartype[d] = vartype[d];
-    P->nlev[d] = nlev[d];
-    P->bw[d] = h;
-    if (vartype[d] == 0) {
-      const int k = P->dc++;
-      P->cont_dim[k] = d;
-      prod_bw_c *= h;  // np.prod(bw[iscontinuous]), sequential in dim order
-      if (!(h > 0.0)) {
-        P->nan_all = 1;  // exp(-0/0) * ... / 0 -> NaN for every candidate
-        P->cont_scale[k] = 0.0;
-      } else {
-        P->cont_scale[k] = sqrt(LOG2E / 2.0) / h;
-        sum_ln_h += log(h);
-      }
-    } else {
-      const int c = nlev[d];
-      if (c == 1 && h == 0.0) {  // single observed level: match -> 1, mismatch -> 0/0 = NaN
-        P->const_dim[P->nconst++] = d;
-        continue;
-      }
-      if (c < 2 || !(h > 0.0) || h != h) {
-        P->unsupported = 1;
-        continue;
-      }
-      const double a = 1.0 - h, b = h / (double)(c - 1);
-      const double lb = log2(b);
-      const double la = (a == 0.0) ? -INFINITY : log2(fabs(a));
-      const int u = P->du++;
-      P->cat_dim[u] = d;
-      m0 += (la > lb) ? la : lb;
-      lb_sum += lb;
-      if (a == 0.0) {
-        P->cat_delta[u] = -1e30f;
-      } else {
-        P->cat_delta[u] = (float)(la - lb);
-        sad += fabsf(P->cat_delta[u]);
-      }
-      P->cat_negf[u] = (a < 0.0) ? 1.f : 0.f;
-      if (a < 0.0) P->has_neg = 1;
-    }
-  }
-  P->m0_log2 = m0;
-  P->lb_sum = lb_sum;
-  P->prod_bw_c = prod_bw_c;
-  P->sum_abs_delta = sad;
-  P->log_norm = -log((double)n) - sum_ln_h - 0.5 * (double)P->dc * log(2.0 * M_PI) + m0 * M_LN2;
-  P->X = X;
-  P->rows = rows;
+  char* stage = (char*)params + HBX_PARAM_STAGE;
+  double* bw_d = (double*)stage;
+  int32_t* nlev_d = (int32_t*)(stage + 8 * HBX_MAX_D);
+  int32_t* info_d = nlev_d + HBX_MAX_D;
+  PrepSet ps;
+  memset(&ps, 0, sizeof(ps));
+  ps.nk = 1;
+  int rc = prep_args(&ps.k[0], X, D, rows, n, vartype, bw_d, nlev_d, params, info_d, table_floats_);
+  if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
-  // categorical mode: one-hot on the f16 matrix cores when every active dim has integer codes in
-  // [0, 1024) and the one-hot width sum(max code + 1) fits OH_MAX_KC K-steps; else VALU matching
-  if (e == hipSuccess && P->du > 0) {
-    hipLaunchKernelGGL(kde_maxcode_kernel, dim3(P->du), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
-    e = hipGetLastError();
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(P->cat_maxcode, ((KdeParams*)params)->cat_maxcode, sizeof(int32_t) * HBX_MAX_D,
-                         hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-  }
-  if (e != hipSuccess) {
-    free(P);
-    return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
-  }
-  P->kc = 0;
-  P->oh_total = 0;
-  for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
-    P->oh_col[t] = 0;
-    P->oh_val[t] = NAN;
-  }
-  if (P->du > 0) {
-    // one-hot positions, every dim's block starting at an even position (a padding position, level
-    // -1, never matches): the sparse matrix-core kernel relies on adjacent pairs never spanning dims
-    int tot = 0;
-    bool ok = true;
-    for (int u = 0; u < P->du; ++u) {
-      if (P->cat_maxcode[u] < 0) ok = false;
-      else tot = ((tot + 1) & ~1) + P->cat_maxcode[u] + 1;
-    }
-    if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
-      P->kc = (2 * tot + 31) / 32;
-      P->oh_total = tot;
-      int t = 0;
-      for (int u = 0; u < P->du; ++u) {
-        if (t & 1) {
-          P->oh_dim[t] = u;
-          P->oh_level[t] = -1;
-          P->oh_col[t] = 0;
-          P->oh_val[t] = NAN;
-          ++t;
-        }
-        for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
-          P->oh_dim[t] = u;
-          P->oh_level[t] = l;
-          P->oh_col[t] = P->cat_dim[u];
-          P->oh_val[t] = (double)l;
-          ++t;
-        }
-      }
-    }
-  }
-  // continuous product on the f16 matrix cores (hi/lo split) when it has >= 8 dims (one full
-  // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
-  // otherwise the exact f32 MFMA product
-  const char* hm_env = getenv("HBX_HMODE");
-  const bool hm_ok = (P->du == 0 || P->kc > 0) && dcp >= 8;
-  P->hmode = (hm_ok && !(hm_env && hm_env[0] == '0')) ? 1 : 0;
-  P->nsc = nsc_of(dcp);
-  if (P->hmode)
-    P->chunk_floats = h_chunk_floats(dcp, P->kc, P->has_neg);
-  else
-    P->chunk_floats = chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
-  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4);  // scoring variant (hbx_kde_logpdf / _acquire)
-  info[1] = P->nan_all;
-  info[2] = P->unsupported;
-  info[3] = P->dc;
-  info[4] = P->du;
-  info[5] = P->nconst;
-  info[6] = P->dc_pad;
-  info[7] = P->du_pad;
-  e = hipMemcpyAsync(params, P, sizeof(KdeParams), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  const int dc_n = P->dc;
-  const bool hmode = P->hmode != 0;
-  static thread_local KdeParams Ph;  // host copy for a possible f32-MFMA rebuild (below)
-  Ph = *P;
-  free(P);
-  if (e != hipSuccess) return hbx_fail(HBX_ERR_HIP, "params upload: %s", hipGetErrorString(e));
-  if (dc_n > 0) {
-    hipLaunchKernelGGL(kde_center_kernel, dim3(dc_n), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
-    HBX_LAUNCH_CHECK();
-  }
-  const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
-  hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 63) / 64), dim3(64), 0, s, X, D, rows,
-                     (KdeParams*)params, table);
-  HBX_LAUNCH_CHECK();
-  if (hmode) {
-    // the f16 C_j pieces need |C_j| <= H_CMAX; otherwise rebuild for the f32-MFMA kernels
-    float cm = 0.f;
-    HBX_HIP(hipMemcpyAsync(&cm, &((KdeParams*)params)->cmax, sizeof(float), hipMemcpyDeviceToHost, s));
-    HBX_HIP(hipStreamSynchronize(s));
-    if (!(cm <= H_CMAX)) {
-      Ph.hmode = 0;
-      Ph.chunk_floats = chunk_floats(dcp, dup, Ph.kc, Ph.kc ? Ph.has_neg : 0);
-      info[0] = Ph.has_neg | (Ph.kc << 1);
-      HBX_HIP(hipMemcpyAsync(params, &Ph, sizeof(KdeParams), hipMemcpyHostToDevice, s));
-      if (dc_n > 0) {
-        hipLaunchKernelGGL(kde_center_kernel, dim3(dc_n), dim3(256), 0, s, X, D, rows, (KdeParams*)params);
-        HBX_LAUNCH_CHECK();
-      }
-      hipLaunchKernelGGL(kde_table_kernel, dim3((nslots + 63) / 64), dim3(64), 0, s, X, D, rows,
-                         (KdeParams*)params, table);
-      HBX_LAUNCH_CHECK();
-      HBX_HIP(hipStreamSynchronize(s));
-    }
-  }
+  HBX_HIP(hipMemcpyAsync(bw_d, bw, 8 * (size_t)D, hipMemcpyHostToDevice, s));
+  HBX_HIP(hipMemcpyAsync(nlev_d, nlev, 4 * (size_t)D, hipMemcpyHostToDevice, s));
+  rc = prep_launch(ps, table, table, s);
+  if (rc) return rc;
+  HBX_HIP(hipMemcpyAsync(info, info_d, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HBX_HIP(hipStreamSynchronize(s));
   return HBX_OK;
 }
+
+}  // extern "C"
+
+// ---- one-call refit (BOHB.new_result, bohb.py:211-251) ------------------------------------------
+// Split metadata hbx_seg_argsort / hbx_kde_fit read from device memory, written by a kernel from its
+// arguments (no host copy).
+struct RefitMeta {
+  int64_t seg[2];
+  int64_t n_good, n_bad;
+  double fac_good, fac_bad;
+  int32_t vt[HBX_MAX_D];
+};
+struct RefitMetaArgs {
+  int64_t n, n_good, n_bad;
+  double fac_good, fac_bad;
+  int32_t D;
+  uint32_t vt[HBX_MAX_D / 32];
+};
+static size_t refit_meta_bytes() { return (sizeof(RefitMeta) + 255) & ~(size_t)255; }
+
+// Append the n_new staged rows ([n_new][D] then n_new losses) at rows n - n_new .. n - 1 of X / loss,
+// and write the split metadata (block 0).
+__global__ __launch_bounds__(256) void kde_refit_meta_kernel(double* __restrict__ X, double* __restrict__ loss,
+                                                             const double* __restrict__ staged, int64_t n_new,
+                                                             RefitMetaArgs a, RefitMeta* __restrict__ m) {
+  const int64_t per = n_new * (int64_t)a.D;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < per + n_new; e += (int64_t)gridDim.x * 256) {
+    if (e < per) X[(a.n - n_new) * (int64_t)a.D + e] = staged[e];
+    else loss[a.n - n_new + (e - per)] = staged[e];
+  }
+  if (blockIdx.x == 0) {
+    for (int d = threadIdx.x; d < a.D; d += 256) m->vt[d] = (a.vt[d >> 5] >> (d & 31)) & 1u;
+    if (threadIdx.x == 0) {
+      m->seg[0] = 0;
+      m->seg[1] = a.n;
+      m->n_good = a.n_good;
+      m->n_bad = a.n_bad;
+      m->fac_good = a.fac_good;
+      m->fac_bad = a.fac_bad;
+    }
+  }
+}
+
+// output block of hbx_kde_refit: order i64[n] | bw_good f64[D] | bw_bad f64[D] | nlev_good i32[D] |
+// nlev_bad i32[D] | info_good i32[8] | info_bad i32[8]
+struct RefitOut {
+  size_t order, bw_good, bw_bad, nlev_good, nlev_bad, info_good, info_bad, total;
+};
+static RefitOut refit_out_layout(int64_t n, int32_t D) {
+  RefitOut o;
+  o.order = 0;
+  o.bw_good = 8 * (size_t)n;
+  o.bw_bad = o.bw_good + 8 * (size_t)D;
+  o.nlev_good = o.bw_bad + 8 * (size_t)D;
+  o.nlev_bad = o.nlev_good + 4 * (size_t)D;
+  o.info_good = o.nlev_bad + 4 * (size_t)D;
+  o.info_bad = o.info_good + 32;
+  o.total = o.info_bad + 32;
+  return o;
+}
+
+extern "C" {
+
+int64_t hbx_kde_refit_out_bytes(int64_t n, int32_t D) { return (int64_t)refit_out_layout(n, D).total; }
+int64_t hbx_kde_refit_scratch_bytes(int64_t n, int32_t D) {
+  return (int64_t)refit_meta_bytes() + hbx_sort_scratch_bytes(n);
+}
+
+// The whole refit of one budget in one call, enqueued without host synchronisation: append the staged
+// rows, stable argsort of the losses, normal-reference bandwidths and level counts of the good (head
+// n_good) and bad (tail n_bad) rows, and both KDEs prepared for scoring.  The caller reads `out` back
+// once (its info records say which scoring kernel each KDE runs).
+int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
+                  int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad, void* params_good,
+                  float* table_good, int64_t table_good_floats, void* params_bad, float* table_bad,
+                  int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!X || !loss || !vartype || !params_good || !table_good || !params_bad || !table_bad || !out || !scratch ||
+      (n_new > 0 && !staged))
+    return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit: null pointer");
+  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
+  if (n < 1 || n > INT32_MAX || n_new < 0 || n_new > n)
+    return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit: n=%lld, n_new=%lld", (long long)n, (long long)n_new);
+  if (n_good < 1 || n_good > n || n_bad < 1 || n_bad > n)
+    return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit: split %lld / %lld of %lld rows", (long long)n_good,
+                    (long long)n_bad, (long long)n);
+  if (scratch_bytes < hbx_kde_refit_scratch_bytes(n, D)) return hbx_fail(HBX_ERR_ARG, "refit scratch too small");
+  hipStream_t s = (hipStream_t)stream;
+  const RefitOut o = refit_out_layout(n, D);
+  char* ob = (char*)out;
+  int64_t* order = (int64_t*)(ob + o.order);
+  double* bw_g = (double*)(ob + o.bw_good);
+  double* bw_b = (double*)(ob + o.bw_bad);
+  int32_t* nl_g = (int32_t*)(ob + o.nlev_good);
+  int32_t* nl_b = (int32_t*)(ob + o.nlev_bad);
+  PrepSet ps;
+  memset(&ps, 0, sizeof(ps));
+  ps.nk = 2;
+  int rc = prep_args(&ps.k[0], X, D, order, (int32_t)n_good, vartype, bw_g, nl_g, params_good,
+                     (int32_t*)(ob + o.info_good), table_good_floats);
+  if (rc) return rc;
+  rc = prep_args(&ps.k[1], X, D, order + (n - n_bad), (int32_t)n_bad, vartype, bw_b, nl_b, params_bad,
+                 (int32_t*)(ob + o.info_bad), table_bad_floats);
+  if (rc) return rc;
+  RefitMetaArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.n = n;
+  ma.n_good = n_good;
+  ma.n_bad = n_bad;
+  ma.fac_good = fac_good;
+  ma.fac_bad = fac_bad;
+  ma.D = D;
+  memcpy(ma.vt, ps.k[0].vt, sizeof(ma.vt));
+  RefitMeta* m = (RefitMeta*)scratch;
+  char* sort_scratch = (char*)scratch + refit_meta_bytes();
+  const int64_t per = n_new * (int64_t)(D + 1);
+  const unsigned gmeta = (unsigned)(per > 0 ? ((per + 255) / 256 < 1024 ? (per + 255) / 256 : 1024) : 1);
+  hipLaunchKernelGGL(kde_refit_meta_kernel, dim3(gmeta), dim3(256), 0, s, X, loss, staged, n_new, ma, m);
+  HBX_LAUNCH_CHECK();
+  rc = hbx_seg_argsort(loss, m->seg, 1, n, n, order, sort_scratch, hbx_sort_scratch_bytes(n), stream);
+  if (rc) return rc;
+  rc = hbx_kde_fit(X, D, m->seg, 1, order, &m->n_good, &m->n_bad, &m->fac_good, &m->fac_bad, m->vt, bw_g, bw_b, nl_g,
+                   nl_b, stream);
+  if (rc) return rc;
+  return prep_launch(ps, table_good, table_bad, s);
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // fp32 log-domain scoring of Nc candidates (fp64 [Nc][D] row-major) against one prepared KDE
 int hbx_kde_logpdf(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
@@ -1120,6 +1418,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   int32_t* count = (int32_t*)(ws + w.count);
   int32_t* flags = (int32_t*)(ws + w.flags);
   int32_t* segcnt = (int32_t*)(ws + w.segcnt);
+  int32_t* segnear = (int32_t*)(ws + w.segnear);
+  int32_t* near = (int32_t*)(ws + w.near);
   uint64_t* best = (uint64_t*)(ws + w.best);
   uint64_t* key = (uint64_t*)(ws + w.key);
   int32_t* first1 = (int32_t*)(ws + w.first1);
@@ -1137,7 +1437,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   if (B == 0) return HBX_OK;  // batched call without candidates: no records
   if (batch_res)
     hipLaunchKernelGGL(acq_init_batch_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, U, flags,
-                       segcnt, best, key, first1, count);
+                       segcnt, best, key, first1, count, segnear);
   else
     hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res);
   HBX_LAUNCH_CHECK();
@@ -1164,7 +1464,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   }
   if (!batch_res) {
     hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
-                       index_base, res);
+                       index_base, (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, res);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }
@@ -1173,8 +1473,12 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     HBX_LAUNCH_CHECK();
     hipLaunchKernelGGL(kde_batch_key_kernel, grid, dim3(256), 0, s, list, count, sg, exact_l, exact_g, best, key);
     HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kde_batch_near_kernel, grid, dim3(256), 0, s, list, count, sg, exact_l, exact_g, key,
+                       (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, segnear);
+    HBX_LAUNCH_CHECK();
     hipLaunchKernelGGL(kde_batch_final_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, key, segcnt,
-                       flags, exact_l, exact_g, index_base, batch_res);
+                       flags, segnear, list, exact_l, exact_g, (const KdeParams*)params_good,
+                       (const KdeParams*)params_bad, el, eg, index_base, batch_res);
     HBX_LAUNCH_CHECK();
   }
   return HBX_OK;
@@ -1252,5 +1556,34 @@ int hbx_event_elapsed_ms(void* start, void* stop, float* ms) {
 }
 
 void* hbx_kde_result_ptr(void* workspace) { return (char*)workspace + ws_layout(0, 0).res; }
+
+// numpy's float64 exp (hbx_npexp.h) element-wise: the known-answer check of the exact re-score's exp
+__global__ void np_exp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = hbx_npexp::exp(x[i]);
+}
+
+int hbx_np_exp(const double* x, int64_t n, double* y, void* stream) {
+  if ((!x || !y) && n > 0) return hbx_fail(HBX_ERR_ARG, "hbx_np_exp: null pointer");
+  if (n <= 0) return HBX_OK;
+  hipLaunchKernelGGL(np_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n, y);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// Byte offsets inside an acquisition workspace of (Nc, seg, nmax) -- hbx_kde_acquire: seg = Nc -- of
+// what a host re-resolution of a near tie reads: out[0] shortlist count (i32), [1] shortlist (i32
+// candidate indices), [2] near list (hbx_kde_acquire: the near set's candidate indices, res.near of
+// them; batched: a 0/1 flag per shortlist entry), [3] exact l, [4] exact g (f64 per shortlist entry).
+int hbx_kde_ws_offsets(int64_t Nc, int64_t seg, int64_t nmax, int64_t* out) {
+  if (!out || seg < 1) return hbx_fail(HBX_ERR_ARG, "hbx_kde_ws_offsets: bad arguments");
+  const WsLayout w = ws_layout(Nc, nmax, seg >= Nc ? 1 : (Nc + seg - 1) / seg);
+  out[0] = (int64_t)w.count;
+  out[1] = (int64_t)w.list;
+  out[2] = (int64_t)w.near;
+  out[3] = (int64_t)w.exact_l;
+  out[4] = (int64_t)w.exact_g;
+  return HBX_OK;
+}
 
 }  // extern "C"

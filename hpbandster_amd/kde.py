@@ -20,8 +20,9 @@ import numpy as np
 
 from . import _native as N
 
-RESULT_FMT = "<qdddqii"  # AcqResult: index, score, pdf_l, pdf_g, shortlist, flags, pad
+RESULT_FMT = "<qdfiiidd"  # AcqResult: index, score, rel, flags, shortlist, near, pdf_l, pdf_g
 RESULT_BYTES = struct.calcsize(RESULT_FMT)
+ACQ_OVERFLOW, ACQ_NEAR_TIE, ACQ_RESOLVED = 1, 2, 4  # include/hbx.h HBX_ACQ_*
 
 
 def _torch():
@@ -53,20 +54,33 @@ def bandwidth_factor(nobs, D):
 
 
 class AcqResult(object):
-    __slots__ = ("index", "score", "pdf_l", "pdf_g", "shortlist", "flags")
+    """One acquisition's winner (include/hbx.h result record).  ``flags`` & ACQ_NEAR_TIE: other
+    candidates' exact scores lie within the spread another numpy build's exp could cause (``rel``);
+    ACQ_RESOLVED: with ties='process' the host re-scored that near set with this process's numpy
+    (exact_host) and picked from it."""
+    __slots__ = ("index", "score", "rel", "flags", "shortlist", "near", "pdf_l", "pdf_g")
 
-    def __init__(self, index, score, pdf_l, pdf_g, shortlist, flags):
+    def __init__(self, index, score, pdf_l, pdf_g, shortlist, flags, rel=0.0, near=1):
         self.index, self.score, self.pdf_l, self.pdf_g = int(index), score, pdf_l, pdf_g
-        self.shortlist, self.flags = int(shortlist), int(flags)
+        self.shortlist, self.flags, self.rel, self.near = int(shortlist), int(flags), float(rel), int(near)
 
     @classmethod
     def from_bytes(cls, b):
-        idx, score, l, g, sl, fl, _ = struct.unpack(RESULT_FMT, bytes(b))
-        return cls(idx, score, l, g, sl, fl)
+        idx, score, rel, fl, sl, near, l, g = struct.unpack(RESULT_FMT, bytes(b))
+        return cls(idx, score, l, g, sl, fl, rel, near)
 
     def __repr__(self):
-        return "AcqResult(index=%d, score=%r, pdf_l=%r, pdf_g=%r, shortlist=%d, flags=%d)" % (
-            self.index, self.score, self.pdf_l, self.pdf_g, self.shortlist, self.flags)
+        return "AcqResult(index=%d, score=%r, pdf_l=%r, pdf_g=%r, shortlist=%d, near=%d, flags=%d)" % (
+            self.index, self.score, self.pdf_l, self.pdf_g, self.shortlist, self.near, self.flags)
+
+
+def _rows_of(cands, idx):
+    """Candidate rows idx (host numpy) of a host array or a device tensor."""
+    idx = np.asarray(idx, dtype=np.int64)
+    if isinstance(cands, np.ndarray):
+        return np.asarray(cands, dtype=np.float64)[idx]
+    torch = _torch()
+    return cands[torch.from_numpy(idx).to(cands.device)].cpu().numpy()
 
 
 class DeviceKDE(object):
@@ -76,7 +90,9 @@ class DeviceKDE(object):
     reads ``.data``, ``.bw`` and ``.pdf``); ``pdf`` evaluates the exact fp64 density on the GPU.
     """
 
-    def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None):
+    def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None, prepared=None):
+        """Prepare a KDE for scoring with ``hbx_kde_prepare`` -- or, with ``prepared`` = (params, table,
+        info) from ``hbx_kde_refit``, wrap an already prepared one."""
         torch = _torch()
         L = N.lib()
         self.var_type = var_type
@@ -90,19 +106,22 @@ class DeviceKDE(object):
         self.device = X_dev.device
         D = self.k_vars
         vt = var_type_codes(var_type)
-        dc, du = int((vt == 0).sum()), int((vt == 1).sum())
-        dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
-        N.check(L.hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
-        self.stride = int(stride[0])
-        self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
-        tf = int(L.hbx_kde_table_floats(self.nobs, int(dcp[0]), int(dup[0])))
-        self.table = torch.empty(tf, dtype=torch.float32, device=self.device)
-        info = np.zeros(8, dtype=np.int32)
-        bw_c = np.ascontiguousarray(self.bw)
-        nlev_c = np.ascontiguousarray(self.nlev)
-        N.check(L.hbx_kde_prepare(N.ptr(X_dev), D, N.ptr(rows_dev), self.nobs, N.ptr(vt), N.ptr(bw_c),
-                                  N.ptr(nlev_c), N.ptr(self.params), N.ptr(self.table), self.table.numel(),
-                                  N.ptr(info), N.stream_handle(stream)))
+        if prepared is None:
+            dc, du = int((vt == 0).sum()), int((vt == 1).sum())
+            dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+            N.check(L.hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
+            with N.on_device(self.device, stream):
+                self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
+                tf = int(L.hbx_kde_table_floats(self.nobs, int(dcp[0]), int(dup[0])))
+                self.table = torch.empty(tf, dtype=torch.float32, device=self.device)
+                info = np.zeros(8, dtype=np.int32)
+                bw_c = np.ascontiguousarray(self.bw)
+                nlev_c = np.ascontiguousarray(self.nlev)
+                N.check(L.hbx_kde_prepare(N.ptr(X_dev), D, N.ptr(rows_dev), self.nobs, N.ptr(vt), N.ptr(bw_c),
+                                          N.ptr(nlev_c), N.ptr(self.params), N.ptr(self.table), self.table.numel(),
+                                          N.ptr(info), N.stream_handle(stream, self.device)))
+        else:
+            self.params, self.table, info = prepared
         self.variant, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
             [int(v) for v in info]
         self.has_neg, self.kc = self.variant & 1, self.variant >> 1
@@ -120,14 +139,15 @@ class DeviceKDE(object):
             if pts.ndim <= 1:
                 pts = pts.reshape(-1, self.k_vars) if pts.size != self.k_vars else pts.reshape(1, -1)
         pts = np.ascontiguousarray(pts.reshape(-1, self.k_vars))
-        p_dev = torch.from_numpy(pts).to(self.device)
-        out = torch.empty(pts.shape[0], dtype=torch.float64, device=self.device)
-        sb = int(L.hbx_kde_pdf_scratch_bytes(self.nobs))
-        scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
-        N.check(L.hbx_kde_pdf_exact(N.ptr(p_dev), pts.shape[0], self.k_vars, N.ptr(self.params), N.ptr(self.X_dev),
-                                    N.ptr(self.rows_dev), self.nobs, N.ptr(out), N.ptr(scratch), sb,
-                                    N.stream_handle(stream)))
-        return np.squeeze(out.cpu().numpy())
+        with N.on_device(self.device, stream):
+            p_dev = torch.from_numpy(pts).to(self.device)
+            out = torch.empty(pts.shape[0], dtype=torch.float64, device=self.device)
+            sb = int(L.hbx_kde_pdf_scratch_bytes(self.nobs))
+            scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
+            N.check(L.hbx_kde_pdf_exact(N.ptr(p_dev), pts.shape[0], self.k_vars, N.ptr(self.params),
+                                        N.ptr(self.X_dev), N.ptr(self.rows_dev), self.nobs, N.ptr(out), N.ptr(scratch),
+                                        sb, N.stream_handle(stream, self.device)))
+            return np.squeeze(out.cpu().numpy())
 
     def sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id=0, stream=None, table=None):
         """BOHB's candidate rule around this (good) KDE's observations, on the GPU (bohb.py:133-147).
@@ -135,9 +155,14 @@ class DeviceKDE(object):
         ``levels``: per dim 0 (continuous) or the number of choices.  Candidate i draws from the
         Philox stream (seed, counter_base + i, stream_id).  Returns (cands [Nc, D] f64, datum [Nc] i64,
         domain_err [Nc] u8) device tensors."""
+        with N.on_device(self.device, stream):
+            return self._sample(levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table)
+
+    def _sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table):
         torch = _torch()
         L = N.lib()
         D = self.k_vars
+        sh = N.stream_handle(stream, self.device)
         if getattr(self, "_bw_dev", None) is None:
             self._bw_dev = torch.from_numpy(np.ascontiguousarray(self.bw, dtype=np.float64)).to(self.device)
         lv = np.ascontiguousarray(np.asarray(levels, dtype=np.int32))
@@ -156,8 +181,7 @@ class DeviceKDE(object):
                 self._tab = torch.empty(int(L.hbx_kde_sample_table_bytes(self.nobs, D)) // 8, dtype=torch.float64,
                                         device=self.device)
                 N.check(L.hbx_kde_sample_table(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs,
-                                               N.ptr(self._bw_dev), N.ptr(self._lv_dev), N.ptr(self._tab),
-                                               N.stream_handle(stream)))
+                                               N.ptr(self._bw_dev), N.ptr(self._lv_dev), N.ptr(self._tab), sh))
             tab = self._tab
         cands = torch.empty((Nc, D), dtype=torch.float64, device=self.device)
         datum = torch.empty(Nc, dtype=torch.int64, device=self.device)
@@ -165,7 +189,7 @@ class DeviceKDE(object):
         N.check(L.hbx_kde_sample(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs, N.ptr(self._bw_dev),
                                  N.ptr(self._lv_dev), N.ptr(tab), float(bw_factor), int(seed) & (2 ** 64 - 1),
                                  int(counter_base) & (2 ** 64 - 1), int(stream_id) & 0xFFFFFFFF, Nc, N.ptr(cands),
-                                 N.ptr(datum), N.ptr(err), N.stream_handle(stream)))
+                                 N.ptr(datum), N.ptr(err), sh))
         return cands, datum, err
 
     def logpdf_est(self, cand_dev, stream=None):
@@ -173,10 +197,12 @@ class DeviceKDE(object):
         torch = _torch()
         L = N.lib()
         Nc = int(cand_dev.shape[0])
-        est = torch.empty((Nc, 4), dtype=torch.float32, device=self.device)
-        N.check(L.hbx_kde_logpdf(N.ptr(cand_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
-                                 self.dc_pad, self.du_pad, self.variant, N.ptr(est), N.stream_handle(stream)))
-        e = est.cpu().numpy()
+        with N.on_device(self.device, stream):
+            est = torch.empty((Nc, 4), dtype=torch.float32, device=self.device)
+            N.check(L.hbx_kde_logpdf(N.ptr(cand_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
+                                     self.dc_pad, self.du_pad, self.variant, N.ptr(est),
+                                     N.stream_handle(stream, self.device)))
+            e = est.cpu().numpy()
         return e[:, 0], e[:, 1], e[:, 2]
 
 
@@ -222,14 +248,26 @@ class KDEPair(object):
             wsb = self._wsb[Nc] = int(N.lib().hbx_kde_workspace_bytes(int(Nc), self.nmax))
         return wsb
 
-    def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True, events=None):
+    def acquire(self, cands, index_base=0, logs=False, stream=None, workspace=None, sync=True, events=None,
+                ties="pinned"):
         """Select the first index minimising max(1e-8, g)/max(l, 1e-8) over the candidates.
 
         ``cands``: [Nc, D] float64 (numpy or a device tensor).  Returns AcqResult (index -1 when no
         candidate has a finite score: the reference then falls back to a random configuration).
         With ``logs`` the fp32 ln l(x), ln g(x) estimates are returned as well.
         With ``sync=False`` the result stays on the device: returns the result tensor view.
+
+        ``ties``: 'pinned' (default) -- the GPU's exact re-score is the reference's float64 arithmetic on
+        the pinned numpy 1.26.4 bit for bit, so its pick is final; 'process' -- candidates flagged
+        ACQ_NEAR_TIE (within the spread another numpy build's exp could cause) are re-scored with this
+        process's numpy (exact_host), reproducing what the reference would pick in this environment.
         """
+        if ties not in ("pinned", "process"):
+            raise ValueError("ties must be 'pinned' or 'process'")
+        with N.on_device(self.good.device, stream):
+            return self._acquire(cands, index_base, logs, stream, workspace, sync, events, ties)
+
+    def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):
         torch = _torch()
         L = N.lib()
         dev = self.good.device
@@ -252,7 +290,7 @@ class KDEPair(object):
         wsp = ws.data_ptr()
         N.check(L.hbx_kde_acquire(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args,
                                   N.ptr(logl), N.ptr(logg), wsp, ws.numel(),
-                                  events.address if events is not None else None, N.stream_handle(stream)))
+                                  events.address if events is not None else None, N.stream_handle(stream, dev)))
         if self._roff is None:
             self._roff = int(L.hbx_kde_result_ptr(wsp)) - wsp
         off = self._roff
@@ -260,17 +298,58 @@ class KDEPair(object):
         if not sync:
             return rview
         res = AcqResult.from_bytes(rview.cpu().numpy().tobytes())
+        if ties == "process" and res.flags & ACQ_NEAR_TIE:
+            self._resolve(res, ws, Nc, Nc, cands if isinstance(cands, np.ndarray) else c_dev, int(index_base))
         if logs:
             return res, logl.cpu().numpy(), logg.cpu().numpy()
         return res
 
+    def _ws_offsets(self, Nc, seg):
+        o = np.zeros(5, dtype=np.int64)
+        N.check(N.lib().hbx_kde_ws_offsets(int(Nc), int(max(seg, 1)), self.nmax, N.ptr(o)))
+        return [int(v) for v in o]
+
+    def _resolve(self, res, ws, Nc, seg, cands, index_base):
+        """HBX_ACQ_NEAR_TIE on a single acquisition: re-score the near set in the reference's numpy
+        arithmetic and take its strict-'<' first-index minimum (exact_host.resolve)."""
+        from . import exact_host
+        o = self._ws_offsets(Nc, seg)
+        idx = ws[o[2]:o[2] + 4 * res.near].view(_torch().int32).cpu().numpy().astype(np.int64)
+        pick = exact_host.resolve(self.good, self.bad, _rows_of(cands, idx), idx)
+        if pick is not None:
+            res.index, res.score, res.pdf_l, res.pdf_g = pick[0] + index_base, pick[1], pick[2], pick[3]
+        res.flags |= ACQ_RESOLVED
+
+    def _resolve_batch(self, recs, ws, Nc, seg, cands):
+        """HBX_ACQ_NEAR_TIE in a batched acquisition: the same, per flagged segment."""
+        from . import exact_host
+        torch = _torch()
+        o = self._ws_offsets(Nc, seg)
+        cnt = int(ws[o[0]:o[0] + 4].view(torch.int32).item())
+        lst = ws[o[1]:o[1] + 4 * cnt].view(torch.int32).cpu().numpy().astype(np.int64)
+        flg = ws[o[2]:o[2] + 4 * cnt].view(torch.int32).cpu().numpy()
+        for b, r in enumerate(recs):
+            if not r.flags & ACQ_NEAR_TIE:
+                continue
+            idx = np.sort(lst[(flg != 0) & (lst // seg == b)])
+            pick = exact_host.resolve(self.good, self.bad, _rows_of(cands, idx), idx)
+            if pick is not None:
+                r.index, r.score, r.pdf_l, r.pdf_g = pick[0] - b * seg, pick[1], pick[2], pick[3]
+            r.flags |= ACQ_RESOLVED
+
     def batch_workspace_bytes(self, Nc, seg):
         return int(N.lib().hbx_kde_batch_workspace_bytes(int(Nc), int(seg), self.nmax))
 
-    def acquire_batch(self, cands, seg, stream=None, workspace=None, results=None, sync=True):
+    def acquire_batch(self, cands, seg, stream=None, workspace=None, results=None, sync=True, ties="pinned"):
         """B = ceil(Nc/seg) acquisitions in one pass: candidates [b*seg, (b+1)*seg) are the candidates
         of get_config call b.  Returns a list of B AcqResult (index relative to the segment start).
         With ``sync=False`` returns the device tensor of the B raw records instead."""
+        if ties not in ("pinned", "process"):
+            raise ValueError("ties must be 'pinned' or 'process'")
+        with N.on_device(self.good.device, stream):
+            return self._acquire_batch(cands, seg, stream, workspace, results, sync, ties)
+
+    def _acquire_batch(self, cands, seg, stream, workspace, results, sync, ties):
         torch = _torch()
         L = N.lib()
         dev = self.good.device
@@ -299,11 +378,14 @@ class KDEPair(object):
                                         N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.variant,
                                         N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.variant,
                                         g.dc_pad, g.du_pad, self.nmax, None, None, N.ptr(out), N.ptr(ws), ws.numel(),
-                                        N.stream_handle(stream)))
+                                        N.stream_handle(stream, dev)))
         if not sync:
             return out[:B * RESULT_BYTES]
         raw = out[:B * RESULT_BYTES].cpu().numpy().tobytes()
-        return [AcqResult.from_bytes(raw[i * RESULT_BYTES:(i + 1) * RESULT_BYTES]) for i in range(B)]
+        recs = [AcqResult.from_bytes(raw[i * RESULT_BYTES:(i + 1) * RESULT_BYTES]) for i in range(B)]
+        if ties == "process" and any(r.flags & ACQ_NEAR_TIE for r in recs):
+            self._resolve_batch(recs, ws, Nc, seg, cands if isinstance(cands, np.ndarray) else c_dev)
+        return recs
 
 
 class ScoreEvents(object):
@@ -340,20 +422,13 @@ class ScoreEvents(object):
             pass
 
 
-def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=None, stream=None,
-             split_rule="bohb"):
-    """Refit the good/bad KDEs of one budget on the GPU (BOHB.new_result, bohb.py:220-251).
+def split_sizes(n, D, min_points, top_n_percent=15, split_rule="bohb"):
+    """(n_good, n_bad) clipped to n, or None where the reference returns without building a model.
 
-    Returns a KDEPair, or None where the reference returns without building a model.
-    ``split_rule`` 'bohb' uses integer floor sizes (bohb.py:224-225) and requires rows > D;
-    'kde_ei' uses int(max(top%*N/100., mp)) (kde_ei.py:190-191) and requires rows >= D.
+    'bohb': integer floor sizes (bohb.py:224-225), a model needs rows > D (bohb.py:234-237);
+    'kde_ei': int(max(top% * N / 100., mp)) (kde_ei.py:190-191), rows >= D (rows == D raises in
+    KDEMultivariate, kernel_density.py:107-109, as in the reference).
     """
-    torch = _torch()
-    L = N.lib()
-    device = device or default_device()
-    X = np.ascontiguousarray(np.asarray(configs, dtype=np.float64))
-    loss = np.ascontiguousarray(np.asarray(losses, dtype=np.float64))
-    n, D = X.shape
     if split_rule == "bohb":
         n_good, n_bad = bohb_split_sizes(n, min_points, top_n_percent)
         if min(n_good, n) <= D or min(n_bad, n) <= D:
@@ -364,46 +439,174 @@ def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=Non
         if min(n_good, n) < D or min(n_bad, n) < D:
             return None
         if min(n_good, n) <= D or min(n_bad, n) <= D:
-            # KDEMultivariate raises here (kernel_density.py:107-109), as the reference does
             raise ValueError("The number of observations must be larger than the number of variables.")
     # numpy slicing semantics: idx[:n_good] / idx[-n_bad:] clip at n
-    n_good, n_bad = min(n_good, n), min(n_bad, n)
-    vt = var_type_codes(var_type)
-    # few, large copies (each host<->device copy of a small tensor costs a round trip): observations
-    # and losses in one f64 buffer, segment bounds and split sizes in one int64 tensor, the two
-    # bandwidth factors and the var types beside them
-    buf = torch.from_numpy(np.concatenate([X.reshape(-1), loss])).to(device)
-    X_dev = buf[:n * D].view(n, D)
-    loss_dev = buf[n * D:]
-    meta = torch.from_numpy(np.array([0, n, n_good, n_bad], dtype=np.int64)).to(device)
-    seg, ng, nb = meta[0:2], meta[2:3], meta[3:4]
-    facs = torch.from_numpy(np.array([bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D)])).to(device)
-    fg, fb = facs[0:1], facs[1:2]
-    # outputs in one buffer, read back with one copy: order i64[n], bw_g, bw_b f64[D], nl_g, nl_b i32[D]
-    outall = torch.empty(8 * n + 24 * D, dtype=torch.uint8, device=device)
-    order = outall[:8 * n].view(torch.int64)
-    outb = outall[8 * n:]
-    sb = int(L.hbx_sort_scratch_bytes(n))
-    scratch = torch.empty(sb, dtype=torch.uint8, device=device)
-    sh = N.stream_handle(stream)
-    N.check(L.hbx_seg_argsort(N.ptr(loss_dev), N.ptr(seg), 1, n, n, N.ptr(order), N.ptr(scratch), sb, sh))
-    vt_dev = torch.from_numpy(vt).to(device)
-    bw_g, bw_b = outb[:8 * D].view(torch.float64), outb[8 * D:16 * D].view(torch.float64)
-    nl_g, nl_b = outb[16 * D:20 * D].view(torch.int32), outb[20 * D:].view(torch.int32)
-    N.check(L.hbx_kde_fit(N.ptr(X_dev), D, N.ptr(seg), 1, N.ptr(order), N.ptr(ng), N.ptr(nb), N.ptr(fg), N.ptr(fb),
-                          N.ptr(vt_dev), N.ptr(bw_g), N.ptr(bw_b), N.ptr(nl_g), N.ptr(nl_b), sh))
-    ah = outall.cpu().numpy()
-    order_h = ah[:8 * n].view(np.int64)
-    oh = ah[8 * n:]
-    bw_gh, bw_bh = oh[:8 * D].view(np.float64).copy(), oh[8 * D:16 * D].view(np.float64).copy()
-    nl_gh, nl_bh = oh[16 * D:20 * D].view(np.int32).copy(), oh[20 * D:].view(np.int32).copy()
-    if (nl_gh < 0).any() or (nl_bh < 0).any():
-        raise N.HbxError("categorical codes must be integers in [0, 1024)")
-    rows_g = order[:n_good]
-    rows_b = order[n - n_bad:]
-    good = DeviceKDE(X_dev, rows_g, var_type, bw_gh, nl_gh, X[order_h[:n_good]], stream)
-    bad = DeviceKDE(X_dev, rows_b, var_type, bw_bh, nl_bh, X[order_h[n - n_bad:]], stream)
-    return KDEPair(good, bad)
+    return min(n_good, n), min(n_bad, n)
+
+
+class ObservationStore(object):
+    """One budget's observations (``get_array()`` rows and losses) resident in HBM, appended to as
+    results arrive (bohb.py:211-213), so a refit moves only the new rows to the device: one pinned
+    host->device copy, one ``hbx_kde_refit`` call (split, bandwidths, level counts, both KDEs'
+    preparation; no host synchronisation inside) and one device->host copy of the split and bandwidths.
+
+    Each refit returns a new immutable KDEPair; rows already on the device are never rewritten, so
+    models handed out earlier stay valid while later rows are appended (growth reallocates).
+    """
+
+    def __init__(self, D, var_type, device=None, capacity=256):
+        self.D = int(D)
+        self.var_type = var_type
+        self.vt = np.ascontiguousarray(var_type_codes(var_type))
+        self.device = device or default_device()
+        self.n = 0          # rows on the device
+        self.nh = 0         # rows on the host (added)
+        self._hcap = 0
+        self._Xh = self._lh = None
+        self._cap = 0
+        self.X_dev = self.loss_dev = None
+        self._stage_h = None
+        self._out_h = None
+        self._init_cap = int(capacity)
+        dc, du = int((self.vt == 0).sum()), int((self.vt == 1).sum())
+        dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+        N.check(N.lib().hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
+        self.dc_pad, self.du_pad = int(dcp[0]), int(dup[0])
+
+    def _reserve(self, n):
+        torch = _torch()
+        if n <= self._cap:
+            return
+        cap = max(self._init_cap, self._cap)
+        while cap < n:
+            cap *= 2
+        X = torch.empty((cap, self.D), dtype=torch.float64, device=self.device)
+        L = torch.empty(cap, dtype=torch.float64, device=self.device)
+        if self.n:
+            X[:self.n].copy_(self.X_dev[:self.n])
+            L[:self.n].copy_(self.loss_dev[:self.n])
+        self.X_dev, self.loss_dev, self._cap = X, L, cap
+
+    def _pinned(self, attr, nbytes):
+        torch = _torch()
+        buf = getattr(self, attr)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
+            setattr(self, attr, buf)
+        return buf
+
+    def add(self, rows, losses):
+        """Append observations on the host side (O(rows x D)); the next refit moves them."""
+        rows = np.asarray(rows, dtype=np.float64).reshape(-1, self.D)
+        losses = np.asarray(losses, dtype=np.float64).reshape(-1)
+        if losses.shape[0] != rows.shape[0]:
+            raise N.HbxError("observation store: %d rows, %d losses" % (rows.shape[0], losses.shape[0]))
+        m = self.nh + rows.shape[0]
+        if m > self._hcap:
+            cap = max(self._init_cap, self._hcap)
+            while cap < m:
+                cap *= 2
+            Xh = np.empty((cap, self.D))
+            lh = np.empty(cap)
+            if self.nh:
+                Xh[:self.nh] = self._Xh[:self.nh]
+                lh[:self.nh] = self._lh[:self.nh]
+            self._Xh, self._lh, self._hcap = Xh, lh, cap
+        self._Xh[self.nh:m] = rows
+        self._lh[self.nh:m] = losses
+        self.nh = m
+
+    @property
+    def X_host(self):
+        return self._Xh[:self.nh]
+
+    @property
+    def losses_host(self):
+        return self._lh[:self.nh]
+
+    def refit(self, min_points, top_n_percent=15, split_rule="bohb", stream=None):
+        """Refit on every row added so far.  Returns a KDEPair, or None where the reference builds no
+        model (too few rows for a KDE)."""
+        n = self.nh
+        sizes = split_sizes(n, self.D, min_points, top_n_percent, split_rule)
+        if sizes is None:
+            return None
+        with N.on_device(self.device, stream):
+            return self._refit(self._Xh[:n], self._lh[:n], n, sizes, stream)
+
+    def _refit(self, X_host, losses, n, sizes, stream):
+        torch = _torch()
+        L = N.lib()
+        D = self.D
+        n_good, n_bad = sizes
+        n_new = n - self.n
+        self._reserve(n)
+        cur = stream if stream is not None else torch.cuda.current_stream(self.device)
+        sh = cur.cuda_stream
+        staged = None
+        if n_new:  # the new rows then their losses, one pinned copy
+            m = n_new * (D + 1)
+            st = self._pinned("_stage_h", 8 * m)
+            sv = st[:8 * m].numpy().view(np.float64)
+            sv[:n_new * D] = X_host[self.n:].reshape(-1)
+            sv[n_new * D:] = losses[self.n:]
+            staged = torch.empty(m, dtype=torch.float64, device=self.device)
+            staged.view(torch.uint8).copy_(st[:8 * m], non_blocking=True)
+        ob = int(L.hbx_kde_refit_out_bytes(n, D))
+        out = torch.empty(ob, dtype=torch.uint8, device=self.device)
+        sb = int(L.hbx_kde_refit_scratch_bytes(n, D))
+        scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
+        pb = int(L.hbx_kde_param_bytes())
+        pg = torch.empty(pb, dtype=torch.uint8, device=self.device)
+        pbad = torch.empty(pb, dtype=torch.uint8, device=self.device)
+        tg = torch.empty(int(L.hbx_kde_table_floats(n_good, self.dc_pad, self.du_pad)), dtype=torch.float32,
+                         device=self.device)
+        tb = torch.empty(int(L.hbx_kde_table_floats(n_bad, self.dc_pad, self.du_pad)), dtype=torch.float32,
+                         device=self.device)
+        N.check(L.hbx_kde_refit(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt), N.ptr(staged), n_new,
+                                n_good, n_bad, bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D),
+                                N.ptr(pg), N.ptr(tg), tg.numel(), N.ptr(pbad), N.ptr(tb), tb.numel(),
+                                N.ptr(out), N.ptr(scratch), sb, sh))
+        self.n = n
+        oh = self._pinned("_out_h", ob)
+        oh[:ob].copy_(out, non_blocking=True)
+        cur.synchronize()
+        ah = oh[:ob].numpy()
+        order_h = ah[:8 * n].view(np.int64).copy()
+        o = 8 * n
+        bw_gh = ah[o:o + 8 * D].view(np.float64).copy()
+        bw_bh = ah[o + 8 * D:o + 16 * D].view(np.float64).copy()
+        nl_gh = ah[o + 16 * D:o + 20 * D].view(np.int32).copy()
+        nl_bh = ah[o + 20 * D:o + 24 * D].view(np.int32).copy()
+        info_g = ah[o + 24 * D:o + 24 * D + 32].view(np.int32).copy()
+        info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32).copy()
+        if (nl_gh < 0).any() or (nl_bh < 0).any():
+            raise N.HbxError("categorical codes must be integers in [0, 1024)")
+        order = out[:8 * n].view(torch.int64)
+        X_dev = self.X_dev
+        good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, X_host[order_h[:n_good]],
+                         prepared=(pg, tg, info_g))
+        bad = DeviceKDE(X_dev, order[n - n_bad:], self.var_type, bw_bh, nl_bh, X_host[order_h[n - n_bad:]],
+                        prepared=(pbad, tb, info_b))
+        pair = KDEPair(good, bad)
+        pair._keep = (out,)  # the rows tensors are views of the refit's output block
+        return pair
+
+
+def fit_pair(configs, losses, var_type, min_points, top_n_percent=15, device=None, stream=None,
+             split_rule="bohb"):
+    """Refit the good/bad KDEs of one budget on the GPU (BOHB.new_result, bohb.py:220-251) from host
+    arrays: all rows staged at once through an ObservationStore.
+
+    Returns a KDEPair, or None where the reference returns without building a model.
+    ``split_rule`` 'bohb' uses integer floor sizes (bohb.py:224-225) and requires rows > D;
+    'kde_ei' uses int(max(top%*N/100., mp)) (kde_ei.py:190-191) and requires rows >= D.
+    """
+    X = np.ascontiguousarray(np.asarray(configs, dtype=np.float64))
+    n, D = X.shape
+    store = ObservationStore(D, var_type, device=device, capacity=max(n, 1))
+    store.add(X, losses)
+    return store.refit(min_points, top_n_percent, split_rule, stream=stream)
 
 
 def fit_pair_from_rows(X, good_rows, bad_rows, var_type, bw_good, bw_bad, nlev_good, nlev_bad, device=None):
@@ -411,9 +614,10 @@ def fit_pair_from_rows(X, good_rows, bad_rows, var_type, bw_good, bw_bad, nlev_g
     torch = _torch()
     device = device or default_device()
     X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
-    X_dev = torch.from_numpy(X).to(device)
-    rg = torch.from_numpy(np.asarray(good_rows, dtype=np.int64)).to(device)
-    rb = torch.from_numpy(np.asarray(bad_rows, dtype=np.int64)).to(device)
-    good = DeviceKDE(X_dev, rg, var_type, bw_good, nlev_good, X[np.asarray(good_rows)])
-    bad = DeviceKDE(X_dev, rb, var_type, bw_bad, nlev_bad, X[np.asarray(bad_rows)])
+    with N.on_device(device):
+        X_dev = torch.from_numpy(X).to(device)
+        rg = torch.from_numpy(np.asarray(good_rows, dtype=np.int64)).to(device)
+        rb = torch.from_numpy(np.asarray(bad_rows, dtype=np.int64)).to(device)
+        good = DeviceKDE(X_dev, rg, var_type, bw_good, nlev_good, X[np.asarray(good_rows)])
+        bad = DeviceKDE(X_dev, rb, var_type, bw_bad, nlev_bad, X[np.asarray(bad_rows)])
     return KDEPair(good, bad)

@@ -2,7 +2,8 @@
 
 ``advance = argsort(argsort(losses)) < k`` per bracket, over the REVIEW (finite-loss) entries;
 CRASHED entries (non-finite loss) never advance.  Many brackets are ranked in one launch
-(one workgroup per bracket), which is what config #5 of the benchmark exercises.
+(a radix select of the k-th loss per bracket, one wave each), which is what config #5 of the
+benchmark exercises.
 """
 
 import numpy as np
@@ -14,11 +15,18 @@ from .kde import default_device
 def promote_segments(loss, seg_off, k, device=None, stream=None, return_order=False):
     """loss: fp64 [N] (numpy or device tensor); seg_off: int64 [B+1]; k: per-bracket threshold [B].
 
-    Returns a bool numpy mask [N] (or the device uint8 tensor with ``return_device``).
+    Returns a bool numpy mask [N]; with ``return_order`` the device tensors (advance u8, sorted
+    positions i64, advancing count per bracket i64).
     """
     import torch
     L = N.lib()
     device = device or default_device()
+    with N.on_device(device, stream):
+        return _promote_segments(L, loss, seg_off, k, device, stream, return_order)
+
+
+def _promote_segments(L, loss, seg_off, k, device, stream, return_order):
+    import torch
 
     def dev(a, dt):
         if isinstance(a, np.ndarray) or not hasattr(a, "data_ptr"):
@@ -32,19 +40,43 @@ def promote_segments(loss, seg_off, k, device=None, stream=None, return_order=Fa
     B = seg_h.shape[0] - 1
     Ntot = int(loss_d.shape[0])
     max_seg = int(np.max(np.diff(seg_h))) if B > 0 else 0
-    order = torch.empty(Ntot, dtype=torch.int64, device=device)
+    # the sorted order only on request: brackets <= 1024 then take the O(n) select (no scratch)
+    order = torch.empty(Ntot, dtype=torch.int64, device=device) if return_order else None
     adv = torch.empty(Ntot, dtype=torch.uint8, device=device)
     nadv = torch.empty(max(B, 1), dtype=torch.int64, device=device)
-    sb = int(L.hbx_sort_scratch_bytes(Ntot))
-    scratch = torch.empty(sb, dtype=torch.uint8, device=device)
+    scratch, sb = None, 0
+    if return_order or max_seg > 1024:
+        sb = int(L.hbx_sort_scratch_bytes(Ntot))
+        scratch = torch.empty(sb, dtype=torch.uint8, device=device)
     N.check(L.hbx_sh_promote(N.ptr(loss_d), N.ptr(seg_d), B, max_seg, Ntot, N.ptr(k_d), N.ptr(order), N.ptr(adv),
-                             N.ptr(nadv), N.ptr(scratch), sb, N.stream_handle(stream)))
+                             N.ptr(nadv), N.ptr(scratch), sb, N.stream_handle(stream, device)))
     if return_order:
         return adv, order, nadv
     return adv.cpu().numpy().astype(bool)
 
 
-def advance_mask(losses, k, device=None):
-    """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182)."""
-    losses = np.asarray(losses, dtype=np.float64)
-    return promote_segments(losses, np.array([0, losses.shape[0]], dtype=np.int64), [k], device=device)
+def advance_mask(losses, k, device=None, stream=None):
+    """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
+
+    What SuccessiveHalving.process_results calls once per bracket: segment bounds, k and the losses
+    travel in one host->device copy, the select kernel runs, the mask comes back in one copy."""
+    import torch
+    losses = np.asarray(losses, dtype=np.float64).reshape(-1)
+    n = losses.shape[0]
+    if n == 0:
+        return np.zeros(0, dtype=bool)
+    if n > 1024:
+        return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream)
+    device = device or default_device()
+    L = N.lib()
+    buf = np.empty(n + 3, dtype=np.float64)
+    buf[:2].view(np.int64)[:] = (0, n)
+    buf[2] = float(k)
+    buf[3:] = losses
+    with N.on_device(device, stream):
+        d = torch.from_numpy(buf).to(device)
+        adv = torch.empty(n, dtype=torch.uint8, device=device)
+        base = d.data_ptr()
+        N.check(L.hbx_sh_promote(base + 24, base, 1, n, n, base + 16, None, N.ptr(adv), None, None, 0,
+                                 N.stream_handle(stream, device)))
+        return adv.cpu().numpy().astype(bool)

@@ -14,6 +14,7 @@
  * Reference interfaces replaced (paths relative to the HpBandSter snapshot):
  *   hbx_seg_argsort + hbx_kde_fit   <- bohb.py:220-246 (BOHB.new_result refit:
  *                                      np.argsort + sm.nonparametric.KDEMultivariate(..,'normal_reference'))
+ *   hbx_kde_refit                   <- bohb.py:211-251 (the same refit plus both KDEs' preparation, one call)
  *   hbx_kde_prepare                 <- KDEMultivariate.__init__ model state (statsmodels 0.12.2
  *                                      kernel_density.py:101-115)
  *   hbx_kde_acquire                 <- bohb.py:124-169 (the num_samples loop: pdf of l and g per
@@ -21,6 +22,8 @@
  *   hbx_kde_logpdf                  <- KDEMultivariate.pdf (kernel_density.py:162-196), fp32 log domain
  *   hbx_kde_pdf_exact               <- KDEMultivariate.pdf, fp64, reference operation order
  *   hbx_sh_promote                  <- HB_iteration.py:149-190 (SuccessiveHalving.process_results ranks)
+ *   hbx_argmax_allreduce            <- bohb.py:150-152 'if val < best' across candidate shards on many GPUs
+ *                                      (the reference has no multi-GPU path)
  */
 #ifndef HBX_H_
 #define HBX_H_
@@ -64,6 +67,26 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
                 const int64_t* n_good, const int64_t* n_bad, const double* fac_good, const double* fac_bad,
                 const int32_t* vartype, double* bw_good, double* bw_bad, int32_t* nlev_good, int32_t* nlev_bad,
                 void* stream);
+
+/* One-call refit of one budget's KDE pair (bohb.py:211-251: append the new observation(s), np.argsort
+ * of the losses, good = head n_good / bad = tail n_bad rows, KDEMultivariate(.., 'normal_reference') for
+ * both), enqueued on `stream` without host synchronisation; the caller reads `out` back once.
+ *   X / loss: device f64[cap][D] / f64[cap] holding the budget's rows 0..n-1 after the call: rows
+ *     n-n_new .. n-1 are copied in from `staged` (device f64[n_new*D + n_new]: rows, then losses;
+ *     n_new = 0: X / loss are complete already).
+ *   vartype: host i32[D] (0 = continuous, 1 = categorical); n_good / n_bad (bohb.py:224-225, clipped to
+ *     n) and fac_* = n_good**(-1/(4+D)) / n_bad**(...) from the host's pow().
+ *   params_* / table_*: as hbx_kde_prepare (tables of hbx_kde_table_floats(n_good|n_bad, ...) floats).
+ *   out: device, hbx_kde_refit_out_bytes(n, D) bytes = order i64[n] | bw_good f64[D] | bw_bad f64[D] |
+ *     nlev_good i32[D] | nlev_bad i32[D] | info_good i32[8] | info_bad i32[8] (info as hbx_kde_prepare);
+ *     the KDEs' rows are order[0..n_good) and order[n-n_bad..n) -- keep `out` alive with the model.
+ *   scratch: device, hbx_kde_refit_scratch_bytes(n, D) bytes. */
+int64_t hbx_kde_refit_out_bytes(int64_t n, int32_t D);
+int64_t hbx_kde_refit_scratch_bytes(int64_t n, int32_t D);
+int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
+                  int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad, void* params_good,
+                  float* table_good, int64_t table_good_floats, void* params_bad, float* table_bad,
+                  int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream);
 
 /* ---- KDE model preparation ----------------------------------------------------------------- */
 /* Template bucket of the scoring kernel for dc continuous / du categorical dims
@@ -127,16 +150,36 @@ int hbx_event_create(void** ev);
 int hbx_event_destroy(void* ev);
 int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
-/* Device address of the result record {i64 index, f64 score, f64 pdf_l, f64 pdf_g,
- * i64 shortlist, i32 flags, i32 pad} inside an acquisition workspace. */
+/* Device address of the result record inside an acquisition workspace (48 bytes):
+ *   {i64 index, f64 score, f32 rel, i32 flags, i32 shortlist, i32 near, f64 pdf_l, f64 pdf_g}
+ * index: first index of the minimal exact score (-1: no finite score); rel: bound of
+ * |score - the same score in numpy's arithmetic| / score; near: candidates whose scores lie within those
+ * bounds of the winner's (itself included).  flags: HBX_ACQ_OVERFLOW (1: every candidate re-scored),
+ * HBX_ACQ_NEAR_TIE (2: near > 1 -- the fp64 re-score here and numpy may order them differently, so the
+ * near set (hbx_kde_ws_offsets) must be re-scored in the reference's own arithmetic to pick the
+ * reference's index; the Python wrapper does this on the host and sets HBX_ACQ_RESOLVED, 4). */
+#define HBX_ACQ_OVERFLOW 1
+#define HBX_ACQ_NEAR_TIE 2
+#define HBX_ACQ_RESOLVED 4
 void* hbx_kde_result_ptr(void* workspace);
+/* Byte offsets of [shortlist count (i32), shortlist (i32 candidate indices), near list, exact l (f64),
+ * exact g (f64)] inside the workspace of an acquisition over (Nc, seg, nmax) candidates (seg = Nc for
+ * hbx_kde_acquire).  hbx_kde_acquire's near list holds the near set's candidate indices (record.near of
+ * them); hbx_kde_acquire_batch's holds a 0/1 flag per shortlist entry. */
+int hbx_kde_ws_offsets(int64_t Nc, int64_t seg, int64_t nmax, int64_t* out);
 
 int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax);
 
-/* Exact fp64 pdf of one prepared KDE at Np points (device f64[Np][D]) -> out (device f64[Np]). */
+/* Exact fp64 pdf of one prepared KDE at Np points (device f64[Np][D]) -> out (device f64[Np]).  Same
+ * float64 operations in the same order as statsmodels 0.12.2 on the pinned numpy 1.26.4 (its SVML exp
+ * restated bit for bit, numpy's pairwise sums): bit-identical to the reference's KDEMultivariate.pdf. */
 int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                       const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
                       void* stream);
+
+/* numpy 1.26.4's float64 exp (what the reference's np.exp computes on AVX512_SKX hosts), element-wise
+ * on the device: the known-answer check of the exact re-score's exp.  x, y: device f64[n]. */
+int hbx_np_exp(const double* x, int64_t n, double* y, void* stream);
 
 /* ---- candidate sampler (bohb.py:133-147, on the GPU) --------------------------------------- */
 /* Philox4x32-10 block function (host): out[4] = philox(counter[4], key[2]).  Exposed for the
@@ -179,10 +222,31 @@ int hbx_kde_cv_terms(const double* X, int64_t n, int32_t D, const int32_t* varty
                      const double* lev, const int32_t* lev_off, const int32_t* loo_levels, double c4, double c2,
                      double bwprod, double* F, double* L, void* stream);
 
+/* ---- multi-GPU winner exchange (candidate sharding; bohb.py:133-152 sharded) ----- */
+/* Each rank runs hbx_kde_acquire on its contiguous shard with index_base = its first global index; the
+ * ranks' result records then meet in ONE RCCL all-gather over xGMI and are reduced on the device by
+ * (score, global index): the smallest score, ties to the smallest index -- the reference's strict '<'
+ * in index order.  Winners within each other's error bounds set HBX_ACQ_NEAR_TIE (record.near = ranks
+ * involved) for a host re-resolution.  ("argmax" of l/g = argmin of the BOHB score g/l.)
+ *   local: this rank's device result record (hbx_kde_result_ptr); gather: device scratch of
+ *   hbx_argmax_gather_bytes(nranks) holding every rank's record afterwards; out: device record of the
+ *   global winner; rccl_comm: an ncclComm_t (hbx_rccl_comm_init, or the caller's own). */
+int64_t hbx_rccl_unique_id_bytes(void);
+int hbx_rccl_get_unique_id(void* id_out);
+int hbx_rccl_comm_init(void** comm, int32_t nranks, const void* id, int32_t rank, int32_t device);
+int hbx_rccl_comm_destroy(void* comm);
+int64_t hbx_argmax_gather_bytes(int32_t nranks);
+int hbx_argmax_allreduce(const void* local, void* gather, void* out, int32_t nranks, void* rccl_comm, void* stream);
+/* The same reduction over records gathered by another transport (device AcqResult[nranks] -> out). */
+int hbx_argmax_records(const void* all, int32_t nranks, void* out, void* stream);
+
 /* ---- successive-halving promotion -------------------------------------------------------- */
 /* advance[i] = rank_i < k[b] among the finite losses of bracket b (non-finite = CRASHED, never
- * advance).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B]; order: device
- * i64[N] (sorted positions, output); advance: device u8[N]; n_advance: device i64[B], nullable. */
+ * advance; ties ranked by position).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B];
+ * order: device i64[N] (sorted positions per bracket, output) or NULL when only the mask is wanted --
+ * brackets of <= 1024 configurations then take an O(n) radix select of the k-th loss and need no
+ * scratch (scratch may be NULL); advance: device u8[N]; n_advance: device i64[B], nullable.
+ * scratch: hbx_sort_scratch_bytes(N) bytes when order is requested or a bracket exceeds 1024. */
 int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                    const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                    int64_t scratch_bytes, void* stream);

@@ -24,6 +24,10 @@ def lib():
         vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
         L.oracle_kde_pdf.argtypes = [vp, i64, i32, vp, vp, vp, vp, i64, vp, i32]
         L.oracle_kde_pdf.restype = None
+        L.oracle_kde_pdf_mode.argtypes = [vp, i64, i32, vp, vp, vp, vp, i64, vp, i32, i32]
+        L.oracle_kde_pdf_mode.restype = None
+        L.oracle_np_exp.argtypes = [vp, i64, vp]
+        L.oracle_np_exp.restype = None
         L.oracle_bohb_select.argtypes = [vp, vp, i64, vp]
         L.oracle_bohb_select.restype = i64
         L.oracle_max_threads.restype = i32
@@ -31,15 +35,26 @@ def lib():
     return _lib
 
 
-def kde_pdf(data, bw, var_type, nlev, pts, nthreads=0):
+def np_exp(x):
+    """numpy 1.26.4's float64 exp (the pinned reference's), bit for bit (oracle/np_arith.h)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().oracle_np_exp(x.ctypes.data, x.size, y.ctypes.data)
+    return y
+
+
+def kde_pdf(data, bw, var_type, nlev, pts, nthreads=0, exact=False):
+    """KDEMultivariate.pdf at pts.  exact=True: the reference's float64 arithmetic bit for bit
+    (numpy 1.26.4's exp and pairwise sums); False: libm exp, sequential sums (CPU baseline)."""
     data = np.ascontiguousarray(data, dtype=np.float64)
     pts = np.ascontiguousarray(np.atleast_2d(pts), dtype=np.float64)
     vt = np.array([0 if c == "c" else 1 for c in var_type], dtype=np.int32)
     bw = np.ascontiguousarray(bw, dtype=np.float64)
     nlev = np.ascontiguousarray(nlev, dtype=np.int32)
     out = np.empty(pts.shape[0])
-    lib().oracle_kde_pdf(data.ctypes.data, data.shape[0], data.shape[1], vt.ctypes.data, bw.ctypes.data,
-                         nlev.ctypes.data, pts.ctypes.data, pts.shape[0], out.ctypes.data, int(nthreads))
+    lib().oracle_kde_pdf_mode(data.ctypes.data, data.shape[0], data.shape[1], vt.ctypes.data, bw.ctypes.data,
+                              nlev.ctypes.data, pts.ctypes.data, pts.shape[0], out.ctypes.data, int(nthreads),
+                              1 if exact else 0)
     return out
 
 

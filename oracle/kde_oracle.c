@@ -12,50 +12,75 @@
  *   pdf               kernel_density.py:190-193: gpke / nobs
  *   minimize_me       hpbandster bohb.py:129 max(1e-8, g) / max(l, 1e-8) (Python max semantics)
  *   argmin            bohb.py:149-152 strict '<' against best = +inf (first index wins)
- * The observation sum is sequential (numpy sums pairwise), so values agree with the reference to
- * rounding (~1e-15 relative), not bit for bit; selections agree on tie-free inputs.
+ * Two modes.  exact = 1: the reference's float64 arithmetic bit for bit -- numpy's exp as the pinned
+ * numpy 1.26.4 evaluates it and numpy's pairwise summation (np_arith.h) -- the checker.  exact = 0:
+ * libm exp and a sequential sum (values agree to rounding, ~1e-15 relative), the fast CPU baseline.
  *
  * Build: oracle/Makefile (gcc -O3 -fopenmp -shared) -> oracle/_build/libkde_oracle.so.
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
 
+#include "np_arith.h"
+
 static const double INV_SQRT_2PI = 0.3989422804014327; /* 1. / np.sqrt(2 * np.pi) */
 
 /* pdf of one KDE (data [n][D]) at Np points (pts [Np][D]) -> out[Np].  vartype: 0 = 'c', 1 = 'u'. */
-void oracle_kde_pdf(const double* data, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
-                    const int32_t* nlev, const double* pts, int64_t Np, double* out, int32_t nthreads) {
+void oracle_kde_pdf_mode(const double* data, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
+                         const int32_t* nlev, const double* pts, int64_t Np, double* out, int32_t nthreads,
+                         int32_t exact) {
   double prod_bw_c = 1.0;
   for (int d = 0; d < D; ++d)
     if (vartype[d] == 0) prod_bw_c *= bw[d];
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(dynamic, 4)
+#pragma omp parallel
 #endif
-  for (int64_t p = 0; p < Np; ++p) {
-    const double* x = pts + p * D;
-    double acc = 0.0;
-    for (int64_t j = 0; j < n; ++j) {
-      const double* xr = data + j * D;
-      double prod = 1.0;
-      for (int d = 0; d < D; ++d) {
-        const double h = bw[d];
-        double k;
-        if (vartype[d] == 0) {
-          const double diff = xr[d] - x[d];
-          k = INV_SQRT_2PI * exp(-(diff * diff) / ((h * h) * 2.));
-        } else {
-          k = (xr[d] == x[d]) ? (1. - h) : (h / (double)(nlev[d] - 1));
+  {
+    double* dens = exact ? (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1)) : 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+    for (int64_t p = 0; p < Np; ++p) {
+      const double* x = pts + p * D;
+      double acc = 0.0;
+      for (int64_t j = 0; j < n; ++j) {
+        const double* xr = data + j * D;
+        double prod = 1.0;
+        for (int d = 0; d < D; ++d) {
+          const double h = bw[d];
+          double k;
+          if (vartype[d] == 0) {
+            const double diff = xr[d] - x[d];
+            const double a = -(diff * diff) / ((h * h) * 2.);
+            k = INV_SQRT_2PI * (exact ? np_exp(a) : exp(a));
+          } else {
+            k = (xr[d] == x[d]) ? (1. - h) : (h / (double)(nlev[d] - 1));
+          }
+          prod = (d == 0) ? k : prod * k;
         }
-        prod = (d == 0) ? k : prod * k;
+        if (exact) dens[j] = prod / prod_bw_c;
+        else acc += prod / prod_bw_c;
       }
-      acc += prod / prod_bw_c;
+      if (exact) acc = np_sum(dens, n);
+      out[p] = acc / (double)n;
     }
-    out[p] = acc / (double)n;
+    free(dens);
   }
+}
+
+void oracle_kde_pdf(const double* data, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
+                    const int32_t* nlev, const double* pts, int64_t Np, double* out, int32_t nthreads) {
+  oracle_kde_pdf_mode(data, n, D, vartype, bw, nlev, pts, Np, out, nthreads, 0);
+}
+
+/* numpy 1.26.4's exp (SVML), element-wise: for the oracle's own known-answer tests */
+void oracle_np_exp(const double* x, int64_t n, double* y) {
+  for (int64_t i = 0; i < n; ++i) y[i] = np_exp(x[i]);
 }
 
 /* first index of the minimum of max(1e-8, g)/max(l, 1e-8) over finite scores; -1 if none */

@@ -285,6 +285,41 @@ def gen_kde_cases(ref):
 
 
 # ----------------------------------------------------------------------------------------
+# near ties: candidates whose reference scores differ from the best one by a few ulps (the GPU's fp64
+# exp and numpy's may order them differently -- the engine must re-resolve them in numpy's arithmetic)
+
+
+def near_tie_candidates(ref, X, L, base, dc, du, levels, seed, max_ulps):
+    """base candidates + copies of the reference's best one with continuous coordinates moved by
+    1..max_ulps ulps (and exact duplicates), shuffled so copies sit before and after it."""
+    space, cg = fit_through_bohb(ref, X, L, dc, du, levels)
+    model = cg.kde_models[1.0]
+    l = np.atleast_1d(model["good"].pdf(base))
+    g = np.atleast_1d(model["bad"].pdf(base))
+    best = py_argmin([py_score(a, b) for a, b in zip(l, g)])
+    rs = np.random.RandomState(seed)
+    copies = []
+    for k in range(48):
+        c = base[best].copy()
+        if k % 8 != 0:  # every 8th copy is an exact duplicate
+            for _ in range(1 + k % 3):
+                d = rs.randint(dc)
+                for _ in range(rs.randint(1, max_ulps + 1)):
+                    c[d] = np.nextafter(c[d], np.inf if rs.rand() < 0.5 else -np.inf)
+        copies.append(c)
+    C = np.vstack([base, np.array(copies)])
+    return C[rs.permutation(C.shape[0])]
+
+
+def gen_neartie_cases(ref):
+    S = ref.synth
+    X = S.make_observations(300, 8, 0, 2); L = S.make_losses(300); B = S.make_candidates(200, 8, 0, 2)
+    kde_case(ref, "neartie_c", X, L, near_tie_candidates(ref, X, L, B, 8, 0, 2, 61, 2), 8, 0, 2)
+    X = S.make_observations(400, 5, 3, [2, 3, 4]); L = S.make_losses(400); B = S.make_candidates(200, 5, 3, [2, 3, 4])
+    kde_case(ref, "neartie_m", X, L, near_tie_candidates(ref, X, L, B, 5, 3, [2, 3, 4], 62, 40), 5, 3, [2, 3, 4])
+
+
+# ----------------------------------------------------------------------------------------
 # get_config: the reference's own sampler + selection, recording every candidate it scored
 
 
@@ -480,14 +515,37 @@ def gen_e2e(ref):
         len(records), sum(r["model_based"] for r in records), len(runs["runs"])))
 
 
+# ----------------------------------------------------------------------------------------
+# numpy's float64 exp as the reference's numpy evaluates it (known-answer vectors for the engine's and
+# the oracle's restatement of it)
+
+
+def gen_npexp(ref):
+    rs = np.random.RandomState(71)
+    x = np.concatenate([
+        -rs.rand(5000) * 50, (rs.rand(5000) - 0.5) * 1500, (rs.rand(1500) - 0.5) * 1e-6,
+        -(rs.randn(5000) ** 2) / (2 * 0.01 ** 2), -707.7 - rs.rand(2500) * 40, -745.2 + rs.rand(1500) * 2,
+        np.array([0.0, -0.0, 5e-324, -5e-324, 1e-300, -1e-300, 2.0 ** -54, -2.0 ** -54, 709.78, 709.79, -745.13,
+                  -745.14, -708.3964, -707.7032713517042, np.inf, -np.inf])])
+    np.savez_compressed(os.path.join(HERE, "np_exp.npz"), x=x, y=np.exp(x), numpy=np.array(np.__version__))
+    print("wrote np_exp.npz (%d values, numpy %s)" % (x.size, np.__version__))
+
+
+GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp"]
+
+
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None, help="subset of %s" % GENERATORS)
+    a = ap.parse_args()
     t0 = time.time()
     ref = load_reference()
-    gen_kde_cases(ref)
-    gen_get_config(ref)
-    gen_sh(ref)
-    gen_brackets(ref)
-    gen_e2e(ref)
+    todo = a.only or GENERATORS
+    fns = {"kde": gen_kde_cases, "neartie": gen_neartie_cases, "getcfg": gen_get_config, "sh": gen_sh,
+           "brackets": gen_brackets, "e2e": gen_e2e, "npexp": gen_npexp}
+    for name in todo:
+        fns[name](ref)
     with open(os.path.join(HERE, "PROVENANCE.json"), "w") as fh:
         json.dump(dict(generator="tests/golden/gen_golden.py", interpreter=sys.version.split()[0],
                        numpy=np.__version__, scipy=__import__("scipy").__version__,

@@ -33,7 +33,7 @@ def test_batch_matches_reference_per_segment(device, name, seg):
         a, e = b * seg, min((b + 1) * seg, len(C))
         assert r.index == O.py_argmin(S[a:e]), (name, seg, b)
         if r.index >= 0:
-            np.testing.assert_allclose(r.score, S[a + r.index], rtol=1e-13)
+            assert r.score == S[a + r.index]
         if b % 5 == 0:  # the same call on the segment alone: bit-identical record
             one = pair.acquire(C[a:e])
             assert (one.index, one.shortlist, one.flags) == (r.index, r.shortlist, r.flags)

@@ -2,7 +2,8 @@
 
 Tolerances (north star): chosen indices and promotion masks bit-exact; fp32 log-densities within
 1e-5 relative of the reference fp64 path (|d ln pdf| <= 1e-5 * max(1, |ln pdf|)); the exact fp64
-path within 1e-13 relative (numpy versions differ in exp() by an ulp).
+path bit-identical to the reference (statsmodels on the pinned numpy 1.26.4, whose SVML exp the engine
+restates).
 """
 import numpy as np
 import pytest
@@ -75,14 +76,28 @@ def test_logpdf_fp32_within_tolerance(device, name, hmode, monkeypatch):
 
 
 @pytest.mark.parametrize("name", G.kde_case_names())
-def test_exact_pdf_matches_reference(device, name):
+def test_exact_pdf_bit_identical_to_reference(device, name):
+    """The fp64 re-score against the reference's own KDEMultivariate.pdf outputs: bit for bit (same
+    float64 operations in the same order, numpy's exp restated exactly)."""
     c = G.load_kde_case(name)
     pair = _pair_from_fixture(c)
     C = c["cands"][:128]
     l = np.atleast_1d(pair.good.pdf(C))
     g = np.atleast_1d(pair.bad.pdf(C))
-    np.testing.assert_allclose(l, c["pdf_l"][:len(C)], rtol=1e-13, atol=0, equal_nan=True)
-    np.testing.assert_allclose(g, c["pdf_g"][:len(C)], rtol=1e-13, atol=0, equal_nan=True)
+    np.testing.assert_array_equal(l, c["pdf_l"][:len(C)])
+    np.testing.assert_array_equal(g, c["pdf_g"][:len(C)])
+
+
+def test_np_exp_known_answers(device):
+    """The device restatement of numpy's float64 exp against numpy 1.26.4's own outputs (the pinned
+    reference interpreter), 2e4 inputs over every range including subnormal results and overflow."""
+    import torch
+    from hpbandster_amd import _native as N
+    z = np.load(G.GOLDEN + "/np_exp.npz")
+    x = torch.from_numpy(z["x"]).to(device)
+    y = torch.empty_like(x)
+    N.check(N.lib().hbx_np_exp(N.ptr(x), x.numel(), N.ptr(y), N.stream_handle(None, device)))
+    np.testing.assert_array_equal(y.cpu().numpy().view(np.uint64), z["y"].view(np.uint64))
 
 
 @pytest.mark.parametrize("hmode", ["1", "0"])
@@ -94,8 +109,7 @@ def test_acquire_chosen_index_bit_exact(device, name, hmode, monkeypatch):
     res = pair.acquire(c["cands"])
     assert res.index == c["chosen"], (name, res, c["chosen"])
     if res.index >= 0:
-        ref = c["scores"][res.index]
-        np.testing.assert_allclose(res.score, ref, rtol=1e-13)
+        assert res.score == c["scores"][res.index]  # the reference's exact score, bit for bit
         assert res.shortlist >= 1
 
 
@@ -172,8 +186,9 @@ def test_rescue_path_far_candidates(device):
 def test_exact_split_units_match_whole_sum(device, n_obs):
     """The acquisition's exact re-score spreads one candidate's observations over tree units (one
     block each) and recombines them; DeviceKDE.pdf sums every unit in one block.  Same additions in
-    the same order -> bit-identical pdfs; and both within 1e-13 of the reference's numpy sum (numpy
-    sums over 8192-element buffers: n=20000 has three)."""
+    the same order -> bit-identical pdfs; and both bit-identical to the C oracle's restatement of the
+    reference arithmetic (numpy sums over 8192-element buffers: n=20000 has three)."""
+    from oracle import c_oracle
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
     X = S.make_observations(n_obs, 24, 8, 4)
@@ -186,11 +201,9 @@ def test_exact_split_units_match_whole_sum(device, n_obs):
     w = C[res.index:res.index + 1]
     assert np.asarray(pair.good.pdf(w)).item() == res.pdf_l
     assert np.asarray(pair.bad.pdf(w)).item() == res.pdf_g
-    ref_l = O.pdf_many(pair.good.data, pair.good.bw, vt, w)[0]
-    ref_g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, w)[0]
-    np.testing.assert_allclose([res.pdf_l, res.pdf_g], [ref_l, ref_g], rtol=1e-13)
-    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
-    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
+    l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+    g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    assert (res.pdf_l, res.pdf_g) == (l[res.index], g[res.index])
     assert res.index == O.select(l, g)[0]
 
 
@@ -315,3 +328,27 @@ def test_pair_launch_identical_to_two_launches(device, shape, monkeypatch):
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
         assert r1.index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("name", ["neartie_c", "neartie_m"])
+def test_near_ties_pinned_and_process(device, name):
+    """Near ties (copies of the reference's best candidate moved by a few ulps, exact duplicates).
+    Pinned policy: the reference's own pick (its exact scores bit for bit), the near set flagged.
+    Process policy: the pick this process's numpy makes (numpy restatement run here), single and
+    batched, and through the two-stage sharded exchange at world size 1."""
+    from hpbandster_amd.kde import ACQ_NEAR_TIE, ACQ_RESOLVED
+    c = G.load_kde_case(name)
+    pair = _pair_from_fixture(c)
+    C = c["cands"]
+    res = pair.acquire(C)
+    assert res.index == c["chosen"] and res.score == c["scores"][c["chosen"]]
+    assert res.flags & ACQ_NEAR_TIE and res.near > 1
+    l = O.pdf_many(pair.good.data, pair.good.bw, c["var_type"], C, pair.good.nlev)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, c["var_type"], C, pair.bad.nlev)
+    want = O.select(l, g)[0]
+    rp = pair.acquire(C, ties="process")
+    assert rp.index == want and rp.flags & ACQ_RESOLVED
+    assert (rp.pdf_l, rp.pdf_g) == (l[want], g[want])
+    rb = pair.acquire_batch(C, C.shape[0], ties="process")
+    assert rb[0].index == want
+    assert pair.acquire_batch(C, C.shape[0])[0].index == c["chosen"]

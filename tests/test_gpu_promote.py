@@ -128,6 +128,8 @@ def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
     loss[rs.rand(seg[-1]) < 0.04] = np.inf
     loss[rs.rand(seg[-1]) < 0.04] = np.nan
     loss[rs.rand(seg[-1]) < 0.02] = -np.inf
+    loss[rs.rand(seg[-1]) < 0.03] = -0.0  # equal to 0.0 for numpy's sort: ties by position
+    loss[rs.rand(seg[-1]) < 0.03] = 0.0
     L = N.lib()
     ld = torch.from_numpy(loss).to(device)
     segd = torch.from_numpy(seg).to(device)
@@ -145,3 +147,60 @@ def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
     for b in range(B):
         s, e = seg[b], seg[b + 1]
         np.testing.assert_array_equal(outs[0][s:e], np.argsort(loss[s:e], kind="stable"))
+
+
+@pytest.mark.parametrize("B,n", [(400, 1024), (97, 200), (5, 1), (64, 3), (2000, 81)])
+def test_select_kernel_identical_to_sort(device, B, n):
+    """Mask-only promotion (order not requested) runs the radix select of the k-th (loss, position);
+    with the order requested the wave sort runs.  Masks and counts identical on tie-heavy brackets
+    with empty, all-equal, all-crashed ones and k = 0, fractional, NaN and larger than the bracket."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(3 * B + n)
+    lens = rs.randint(0, n + 1, size=B)
+    lens[0] = n
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = np.round(rs.rand(seg[-1]) * 30) / 30
+    loss[rs.rand(seg[-1]) < 0.3] = 0.5
+    loss[rs.rand(seg[-1]) < 0.05] = np.inf
+    loss[rs.rand(seg[-1]) < 0.03] = np.nan
+    loss[rs.rand(seg[-1]) < 0.01] = -np.inf
+    loss[rs.rand(seg[-1]) < 0.01] = -0.0
+    loss[rs.rand(seg[-1]) < 0.01] = 0.0
+    if B > 3:
+        loss[seg[1]:seg[2]] = 0.25       # all equal
+        loss[seg[2]:seg[3]] = np.nan     # all crashed
+    k = np.maximum(lens * rs.choice([0.0, 0.34, 0.5, 0.999, 1.7], size=B), 0.0)
+    k[::7] = np.floor(k[::7])
+    if B > 5:
+        k[4] = np.nan
+        k[5] = np.inf
+    a_sel = promote.promote_segments(loss, seg, k, device=device)
+    a_srt, _, c_srt = promote.promote_segments(loss, seg, k, device=device, return_order=True)
+    np.testing.assert_array_equal(a_sel, a_srt.cpu().numpy().astype(bool))
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(a_sel[s:e], O.sh_advance(loss[s:e], k[b]))
+
+
+def test_select_kernel_counts_and_extreme_keys(device):
+    """Counts from the select kernel; keys differing only in the lowest bits and across signs."""
+    import torch
+    from hpbandster_amd import _native as N
+    base = np.array([1.0, np.nextafter(1.0, 2), np.nextafter(np.nextafter(1.0, 2), 2), -1.0, -np.nextafter(1.0, 2),
+                     5e-324, -5e-324, 0.0, -0.0, 1e308, -1e308])
+    rs = np.random.RandomState(5)
+    L = N.lib()
+    for trial in range(20):
+        loss = rs.permutation(np.concatenate([base, rs.choice(base, 40)]))
+        n = loss.shape[0]
+        for kk in range(0, n + 2):
+            ld = torch.from_numpy(loss).to(device)
+            seg = torch.tensor([0, n], dtype=torch.int64, device=device)
+            kd = torch.tensor([float(kk)], dtype=torch.float64, device=device)
+            adv = torch.empty(n, dtype=torch.uint8, device=device)
+            cnt = torch.empty(1, dtype=torch.int64, device=device)
+            N.check(L.hbx_sh_promote(N.ptr(ld), N.ptr(seg), 1, n, n, N.ptr(kd), None, N.ptr(adv), N.ptr(cnt), None, 0,
+                                     N.stream_handle()))
+            want = O.sh_advance(loss, kk)
+            np.testing.assert_array_equal(adv.cpu().numpy().astype(bool), want, err_msg="k=%d" % kk)
+            assert int(cnt.item()) == int(want.sum())
