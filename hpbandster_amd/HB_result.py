@@ -18,18 +18,23 @@ class Run(object):
         self.info = info
         self.time_stamps = time_stamps
 
-    def __repr__(self):
-        return "config_id: %s\tbudget: %f\tloss: %s\ntime_stamps: %s\ninfo: %s\n" % (
-            self.config_id, self.budget, self.loss, self.time_stamps, self.info)
+    def __repr__(self):  # the reference's format (HB_result.py:17-24)
+        return ("config_id: %s\t" % (self.config_id,) + "budget: %f\t" % self.budget + "loss: %s\n" % self.loss +
+                "time_stamps: {submitted} (submitted), {started} (started), {finished} (finished)\n".format(
+                    **self.time_stamps) + "info: %s\n" % self.info)
+
+    def __getitem__(self, k):  # dictionary-style access, as the reference allows
+        return getattr(self, k)
 
 
 run = Run  # reference name
 
 
 def extract_HB_learning_curves(runs):
-    """Learning curve = (budget, loss) of every finished run, by budget."""
-    lc = [(r.budget, r.loss) for r in sorted(runs, key=lambda r: r.budget) if r.loss is not None]
-    return [lc]
+    """Learning curve = (budget, loss) of every run by budget, crashed ones (loss None) included
+    (HB_result.py:33-58)."""
+    sr = sorted(runs, key=lambda r: r.budget)
+    return [[(r.budget, r.loss) for r in sr]]
 
 
 class HB_result(object):
@@ -61,7 +66,7 @@ class HB_result(object):
                     runs.append(Run(config_id, b, None, None, d['time_stamps'][b], err))
                 else:
                     runs.append(Run(config_id, b, r['loss'], r['info'], d['time_stamps'][b], err))
-            except (KeyError, TypeError):
+            except Exception:  # the reference skips any malformed entry (HB_result.py:180-181)
                 pass
         runs.sort(key=lambda r: r.budget)
         return runs
@@ -90,11 +95,12 @@ class HB_result(object):
                 out['times_finished'].append(r.time_stamps['finished'])
                 out['budgets'].append(r.budget)
                 out['losses'].append(r.loss)
-        if out['config_ids']:
-            out['config_ids'].append(out['config_ids'][-1])
-            out['times_finished'].append(all_runs[-1].time_stamps['finished'])
-            out['budgets'].append(out['budgets'][-1])
-            out['losses'].append(out['losses'][-1])
+        # the final point repeats the incumbent at the last finish time; like the reference this raises
+        # IndexError when no run finished (HB_result.py:150-155)
+        out['config_ids'].append(out['config_ids'][-1])
+        out['times_finished'].append(all_runs[-1].time_stamps['finished'])
+        out['budgets'].append(out['budgets'][-1])
+        out['losses'].append(out['losses'][-1])
         return out
 
     def get_learning_curves(self, lc_extractor=extract_HB_learning_curves, config_ids=None):

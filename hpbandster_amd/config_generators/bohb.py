@@ -62,6 +62,14 @@ class BOHB(base_config_generator):
                 self.kde_vartypes += 'c'
                 self.vartypes += [0]
         self.vartypes = np.array(self.vartypes, dtype=int)
+        # engine limits: D <= 256 dims; categorical codes are level indices < 1024 (the
+        # level count runs on a 1024-bit map); beyond 64 continuous / 32 categorical dims the KDEs are
+        # exact-only (every candidate re-scored in fp64, no fp32 pre-selection)
+        if len(self.vartypes) > _native.lib().hbx_max_dims():
+            raise ValueError("hpbandster_amd supports at most %d hyperparameters (got %d)"
+                             % (_native.lib().hbx_max_dims(), len(self.vartypes)))
+        if (self.vartypes > 1024).any():
+            raise ValueError("hpbandster_amd supports categorical hyperparameters with at most 1024 choices")
 
         self.cat_probs = []
         self.configs = dict()
@@ -154,8 +162,20 @@ class BOHB(base_config_generator):
                 continue
             if pair is None:
                 pair = self.kde_models[max(self.kde_models.keys())]  # bohb.py:124
+            if self.sampler == "gpu":
+                plan.append(len(blocks) * self.num_samples)
+                blocks.append(None)
+                continue
+            try:  # a sampling error falls back to a random configuration for this call only, after
+                # consuming the global RNG exactly as the sequential call would (bohb.py:163-166)
+                block = self.sample_candidates(pair['good'], self.num_samples)
+            except Exception:
+                self.logger.warning("Sampling based optimization with %i samples failed\n %s \nUsing random "
+                                    "configuration" % (self.num_samples, traceback.format_exc()))
+                plan.append(None)
+                continue
             plan.append(len(blocks) * self.num_samples)
-            blocks.append(None if self.sampler == "gpu" else self.sample_candidates(pair['good'], self.num_samples))
+            blocks.append(block)
         results, bad = [], None
         if blocks:
             if self.sampler == "gpu":  # one draw for all calls: same Philox counters as call by call

@@ -47,7 +47,8 @@ struct KdeParams {
   int32_t stride;     // floats per observation row of the fp32 table
   int32_t dc_pad;     // continuous slots in the table (template bucket)
   int32_t du_pad;     // categorical slots in the table (template bucket)
-  int32_t pad0;
+  int32_t exact_only; // no fp32 scoring bucket fits (> 64 continuous / > 32 categorical dims): every
+                      // candidate is re-scored in fp64 (variant bit 5)
   double log_norm;    // ln pdf = ln(S) + log_norm  (S = sum of 2^(t - M0))
   double m0_log2;     // M0: upper bound of the per-pair log2 kernel product
   double lb_sum;      // sum over active categorical dims of log2(h/(c-1))

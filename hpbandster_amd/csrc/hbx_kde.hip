@@ -38,8 +38,10 @@ __host__ __device__ static void bucket_dims(int dc, int du, int* dc_pad, int* du
 
 __host__ __device__ static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
-// capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket
+// capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket (exact-only KDEs,
+// outside every bucket, keep no table: one float)
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
+  if (dc_pad < 0 || du_pad < 0) return 1;
   int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
   const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1);
   a = a > b ? a : b;
@@ -93,7 +95,8 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     P->D = D;
     P->dc_pad = dcp;
     P->du_pad = dup;
-    P->stride = table_stride(dcp, dup);
+    P->exact_only = (dcp < 0 || dup < 0) ? 1 : 0;
+    P->stride = P->exact_only ? 0 : table_stride(dcp, dup);
     for (int d = 0; d < D; ++d) {
       const double h = A.bw[d];
       const bool cat = prep_cat(A, d);
@@ -180,6 +183,12 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // One-hot positions: every dim's block starts at an even position (a padding position, level -1,
   // never matches) -- the sparse matrix-core kernel relies on adjacent pairs never spanning dims.
   const int du = P->du, dcp = P->dc_pad, dup = P->du_pad;
+  if (P->exact_only) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
+    P->hmode = 0;
+    P->nsc = 0;
+    P->chunk_floats = 0;
+    return;
+  }
   if (du > 0) {
     int tot = 0;
     bool ok = true;
@@ -377,7 +386,7 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
     P->cmax = P->cmax2;
   }
   int32_t* info = A.info;
-  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4);
+  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4) | (P->exact_only << 5);
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
@@ -405,9 +414,7 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
     }
   }
   int dcp, dup;
-  bucket_dims(dc, du, &dcp, &dup);
-  if (dcp < 0 || dup < 0)
-    return hbx_fail(HBX_ERR_UNSUPPORTED, "no scoring kernel for %d continuous / %d categorical dims", dc, du);
+  bucket_dims(dc, du, &dcp, &dup);  // outside every bucket: an exact-only KDE (no table)
   if (table_floats_ < table_floats(n, dcp, dup))
     return hbx_fail(HBX_ERR_ARG, "table too small: %lld < %lld floats", (long long)table_floats_,
                     (long long)table_floats(n, dcp, dup));
@@ -421,7 +428,7 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
   A->n = n;
   A->D = D;
   A->hm_allowed = !(hm_env && hm_env[0] == '0');
-  A->nblk_table = (int32_t)prep_table_blocks(n);
+  A->nblk_table = (dcp < 0 || dup < 0) ? 0 : (int32_t)prep_table_blocks(n);
   return HBX_OK;
 }
 
@@ -432,10 +439,12 @@ static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s)
   hipLaunchKernelGGL(kde_center_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
   HBX_LAUNCH_CHECK();
   const unsigned tb = (unsigned)(ps.k[0].nblk_table + (ps.nk > 1 ? ps.k[1].nblk_table : 0));
-  hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 0);
-  HBX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 1);
-  HBX_LAUNCH_CHECK();
+  if (tb > 0) {
+    hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 0);
+    HBX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 1);
+    HBX_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(kde_prep_finish_kernel, dim3(1), dim3(64), 0, s, ps);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
@@ -862,6 +871,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void kde_pdf_exact_kernel(const doub
 __device__ __forceinline__ double exact_rel(const KdeParams* __restrict__ P, const KdeEst e) {
   const double base = (8.0 * (double)P->D + 160.0) * 0x1p-52;
   if (!P->has_neg) return base;
+  if (e.err < -1.5f) return INFINITY;  // exact-only acquisition: no fp32 estimate of the condition
   const float m = fmaxf(e.lpos, e.lneg);
   if (!(m > -INFINITY)) return base;
   const float a = __expf(e.lpos - m), b = __expf(e.lneg - m);
@@ -1056,6 +1066,33 @@ __global__ __launch_bounds__(256) void kde_batch_final_kernel(int64_t B, const u
   res[b] = r;
 }
 
+// Exact-only acquisition (KDEs outside every fp32 scoring bucket): every candidate joins the fp64
+// re-score -- no estimate (err = -2 marks it), each segment flagged so the shortlist takes it whole.
+__global__ __launch_bounds__(256) void kde_exact_only_init_kernel(int64_t Nc, uint32_t seg, KdeEst* __restrict__ el,
+                                                                  KdeEst* __restrict__ eg, float* __restrict__ lo,
+                                                                  int32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= Nc) return;
+  const KdeEst e = {0.f, -INFINITY, -2.f, 0.f};
+  el[i] = e;
+  eg[i] = e;
+  lo[i] = 0.f;
+  if ((uint32_t)i % seg == 0) flags[(uint32_t)i / seg] = HBX_ACQ_OVERFLOW;
+}
+
+// ln of the exact pdfs for the logl/logg outputs of an exact-only acquisition
+__global__ __launch_bounds__(256) void kde_exact_logs_kernel(const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ count,
+                                                             const double* __restrict__ exact_l,
+                                                             const double* __restrict__ exact_g,
+                                                             float* __restrict__ logl, float* __restrict__ logg) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *count) return;
+  const int i = list[p];
+  if (logl) logl[i] = (float)log(exact_l[p]);
+  if (logg) logg[i] = (float)log(exact_g[p]);
+}
+
 // ------------------------------------------------------------------------------------------
 // launch-side dispatch over the (dc_pad, du_pad, signed) template buckets
 
@@ -1208,9 +1245,12 @@ int64_t hbx_kde_table_floats(int32_t n, int32_t dc_pad, int32_t du_pad) { return
 int hbx_kde_bucket(int32_t dc, int32_t du, int32_t* dc_pad, int32_t* du_pad, int32_t* stride) {
   int a, b;
   bucket_dims(dc, du, &a, &b);
-  if (a < 0 || b < 0)
-    return hbx_fail(HBX_ERR_UNSUPPORTED, "no scoring kernel for %d continuous / %d categorical dims "
-                    "(max 64 / 32)", dc, du);
+  if (a < 0 || b < 0) {  // outside every fp32 scoring bucket: exact-only KDEs
+    *dc_pad = *du_pad = -1;
+    *stride = 0;
+    return hbx_fail(HBX_ERR_UNSUPPORTED, "no fp32 scoring kernel for %d continuous / %d categorical dims "
+                    "(max 64 / 32): the KDE is exact-only (every candidate re-scored in fp64)", dc, du);
+  }
   *dc_pad = a;
   *du_pad = b;
   *stride = table_stride(a, b);
@@ -1410,9 +1450,11 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   if ((size_t)ws_bytes < w.total)
     return hbx_fail(HBX_ERR_ARG, "workspace too small: %lld < %lld bytes", (long long)ws_bytes,
                     (long long)w.total);
+  const bool exact_only = ((variant_good | variant_bad) >> 5) & 1;
   ScoreFns fg = pick_logpdf(dc_pad, du_pad, variant_good);
   ScoreFns fb = pick_logpdf(dc_pad, du_pad, variant_bad);
-  if (!fg.main || !fb.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
+  if (!exact_only && (!fg.main || !fb.main))
+    return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
   char* ws = (char*)workspace;
   uint32_t* U = (uint32_t*)(ws + w.U);
   int32_t* count = (int32_t*)(ws + w.count);
@@ -1443,12 +1485,17 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   HBX_LAUNCH_CHECK();
   const dim3 grid((unsigned)((Nc + 255) / 256));
   if (Nc > 0) {
-    hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
-    const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
-                       flags, first1);
-    HBX_LAUNCH_CHECK();
+    if (exact_only) {
+      hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
+      HBX_LAUNCH_CHECK();
+    } else {
+      hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
+      const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
+                         flags, first1);
+      HBX_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
                        batch_res ? segcnt : (int32_t*)nullptr, first1);
     HBX_LAUNCH_CHECK();
@@ -1461,6 +1508,11 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                        (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,
                        exact_g);
     HBX_LAUNCH_CHECK();
+    if (exact_only && (logl_out || logg_out)) {
+      hipLaunchKernelGGL(kde_exact_logs_kernel, grid, dim3(256), 0, s, list, count, exact_l, exact_g, logl_out,
+                         logg_out);
+      HBX_LAUNCH_CHECK();
+    }
   }
   if (!batch_res) {
     hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,

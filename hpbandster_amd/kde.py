@@ -53,6 +53,17 @@ def bandwidth_factor(nobs, D):
     return int(nobs) ** (-1. / (4 + int(D)))
 
 
+def scoring_bucket(vt):
+    """(dc_pad, du_pad) of the fp32 scoring kernel for var-type codes vt, or (-1, -1): no bucket fits
+    (> 64 continuous or > 32 categorical dims) and the KDE is exact-only -- every candidate is re-scored
+    in fp64 (hbx_kde_acquire handles it; hbx_kde_logpdf has no estimate for it)."""
+    dc, du = int((vt == 0).sum()), int((vt == 1).sum())
+    dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+    if N.lib().hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)) != 0:
+        return -1, -1
+    return int(dcp[0]), int(dup[0])
+
+
 class AcqResult(object):
     """One acquisition's winner (include/hbx.h result record).  ``flags`` & ACQ_NEAR_TIE: other
     candidates' exact scores lie within the spread another numpy build's exp could cause (``rel``);
@@ -107,12 +118,10 @@ class DeviceKDE(object):
         D = self.k_vars
         vt = var_type_codes(var_type)
         if prepared is None:
-            dc, du = int((vt == 0).sum()), int((vt == 1).sum())
-            dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
-            N.check(L.hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
+            dcp, dup = scoring_bucket(vt)
             with N.on_device(self.device, stream):
                 self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
-                tf = int(L.hbx_kde_table_floats(self.nobs, int(dcp[0]), int(dup[0])))
+                tf = int(L.hbx_kde_table_floats(self.nobs, dcp, dup))
                 self.table = torch.empty(tf, dtype=torch.float32, device=self.device)
                 info = np.zeros(8, dtype=np.int32)
                 bw_c = np.ascontiguousarray(self.bw)
@@ -124,7 +133,8 @@ class DeviceKDE(object):
             self.params, self.table, info = prepared
         self.variant, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
             [int(v) for v in info]
-        self.has_neg, self.kc = self.variant & 1, self.variant >> 1
+        self.has_neg, self.kc = self.variant & 1, (self.variant >> 1) & 7
+        self.exact_only = bool((self.variant >> 5) & 1)
         if unsupported:
             raise N.HbxError("KDE bandwidth/level combination not modelled (bw=%r, nlev=%r)" % (self.bw, self.nlev))
 
@@ -468,10 +478,7 @@ class ObservationStore(object):
         self._stage_h = None
         self._out_h = None
         self._init_cap = int(capacity)
-        dc, du = int((self.vt == 0).sum()), int((self.vt == 1).sum())
-        dcp, dup, stride = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
-        N.check(N.lib().hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)))
-        self.dc_pad, self.du_pad = int(dcp[0]), int(dup[0])
+        self.dc_pad, self.du_pad = scoring_bucket(self.vt)
 
     def _reserve(self, n):
         torch = _torch()

@@ -472,7 +472,9 @@ def gen_e2e(ref):
 
     ref.SyncDispatcher.compute = staticmethod(compute)
     np.random.seed(123)
-    cg = ref.bohb.BOHB(space)
+    logdir = os.path.join(HERE, "e2e_log")
+    # the reference's own json_result_logger writes the run's configs.json / results.json (fixture)
+    cg = ref.bohb.BOHB(space, directory=logdir, overwrite=True)
     records = []
     orig_get = cg.get_config
     sink = {}
@@ -511,8 +513,84 @@ def gen_e2e(ref):
     np.savez_compressed(os.path.join(HERE, "e2e_toy.npz"), **out)
     with open(os.path.join(HERE, "e2e_toy_runs.json"), "w") as fh:
         json.dump(runs, fh)
+    # the reference's reload of that log into an HB_result, and what its API returns
+    sys.modules["hpbandster"].HB_result = ref.HB_result.HB_result
+    hr = ref.utils.logged_results_to_HB_result(logdir)
+
+    def run_rec(r):
+        return [list(r.config_id), r.budget, r.loss, r.info, r.time_stamps, r.error_logs]
+
+    outs = dict(
+        HB_config=hr.HB_config, incumbent=list(hr.get_incumbent_id()), num_iterations=hr.num_iterations(),
+        trajectory_all=hr.get_incumbent_trajectory(all_budgets=True),
+        trajectory_max=hr.get_incumbent_trajectory(all_budgets=False),
+        all_runs=[run_rec(r) for r in hr.get_all_runs()],
+        all_runs_largest=[run_rec(r) for r in hr.get_all_runs(only_largest_budget=True)],
+        learning_curves=[[list(k), v] for k, v in hr.get_learning_curves().items()],
+        id2config=[[list(k), v] for k, v in hr.get_id2config_mapping().items()],
+        runs_by_id={str(list(k)): [run_rec(r) for r in hr.get_runs_by_id(k)] for k in list(hr.data.keys())[:5]},
+        repr_first=repr(hr.get_all_runs()[0]))
+    for t in ("trajectory_all", "trajectory_max"):
+        outs[t]["config_ids"] = [list(c) for c in outs[t]["config_ids"]]
+    with open(os.path.join(HERE, "e2e_hb_result.json"), "w") as fh:
+        json.dump(outs, fh)
     print("wrote e2e_toy.npz (%d get_config calls, %d model-based), e2e_toy_runs.json (%d runs)" % (
         len(records), sum(r["model_based"] for r in records), len(runs["runs"])))
+
+
+# ----------------------------------------------------------------------------------------
+# KDEEI (config_generators/kde_ei.py): the reference's own refits and sampling-mode proposals
+
+
+def gen_kdeei(ref):
+    S = ref.synth
+    cs = ref.cs
+    for name, dc, n, top, upd, crash_rate in (("d4", 4, 80, 10, 1, 0.1), ("d8", 8, 200, 15, 3, 0.0)):
+        space = cs.ConfigurationSpace(seed=13)
+        for d in range(dc):
+            space.add_hyperparameter(cs.UniformFloatHyperparameter("x%02d" % d, 0.0, 1.0))
+        X = S.make_observations(n, dc, 0, 2)
+        L = S.make_losses(n)
+        crashed = np.random.RandomState(17).rand(n) < crash_rate
+        cg = ref.kde_ei.KDEEI(space, top_n_percent=top, update_after_n_points=upd)
+        fits = []
+        for i in range(n):
+            job = ref.Job((0, 0, i), config=vec_to_dict(space, cs, X[i]), budget=1.0)
+            if crashed[i]:
+                job.result, job.exception = None, "crash"
+            else:
+                job.result = {"loss": float(L[i]), "info": None}
+            cg.new_result(job)
+            if 1.0 in cg.kde_models and (not fits or fits[-1][0] is not cg.kde_models[1.0]["good"]):
+                m = cg.kde_models[1.0]
+                fits.append((m["good"], i, np.asarray(m["good"].bw), np.asarray(m["bad"].bw),
+                             np.asarray(m["good"].data), np.asarray(m["bad"].data)))
+        model = cg.kde_models[1.0]
+        records = []
+        for seed in range(10):
+            good_sink, bad_sink = [], []
+            cg.kde_models[1.0] = {"good": _PdfRecorder(model["good"], good_sink),
+                                  "bad": _PdfRecorder(model["bad"], bad_sink)}
+            np.random.seed(2000 + seed)
+            cfg, info = cg.get_config(1.0)
+            cg.kde_models[1.0] = model
+            vec = cs.Configuration(space, values=cfg).get_array()
+            cands = np.array([v for v, _ in bad_sink]) if info["model_based_pick"] else np.zeros((0, dc))
+            ci = py_argmin([py_score(l, g) for (_, l), (_, g) in zip(good_sink, bad_sink)]) if len(cands) else -1
+            records.append(dict(seed=2000 + seed, model_based=bool(info["model_based_pick"]), cands=cands,
+                                chosen=ci, vec=vec))
+        out = dict(dc=dc, n=n, top_n_percent=top, update_after_n_points=upd, X=X, losses=L, crashed=crashed,
+                   n_fits=len(fits), fit_at=np.array([f[1] for f in fits]))
+        for k, (_, at, bg, bb, dg, db) in enumerate(fits[-3:]):
+            out.update({"fit%d_at" % k: at, "fit%d_bw_good" % k: bg, "fit%d_bw_bad" % k: bb,
+                        "fit%d_good" % k: dg, "fit%d_bad" % k: db})
+        for i, r in enumerate(records):
+            for k, v in r.items():
+                out["r%02d_%s" % (i, k)] = v
+        out["n_records"] = len(records)
+        np.savez_compressed(os.path.join(HERE, "kdeei_%s.npz" % name), **out)
+        print("wrote kdeei_%s.npz  fits %d  model-based picks %d/%d" % (
+            name, len(fits), sum(r["model_based"] for r in records), len(records)))
 
 
 # ----------------------------------------------------------------------------------------
@@ -531,7 +609,7 @@ def gen_npexp(ref):
     print("wrote np_exp.npz (%d values, numpy %s)" % (x.size, np.__version__))
 
 
-GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp"]
+GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp", "kdeei"]
 
 
 def main():
@@ -543,7 +621,8 @@ def main():
     ref = load_reference()
     todo = a.only or GENERATORS
     fns = {"kde": gen_kde_cases, "neartie": gen_neartie_cases, "getcfg": gen_get_config, "sh": gen_sh,
-           "brackets": gen_brackets, "e2e": gen_e2e, "npexp": gen_npexp}
+           "brackets": gen_brackets, "e2e": gen_e2e, "npexp": gen_npexp,
+           "kdeei": gen_kdeei}
     for name in todo:
         fns[name](ref)
     with open(os.path.join(HERE, "PROVENANCE.json"), "w") as fh:

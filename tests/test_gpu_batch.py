@@ -118,3 +118,43 @@ def test_get_config_batch_equals_sequential(device):
     for (c1, i1), (c2, i2) in zip(seq, bat):
         assert i1 == i2
         assert c1 == c2
+
+
+def test_get_config_batch_equals_sequential_zero_bandwidth(device):
+    """A continuous hyperparameter that never varied: bandwidth 0, so the host sampler's truncnorm
+    raises (scale 0) and every model-based call falls back to a random configuration (bohb.py:163-166).
+    The batch handles that per call: same results, same global RNG consumption as sequential calls."""
+    from hpbandster_amd import configspace as CS
+    from hpbandster_amd.config_generators import BOHB
+
+    def make():
+        space = CS.ConfigurationSpace(seed=5)
+        for i in range(3):
+            space.add_hyperparameter(CS.UniformFloatHyperparameter("x%d" % i, lower=0, upper=1))
+        cg = BOHB(space, device=device, random_fraction=0.25, num_samples=16)
+        rs = np.random.RandomState(3)
+
+        class Job(object):
+            pass
+
+        for k in range(30):
+            cfg = {"x0": 0.5, "x1": float(rs.rand()), "x2": float(rs.rand())}
+            j = Job()
+            j.id, j.kwargs, j.exception, j.timestamps = (0, 0, k), {"config": cfg, "budget": 1.0}, None, {}
+            j.result = {"loss": float(rs.rand()), "info": None}
+            cg.new_result(j)
+        assert cg.kde_models[1.0].good.bw[0] == 0.0
+        return cg, space
+
+    cg, space = make()
+    np.random.seed(17)
+    space.seed(23)
+    seq = [cg.get_config(1.0) for _ in range(12)]
+    state = np.random.get_state()[1].copy()
+    cg, space = make()
+    np.random.seed(17)
+    space.seed(23)
+    bat = cg.get_config_batch(1.0, 12)
+    np.testing.assert_array_equal(np.random.get_state()[1], state)
+    assert seq == bat
+    assert not any(i["model_based_pick"] for _, i in bat)

@@ -352,3 +352,35 @@ def test_near_ties_pinned_and_process(device, name):
     rb = pair.acquire_batch(C, C.shape[0], ties="process")
     assert rb[0].index == want
     assert pair.acquire_batch(C, C.shape[0])[0].index == c["chosen"]
+
+
+@pytest.mark.parametrize("dc,du,lev", [(70, 0, 0), (3, 33, 3)])
+def test_exact_only_outside_scoring_buckets(device, dc, du, lev):
+    """Spaces beyond the fp32 scoring buckets (> 64 continuous or > 32 categorical dims) run
+    exact-only: every candidate re-scored in fp64 -- pick and pdfs equal the C oracle's exact
+    (reference-arithmetic) ones; refit through the one-call path; batched too."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    from oracle import c_oracle
+    D = dc + du
+    X = S.make_observations(4 * D + 40, dc, du, lev)
+    L = S.make_losses(X.shape[0])
+    vt = S.var_type_string(dc, du)
+    pair = kde.fit_pair(X, L, vt, D + 1, device=device)
+    assert pair.good.exact_only and pair.bad.exact_only
+    C = S.make_candidates(300, dc, du, lev)
+    near = X[pair.good.rows_dev.cpu().numpy()[:50]].copy()  # near the good observations
+    near[:, :dc] += 1e-3
+    C[:near.shape[0]] = near
+    res, logl, logg = pair.acquire(C, logs=True)
+    l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+    g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    want, scores = O.select(l, g)
+    assert res.index == want and res.shortlist == C.shape[0]
+    if want >= 0:
+        assert (res.pdf_l, res.pdf_g) == (l[want], g[want])
+    with np.errstate(divide="ignore"):
+        np.testing.assert_allclose(logl, np.log(l).astype(np.float32), rtol=1e-6)
+    rb = pair.acquire_batch(C, 100)
+    for b in range(3):
+        assert rb[b].index == O.py_argmin(scores[100 * b:100 * b + 100])
