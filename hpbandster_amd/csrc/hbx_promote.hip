@@ -77,28 +77,37 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
 }
 
 // Brackets of up to 1024 configurations without a sorted order requested: the mask needs only the
-// k-th smallest (key, position) of the bracket, found by a bitwise radix select in registers -- O(n)
-// per bracket instead of the O(n log^2 n) sort.  One wave per bracket; element i = 64 r + lane sits in
-// register r of lane `lane` (coalesced loads, 64 consecutive mask bytes per store).  Each lane keeps
-// its 16 elements' state as bit masks (bit r): `alive` = still in the bucket holding the k-th element,
-// `less` = known to rank below it.  Bits are resolved from the highest bit where the finite keys
-// differ downwards; a pass counts the bucket's elements with a 0 at that bit (one wave sum) and keeps
-// the half that holds the k-th.  It stops as soon as the whole bucket advances; keys equal in all 64
-// bits are ranked by position (stable), as sh_promote_wave_kernel / sh_promote_kernel rank them.
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// k-th smallest (key, position) of the bracket, found by a bitwise radix select -- O(n) per bracket
+// instead of the O(n log^2 n) sort.  One wave per bracket; element i = 64 r + lane sits in register r
+// of lane `lane` (coalesced loads issued together, 64 consecutive mask bytes per store).
+//   Bits are resolved from the highest bit where the finite keys differ downwards: a pass counts the
+// bucket's elements (those matching every bit resolved so far) with a 0 at the bit and keeps the half
+// holding the k-th.  While the bucket is large each lane tracks its 16 elements as a bit mask and a
+// pass costs 16 bit extractions and one DPP wave sum; once it holds <= 64 keys they are compacted into
+// one per lane (LDS, position order) and a pass is one compare and one ballot.  It stops as soon as
+// the whole bucket advances.  The mask is then one masked 64-bit compare per element against the
+// resolved prefix; keys equal in all 64 bits are ranked by position (stable), as sh_promote_wave_kernel
+// and sh_promote_kernel rank them.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  // every lane of a 16-lane row now holds the row's value: combine the four rows (scalar, uniform)
+  return op(op((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+            op((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
-__device__ __forceinline__ uint32_t wave_and(uint32_t v) {
+struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpAnd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a & b; } };
+struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+
+// bit `sh` of each of the 16 words, gathered into a 16-bit mask (bit r from word r): 2 VALU per word
+__device__ __forceinline__ uint32_t gather_bit(const uint32_t (&w)[PW_PER_LANE], int sh) {
+  uint32_t m = 0u;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v &= (uint32_t)__shfl_xor((int)v, o);
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
-  return v;
+  for (int r = 0; r < PW_PER_LANE; ++r) m |= __builtin_amdgcn_ubfe(w[r], (uint32_t)sh, 1u) << r;
+  return m;
 }
 
 __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict__ loss,
@@ -107,71 +116,131 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
                                                         uint8_t* __restrict__ advance,
                                                         int64_t* __restrict__ n_advance) {
   constexpr int R = PW_PER_LANE;  // 16 registers x 64 lanes = 1024 elements
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint64_t cbuf[4][64];  // per wave: the compacted bucket
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wv;
   if (b >= B) return;  // whole wave
   const int64_t s = seg_off[b];
   const int n = (int)(seg_off[b + 1] - s);
+  if (n <= 0) {
+    if (lane == 0 && n_advance) n_advance[b] = 0;
+    return;
+  }
+  // all 16 loads issued before any is used (unconditional: indices past n re-read the last element)
+  double v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = loss[s + min(64 * r + lane, n - 1)];
+  // order-preserving keys (hbx_d2ord; -0.0 + 0.0 = +0.0 merges the zeros), the finite mask (CRASHED,
+  // i.e. non-finite, entries are never ranked) and the AND / OR of the finite keys' high words
   uint32_t khi[R], klo[R];
-  uint32_t alive = 0;
-  uint32_t andh = ~0u, andl = ~0u, orh = 0u, orl = 0u;
+  uint32_t fin = 0u, andh = ~0u, orh = 0u;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int i = 64 * r + lane;
-    const double v = i < n ? loss[s + i] : 0.0;
-    const bool fin = i < n && (v - v == 0.0);  // CRASHED (non-finite) entries are never ranked
-    const uint64_t key = fin ? hbx_d2ord(v) : 0ull;
-    khi[r] = (uint32_t)(key >> 32);
-    klo[r] = (uint32_t)key;
-    if (fin) {
-      alive |= 1u << r;
-      andh &= khi[r];
-      andl &= klo[r];
-      orh |= khi[r];
-      orl |= klo[r];
-    }
+    const double z = v[r] + 0.0;
+    const uint32_t hi = (uint32_t)(__double_as_longlong(z) >> 32), lo = (uint32_t)__double_as_longlong(z);
+    const uint32_t sg = (uint32_t)((int32_t)hi >> 31);
+    khi[r] = hi ^ (sg | 0x80000000u);
+    klo[r] = lo ^ sg;
+    const bool f = (64 * r + lane < n) && __builtin_isfinite(v[r]);
+    fin |= (f ? 1u : 0u) << r;
+    andh &= f ? khi[r] : ~0u;
+    orh |= f ? khi[r] : 0u;
   }
-  const int nfin = wave_sum(__popc(alive));
+  const int nfin = (int)wave_reduce_dpp((uint32_t)__popc(fin), OpAdd());
   // rank < k advances: the first kk ranks, kk = min(nfin, ceil(k)) (k > 0; NaN or k <= 0: none)
   const double kb = k[b];
   const int kk = kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0;
   uint32_t adv;
   if (kk == nfin) {
-    adv = alive;
+    adv = fin;
   } else if (kk == 0) {
     adv = 0u;
   } else {
-    uint32_t less = 0u;
-    int need = kk, cnt = nfin;
-    // bits above the highest one where the finite keys differ are common to all of them
-    const uint32_t dh = wave_or(orh) ^ wave_and(andh), dl = wave_or(orl) ^ wave_and(andl);
-    const int top = dh ? 63 - __clz((int)dh) : (dl ? 31 - __clz((int)dl) : -1);
-    for (int bit = top; bit >= 0 && cnt != need; --bit) {
-      uint32_t ones = 0u;
-      const int sh = bit & 31;
+    // bits above the highest one where the finite keys differ are common to all of them: resolved
+    const uint32_t ah = wave_reduce_dpp(andh, OpAnd());
+    const uint32_t dh = wave_reduce_dpp(orh, OpOr()) ^ ah;
+    uint32_t al = 0u, dl = 0u;
+    if (dh == 0u) {  // equal high words: the low words decide (rare)
+      uint32_t andl = ~0u, orl = 0u;
 #pragma unroll
-      for (int r = 0; r < R; ++r) ones |= (((bit >= 32 ? khi[r] : klo[r]) >> sh) & 1u) << r;
+      for (int r = 0; r < R; ++r) {
+        const bool f = (fin >> r) & 1u;
+        andl &= f ? klo[r] : ~0u;
+        orl |= f ? klo[r] : 0u;
+      }
+      al = wave_reduce_dpp(andl, OpAnd());
+      dl = wave_reduce_dpp(orl, OpOr()) ^ al;
+    }
+    int bit = dh ? 63 - __clz((int)dh) : (dl ? 31 - __clz((int)dl) : -1);
+    uint32_t ph = ah, pl = al;  // the resolved prefix (bits above `bit`) of the k-th key
+    int need = kk, cnt = nfin;
+    uint32_t alive = fin;
+    // phase 1: the bucket as per-lane bit masks
+    for (; bit >= 0 && cnt != need && cnt > 64; --bit) {
+      const uint32_t ones = bit >= 32 ? gather_bit(khi, bit - 32) : gather_bit(klo, bit);
       const uint32_t zero = alive & ~ones;
-      const int c0 = wave_sum(__popc(zero));
+      const int c0 = (int)wave_reduce_dpp((uint32_t)__popc(zero), OpAdd());
       if (need <= c0) {
         alive = zero;
         cnt = c0;
       } else {
-        less |= zero;
         alive &= ones;
         need -= c0;
         cnt -= c0;
+        if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
       }
     }
-    // the `need` first bucket elements by position (all of them when cnt == need)
-    adv = less;
-    int taken = 0;
+    if (bit >= 0 && cnt != need) {
+      // phase 2: compact the <= 64 bucket keys into one per lane, in position order
+      int base = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint64_t m = __ballot((alive >> r) & 1u);
-      const int before = __popcll(m & ((1ull << lane) - 1ull));
-      if (((alive >> r) & 1u) && taken + before < need) adv |= 1u << r;
-      taken += __popcll(m);
+      for (int r = 0; r < R; ++r) {
+        const bool a = (alive >> r) & 1u;
+        const uint64_t m = __ballot(a);
+        if (a) cbuf[wv][base + __popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)khi[r] << 32) | klo[r];
+        base += __popcll(m);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint64_t key1 = cbuf[wv][lane < cnt ? lane : 0];
+      bool a1 = lane < cnt;
+      for (; bit >= 0 && cnt != need; --bit) {
+        const bool one = (key1 >> bit) & 1ull;
+        const int c0 = __popcll(__ballot(a1 && !one));
+        if (need <= c0) {
+          a1 = a1 && !one;
+          cnt = c0;
+        } else {
+          a1 = a1 && one;
+          need -= c0;
+          cnt -= c0;
+          if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
+        }
+      }
+    }
+    // bits > bit are resolved: an element advances iff its key's resolved part is below the prefix,
+    // or equal and either the whole bucket advances (cnt == need) or -- keys equal in all 64 bits --
+    // it is among the first `need` of them by position
+    const uint64_t M = bit >= 63 ? 0ull : (bit < 0 ? ~0ull : ~((2ull << bit) - 1ull));
+    const uint64_t P = (((uint64_t)ph << 32) | pl) & M;
+    adv = 0u;
+    if (cnt == need) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) adv |= ((((uint64_t)khi[r] << 32) | klo[r]) & M) <= P ? (1u << r) : 0u;
+      adv &= fin;
+    } else {
+      int taken = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint64_t key = (((uint64_t)khi[r] << 32) | klo[r]) & M;
+        const bool f = (fin >> r) & 1u;
+        const bool eq = f && key == P;
+        const uint64_t m = __ballot(eq);
+        const bool take = (f && key < P) || (eq && taken + __popcll(m & ((1ull << lane) - 1ull)) < need);
+        taken += __popcll(m);
+        adv |= (take ? 1u : 0u) << r;
+      }
     }
   }
 #pragma unroll
