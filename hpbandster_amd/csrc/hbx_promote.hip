@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
 // Brackets of up to 1024 configurations without a sorted order requested: the mask needs only the
 // k-th smallest (key, position) of the bracket, found by a bitwise radix select -- O(n) per bracket
 // instead of the O(n log^2 n) sort.  One wave per bracket; element i = 64 r + lane sits in register r
-// of lane `lane` (coalesced loads issued together, 64 consecutive mask bytes per store).
+// of lane `lane` (coalesced buffer loads issued together, 64 consecutive mask bytes per store).
 //   Bits are resolved from the highest bit where the finite keys differ downwards: a pass counts the
 // bucket's elements (those matching every bit resolved so far) with a 0 at the bit and keeps the half
 // holding the k-th.  While the bucket is large each lane tracks its 16 elements as a bit mask and a
@@ -110,6 +110,8 @@ __device__ __forceinline__ uint32_t gather_bit(const uint32_t (&w)[PW_PER_LANE],
   return m;
 }
 
+constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (raw 32-bit data, range checked)
+
 __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict__ loss,
                                                         const int64_t* __restrict__ seg_off, int64_t B,
                                                         const double* __restrict__ k,
@@ -117,7 +119,8 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
                                                         int64_t* __restrict__ n_advance) {
   constexpr int R = PW_PER_LANE;  // 16 registers x 64 lanes = 1024 elements
   __shared__ uint64_t cbuf[4][64];  // per wave: the compacted bucket
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the wave index made visibly uniform: the bracket's bounds, k and buffer resources live in SGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t b = (int64_t)blockIdx.x * 4 + wv;
   if (b >= B) return;  // whole wave
   const int64_t s = seg_off[b];
@@ -126,10 +129,13 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
     if (lane == 0 && n_advance) n_advance[b] = 0;
     return;
   }
-  // all 16 loads issued before any is used (unconditional: indices past n re-read the last element)
+  // the bracket as buffer resources: loads past n return 0 and stores past n are dropped by the
+  // hardware range check, so all 16 loads (and stores) are unconditional, one address VGPR each
+  const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)(loss + s), (short)0, n * 8, kBufDword3);
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)(advance + s), (short)0, n, kBufDword3);
   double v[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) v[r] = loss[s + min(64 * r + lane, n - 1)];
+  for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane, 512 * r, 0));
   // order-preserving keys (hbx_d2ord; -0.0 + 0.0 = +0.0 merges the zeros), the finite mask (CRASHED,
   // i.e. non-finite, entries are never ranked) and the AND / OR of the finite keys' high words
   uint32_t khi[R], klo[R];
@@ -244,10 +250,7 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int i = 64 * r + lane;
-    if (i < n) advance[s + i] = (uint8_t)((adv >> r) & 1u);
-  }
+  for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((adv >> r) & 1u), ars, lane, 64 * r, 0);
   if (lane == 0 && n_advance) n_advance[b] = kk;
 }
 
