@@ -59,7 +59,8 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   static_assert(GP * 1024 == CHF * 4, "chunk must be a multiple of 1 KB");
   __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave made visibly uniform: LDS-DMA addresses, m0 and row bases are then SGPR arithmetic
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t cbase = ((int64_t)blk * HW + wave) * 16 * RT;
   const bool xpiece = wave < NX;  // this wave issues GL + 1 pieces per chunk
   const int n = P->n, dc = P->dc;
@@ -223,13 +224,21 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL * (PD - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
 
-  // MFMAs of one 16-observation column tile for every row tile
-  auto tile = [&](const float* buf, int jt, f32x4* acc, f32x4* accp) {
+  // B fragments of one 16-observation column tile (and, signed, its parity fragments)
+  constexpr int KPF = (SIGNED && KC > 0) ? KC : 1;
+  auto readb = [&](const float* buf, int jt, f16x8 (&b)[NSH], f16x8 (&bp)[KPF]) {
     const int jo = jt * 16 + ia;
     const _Float16* hb = (const _Float16*)(buf + OBS_CHUNK) + jo * KTP + 8 * kq;
-    f16x8 b[NSH];
 #pragma unroll
     for (int s = 0; s < NSH; ++s) b[s] = *(const f16x8*)(hb + 32 * s);
+    if constexpr (SIGNED) {
+      const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
+#pragma unroll
+      for (int s = 0; s < KC; ++s) bp[s] = *(const f16x8*)(pb + 32 * s);
+    }
+  };
+  // MFMAs of one column tile for every row tile
+  auto mfmas = [&](const f16x8 (&b)[NSH], const f16x8 (&bp)[KPF], f32x4* acc, f32x4* accp) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][0], b[0], ciq[r], 0, 0, 0);
     constexpr int NDENSE = SP ? NSC : NSH;
@@ -250,17 +259,14 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
           acc[r] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(asp[r][s], b16, acc[r], aidx[r][s], 0, 0);
       }
     }
-    if (SIGNED) {
-      const _Float16* pb = (const _Float16*)(buf + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
+    if constexpr (SIGNED) {
 #pragma unroll
       for (int r = 0; r < RT; ++r) accp[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KC; ++s) {
-        const f16x8 bp = *(const f16x8*)(pb + 32 * s);
+      for (int s = 0; s < KC; ++s)
 #pragma unroll
         for (int r = 0; r < RT; ++r)
-          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp, accp[r], 0, 0, 0);
-      }
+          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp[s], accp[r], 0, 0, 0);
     }
   };
 
@@ -271,6 +277,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   // later chunks can exceed the probe's maximum; a sum that leaves [2^-64, 2^100] still takes the
   // rescue.  Costs one chunk of MFMAs (no exp2) per block.
   float dl[RT][4];
+  f16x8 bA[NSH], bB[NSH], bpA[KPF], bpB[KPF];
   {
     f32x4 acc[RT], accp[RT];
     float mx[RT][4];
@@ -280,7 +287,8 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       for (int q = 0; q < 4; ++q) mx[r][q] = -INFINITY;
 #pragma unroll
     for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
-      tile(lds, jt, acc, accp);
+      readb(lds, jt, bA, bpA);
+      mfmas(bA, bpA, acc, accp);
 #pragma unroll
       for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -298,46 +306,37 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       }
   }
 
-  for (int c = 0; c < nchunks; ++c) {
-    const float* buf = lds + (c % NBUF) * CHF;
-    issue(c + PD, (c + PD) % NBUF);  // its buffer was last read in iteration c-1
-    float Sb[RT][4], Snb[RT][4];
+  // Main loop, software-pipelined across tiles and chunks.  Phase t of iteration c runs the MFMAs of
+  // tile t of chunk c on B fragments read one phase earlier, issues the LDS reads of the next tile
+  // (tile 0 of chunk c+1 in phase 3) and, beside the MFMAs, the exp2/sum epilogue of the previous tile
+  // (tile 3 of chunk c-1 in phase 0).  Every MFMA thus waits on LDS reads issued a whole phase
+  // before, and every exp2 sits between MFMAs.  The chunk c+1 barrier comes before phase 3 (whose
+  // reads need chunk c+1); at that point all reads of buffer c have retired, so the LDS-DMA issued at
+  // the top of iteration c+1 into that buffer is safe.  Per-chunk partial sums (Sb: four terms) and
+  // their order into S are those of the unpipelined loop.
+  f32x4 accA[RT], accB[RT], accpA[RT], accpB[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    accB[r] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // exp2 -> 0: the first epilogue adds nothing
+    accpB[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float Sb[RT][4], Snb[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
+  // epilogue of one tile: first = the tile opens a chunk's partial sum
+  auto epi = [&](const f32x4* cur, const f32x4* curp, bool first) {
 #pragma unroll
     for (int r = 0; r < RT; ++r)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
-    // software pipeline: MFMAs of tile jt+1 are issued before the exp2/sum epilogue of tile jt
-    f32x4 acc[RT], accp[RT];
-    tile(buf, 0, acc, accp);
-#pragma unroll
-    for (int jt = 0; jt < OBS_CHUNK / 16; ++jt) {
-      f32x4 cur[RT], curp[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        cur[r] = acc[r];
-        curp[r] = accp[r];
+      for (int q = 0; q < 4; ++q) {
+        const float e = __builtin_amdgcn_exp2f(cur[r][q]);
+        Sb[r][q] = first ? e : Sb[r][q] + e;
+        if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, first ? 0.f : Snb[r][q]);
       }
-      if (jt + 1 < OBS_CHUNK / 16) tile(buf, jt + 1, acc, accp);
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float e = __builtin_amdgcn_exp2f(cur[r][q]);
-          Sb[r][q] = jt == 0 ? e : Sb[r][q] + e;
-          if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, jt == 0 ? 0.f : Snb[r][q]);
-        }
-      if (!SIGNED && jt + 1 < OBS_CHUNK / 16) {
-        // interleave the exp2/sum epilogue of tile jt with the MFMAs of tile jt+1 (hipcc otherwise
-        // emits all MFMAs of the chunk back to back and the VALU work after them): the B-fragment
-        // reads first, a few exps while they land, then one MFMA / one or two VALU ops alternating
-        __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);  // DS_READ: B fragments of tile jt+1
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);    // VALU
-        if (jt == 0)
-          SgbAlternate<0, NMT * RT, 4 * RT - 2>::run();  // exp2 only (no running sum yet)
-        else
-          SgbAlternate<0, NMT * RT, 8 * RT - 2>::run();  // exp2 + add
-      }
-    }
+  };
+  auto close_chunk = [&]() {
 #pragma unroll
     for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -345,14 +344,51 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
         S[r][q] += Sb[r][q];
         if (SIGNED) Sn[r][q] += Snb[r][q];
       }
-    // chunk c+1 complete for this wave (PD-1 chunks stay in flight), this wave's reads of buffer c
-    // retired; then the barrier makes chunk c+1 visible to (and buffer c free from) every wave
+  };
+  // one MFMA, then one or two VALU (an exp2 or an add), alternating; the B-fragment reads first
+  auto schedule = [&]() {
+    if constexpr (!SIGNED) {
+      __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);  // DS_READ: B fragments of the next tile
+      SgbAlternate<0, NMT * RT, 8 * RT>::run();            // exp2 + add of the previous tile
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  readb(lds, 0, bA, bpA);  // tile 0 of chunk 0 (buffer 0)
+  for (int c = 0; c < nchunks; ++c) {
+    const float* buf = lds + (c % NBUF) * CHF;
+    const float* nbuf = lds + ((c + 1) % NBUF) * CHF;
+    issue(c + PD, (c + PD) % NBUF);  // its buffer's reads all retired before the previous barrier
+    // phase 0: MFMAs of tile 0 (bA); reads of tile 1 -> bB; epilogue of tile 3 of chunk c-1
+    readb(buf, 1, bB, bpB);
+    mfmas(bA, bpA, accA, accpA);
+    epi(accB, accpB, false);
+    close_chunk();
+    schedule();
+    // phase 1
+    readb(buf, 2, bA, bpA);
+    mfmas(bB, bpB, accB, accpB);
+    epi(accA, accpA, true);
+    schedule();
+    // phase 2
+    readb(buf, 3, bB, bpB);
+    mfmas(bA, bpA, accA, accpA);
+    epi(accB, accpB, false);
+    schedule();
+    // chunk c+1 complete for this wave (PD-1 chunks stay in flight) and every read of buffer c
+    // retired; the barrier makes chunk c+1 visible to every wave
     if (NX && xpiece)
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((GL + 1) * (PD - 1)) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
     __builtin_amdgcn_s_barrier();
+    // phase 3: MFMAs of tile 3 (bB); reads of tile 0 of chunk c+1 -> bA
+    readb(nbuf, 0, bA, bpA);
+    mfmas(bB, bpB, accB, accpB);
+    epi(accA, accpA, false);
+    schedule();
   }
+  epi(accB, accpB, false);  // tile 3 of the last chunk
+  close_chunk();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 #pragma unroll
   for (int r = 0; r < RT; ++r)

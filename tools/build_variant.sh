@@ -10,5 +10,5 @@ SRC=$2
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/hpbandster_amd/csrc -I $R/include -Wno-unused-result -munsafe-fp-atomics -ffp-contract=off -fno-slp-vectorize"
 /opt/rocm/bin/hipcc $FL $3 -c $R/hpbandster_amd/csrc/$SRC -o $OUT/$1.o
 objs=$(ls $OBJ/*.o | grep -v "/$SRC.o")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libhbx_$1.so $objs $OUT/$1.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libhbx_$1.so $objs $OUT/$1.o -L/opt/rocm/lib -lrccl
 echo $OUT/libhbx_$1.so
