@@ -88,8 +88,15 @@ struct KdeParams {
 
 // A parameter buffer (hbx_kde_param_bytes()) is the KdeParams block followed by a staging area for
 // hbx_kde_prepare's host inputs (bandwidths, level counts) and its info record.
+// After the staging area: per-dim column statistics of the KDE's observations (ColStats), written by
+// the first preparation kernel and read by the parameter kernel.
 #define HBX_PARAM_STAGE ((sizeof(KdeParams) + 255) & ~(size_t)255)
-#define HBX_PARAM_BYTES (HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 64)
+#define HBX_COLSTATS_OFF (HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 64)
+#define HBX_PARAM_BYTES (HBX_COLSTATS_OFF + 8 * HBX_MAX_D + 4 * HBX_MAX_D)
+struct ColStats {
+  double mean[HBX_MAX_D];      // continuous dim: mean of the column (any summation order)
+  int32_t maxcode[HBX_MAX_D];  // categorical dim: largest code, -1 when a code is not an integer in [0, 1024)
+};
 
 // Per-candidate output of the fp32 log-domain scoring kernel, one per KDE.
 struct KdeEst {
@@ -130,3 +137,20 @@ __device__ __forceinline__ uint64_t hbx_d2ord(double d) {
   uint64_t u = (uint64_t)__double_as_longlong(d);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
+
+// Wave-wide reduction of a 32-bit value (DPP within rows of 16 lanes, then the four rows combined in
+// scalar registers): every lane gets the result.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  // every lane of a 16-lane row now holds the row's value: combine the four rows (scalar, uniform)
+  return op(op((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+            op((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpAnd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a & b; } };
+struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+struct OpMax { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };

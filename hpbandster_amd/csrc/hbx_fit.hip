@@ -233,11 +233,44 @@ __global__ __launch_bounds__(128) void kde_fit_stats_kernel(
 }
 
 // One workgroup per (segment, set, dim) -- used when there are too few columns to fill the GPU with
-// one thread each (a single BOHB refit: 2 x D columns).  The gathers of a column are staged in LDS by
-// the whole block; thread 0 then adds them strictly in row order (np.std's axis-0 reduction order,
-// D > 1), so the result is bit-identical to the thread-per-column kernel.  Level counts come from a
-// block-wide bitmap (order-independent).
-#define FIT_TILE 4096
+// one thread each (a single BOHB refit: 2 x D columns).  The column is gathered into LDS by the whole
+// block (once: up to FIT_TILE rows stay resident for both passes); thread 0 then adds strictly in row
+// order (np.std's axis-0 reduction order, D > 1), so the result is bit-identical to the
+// thread-per-column kernel.  Level counts come from a block-wide bitmap (order-independent).
+#define FIT_TILE 16384
+// numpy's axis-0 order: one dependent add per row.  The LDS reads of the next 32 rows are issued
+// before the adds of the current 32, so the read latency hides behind the add chain (same additions,
+// same order).  SQ: add (v - mean)^2.
+template <bool SQ>
+__device__ __forceinline__ double fit_chain(const double* v, int m, double acc, double mean) {
+  auto val = [&](double x) {
+    if (SQ) {
+      const double q = x - mean;
+      return q * q;
+    }
+    return x;
+  };
+  const int m32 = m & ~31;
+  if (m32 > 0) {
+    double r[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r[k] = v[k];
+    for (int i = 32; i < m32; i += 32) {
+      double nx[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) nx[k] = v[i + k];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) acc = acc + val(r[k]);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) r[k] = nx[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) acc = acc + val(r[k]);
+  }
+  for (int i = m32; i < m; ++i) acc = acc + val(v[i]);
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void kde_fit_col_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off,
     const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
@@ -266,52 +299,53 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
   }
   const int64_t* ord = order + s0 + (good ? 0 : (len - ns));
   const double* Xs = X + s0 * (int64_t)D;
+  const bool cat = vartype[d] != 0;
   if (threadIdx.x < 32) bits[threadIdx.x] = 0u;
   if (threadIdx.x == 0) bad_code = 0;
-  double mean = 0.0;
-  for (int pass = 0; pass < 2; ++pass) {
-    double acc = 0.0;  // thread 0
-    for (int64_t c = 0; c < ns; c += FIT_TILE) {
-      const int m = (int)((ns - c) < FIT_TILE ? (ns - c) : FIT_TILE);
-      __syncthreads();
-      for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        const double x = Xs[ord[c + i] * (int64_t)D + d];
-        if (pass == 0) {
-          v[i] = x;
-          if (vartype[d] != 0) {
-            const int iv = (int)x;
-            if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) bad_code = 1;
-            else atomicOr(&bits[iv >> 5], 1u << (iv & 31));
-          }
-        } else {
-          const double q = x - mean;
-          v[i] = q * q;
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        // numpy's axis-0 order: one dependent add per row.  32 LDS reads are issued ahead of their
-        // adds so the read latency hides behind the add chain (same additions, same order).
-        int i = 0;
-        for (; i + 32 <= m; i += 32) {
-          double r[32];
-#pragma unroll
-          for (int k = 0; k < 32; ++k) r[k] = v[i + k];
-#pragma unroll
-          for (int k = 0; k < 32; ++k) acc = acc + r[k];
-        }
-        for (; i < m; ++i) acc = acc + v[i];
+  // gather rows [c, c + m) of the column into v (pass 0 also marks the codes; pass 1 re-gathers only
+  // when the column exceeds one tile)
+  auto gather = [&](int64_t c, int m, bool codes) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+      const double x = Xs[ord[c + i] * (int64_t)D + d];
+      v[i] = x;
+      if (codes && cat) {
+        const int iv = (int)x;
+        if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) bad_code = 1;
+        else atomicOr(&bits[iv >> 5], 1u << (iv & 31));
       }
     }
-    if (threadIdx.x == 0) red = acc;
     __syncthreads();
-    if (pass == 0) mean = red / (double)ns;
+  };
+  double acc = 0.0;  // thread 0
+  for (int64_t c = 0; c < ns; c += FIT_TILE) {
+    const int m = (int)((ns - c) < FIT_TILE ? (ns - c) : FIT_TILE);
+    gather(c, m, true);
+    if (threadIdx.x == 0) acc = fit_chain<false>(v, m, acc, 0.0);
+  }
+  if (threadIdx.x == 0) red = acc;
+  __syncthreads();
+  const double mean = red / (double)ns;
+  acc = 0.0;
+  if (ns <= FIT_TILE) {  // the column is still in LDS: squared deviations in place, then the chain
+    for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+      const double q = v[i] - mean;
+      v[i] = q * q;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) acc = fit_chain<false>(v, (int)ns, 0.0, 0.0);
+  } else {
+    for (int64_t c = 0; c < ns; c += FIT_TILE) {
+      const int m = (int)((ns - c) < FIT_TILE ? (ns - c) : FIT_TILE);
+      gather(c, m, false);
+      if (threadIdx.x == 0) acc = fit_chain<true>(v, m, acc, mean);
+    }
   }
   if (threadIdx.x == 0) {
-    const double var = red / (double)ns;
+    const double var = acc / (double)ns;
     *bwo = (1.06 * sqrt(var)) * (good ? fac_good[b] : fac_bad[b]);
     int cnt = 0;
-    if (vartype[d] != 0) {
+    if (cat) {
       for (int w = 0; w < 32; ++w) cnt += __popc(bits[w]);
       if (bad_code) cnt = -1;
     }

@@ -70,24 +70,80 @@ struct PrepSet {
 
 __device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
 
-// The parameter block of one KDE (one workgroup): per-dim scales and log-ratios (thread 0, serial in
-// dim order), the largest observed code of every active categorical dim (whole block), then the
-// one-hot layout and the kernel mode.
+__device__ __forceinline__ ColStats* col_stats(KdeParams* P) { return (ColStats*)((char*)P + HBX_COLSTATS_OFF); }
+
+// Column statistics of every (KDE, dim), one workgroup each (blocks [k*D, (k+1)*D) belong to KDE k):
+// the mean of a continuous column (the centre of the scaled coordinates: any finite centre is correct
+// -- table and candidates use the same one -- it only keeps the fp32 expansion well conditioned, so the
+// summation order is free) and the largest code of a categorical column.
+__global__ __launch_bounds__(256) void kde_colstats_kernel(PrepSet ps) {
+  const PrepArgs& A = (int)blockIdx.x >= ps.k[0].D ? ps.k[1] : ps.k[0];
+  const int d = blockIdx.x % ps.k[0].D;
+  const int n = A.n, D = A.D;
+  ColStats* cs = col_stats(A.P);
+  __shared__ double red[4];
+  __shared__ int mred[4];
+  if (!prep_cat(A, d)) {
+    double acc = 0.0;
+    for (int j = threadIdx.x; j < n; j += 256) acc += A.X[A.rows[j] * (int64_t)D + d];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) cs->mean[d] = ((red[0] + red[1]) + (red[2] + red[3])) / (double)n;
+  } else {
+    int m = -1;
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const double v = A.X[A.rows[j] * (int64_t)D + d];
+      m = max(m, (!(v >= 0.0 && v < 1024.0) || v != floor(v)) ? 100000 : (int)v);
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) mred[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int mm = max(max(mred[0], mred[1]), max(mred[2], mred[3]));
+      cs->maxcode[d] = mm >= 100000 ? -1 : mm;
+    }
+  }
+}
+
+// The parameter block of one KDE (one workgroup): the per-dim transcendentals in parallel, then the
+// scales, log-ratios and sums (thread 0, serial in dim order), the one-hot layout and the kernel mode.
 __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   const PrepArgs& A = blockIdx.x ? ps.k[1] : ps.k[0];  // (no dynamic index into the kernel arguments)
   KdeParams* P = A.P;
+  const ColStats* cs = col_stats(P);
   const int D = A.D, n = A.n;
   uint32_t* pz = (uint32_t*)P;
   for (int i = threadIdx.x; i < (int)(sizeof(KdeParams) / 4); i += blockDim.x) pz[i] = 0u;
+  // per dim: continuous -> ln h and the scale; categorical -> log2 of the match / mismatch factors
+  // (inputs staged in LDS too: thread 0's serial walk below stores to P, and global loads behind
+  // global stores it may not reorder would each wait a full memory latency)
+  __shared__ double s_t0[HBX_MAX_D], s_t1[HBX_MAX_D], s_h[HBX_MAX_D], s_mean[HBX_MAX_D];
+  __shared__ int32_t s_c[HBX_MAX_D], s_maxc[HBX_MAX_D], s_cm[HBX_MAX_D], s_cd[HBX_MAX_D];
+  __shared__ int32_t s_du, s_dcp, s_dup, s_exo, s_neg;
+  const double LOG2E = 1.4426950408889634;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const double h = A.bw[d];
+    const int c = A.nlev[d];
+    s_h[d] = h;
+    s_c[d] = c;
+    s_mean[d] = cs->mean[d];
+    s_maxc[d] = cs->maxcode[d];
+    if (!prep_cat(A, d)) {
+      s_t0[d] = (h > 0.0) ? log(h) : 0.0;
+      s_t1[d] = (h > 0.0) ? sqrt(LOG2E / 2.0) / h : 0.0;
+    } else {
+      const double a = 1.0 - h, b = h / (double)(c - 1);
+      s_t0[d] = log2(b);
+      s_t1[d] = (a == 0.0) ? -INFINITY : log2(fabs(a));
+    }
+  }
   __syncthreads();
-  __shared__ int s_du;
-  __shared__ int s_catdim[HBX_MAX_D];
-  __shared__ int red[256];
   if (threadIdx.x == 0) {
-    const double LOG2E = 1.4426950408889634;
     double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
     float sad = 0.f;
     int dc = 0, du = 0, nconst = 0, dc_tot = 0, du_tot = 0;
+    s_neg = 0;
     for (int d = 0; d < D; ++d) (prep_cat(A, d) ? du_tot : dc_tot)++;
     int dcp, dup;
     bucket_dims(dc_tot, du_tot, &dcp, &dup);
@@ -95,27 +151,30 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     P->D = D;
     P->dc_pad = dcp;
     P->du_pad = dup;
-    P->exact_only = (dcp < 0 || dup < 0) ? 1 : 0;
-    P->stride = P->exact_only ? 0 : table_stride(dcp, dup);
+    const int exo = (dcp < 0 || dup < 0) ? 1 : 0;
+    P->exact_only = exo;
+    P->stride = exo ? 0 : table_stride(dcp, dup);
     for (int d = 0; d < D; ++d) {
-      const double h = A.bw[d];
+      const double h = s_h[d];
       const bool cat = prep_cat(A, d);
       P->vartype[d] = cat ? 1 : 0;
-      P->nlev[d] = A.nlev[d];
+      P->nlev[d] = s_c[d];
       P->bw[d] = h;
       if (!cat) {
         const int k = dc++;
         P->cont_dim[k] = d;
+        const double m = s_mean[d];
+        P->center[k] = (m == m && m - m == 0.0) ? m : 0.0;
         prod_bw_c *= h;  // np.prod(bw[iscontinuous]), sequential in dim order
         if (!(h > 0.0)) {
           P->nan_all = 1;  // exp(-0/0) * ... / 0 -> NaN for every candidate
           P->cont_scale[k] = 0.0;
         } else {
-          P->cont_scale[k] = sqrt(LOG2E / 2.0) / h;
-          sum_ln_h += log(h);
+          P->cont_scale[k] = s_t1[d];
+          sum_ln_h += s_t0[d];
         }
       } else {
-        const int c = A.nlev[d];
+        const int c = s_c[d];
         if (c == 1 && h == 0.0) {  // single observed level: match -> 1, mismatch -> 0/0 = NaN
           P->const_dim[nconst++] = d;
           continue;
@@ -124,26 +183,33 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
           P->unsupported = 1;
           continue;
         }
-        const double a = 1.0 - h, b = h / (double)(c - 1);
-        const double lb = log2(b);
-        const double la = (a == 0.0) ? -INFINITY : log2(fabs(a));
+        const double a = 1.0 - h;
+        const double lb = s_t0[d], la = s_t1[d];
         const int u = du++;
         P->cat_dim[u] = d;
-        s_catdim[u] = d;
+        P->cat_maxcode[u] = s_maxc[d];
+        s_cm[u] = s_maxc[d];
+        s_cd[u] = d;
         m0 += (la > lb) ? la : lb;
         lb_sum += lb;
         if (a == 0.0) {
           P->cat_delta[u] = -1e30f;
         } else {
-          P->cat_delta[u] = (float)(la - lb);
-          sad += fabsf(P->cat_delta[u]);
+          const float dl = (float)(la - lb);
+          P->cat_delta[u] = dl;
+          sad += fabsf(dl);
         }
         P->cat_negf[u] = (a < 0.0) ? 1.f : 0.f;
         if (a < 0.0) P->has_neg = 1;
+        if (a < 0.0) s_neg = 1;
       }
     }
     P->dc = dc;
     P->du = du;
+    s_du = du;
+    s_dcp = dcp;
+    s_dup = dup;
+    s_exo = exo;
     P->nconst = nconst;
     P->m0_log2 = m0;
     P->lb_sum = lb_sum;
@@ -152,26 +218,6 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     P->log_norm = -log((double)n) - sum_ln_h - 0.5 * (double)dc * log(2.0 * M_PI) + m0 * M_LN2;
     P->X = A.X;
     P->rows = A.rows;
-    s_du = du;
-  }
-  __syncthreads();
-  // largest observed code per active categorical dim; -1 if some code is not an integer in [0, 1024)
-  for (int u = 0; u < s_du; ++u) {
-    const int d = s_catdim[u];
-    int m = -1, bad = 0;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const double v = A.X[A.rows[j] * (int64_t)D + d];
-      if (!(v >= 0.0 && v < 1024.0) || v != floor(v)) bad = 1;
-      else m = max(m, (int)v);
-    }
-    red[threadIdx.x] = bad ? 100000 : m;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) P->cat_maxcode[u] = red[0] >= 100000 ? -1 : red[0];
-    __syncthreads();
   }
   if (threadIdx.x != 0) return;
   for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
@@ -182,22 +228,25 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // [0, 1024) and the one-hot width sum(max code + 1) fits OH_MAX_KC K-steps; else VALU matching.
   // One-hot positions: every dim's block starts at an even position (a padding position, level -1,
   // never matches) -- the sparse matrix-core kernel relies on adjacent pairs never spanning dims.
-  const int du = P->du, dcp = P->dc_pad, dup = P->du_pad;
-  if (P->exact_only) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
+  // (read back from LDS, not from the P just written: see above)
+  const int du = s_du, dcp = s_dcp, dup = s_dup, has_neg = s_neg;
+  if (s_exo) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
     P->hmode = 0;
     P->nsc = 0;
     P->chunk_floats = 0;
     return;
   }
+  int kc = 0;
   if (du > 0) {
     int tot = 0;
     bool ok = true;
     for (int u = 0; u < du; ++u) {
-      if (P->cat_maxcode[u] < 0) ok = false;
-      else tot = ((tot + 1) & ~1) + P->cat_maxcode[u] + 1;
+      if (s_cm[u] < 0) ok = false;
+      else tot = ((tot + 1) & ~1) + s_cm[u] + 1;
     }
     if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
-      P->kc = (2 * tot + 31) / 32;
+      kc = (2 * tot + 31) / 32;
+      P->kc = kc;
       P->oh_total = tot;
       int t = 0;
       for (int u = 0; u < du; ++u) {
@@ -206,10 +255,10 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
           P->oh_level[t] = -1;
           ++t;
         }
-        for (int l = 0; l <= P->cat_maxcode[u]; ++l) {
+        for (int l = 0; l <= s_cm[u]; ++l) {
           P->oh_dim[t] = u;
           P->oh_level[t] = l;
-          P->oh_col[t] = P->cat_dim[u];
+          P->oh_col[t] = s_cd[u];
           P->oh_val[t] = (double)l;
           ++t;
         }
@@ -219,47 +268,26 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // continuous product on the f16 matrix cores (hi/lo split) when it has >= 8 dims (one full
   // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
   // otherwise the exact f32 MFMA product.  |C_j| beyond the f16 range is caught after the table.
-  const bool hm_ok = (du == 0 || P->kc > 0) && dcp >= 8;
-  P->hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
+  const bool hm_ok = (du == 0 || kc > 0) && dcp >= 8;
+  const int hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
+  P->hmode = hmode;
   P->nsc = nsc_of(dcp);
-  P->chunk_floats = P->hmode ? h_chunk_floats(dcp, P->kc, P->has_neg)
-                             : chunk_floats(dcp, dup, P->kc, P->kc ? P->has_neg : 0);
-}
-
-// Per continuous slot: mean of the KDE's data column, the centre of the scaled coordinates.  Any
-// finite centre is correct (table and candidates use the same one); it only keeps the fp32 expansion
-// well conditioned, so the summation order is free.  Blocks [k*D, (k+1)*D) belong to KDE k.
-__global__ __launch_bounds__(256) void kde_center_kernel(PrepSet ps) {
-  const PrepArgs& A = (int)blockIdx.x >= ps.k[0].D ? ps.k[1] : ps.k[0];
-  const int k = blockIdx.x % ps.k[0].D;
-  KdeParams* P = A.P;
-  if (k >= P->dc) return;
-  const int d = P->cont_dim[k];
-  const int n = A.n;
-  __shared__ double red[4];
-  double acc = 0.0;
-  for (int j = threadIdx.x; j < n; j += 256) acc += A.X[A.rows[j] * (int64_t)A.D + d];
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double m = ((red[0] + red[1]) + (red[2] + red[3])) / (double)n;
-    P->center[k] = (m == m && m - m == 0.0) ? m : 0.0;
-  }
+  P->chunk_floats = hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0);
 }
 
 // Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
 // C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per observation row (a serial walk over
 // its dims), 64-thread blocks so a 1e4-row table spreads over ~150 CUs.  `hm` / `chunk_f` select the
 // layout; |C_j| and |X'| maxima go to *cmax_acc / P->xmax.
-__device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
-                                               KdeParams* __restrict__ P, float* __restrict__ table, int j, bool hm,
-                                               int chunk_f, float* cmax_acc) {
+__device__ __forceinline__ void kde_table_body(const double* __restrict__ x, const KdeParams* __restrict__ P,
+                                               KdeParams* __restrict__ Pw, float* __restrict__ table, int j,
+                                               bool hm, int chunk_f, float* cmax_acc) {
+  // P: the parameters as read (an LDS copy); Pw: the global block, written (xmax, cmax / cmax2,
+  // const_level) -- fields disjoint from every one read here
   const int n = P->n;
   const int nslots = ((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK;
   const bool ok = j < n;
   const bool slot = j < nslots;
-  const double* x = X + (ok ? rows[j] : rows[0]) * (int64_t)D;
   const int dc = P->dc, du = P->du, dcp = P->dc_pad, dup = P->du_pad;
   const int KP = kp_of(dcp);
   float* ch = table + (int64_t)(j / OBS_CHUNK) * chunk_f;
@@ -267,6 +295,10 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int
   const int KTP = h_ktp(dcp, P->kc);
   _Float16* hrow = (_Float16*)(ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
+  // hmode rows are written 16 bytes (8 halves) at a time: two dims' h, l, h, l per store
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  h8 grp = {};
+#pragma unroll 8
   for (int k = 0; k < (hm ? dcp : KP - 2); ++k) {
     float v = 0.f;
     if (ok && k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
@@ -276,21 +308,24 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int
         const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
         const _Float16 h = (_Float16)vc;
         const _Float16 l = (_Float16)(vc - (float)h);
-        hrow[4 * k + 0] = h;
-        hrow[4 * k + 1] = l;
-        hrow[4 * k + 2] = h;
-        hrow[4 * k + 3] = l;
+        const int o = 4 * (k & 1);
+        grp[o + 0] = h;
+        grp[o + 1] = l;
+        grp[o + 2] = h;
+        grp[o + 3] = l;
+        if (k & 1) *(h8*)(hrow + 4 * (k - 1)) = grp;
       } else {
         ch[(2 + k) * KROW + jj] = v;
       }
     }
-    float a = fabsf(v);
-    for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
-    if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&P->xmax[k], __float_as_uint(a));
+    // |X'| maximum of the wave (non-negative floats order as their bit patterns)
+    const uint32_t a = wave_reduce_dpp(__float_as_uint(fabsf(v)), OpMax());
+    if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&Pw->xmax[k], a);
   }
-  if (hm && slot) {
-    for (int k = 4 * dcp; k < 32 * P->nsc; ++k) hrow[k] = (_Float16)0.f;
-    for (int k = 32 * (P->nsc + P->kc); k < KTP; ++k) hrow[k] = (_Float16)0.f;
+  const h8 z8 = {};
+  if (hm && slot) {  // dc_pad is a multiple of 8: the dims filled whole groups
+    for (int k = 4 * dcp; k < 32 * P->nsc; k += 8) *(h8*)(hrow + k) = z8;
+    for (int k = 32 * (P->nsc + P->kc); k < KTP; k += 8) *(h8*)(hrow + k) = z8;
   }
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
@@ -308,23 +343,29 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int
       oh = (_Float16*)(ch + KP * KROW) + jj * W;
       par = (_Float16*)(ch + KP * KROW) + OBS_CHUNK * W + jj * W;
     }
+    h8 og = {}, pg = {};
+#pragma unroll 8
     for (int k = 0; k < W; ++k) {
       const int t = k >> 1, p = k & 1;
       float v = 0.f, pv = 0.f;
       if (ok && t < P->oh_total) {
         const int u = P->oh_dim[t];
-        if (x[P->cat_dim[u]] == (double)P->oh_level[t]) {
+        if (x[P->oh_col[t]] == P->oh_val[t]) {  // oh_col = cat_dim[oh_dim], oh_val = the level
           const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
           const float hi = (float)(_Float16)dl;
           v = (p == 0) ? hi : (fabsf(dl) < 60000.f ? dl - hi : 0.f);
           pv = (p == 0 && P->cat_negf[u] != 0.f) ? 1.f : 0.f;
         }
       }
-      oh[k] = (_Float16)v;
-      if (P->has_neg) par[k] = (_Float16)pv;
+      og[k & 7] = (_Float16)v;
+      pg[k & 7] = (_Float16)pv;
+      if ((k & 7) == 7) {  // W is a multiple of 32 and every row 16-byte aligned
+        *(h8*)(oh + k - 7) = og;
+        if (P->has_neg) *(h8*)(par + k - 7) = pg;
+      }
     }
     if (hm && P->has_neg)
-      for (int k = W; k < h_kpp(P->kc); ++k) par[k] = (_Float16)0.f;
+      for (int k = W; k < h_kpp(P->kc); k += 8) *(h8*)(par + k) = z8;
   }
   C += P->lb_sum - P->m0_log2;
   const float Cf = ok ? (float)C : -1e30f;
@@ -348,11 +389,10 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ X, int
         for (int k = 0; k < KP; ++k) ch[k * KROW + OBS_CHUNK + jj] = 0.f;
     }
   }
-  float a = ok ? fabsf(Cf) : 0.f;
-  for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
-  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)cmax_acc, __float_as_uint(a));
+  const uint32_t a = wave_reduce_dpp(__float_as_uint(ok ? fabsf(Cf) : 0.f), OpMax());
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)cmax_acc, a);
   if (j == 0)
-    for (int q = 0; q < P->nconst; ++q) P->const_level[q] = x[P->const_dim[q]];
+    for (int q = 0; q < P->nconst; ++q) Pw->const_level[q] = x[P->const_dim[q]];
 }
 
 // f32-MFMA layout of an hmode KDE whose C_j left the f16 range of the three-piece split
@@ -360,16 +400,60 @@ __device__ __forceinline__ bool table_needs_rebuild(const KdeParams* P) { return
 
 // pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
 // block of a KDE that needs none exits at once)
+// The block's 64 observation rows are staged in LDS first (all loads in flight at once, coalesced
+// within each row) when D <= 64; the per-dim walk then reads LDS instead of waiting on one dependent
+// global load per dim.
+#define TABLE_STAGE_D 64
 __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0, float* table1, int pass) {
   const bool second = ps.nk > 1 && (int)blockIdx.x >= ps.k[0].nblk_table;
   const PrepArgs& A = ps.k[second ? 1 : 0];
   KdeParams* P = A.P;
-  const int j = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64 + threadIdx.x;
-  if (pass == 0) {
-    kde_table_body(A.X, A.D, A.rows, P, second ? table1 : table0, j, P->hmode != 0, P->chunk_floats, &P->cmax);
-  } else if (table_needs_rebuild(P)) {
-    kde_table_body(A.X, A.D, A.rows, P, second ? table1 : table0, j, false,
-                   chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0), &P->cmax2);
+  const int j0 = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64;
+  const int j = j0 + threadIdx.x;
+  if (pass != 0 && !table_needs_rebuild(P)) return;
+  // the parameter block is copied to LDS: loads from the global block the kernel also writes (atomics)
+  // would be vector loads, one memory latency each along the per-dim walk
+  __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
+  for (int i = threadIdx.x; i < (int)((sizeof(KdeParams) + 15) / 16); i += 64) pl[i] = ((const uint4*)P)[i];
+  __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
+  const int D = A.D, n = A.n;
+  const KdeParams* Pl = (const KdeParams*)pl;
+  float* tab = second ? table1 : table0;
+  // two inlined copies of the body: rows read from LDS (every load a ds_read) or from global memory
+  // (a generic pointer would make each row read wait for the outstanding table stores as well)
+  auto run = [&](const double* x) {
+    if (pass == 0)
+      kde_table_body(x, Pl, P, tab, j, Pl->hmode != 0, Pl->chunk_floats, &P->cmax);
+    else
+      kde_table_body(x, Pl, P, tab, j, false, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
+                     &P->cmax2);
+  };
+  if (D <= TABLE_STAGE_D) {
+    const int DS = D | 1;  // odd row stride: the 64 threads' reads of one dim hit distinct banks
+    __shared__ int64_t rs[64];
+    rs[threadIdx.x] = A.rows[j < n ? j : 0];
+    __syncthreads();
+    // 16 independent loads in flight per thread per batch (coalesced within each row); past the end
+    // the last element is re-read and re-stored (same value, same place)
+    const int tot = 64 * D;
+    for (int e0 = 0; e0 < tot; e0 += 16 * 64) {
+      double t[16];
+      int at[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = min(e0 + q * 64 + (int)threadIdx.x, tot - 1);
+        const int i = e / D, c = e - i * D;
+        at[q] = i * DS + c;
+        t[q] = A.X[rs[i] * (int64_t)D + c];
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) xs[at[q]] = t[q];
+    }
+    __syncthreads();
+    run(xs + threadIdx.x * DS);
+  } else {
+    __syncthreads();  // the parameter copy
+    run(A.X + A.rows[j < n ? j : 0] * (int64_t)D);
   }
 }
 
@@ -434,9 +518,9 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
 
 // enqueue the preparation of ps.nk KDEs (no host synchronisation)
 static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s) {
-  hipLaunchKernelGGL(kde_params_kernel, dim3(ps.nk), dim3(256), 0, s, ps);
+  hipLaunchKernelGGL(kde_colstats_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
   HBX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kde_center_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
+  hipLaunchKernelGGL(kde_params_kernel, dim3(ps.nk), dim3(256), 0, s, ps);
   HBX_LAUNCH_CHECK();
   const unsigned tb = (unsigned)(ps.k[0].nblk_table + (ps.nk > 1 ? ps.k[1].nblk_table : 0));
   if (tb > 0) {

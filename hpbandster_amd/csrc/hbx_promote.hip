@@ -88,19 +88,6 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
 // the whole bucket advances.  The mask is then one masked 64-bit compare per element against the
 // resolved prefix; keys equal in all 64 bits are ranked by position (stable), as sh_promote_wave_kernel
 // and sh_promote_kernel rank them.
-template <typename Op>
-__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t v, Op op) {
-  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
-  // every lane of a 16-lane row now holds the row's value: combine the four rows (scalar, uniform)
-  return op(op((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
-            op((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
-}
-struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
-struct OpAnd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a & b; } };
-struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
 
 // bit `sh` of each of the 16 words, gathered into a 16-bit mask (bit r from word r): 2 VALU per word
 __device__ __forceinline__ uint32_t gather_bit(const uint32_t (&w)[PW_PER_LANE], int sh) {

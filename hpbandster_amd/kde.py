@@ -103,14 +103,15 @@ class DeviceKDE(object):
 
     def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None, prepared=None):
         """Prepare a KDE for scoring with ``hbx_kde_prepare`` -- or, with ``prepared`` = (params, table,
-        info) from ``hbx_kde_refit``, wrap an already prepared one."""
+        info) from ``hbx_kde_refit``, wrap an already prepared one.  ``data_host``: the observation rows
+        (n x D), or a pair (host rows, row indices) gathered on first use of ``.data``."""
         torch = _torch()
         L = N.lib()
         self.var_type = var_type
         self.k_vars = len(var_type)
         self.bw = np.asarray(bw, dtype=np.float64)
         self.nlev = np.asarray(nlev, dtype=np.int32)
-        self.data = data_host
+        self._data = data_host
         self.nobs = int(rows_dev.shape[0])
         self.X_dev = X_dev
         self.rows_dev = rows_dev
@@ -137,6 +138,14 @@ class DeviceKDE(object):
         self.exact_only = bool((self.variant >> 5) & 1)
         if unsupported:
             raise N.HbxError("KDE bandwidth/level combination not modelled (bw=%r, nlev=%r)" % (self.bw, self.nlev))
+
+    @property
+    def data(self):
+        """KDEMultivariate.data: this KDE's observations (host, n x D), in the split's row order."""
+        if isinstance(self._data, tuple):
+            src, idx = self._data
+            self._data = src[idx]
+        return self._data
 
     def pdf(self, data_predict=None, stream=None):
         """Exact fp64 pdf on the GPU (KDEMultivariate.pdf semantics, np.squeeze'd)."""
@@ -591,9 +600,9 @@ class ObservationStore(object):
             raise N.HbxError("categorical codes must be integers in [0, 1024)")
         order = out[:8 * n].view(torch.int64)
         X_dev = self.X_dev
-        good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, X_host[order_h[:n_good]],
+        good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, (X_host, order_h[:n_good]),
                          prepared=(pg, tg, info_g))
-        bad = DeviceKDE(X_dev, order[n - n_bad:], self.var_type, bw_bh, nl_bh, X_host[order_h[n - n_bad:]],
+        bad = DeviceKDE(X_dev, order[n - n_bad:], self.var_type, bw_bh, nl_bh, (X_host, order_h[n - n_bad:]),
                         prepared=(pbad, tb, info_b))
         pair = KDEPair(good, bad)
         pair._keep = (out,)  # the rows tensors are views of the refit's output block
