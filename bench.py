@@ -311,8 +311,22 @@ def promote_dropin(device, n=1000, reps=50):
         for sh in shs:
             fn(sh)
         res[name] = (time.perf_counter() - t0) / reps * 1e3
+    # the ranking step alone: advance_mask (pinned copies + select kernel + one sync) vs numpy's
+    from hpbandster_amd import promote
+    losses = rs.rand(n)
+    k = n // 3
+    promote.advance_mask(losses, k, device=device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        promote.advance_mask(losses, k, device=device)
+    rank_gpu = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        np.argsort(np.argsort(losses)) < k
+    rank_host = (time.perf_counter() - t0) / reps * 1e3
     return {"workload": "process_results_one_bracket_n%d" % n, "ms_per_call": res["gpu"],
-            "host_numpy_ms_per_call": res["host_numpy"]}
+            "host_numpy_ms_per_call": res["host_numpy"], "rank_step_ms": rank_gpu,
+            "host_rank_step_ms": rank_host}
 
 
 def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):

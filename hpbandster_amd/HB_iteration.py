@@ -84,25 +84,37 @@ class SuccessiveHalving(object):
         return self.num_configs[self.SH_iter]
 
     def process_results(self):
+        """HB_iteration.py:149-190: rank the REVIEW configurations of this stage on the GPU
+        (promote.advance_mask), mark the top k QUEUED at the next budget, the rest TERMINATED.  One
+        pass over the dict for the ids and budgets, one for the losses, one for the updates."""
         self.SH_iter += 1
-        config_ids = [cid for cid in self.data.keys() if self.data[cid]['status'] == 'REVIEW']
+        config_ids, budgets = [], []
+        for cid, d in self.data.items():
+            if d['status'] == 'REVIEW':
+                config_ids.append(cid)
+                budgets.append(d['budget'])
         if self.SH_iter >= len(self.num_configs):
             self.cleanup()
             return
         if len(config_ids) > 0:
-            budgets = [self.data[cid]['budget'] for cid in config_ids]
             if len(set(budgets)) > 1:
                 raise RuntimeError('Not all configurations have the same budget!')
             budget = budgets[0]
-            losses = np.array([self.data[cid]['results'][budget]['loss'] for cid in config_ids], dtype=np.float64)
+            data = self.data
+            losses = np.fromiter((data[cid]['results'][budget]['loss'] for cid in config_ids), dtype=np.float64,
+                                 count=len(config_ids))
             advance = promote.advance_mask(losses, self._advance_threshold(), device=self.device)
-            for i, cid in enumerate(config_ids):
-                if advance[i]:
-                    self.data[cid]['status'] = 'QUEUED'
-                    self.data[cid]['budget'] = self.budgets[self.SH_iter]
-                    self.actual_num_configs[self.SH_iter] += 1
+            nb = self.budgets[self.SH_iter]
+            moved = 0
+            for cid, a in zip(config_ids, advance.tolist()):
+                d = data[cid]
+                if a:
+                    d['status'] = 'QUEUED'
+                    d['budget'] = nb
+                    moved += 1
                 else:
-                    self.data[cid]['status'] = 'TERMINATED'
+                    d['status'] = 'TERMINATED'
+            self.actual_num_configs[self.SH_iter] += moved
 
     def cleanup(self):
         self.is_finished = True

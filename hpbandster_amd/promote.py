@@ -6,6 +6,8 @@ CRASHED entries (non-finite loss) never advance.  Many brackets are ranked in on
 benchmark exercises.
 """
 
+import threading
+
 import numpy as np
 
 from . import _native as N
@@ -55,11 +57,47 @@ def _promote_segments(L, loss, seg_off, k, device, stream, return_order):
     return adv.cpu().numpy().astype(bool)
 
 
+class _Staging(object):
+    """Per-thread, per-device buffers of advance_mask: pinned host in/out and their device twins,
+    grown on demand.  Every call synchronises its stream before returning, so a buffer is free again
+    when the next call of the same thread starts."""
+
+    def __init__(self, device):
+        self.device = device
+        self.cap = 0
+
+    def get(self, n):
+        import torch
+        if n > self.cap:
+            cap = max(1024, 1 << (int(n) - 1).bit_length())
+            self.h_in = torch.empty(cap + 3, dtype=torch.float64, pin_memory=True)
+            self.h_out = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self.d_in = torch.empty(cap + 3, dtype=torch.float64, device=self.device)
+            self.d_out = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            self.cap = cap
+        return self
+
+
+_tls = threading.local()
+
+
+def _staging(device):
+    import torch
+    key = str(torch.device(device))
+    st = getattr(_tls, "staging", None)
+    if st is None:
+        st = _tls.staging = {}
+    if key not in st:
+        st[key] = _Staging(device)
+    return st[key]
+
+
 def advance_mask(losses, k, device=None, stream=None):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
     What SuccessiveHalving.process_results calls once per bracket: segment bounds, k and the losses
-    travel in one host->device copy, the select kernel runs, the mask comes back in one copy."""
+    travel in one pinned host->device copy, the select kernel runs, the mask comes back in one pinned
+    copy, one stream synchronisation."""
     import torch
     losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
@@ -69,14 +107,17 @@ def advance_mask(losses, k, device=None, stream=None):
         return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream)
     device = device or default_device()
     L = N.lib()
-    buf = np.empty(n + 3, dtype=np.float64)
-    buf[:2].view(np.int64)[:] = (0, n)
-    buf[2] = float(k)
-    buf[3:] = losses
     with N.on_device(device, stream):
-        d = torch.from_numpy(buf).to(device)
-        adv = torch.empty(n, dtype=torch.uint8, device=device)
-        base = d.data_ptr()
-        N.check(L.hbx_sh_promote(base + 24, base, 1, n, n, base + 16, None, N.ptr(adv), None, None, 0,
-                                 N.stream_handle(stream, device)))
-        return adv.cpu().numpy().astype(bool)
+        st = _staging(device).get(n)
+        hb = st.h_in.numpy()
+        hb[:2].view(np.int64)[:] = (0, n)
+        hb[2] = float(k)
+        hb[3:3 + n] = losses
+        cur = stream if stream is not None else torch.cuda.current_stream(device)
+        st.d_in[:n + 3].copy_(st.h_in[:n + 3], non_blocking=True)
+        base = st.d_in.data_ptr()
+        N.check(L.hbx_sh_promote(base + 24, base, 1, n, n, base + 16, None, N.ptr(st.d_out), None, None, 0,
+                                 cur.cuda_stream))
+        st.h_out[:n].copy_(st.d_out[:n], non_blocking=True)
+        cur.synchronize()
+        return st.h_out[:n].numpy().astype(bool)
