@@ -57,7 +57,11 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   constexpr int GP = CHF * 4 / 1024;
   constexpr int GL = GP / HW, NX = GP % HW;
   static_assert(GP * 1024 == CHF * 4, "chunk must be a multiple of 1 KB");
-  __shared__ __align__(16) float lds[NBUF * CHF];          // the kernel's only LDS object
+  // after the ring: per (wave, row tile) the candidates' c_i, bound term and probe shift (read by the
+  // epilogue only, so they need no registers across the main loop)
+  constexpr int AUXF = HW * RT * 48;
+  static_assert(NBUF * CHF * 4 + AUXF * 4 <= 160 * 1024, "ring + epilogue values exceed the LDS");
+  __shared__ __align__(16) float lds[NBUF * CHF + AUXF];   // the kernel's only LDS object
 
   // wave made visibly uniform: LDS-DMA addresses, m0 and row bases are then SGPR arithmetic
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -186,10 +190,16 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   }
   // accumulator rows of this lane: candidates cbase + 16 r + 4 kq + q
   f32x4 ciq[RT];
+  float* aux = lds + NBUF * CHF + wave * RT * 48;
 #pragma unroll
-  for (int r = 0; r < RT; ++r)
+  for (int r = 0; r < RT; ++r) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) ciq[r][q] = __shfl(ci_a[r], 4 * kq + q);
+    if (kq == 0) {  // lane ia holds candidate 16 r + ia's values
+      aux[r * 48 + ia] = ci_a[r];
+      aux[r * 48 + 16 + ia] = bnd_a[r];
+    }
+  }
 
   float S[RT][4], Sn[RT][4];
 #pragma unroll
@@ -270,6 +280,48 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
     }
   };
 
+  // The MFMAs of one column tile, each B fragment re-read in place (from tile jt of `nb`) right after
+  // the last MFMA that consumes it: one register set, and every read has the rest of the phase to land.
+  auto mfmas_rd = [&](f16x8 (&b)[NSH], f16x8 (&bp)[KPF], f32x4* acc, f32x4* accp, const float* nb, int jt) {
+    const int jo = jt * 16 + ia;
+    const _Float16* hb = (const _Float16*)(nb + OBS_CHUNK) + jo * KTP + 8 * kq;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][0], b[0], ciq[r], 0, 0, 0);
+    constexpr int NDENSE = SP ? NSC : NSH;
+    b[0] = *(const f16x8*)(hb);
+#pragma unroll
+    for (int s = 1; s < NDENSE; ++s) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][s], b[s], acc[r], 0, 0, 0);
+      b[s] = *(const f16x8*)(hb + 32 * s);
+    }
+    if constexpr (SP) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const f16x8 lo = b[NSC + 2 * s], hi = b[NSC + 2 * s + 1];
+        const f16x16 b16 = {lo[0], lo[1], lo[2], lo[3], lo[4], lo[5], lo[6], lo[7],
+                            hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          acc[r] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(asp[r][s], b16, acc[r], aidx[r][s], 0, 0);
+        b[NSC + 2 * s] = *(const f16x8*)(hb + 32 * (NSC + 2 * s));
+        b[NSC + 2 * s + 1] = *(const f16x8*)(hb + 32 * (NSC + 2 * s + 1));
+      }
+    }
+    if constexpr (SIGNED) {
+      const _Float16* pb = (const _Float16*)(nb + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jo * KPP + 8 * kq;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) accp[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          accp[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r][NSC + s], bp[s], accp[r], 0, 0, 0);
+        bp[s] = *(const f16x8*)(pb + 32 * s);
+      }
+    }
+  };
+
   // Per-candidate shift: the exponent's maximum over chunk 0 (a lower bound of the maximum over all
   // observations) is moved to 0 through the accumulator input.  Without it candidates far from every
   // observation -- most of what BOHB's own sampler proposes at D = 32, where the truncnorm scale is
@@ -277,7 +329,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   // later chunks can exceed the probe's maximum; a sum that leaves [2^-64, 2^100] still takes the
   // rescue.  Costs one chunk of MFMAs (no exp2) per block.
   float dl[RT][4];
-  f16x8 bA[NSH], bB[NSH], bpA[KPF], bpB[KPF];
+  f16x8 bA[NSH], bpA[KPF];
   {
     f32x4 acc[RT], accp[RT];
     float mx[RT][4];
@@ -303,6 +355,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
         const float d = rintf(-mx[r][q]);
         dl[r][q] = (d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
         ciq[r][q] += dl[r][q];
+        if (ia == 0) aux[r * 48 + 32 + 4 * kq + q] = dl[r][q];
       }
   }
 
@@ -353,25 +406,33 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
     }
     __builtin_amdgcn_sched_barrier(0);
   };
-  readb(lds, 0, bA, bpA);  // tile 0 of chunk 0 (buffer 0)
+  // fragment prefetch where the register budget allows (small buckets); the large ones read each
+  // tile's fragments right before its MFMAs
+  constexpr bool PREF = (NSH + (SIGNED ? KC : 0)) <= 8;
+  auto phase = [&](const float* cb, int t, const float* nb, int tn, f32x4* acc, f32x4* accp) {
+    if constexpr (PREF) {
+      mfmas_rd(bA, bpA, acc, accp, nb, tn);
+    } else {
+      readb(cb, t, bA, bpA);
+      mfmas(bA, bpA, acc, accp);
+    }
+  };
+  if (PREF) readb(lds, 0, bA, bpA);  // tile 0 of chunk 0 (buffer 0)
   for (int c = 0; c < nchunks; ++c) {
     const float* buf = lds + (c % NBUF) * CHF;
     const float* nbuf = lds + ((c + 1) % NBUF) * CHF;
     issue(c + PD, (c + PD) % NBUF);  // its buffer's reads all retired before the previous barrier
-    // phase 0: MFMAs of tile 0 (bA); reads of tile 1 -> bB; epilogue of tile 3 of chunk c-1
-    readb(buf, 1, bB, bpB);
-    mfmas(bA, bpA, accA, accpA);
+    // phase 0: MFMAs of tile 0, then its fragments re-read for tile 1; epilogue of tile 3 of chunk c-1
+    phase(buf, 0, buf, 1, accA, accpA);
     epi(accB, accpB, false);
     close_chunk();
     schedule();
     // phase 1
-    readb(buf, 2, bA, bpA);
-    mfmas(bB, bpB, accB, accpB);
+    phase(buf, 1, buf, 2, accB, accpB);
     epi(accA, accpA, true);
     schedule();
     // phase 2
-    readb(buf, 3, bB, bpB);
-    mfmas(bA, bpA, accA, accpA);
+    phase(buf, 2, buf, 3, accA, accpA);
     epi(accB, accpB, false);
     schedule();
     // chunk c+1 complete for this wave (PD-1 chunks stay in flight) and every read of buffer c
@@ -381,9 +442,8 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
     else
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
     __builtin_amdgcn_s_barrier();
-    // phase 3: MFMAs of tile 3 (bB); reads of tile 0 of chunk c+1 -> bA
-    readb(nbuf, 0, bA, bpA);
-    mfmas(bB, bpB, accB, accpB);
+    // phase 3: MFMAs of tile 3; fragments of tile 0 of chunk c+1 read
+    phase(buf, 3, nbuf, 0, accB, accpB);
     epi(accA, accpA, false);
     schedule();
   }
@@ -401,10 +461,9 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       }
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
-    const int src_lane = (4 * kq + (ia & 3)) & 15;
-    const float ci_q = __shfl(ci_a[r], src_lane);
-    const float bnd_q = __shfl(bnd_a[r], src_lane);
     if (ia < 4) {
+      const int cq = 4 * kq + ia;  // this lane's candidate within the row tile
+      const float ci_q = aux[r * 48 + cq], bnd_q = aux[r * 48 + 16 + cq], dq = aux[r * 48 + 32 + cq];
       const int q = ia;
       const int64_t ii = cbase + 16 * r + 4 * kq + q;
       // select tree on named values (a runtime index into S would put S in scratch memory)
@@ -412,7 +471,6 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
       const float s0 = S[r][0], s1 = S[r][1], s2 = S[r][2], s3 = S[r][3];
       const float n0 = Sn[r][0], n1 = Sn[r][1], n2 = Sn[r][2], n3 = Sn[r][3];
       const float Sq = b1 ? (b0 ? s3 : s2) : (b0 ? s1 : s0);
-      const float dq = b1 ? (b0 ? dl[r][3] : dl[r][2]) : (b0 ? dl[r][1] : dl[r][0]);
       const float Snq = b1 ? (b0 ? n3 : n2) : (b0 ? n1 : n0);
       if (ii < Nc) {
         const double* x = cand + ii * (int64_t)D;

@@ -1,0 +1,29 @@
+#!/bin/bash
+# One round's measurement set on the GPU box (run via gpurun): the default bench line, a rocprofv3
+# kernel trace of the bench workload, and PMC passes (traffic, issue, clock) -- each pass its own run.
+#   bash tools/profile_round.sh r02      -> gpurun_out/r02/
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1
+mkdir -p $OUT
+cd $R
+timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --steps 5 --warmup 1 --no-cpu --no-config5"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace.log; exit 2; }
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE GRBM_GUI_ACTIVE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set -d $OUT/pmc$i -o run --output-format csv -- python3 $B > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 3; }
+done
+cd $R
+W=kde_acquisition_d32_24c8u_obs10000_cand1000000
+python3 tools/pmc_summary.py $OUT --traffic-out $OUT/pmc_traffic.json --workload $W > $OUT/pmc_summary.txt || exit 4
+python3 tools/ksteady.py $(ls $OUT/trace/*kernel_trace.csv | head -1) > $OUT/kernel_steady.txt || exit 5
+cp $(ls $OUT/trace/*kernel_stats.csv | head -1) $OUT/kernel_stats.csv
+rm -rf $OUT/pmc[0-9]/ $OUT/trace/*kernel_trace.csv
+head -5 $OUT/kernel_steady.txt
+echo profile done
