@@ -504,6 +504,20 @@ def load_traffic(workload):
     return None
 
 
+def load_clock(workload):
+    """Effective engine clock under the scoring kernel (GRBM_GUI_ACTIVE / 8 / duration) from the
+    committed PMC record of this workload (tools/profile_round.sh), else None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload:
+            return d.get("clock_ghz")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def main():
     a = parse()
     import torch
@@ -608,6 +622,10 @@ def main():
         peak_pairs = N_SIMD * CLOCK_GHZ * 1e9 * 256 / m["bound_cycles"]
         issue_bound = dict(m, clock_ghz=CLOCK_GHZ, peak_pairs_per_s=peak_pairs, achieved_pairs_per_s=kernel_rate,
                            frac=kernel_rate / peak_pairs)
+        clk = load_clock(workload)
+        if clk:  # the same model at the clock the chip was measured to hold under this kernel
+            issue_bound["measured_clock_ghz"] = clk
+            issue_bound["frac_at_measured_clock"] = kernel_rate / (N_SIMD * clk * 1e9 * 256 / m["bound_cycles"])
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",

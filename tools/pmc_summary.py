@@ -14,6 +14,8 @@ ap.add_argument("dir")
 ap.add_argument("--traffic-out")
 ap.add_argument("--workload")
 ap.add_argument("--kernel", default="kde_logpdf_h_pair_kernel")
+ap.add_argument("--trace", help="kernel_trace.csv of the same command: the kernel's median duration, for the "
+                                "effective clock GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md)")
 a = ap.parse_args()
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
@@ -41,7 +43,19 @@ if a.traffic_out:
     rec = {"workload": a.workload, "kernel": a.kernel, "fetch_size_kb_raw": fetch, "write_size_kb": write,
            "bytes_per_launch": 2 * fetch * 1024 + write * 1024,
            "note": "HBM-side bytes per launch (%s) = 2 x FETCH_SIZE + WRITE_SIZE "
-                   "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md); from tools/profile_pmc.sh"
+                   "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md); from tools/profile_round.sh"
                    % ("l and g in one launch" if "pair" in a.kernel else "mean over the l and g launches")}
+    if a.trace:
+        import statistics
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in csv.DictReader(open(a.trace))
+                if a.kernel in r["Kernel_Name"]]
+        grbm = sum(out[k].get("GRBM_GUI_ACTIVE", 0) * out[k]["dispatches"] for k in ks) / \
+            sum(out[k]["dispatches"] for k in ks)
+        if durs and grbm:
+            med = statistics.median(durs)
+            rec["kernel_median_s"] = med
+            rec["clock_ghz"] = grbm / 8 / med / 1e9
+            rec["clock_note"] = ("effective engine clock during the kernel: GRBM_GUI_ACTIVE (sum over 8 XCDs) / 8 / "
+                                 "median kernel duration of the traced run")
     json.dump(rec, open(a.traffic_out, "w"), indent=1)
     print(json.dumps(rec))
