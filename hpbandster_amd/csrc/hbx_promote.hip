@@ -89,14 +89,6 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
 // resolved prefix; keys equal in all 64 bits are ranked by position (stable), as sh_promote_wave_kernel
 // and sh_promote_kernel rank them.
 
-// bit `sh` of each of the 16 words, gathered into a 16-bit mask (bit r from word r): 2 VALU per word
-__device__ __forceinline__ uint32_t gather_bit(const uint32_t (&w)[PW_PER_LANE], int sh) {
-  uint32_t m = 0u;
-#pragma unroll
-  for (int r = 0; r < PW_PER_LANE; ++r) m |= __builtin_amdgcn_ubfe(w[r], (uint32_t)sh, 1u) << r;
-  return m;
-}
-
 constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (raw 32-bit data, range checked)
 
 __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict__ loss,
@@ -123,121 +115,174 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
   double v[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane, 512 * r, 0));
-  // order-preserving keys (hbx_d2ord; -0.0 + 0.0 = +0.0 merges the zeros), the finite mask (CRASHED,
-  // i.e. non-finite, entries are never ranked) and the AND / OR of the finite keys' high words
-  uint32_t khi[R], klo[R];
-  uint32_t fin = 0u, andh = ~0u, orh = 0u;
+  // order-preserving keys (hbx_d2ord; -0.0 + 0.0 = +0.0 merges the zeros) and the min / max of the
+  // high words over the bracket (rows past n skipped, the partial row masked: uniform branches).
+  // Finite keys have high words in [0x00100000, 0xFFEFFFFF]; a bracket without CRASHED (non-finite)
+  // entries -- the common case -- then needs no per-element finite mask at all.
+  const int nrow = (n + 63) >> 6;  // rows holding elements
+  uint64_t key[R];
+  uint32_t mnh = ~0u, mxh = 0u;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const double z = v[r] + 0.0;
     const uint32_t hi = (uint32_t)(__double_as_longlong(z) >> 32), lo = (uint32_t)__double_as_longlong(z);
     const uint32_t sg = (uint32_t)((int32_t)hi >> 31);
-    khi[r] = hi ^ (sg | 0x80000000u);
-    klo[r] = lo ^ sg;
-    const bool f = (64 * r + lane < n) && __builtin_isfinite(v[r]);
-    fin |= (f ? 1u : 0u) << r;
-    andh &= f ? khi[r] : ~0u;
-    orh |= f ? khi[r] : 0u;
+    const uint32_t kh = hi ^ (sg | 0x80000000u);
+    key[r] = ((uint64_t)kh << 32) | (lo ^ sg);
+    if (64 * r + 64 <= n) {
+      mnh = min(mnh, kh);
+      mxh = max(mxh, kh);
+    } else if (r < nrow) {
+      const bool ok = 64 * r + lane < n;
+      mnh = min(mnh, ok ? kh : ~0u);
+      mxh = max(mxh, ok ? kh : 0u);
+    }
   }
-  const int nfin = (int)wave_reduce_dpp((uint32_t)__popc(fin), OpAdd());
-  // rank < k advances: the first kk ranks, kk = min(nfin, ceil(k)) (k > 0; NaN or k <= 0: none)
-  const double kb = k[b];
-  const int kk = kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0;
-  uint32_t adv;
-  if (kk == nfin) {
-    adv = fin;
-  } else if (kk == 0) {
-    adv = 0u;
-  } else {
-    // bits above the highest one where the finite keys differ are common to all of them: resolved
-    const uint32_t ah = wave_reduce_dpp(andh, OpAnd());
-    const uint32_t dh = wave_reduce_dpp(orh, OpOr()) ^ ah;
-    uint32_t al = 0u, dl = 0u;
+  mnh = ~wave_reduce_dpp(~mnh, OpMax());
+  mxh = wave_reduce_dpp(mxh, OpMax());
+  const bool allfin = mnh >= 0x00100000u && mxh <= 0xFFEFFFFFu;  // uniform
+  // per-lane element mask: bit r = element 64 r + lane exists (and, with CRASHED entries, is finite)
+  const int nr = min(max((n - lane + 63) >> 6, 0), R);
+  uint32_t fin = (1u << nr) - 1u;
+  int nfin = n;
+  uint32_t ph, pl = 0u, dh, dl = 0u;  // resolved prefix of the k-th key; bits where the keys differ
+  if (allfin) {
+    dh = mnh ^ mxh;
+    ph = mnh;
     if (dh == 0u) {  // equal high words: the low words decide (rare)
+      uint32_t mnl = ~0u, mxl = 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool f = (fin >> r) & 1u;
+        mnl = min(mnl, f ? (uint32_t)key[r] : ~0u);
+        mxl = max(mxl, f ? (uint32_t)key[r] : 0u);
+      }
+      mnl = ~wave_reduce_dpp(~mnl, OpMax());
+      mxl = wave_reduce_dpp(mxl, OpMax());
+      dl = mnl ^ mxl;
+      pl = mnl;
+    }
+  } else {  // CRASHED entries present: finite mask, AND / OR of the finite keys
+    uint32_t andh = ~0u, orh = 0u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t kh = (uint32_t)(key[r] >> 32);
+      const bool f = ((fin >> r) & 1u) && kh >= 0x00100000u && kh <= 0xFFEFFFFFu;  // finite
+      fin &= ~((f ? 0u : 1u) << r);
+      andh &= f ? kh : ~0u;
+      orh |= f ? kh : 0u;
+    }
+    nfin = (int)wave_reduce_dpp((uint32_t)__popc(fin), OpAdd());
+    ph = wave_reduce_dpp(andh, OpAnd());
+    dh = wave_reduce_dpp(orh, OpOr()) ^ ph;
+    if (dh == 0u) {
       uint32_t andl = ~0u, orl = 0u;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const bool f = (fin >> r) & 1u;
-        andl &= f ? klo[r] : ~0u;
-        orl |= f ? klo[r] : 0u;
+        andl &= f ? (uint32_t)key[r] : ~0u;
+        orl |= f ? (uint32_t)key[r] : 0u;
       }
-      al = wave_reduce_dpp(andl, OpAnd());
-      dl = wave_reduce_dpp(orl, OpOr()) ^ al;
+      pl = wave_reduce_dpp(andl, OpAnd());
+      dl = wave_reduce_dpp(orl, OpOr()) ^ pl;
     }
-    int bit = dh ? 63 - __clz((int)dh) : (dl ? 31 - __clz((int)dl) : -1);
-    uint32_t ph = ah, pl = al;  // the resolved prefix (bits above `bit`) of the k-th key
-    int need = kk, cnt = nfin;
-    uint32_t alive = fin;
-    // phase 1: the bucket as per-lane bit masks
-    for (; bit >= 0 && cnt != need && cnt > 64; --bit) {
-      const uint32_t ones = bit >= 32 ? gather_bit(khi, bit - 32) : gather_bit(klo, bit);
-      const uint32_t zero = alive & ~ones;
-      const int c0 = (int)wave_reduce_dpp((uint32_t)__popc(zero), OpAdd());
+  }
+  // rank < k advances: the first kk ranks, kk = min(nfin, ceil(k)) (k > 0; NaN or k <= 0: none)
+  const double kb = k[b];
+  const int kk = kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0;
+  if (kk == nfin || kk == 0) {  // all the finite entries, or none
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk ? (fin >> r) & 1u : 0u), ars, lane, 64 * r, 0);
+    if (lane == 0 && n_advance) n_advance[b] = kk;
+    return;
+  }
+  // bits above the highest one where the finite keys differ are common to all of them: resolved
+  int bit = dh ? 63 - __clz((int)dh) : (dl ? 31 - __clz((int)dl) : -1);
+  if (bit >= 32) {  // the prefix keeps only the bits above `bit`
+    ph &= ~((2u << (bit - 32)) - 1u);
+    pl = 0u;
+  } else if (bit >= 0) {
+    pl &= ~((2u << bit) - 1u);
+  }
+  int need = kk, cnt = nfin;
+  uint32_t alive = fin;
+  // phase 1: the bucket as per-lane bit masks
+  for (; bit >= 0 && cnt != need && cnt > 64; --bit) {
+    uint32_t ones = 0u;
+    if (bit >= 32) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ones |= __builtin_amdgcn_ubfe((uint32_t)(key[r] >> 32), (uint32_t)(bit - 32), 1u) << r;
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ones |= __builtin_amdgcn_ubfe((uint32_t)key[r], (uint32_t)bit, 1u) << r;
+    }
+    const uint32_t zero = alive & ~ones;
+    const int c0 = (int)wave_reduce_dpp((uint32_t)__popc(zero), OpAdd());
+    if (need <= c0) {
+      alive = zero;
+      cnt = c0;
+    } else {
+      alive &= ones;
+      need -= c0;
+      cnt -= c0;
+      if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
+    }
+  }
+  if (bit >= 0 && cnt != need) {
+    // phase 2: compact the <= 64 bucket keys into one per lane, in position order
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool a = (alive >> r) & 1u;
+      const uint64_t m = __ballot(a);
+      if (a) cbuf[wv][base + __popcll(m & ((1ull << lane) - 1ull))] = key[r];
+      base += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t key1 = cbuf[wv][lane < cnt ? lane : 0];
+    bool a1 = lane < cnt;
+    for (; bit >= 0 && cnt != need; --bit) {
+      const bool one = (key1 >> bit) & 1ull;
+      const int c0 = __popcll(__ballot(a1 && !one));
       if (need <= c0) {
-        alive = zero;
+        a1 = a1 && !one;
         cnt = c0;
       } else {
-        alive &= ones;
+        a1 = a1 && one;
         need -= c0;
         cnt -= c0;
         if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
       }
     }
-    if (bit >= 0 && cnt != need) {
-      // phase 2: compact the <= 64 bucket keys into one per lane, in position order
-      int base = 0;
+  }
+  // bits > bit are resolved (prefix P): an element advances iff its key's resolved part is below P,
+  // or equal and either the whole bucket advances (cnt == need: key < P + 2^(bit+1), one 64-bit
+  // compare) or -- keys equal in all 64 bits -- it is among the first `need` of them by position
+  const uint64_t P = ((uint64_t)ph << 32) | pl;
+  if (cnt == need) {
+    // bit <= 62 (at least one pass ran); -1 when all 64 bits were resolved.  No overflow: finite keys
+    // stay below 0xFFF0000000000000
+    const uint64_t T = P + (bit >= 0 ? (2ull << bit) : 1ull);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const bool a = (alive >> r) & 1u;
-        const uint64_t m = __ballot(a);
-        if (a) cbuf[wv][base + __popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)khi[r] << 32) | klo[r];
-        base += __popcll(m);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint64_t key1 = cbuf[wv][lane < cnt ? lane : 0];
-      bool a1 = lane < cnt;
-      for (; bit >= 0 && cnt != need; --bit) {
-        const bool one = (key1 >> bit) & 1ull;
-        const int c0 = __popcll(__ballot(a1 && !one));
-        if (need <= c0) {
-          a1 = a1 && !one;
-          cnt = c0;
-        } else {
-          a1 = a1 && one;
-          need -= c0;
-          cnt -= c0;
-          if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
-        }
-      }
+    for (int r = 0; r < R; ++r) {
+      const bool adv = key[r] < T && (allfin || ((fin >> r) & 1u));
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(adv ? 1 : 0), ars, lane, 64 * r, 0);
     }
-    // bits > bit are resolved: an element advances iff its key's resolved part is below the prefix,
-    // or equal and either the whole bucket advances (cnt == need) or -- keys equal in all 64 bits --
-    // it is among the first `need` of them by position
-    const uint64_t M = bit >= 63 ? 0ull : (bit < 0 ? ~0ull : ~((2ull << bit) - 1ull));
-    const uint64_t P = (((uint64_t)ph << 32) | pl) & M;
-    adv = 0u;
-    if (cnt == need) {
+  } else {
+    int taken = 0;
 #pragma unroll
-      for (int r = 0; r < R; ++r) adv |= ((((uint64_t)khi[r] << 32) | klo[r]) & M) <= P ? (1u << r) : 0u;
-      adv &= fin;
-    } else {
-      int taken = 0;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint64_t key = (((uint64_t)khi[r] << 32) | klo[r]) & M;
-        const bool f = (fin >> r) & 1u;
-        const bool eq = f && key == P;
-        const uint64_t m = __ballot(eq);
-        const bool take = (f && key < P) || (eq && taken + __popcll(m & ((1ull << lane) - 1ull)) < need);
-        taken += __popcll(m);
-        adv |= (take ? 1u : 0u) << r;
-      }
+    for (int r = 0; r < R; ++r) {
+      const bool f = (fin >> r) & 1u;
+      const bool eq = f && key[r] == P;
+      const uint64_t m = __ballot(eq);
+      const bool take = (f && key[r] < P) || (eq && taken + __popcll(m & ((1ull << lane) - 1ull)) < need);
+      taken += __popcll(m);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1 : 0), ars, lane, 64 * r, 0);
     }
   }
-#pragma unroll
-  for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((adv >> r) & 1u), ars, lane, 64 * r, 0);
   if (lane == 0 && n_advance) n_advance[b] = kk;
 }
 

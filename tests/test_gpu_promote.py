@@ -149,11 +149,13 @@ def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
         np.testing.assert_array_equal(outs[0][s:e], np.argsort(loss[s:e], kind="stable"))
 
 
+@pytest.mark.parametrize("crashed", [True, False])
 @pytest.mark.parametrize("B,n", [(400, 1024), (97, 200), (5, 1), (64, 3), (2000, 81)])
-def test_select_kernel_identical_to_sort(device, B, n):
+def test_select_kernel_identical_to_sort(device, B, n, crashed):
     """Mask-only promotion (order not requested) runs the radix select of the k-th (loss, position);
     with the order requested the wave sort runs.  Masks and counts identical on tie-heavy brackets
-    with empty, all-equal, all-crashed ones and k = 0, fractional, NaN and larger than the bracket."""
+    with empty, all-equal, all-crashed ones and k = 0, fractional, NaN and larger than the bracket.
+    Without CRASHED (non-finite) entries every bracket takes the select kernel's all-finite path."""
     from hpbandster_amd import promote
     rs = np.random.RandomState(3 * B + n)
     lens = rs.randint(0, n + 1, size=B)
@@ -161,14 +163,15 @@ def test_select_kernel_identical_to_sort(device, B, n):
     seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     loss = np.round(rs.rand(seg[-1]) * 30) / 30
     loss[rs.rand(seg[-1]) < 0.3] = 0.5
-    loss[rs.rand(seg[-1]) < 0.05] = np.inf
-    loss[rs.rand(seg[-1]) < 0.03] = np.nan
-    loss[rs.rand(seg[-1]) < 0.01] = -np.inf
+    if crashed:
+        loss[rs.rand(seg[-1]) < 0.05] = np.inf
+        loss[rs.rand(seg[-1]) < 0.03] = np.nan
+        loss[rs.rand(seg[-1]) < 0.01] = -np.inf
     loss[rs.rand(seg[-1]) < 0.01] = -0.0
     loss[rs.rand(seg[-1]) < 0.01] = 0.0
     if B > 3:
         loss[seg[1]:seg[2]] = 0.25       # all equal
-        loss[seg[2]:seg[3]] = np.nan     # all crashed
+        loss[seg[2]:seg[3]] = np.nan if crashed else -0.0  # all crashed / all zero
     k = np.maximum(lens * rs.choice([0.0, 0.34, 0.5, 0.999, 1.7], size=B), 0.0)
     k[::7] = np.floor(k[::7])
     if B > 5:
