@@ -25,6 +25,23 @@ struct SgbAlternate<NM, NM, NV> {
   static __device__ __forceinline__ void run() {}
 };
 
+// The same with the in-place B-fragment re-reads of a prefetching phase: after the last of the RT
+// MFMAs of K-step s, its fragment reads (1 for a dense step, 2 for a sparse one: s >= NDENSE)
+template <int I, int NM, int NV, int RT, int NDENSE>
+struct SgbPrefetch {
+  static __device__ __forceinline__ void run() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    constexpr int n = NV / NM + (I < NV % NM ? 1 : 0);
+    if constexpr (I % RT == RT - 1) __builtin_amdgcn_sched_group_barrier(0x100, (I / RT) < NDENSE ? 1 : 2, 0);
+    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x002, n, 0);
+    SgbPrefetch<I + 1, NM, NV, RT, NDENSE>::run();
+  }
+};
+template <int NM, int NV, int RT, int NDENSE>
+struct SgbPrefetch<NM, NM, NV, RT, NDENSE> {
+  static __device__ __forceinline__ void run() {}
+};
+
 // The kernel body, for block `blk` of one KDE's grid (the single-KDE kernel and the l+g pair kernel
 // below both run it).
 template <int NSC, int KC, bool SIGNED>
@@ -379,14 +396,21 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
 #pragma unroll
     for (int q = 0; q < 4; ++q) Sb[r][q] = Snb[r][q] = 0.f;
   // epilogue of one tile: first = the tile opens a chunk's partial sum
+  // (all exp2s first, then the adds: in program order the sched groups then never put an add right
+  // behind the exp2 it waits for)
   auto epi = [&](const f32x4* cur, const f32x4* curp, bool first) {
+    float e[RT][4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[r][q] = __builtin_amdgcn_exp2f(cur[r][q]);
 #pragma unroll
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float e = __builtin_amdgcn_exp2f(cur[r][q]);
-        Sb[r][q] = first ? e : Sb[r][q] + e;
-        if (SIGNED) Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e, first ? 0.f : Snb[r][q]);
+        Sb[r][q] = first ? e[r][q] : Sb[r][q] + e[r][q];
+        if (SIGNED)
+          Snb[r][q] = fmaf(2.f * __builtin_amdgcn_fractf(0.5f * curp[r][q]), e[r][q], first ? 0.f : Snb[r][q]);
       }
   };
   auto close_chunk = [&]() {
@@ -398,17 +422,21 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
         if (SIGNED) Sn[r][q] += Snb[r][q];
       }
   };
-  // one MFMA, then one or two VALU (an exp2 or an add), alternating; the B-fragment reads first
-  auto schedule = [&]() {
-    if constexpr (!SIGNED) {
-      __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);  // DS_READ: B fragments of the next tile
-      SgbAlternate<0, NMT * RT, 8 * RT>::run();            // exp2 + add of the previous tile
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
   // fragment prefetch where the register budget allows (small buckets); the large ones read each
   // tile's fragments right before its MFMAs
   constexpr bool PREF = (NSH + (SIGNED ? KC : 0)) <= 8;
+  // one MFMA, then one or two VALU (an exp2 or an add), alternating; the B-fragment reads first
+  auto schedule = [&]() {
+    if constexpr (!SIGNED) {
+      if constexpr (PREF) {  // fragment re-reads right behind their last MFMA
+        SgbPrefetch<0, NMT * RT, 8 * RT, RT, (SP ? NSC : NSH)>::run();
+      } else {  // this tile's fragments first
+        __builtin_amdgcn_sched_group_barrier(0x100, NSH, 0);
+        SgbAlternate<0, NMT * RT, 8 * RT>::run();  // exp2 + add of the previous tile
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
   auto phase = [&](const float* cb, int t, const float* nb, int tn, f32x4* acc, f32x4* accp) {
     if constexpr (PREF) {
       mfmas_rd(bA, bpA, acc, accp, nb, tn);
