@@ -226,13 +226,15 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
   // LDS-DMA (global_load_lds_dwordx4): each wave copies its G 1-KB pieces of a chunk straight into
   // the ring; completion is tracked by a counted vmcnt + one raw barrier per chunk
-  auto issue = [&](int c, int slot) {
+  // part < 0: all pieces; else only pieces g with g % 3 == part (the main loop spreads a chunk's
+  // LDS-DMA instructions over its first three phases)
+  auto issue = [&](int c, int slot, int part = -1) {
     const float* src = table + (int64_t)(c < nchunks ? c : nchunks - 1) * CHF;
     float* dst = lds + slot * CHF;
 #pragma unroll
     for (int g = 0; g < GL + (NX ? 1 : 0); ++g) {
       const int piece = wave + g * HW;
-      if (g < GL || xpiece)
+      if ((part < 0 || g % 3 == part) && (g < GL || xpiece))
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
                                          (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
     }
@@ -449,17 +451,21 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   for (int c = 0; c < nchunks; ++c) {
     const float* buf = lds + (c % NBUF) * CHF;
     const float* nbuf = lds + ((c + 1) % NBUF) * CHF;
-    issue(c + PD, (c + PD) % NBUF);  // its buffer's reads all retired before the previous barrier
+    // chunk c+PD's LDS-DMA, spread over phases 0-2 (its buffer's reads all retired before the previous
+    // barrier; all pieces are in flight before this iteration's barrier, so its counted vmcnt holds)
+    issue(c + PD, (c + PD) % NBUF, 0);
     // phase 0: MFMAs of tile 0, then its fragments re-read for tile 1; epilogue of tile 3 of chunk c-1
     phase(buf, 0, buf, 1, accA, accpA);
     epi(accB, accpB, false);
     close_chunk();
     schedule();
     // phase 1
+    issue(c + PD, (c + PD) % NBUF, 1);
     phase(buf, 1, buf, 2, accB, accpB);
     epi(accA, accpA, true);
     schedule();
     // phase 2
+    issue(c + PD, (c + PD) % NBUF, 2);
     phase(buf, 2, buf, 3, accA, accpA);
     epi(accB, accpB, false);
     schedule();
