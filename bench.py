@@ -572,7 +572,7 @@ def main():
             rv = xchg.exchange(rv)
         # the winner reaches the host (what BOHB needs); the exact scores are the pinned reference's
         # float64 values bit for bit, so the (score, index) reduction is the reference's pick
-        r = kde.AcqResult.from_bytes(rv.cpu().numpy().tobytes())
+        r = kde.AcqResult.from_bytes(kde.fetch_bytes(rv))
         return r.index, r.score
 
     for _ in range(a.warmup):

@@ -1561,6 +1561,14 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   hipStream_t s = (hipStream_t)stream;
   const uint32_t sg = (uint32_t)(batch_res ? seg : (Nc > 0 ? Nc : 1));
   if (B == 0) return HBX_OK;  // batched call without candidates: no records
+  // the scoring launch goes first (it touches none of the per-acquisition state), so the GPU starts on
+  // it while the host is still enqueueing the rest
+  const bool scored = Nc > 0 && !exact_only;
+  if (scored) {
+    hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
+    const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
+    if (rc) return rc;
+  }
   if (batch_res)
     hipLaunchKernelGGL(acq_init_batch_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, U, flags,
                        segcnt, best, key, first1, count, segnear);
@@ -1573,9 +1581,6 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
       hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
       HBX_LAUNCH_CHECK();
     } else {
-      hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
-      const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
-      if (rc) return rc;
       hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
                          flags, first1);
       HBX_LAUNCH_CHECK();

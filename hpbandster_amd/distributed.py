@@ -166,19 +166,19 @@ def acquire_sharded(pair, cands_local, index_base, exchange, stream=None, worksp
     re-score of the ranks' near sets in this process's numpy and a second exchange of those scores."""
     import torch
     from . import exact_host
-    from .kde import AcqResult, RESULT_FMT, ACQ_NEAR_TIE, ACQ_RESOLVED, _rows_of
+    from .kde import AcqResult, RESULT_FMT, ACQ_NEAR_TIE, ACQ_RESOLVED, _rows_of, fetch_bytes
     Nc = int(cands_local.shape[0])
     with N.on_device(pair.good.device, stream):
         ws = workspace if workspace is not None else torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8,
                                                                  device=pair.good.device)
         rv = pair.acquire(cands_local, index_base=index_base, stream=stream, workspace=ws, sync=False,
                           events=events)
-        g = _unpack(exchange.exchange(rv, stream).cpu().numpy().tobytes())
+        g = _unpack(fetch_bytes(exchange.exchange(rv, stream), stream))
         if ties != "process" or not g.flags & ACQ_NEAR_TIE:
             return g.index, g.score, g
         recs = exchange.records()
         best, near = reduce_records_host(recs)
-        mine = _unpack(rv.cpu().numpy().tobytes())
+        mine = _unpack(fetch_bytes(rv, stream))
         pick = None
         if exchange.rank in near:
             if mine.flags & ACQ_NEAR_TIE:  # this rank's own near set (candidate indices local to the shard)
@@ -192,6 +192,6 @@ def acquire_sharded(pair, cands_local, index_base, exchange, stream=None, worksp
         else:
             raw = struct.pack(RESULT_FMT, pick[0] + index_base, pick[1], 0.0, ACQ_RESOLVED, 0, 1, pick[2], pick[3])
         rec = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(pair.good.device)
-        g2 = _unpack(exchange.exchange(rec, stream).cpu().numpy().tobytes())
+        g2 = _unpack(fetch_bytes(exchange.exchange(rec, stream), stream))
         g2.flags |= ACQ_RESOLVED
         return g2.index, g2.score, g2

@@ -15,6 +15,7 @@ rounds exactly like the reference's Python pow), and the small parameter block u
 
 import math
 import struct
+import threading
 
 import numpy as np
 
@@ -62,6 +63,31 @@ def scoring_bucket(vt):
     if N.lib().hbx_kde_bucket(dc, du, N.ptr(dcp), N.ptr(dup), N.ptr(stride)) != 0:
         return -1, -1
     return int(dcp[0]), int(dup[0])
+
+
+_pinned_tls = threading.local()
+
+
+def fetch_bytes(dev_bytes, stream=None):
+    """Bytes of a small device uint8 tensor (a result record) on the host: one copy into a per-thread,
+    per-device pinned buffer on ``stream`` (default: the tensor's device's current stream), one
+    stream synchronisation -- instead of a pageable copy."""
+    torch = _torch()
+    n = int(dev_bytes.numel())
+    dev = dev_bytes.device
+    cache = getattr(_pinned_tls, "bufs", None)
+    if cache is None:
+        cache = _pinned_tls.bufs = {}
+    key = (dev.index, n > 4096)
+    buf = cache.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 4096), dtype=torch.uint8, pin_memory=True)
+        cache[key] = buf
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(s):
+        buf[:n].copy_(dev_bytes, non_blocking=True)
+    s.synchronize()
+    return buf[:n].numpy().tobytes()
 
 
 class AcqResult(object):
@@ -316,7 +342,7 @@ class KDEPair(object):
         rview = ws[off:off + RESULT_BYTES]
         if not sync:
             return rview
-        res = AcqResult.from_bytes(rview.cpu().numpy().tobytes())
+        res = AcqResult.from_bytes(fetch_bytes(rview, stream))
         if ties == "process" and res.flags & ACQ_NEAR_TIE:
             self._resolve(res, ws, Nc, Nc, cands if isinstance(cands, np.ndarray) else c_dev, int(index_base))
         if logs:
@@ -400,7 +426,7 @@ class KDEPair(object):
                                         N.stream_handle(stream, dev)))
         if not sync:
             return out[:B * RESULT_BYTES]
-        raw = out[:B * RESULT_BYTES].cpu().numpy().tobytes()
+        raw = fetch_bytes(out[:B * RESULT_BYTES], stream)
         recs = [AcqResult.from_bytes(raw[i * RESULT_BYTES:(i + 1) * RESULT_BYTES]) for i in range(B)]
         if ties == "process" and any(r.flags & ACQ_NEAR_TIE for r in recs):
             self._resolve_batch(recs, ws, Nc, seg, cands if isinstance(cands, np.ndarray) else c_dev)
