@@ -127,7 +127,9 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     nobs = Xg.shape[0] + Xb.shape[0]
     out = {"value": n * nobs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
            "sample": "%d of the %d candidates x %d observations (D=%d), fp64 C oracle (reference arithmetic), "
-                     "%d threads, %.1f s" % (n, cands.shape[0], nobs, X.shape[1], threads, dt)}
+                     "%d threads (%s), %.1f s" % (n, cands.shape[0], nobs, X.shape[1], threads,
+                                                  "OMP_NUM_THREADS: this job's CPU share of the host"
+                                                  if hi["omp_num_threads"] else "affinity mask", dt)}
     out.update(hi)
     m, t_ref = 0, 0.0
     t0 = time.perf_counter()
