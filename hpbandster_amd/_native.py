@@ -63,6 +63,7 @@ SIGNATURES = {
     "hbx_np_exp": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_pdf_scratch_bytes": (c_i64, [c_i64]),
     "hbx_kde_pdf_exact": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_kde_logpdf_exact": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hbx_rccl_unique_id_bytes": (c_i64, []),
     "hbx_rccl_get_unique_id": (c_i32, [c_vp]),
     "hbx_rccl_comm_init": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32]),

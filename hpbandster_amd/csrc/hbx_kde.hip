@@ -945,6 +945,95 @@ __global__ __launch_bounds__(EXACT_THREADS) void kde_pdf_exact_kernel(const doub
   }
 }
 
+// ln pdf of one KDE at Np points in fp64 log space (one block per point): per observation j the
+// log kernel product t_j = sum_c -(x_c - X_jc)^2 / (2 h_c^2) + sum_u ln K_u (SM:kernels.py:62-64,125
+// with the constants pulled out), then ln pdf = logsumexp_j(t_j) - ln n - sum_c ln(h_c sqrt(2 pi)).
+// No expansion and no fp64 underflow: accurate to ~1e-15 where the reference's own pdf is positive
+// and still finite where the reference's fp64 pdf underflows to 0.  KDEs with negative categorical
+// factors (bandwidth > 1 - 1/c) or structural NaNs are not handled here (NaN out): callers use the
+// exact pdf there.  The mathematically exact counterpart of hbx_kde_logpdf's fp32 estimate.
+__global__ __launch_bounds__(256) void kde_logpdf_exact_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
+                                                              const KdeParams* __restrict__ P,
+                                                              const double* __restrict__ X,
+                                                              const int64_t* __restrict__ rows,
+                                                              double* __restrict__ out) {
+  __shared__ double c0[HBX_MAX_D], c1[HBX_MAX_D], xd[HBX_MAX_D];
+  __shared__ int32_t cont[HBX_MAX_D];
+  __shared__ double rm[4], rs[4];
+  __shared__ double lconst;
+  const int n = P->n;
+  for (int64_t p = blockIdx.x; p < Np; p += gridDim.x) {
+    const double* x = pts + p * D;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      const double h = P->bw[d];
+      const bool c = P->vartype[d] == 0;
+      cont[d] = c;
+      c0[d] = c ? 1.0 / ((h * h) * 2.) : log(1. - h);          // continuous: 1/(2h^2); categorical: ln(1-h)
+      c1[d] = c ? 0.0 : log(h / (double)(P->nlev[d] - 1));     // categorical mismatch: ln(h/(c-1))
+      xd[d] = x[d];
+    }
+    if (threadIdx.x == 0) {
+      double lc = -log((double)n);
+      for (int d = 0; d < D; ++d)
+        if (P->vartype[d] == 0) lc -= log(P->bw[d]) + 0.91893853320467274178;  // ln(h sqrt(2 pi))
+      lconst = lc;
+    }
+    __syncthreads();
+    double m = -INFINITY, sm = 0.0;  // this thread's running logsumexp
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      const double* xr = X + rows[j] * (int64_t)D;
+      double t = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double v = xr[d];
+        if (cont[d]) {
+          const double diff = v - xd[d];
+          t -= diff * diff * c0[d];
+        } else {
+          t += (v == xd[d]) ? c0[d] : c1[d];
+        }
+      }
+      if (t > m) {
+        sm = sm * exp(m - t) + 1.0;
+        m = t;
+      } else if (t > -INFINITY) {
+        sm += exp(t - m);
+      } else if (t != t) {
+        m = NAN;
+      }
+    }
+    // block logsumexp of the (m, sm) pairs
+    for (int o = 32; o > 0; o >>= 1) {
+      const double m2 = __shfl_xor(m, o), s2 = __shfl_xor(sm, o);
+      const double mm = fmax(m, m2);
+      if (m != m || m2 != m2) {
+        m = NAN;
+      } else if (mm > -INFINITY) {
+        sm = (m > -INFINITY ? sm * exp(m - mm) : 0.0) + (m2 > -INFINITY ? s2 * exp(m2 - mm) : 0.0);
+        m = mm;
+      }
+    }
+    if ((threadIdx.x & 63) == 0) {
+      rm[threadIdx.x >> 6] = m;
+      rs[threadIdx.x >> 6] = sm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double M = -INFINITY, Sx = 0.0;
+      bool nan = false;
+      for (int w = 0; w < 4; ++w) {
+        if (rm[w] != rm[w]) nan = true;
+        else if (rm[w] > -INFINITY) {
+          const double mm = fmax(M, rm[w]);
+          Sx = (M > -INFINITY ? Sx * exp(M - mm) : 0.0) + rs[w] * exp(rm[w] - mm);
+          M = mm;
+        }
+      }
+      out[p] = (nan || P->has_neg || P->nan_all || P->nconst) ? NAN : (M > -INFINITY ? M + log(Sx) + lconst : -INFINITY);
+    }
+    __syncthreads();
+  }
+}
+
 // Bound of |exact pdf here - pdf in numpy's arithmetic| / pdf for one KDE at one candidate.  Both run
 // the same IEEE operations in the same order (SM:_kernel_base.py:509-516: per-dim kernels, dim-ordered
 // product, / prod(bw_c), numpy's pairwise sum, / n) except exp, where ocml's and numpy's results may
@@ -1677,6 +1766,20 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
   hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(EXACT_THREADS), 0, (hipStream_t)stream, pts, Np, D,
+                     (const KdeParams*)params, X, rows, out);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// ln pdf in fp64 log space (kde_logpdf_exact_kernel): the accurate log-domain value, NaN where the
+// KDE has negative categorical factors or structural NaNs (use hbx_kde_pdf_exact there).
+int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
+                         const int64_t* rows, double* out, void* stream) {
+  if (!pts || !params || !X || !rows || !out) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_exact: null");
+  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_exact: D=%d", D);
+  if (Np <= 0) return HBX_OK;
+  const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
+  hipLaunchKernelGGL(kde_logpdf_exact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, pts, Np, D,
                      (const KdeParams*)params, X, rows, out);
   HBX_LAUNCH_CHECK();
   return HBX_OK;

@@ -176,6 +176,11 @@ int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax);
 int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                       const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
                       void* stream);
+/* ln KDEMultivariate.pdf (SM:kernel_density.py:162-196) in fp64 log space: logsumexp over the
+ * observations of the log kernel products (no fp64 underflow, ~1e-15 relative).  NaN for KDEs with
+ * negative categorical factors or structural NaNs -- use hbx_kde_pdf_exact there.  out: device f64[Np]. */
+int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
+                         const int64_t* rows, double* out, void* stream);
 
 /* numpy 1.26.4's float64 exp (what the reference's np.exp computes on AVX512_SKX hosts), element-wise
  * on the device: the known-answer check of the exact re-score's exp.  x, y: device f64[n]. */

@@ -88,6 +88,26 @@ def test_exact_pdf_bit_identical_to_reference(device, name):
     np.testing.assert_array_equal(g, c["pdf_g"][:len(C)])
 
 
+@pytest.mark.parametrize("name", G.kde_case_names())
+def test_logpdf_contract_against_reference(device, name):
+    """DeviceKDE.logpdf (fp32 estimate where its bound allows, fp64 log space / exact pdf otherwise)
+    within the north-star 1e-5 of the reference's own ln pdf wherever that is finite; the fp64
+    log-space kernel alone within 1e-12 of it (KDEs with positive factors)."""
+    c = G.load_kde_case(name)
+    pair = _pair_from_fixture(c)
+    C = c["cands"][:128]
+    for k, ref in ((pair.good, c["pdf_l"][:len(C)]), (pair.bad, c["pdf_g"][:len(C)])):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            lref = np.log(ref)
+        fin = np.isfinite(lref)
+        lp = k.logpdf(C)
+        assert np.array_equal(np.isnan(lp), np.isnan(lref))
+        assert (np.abs(lp[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))).max(initial=0.0) <= 1e-5
+        if not (k.has_neg or k.nan_all or k.nconst):
+            lx = k._logpdf_exact(np.ascontiguousarray(C), None)
+            assert (np.abs(lx[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))).max(initial=0.0) <= 1e-12
+
+
 def test_np_exp_known_answers(device):
     """The device restatement of numpy's float64 exp against numpy 1.26.4's own outputs (the pinned
     reference interpreter), 2e4 inputs over every range including subnormal results and overflow."""
@@ -236,6 +256,10 @@ def test_hmode_falls_back_when_cj_exceeds_f16_range(device):
         # -|x'|^2 - |X'|^2 + 2x'.X' cancels terms of ~1e5 (documented in DESIGN.md); the estimate is
         # still within its rigorous bound, which is what keeps the selection exact
         assert err.max() <= 5e-2
+        # DeviceKDE.logpdf keeps the contract everywhere: estimates inside it, exact pdfs for the rest
+        lp = k.logpdf(C)
+        assert np.array_equal(np.isfinite(lp), fin)
+        assert (np.abs(lp[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))).max() <= 1e-5
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C)
     assert res.index == O.select(l, g)[0]
@@ -270,6 +294,8 @@ def test_hmode_categorical_layouts_match_oracle(device, dc, levels):
         # the rigorous per-candidate bound that keeps the selection exact
         assert err.max() <= (1e-5 if dc + du <= 32 else 3e-5), err.max()
         assert np.median(err) <= 1e-6
+        lp = k.logpdf(C)  # the contract at every D
+        assert (np.abs(lp[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))).max() <= 1e-5
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
     assert res.index == O.select(l, g)[0]
