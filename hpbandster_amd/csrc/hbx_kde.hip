@@ -1068,18 +1068,35 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
 
 __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ count,
-                                                        const double* __restrict__ exact_l,
-                                                        const double* __restrict__ exact_g,
+                                                        const double* exact_l,  // (written in this kernel
+                                                        const double* exact_g,  //  through exact_lw / _gw)
                                                         const int32_t* __restrict__ flags, int64_t index_base,
                                                         const KdeParams* __restrict__ Pg,
                                                         const KdeParams* __restrict__ Pb,
                                                         const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
-                                                        int32_t* __restrict__ near_list, AcqResult* __restrict__ res) {
+                                                        int32_t* __restrict__ near_list, AcqResult* __restrict__ res,
+                                                        int32_t nbuf, const double* __restrict__ part,
+                                                        double* exact_lw, double* exact_gw) {
   __shared__ double bs[256];
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
   __shared__ int32_t nnear;
   const int cnt = *count;
+  if (part && cnt <= EXACT_SPLIT_CAP) {  // the split re-score's unit sums -> pdfs (kde_exact_combine's work)
+    for (int pk = threadIdx.x; pk < 2 * cnt; pk += 256) {
+      const bool isl = pk & 1;
+      const int n = (isl ? Pg : Pb)->n;
+      const double* us = part + (int64_t)pk * nbuf * PW_UNITS;
+      double acc = 0.0;
+      for (int c = 0, b = 0; c < n; c += PW_BUF, ++b) {
+        const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
+        acc = acc + pw_combine_units(m, us + b * PW_UNITS);
+      }
+      (isl ? exact_lw : exact_gw)[pk >> 1] = acc / (double)n;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
   double best = INFINITY;
   int64_t bidx = INT64_MAX;
   int32_t bpos = -1;
@@ -1665,6 +1682,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res);
   HBX_LAUNCH_CHECK();
   const dim3 grid((unsigned)((Nc + 255) / 256));
+  bool fuse_combine = false;
   if (Nc > 0) {
     if (exact_only) {
       hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
@@ -1682,10 +1700,14 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                        (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
                        rows_bad, list, count, nbuf, part, exact_l, exact_g);
     HBX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 255) / 256), dim3(256), 0, s,
-                       (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,
-                       exact_g);
-    HBX_LAUNCH_CHECK();
+    // single acquisition: the final kernel combines the unit sums itself (one launch less)
+    fuse_combine = !batch_res && !(exact_only && (logl_out || logg_out));
+    if (!fuse_combine) {
+      hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 255) / 256), dim3(256), 0, s,
+                         (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,
+                         exact_g);
+      HBX_LAUNCH_CHECK();
+    }
     if (exact_only && (logl_out || logg_out)) {
       hipLaunchKernelGGL(kde_exact_logs_kernel, grid, dim3(256), 0, s, list, count, exact_l, exact_g, logl_out,
                          logg_out);
@@ -1694,7 +1716,9 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   }
   if (!batch_res) {
     hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
-                       index_base, (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, res);
+                       index_base, (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, res,
+                       (int32_t)((nmax + PW_BUF - 1) / PW_BUF), fuse_combine ? part : (const double*)nullptr,
+                       exact_l, exact_g);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }
