@@ -39,18 +39,29 @@ N_SIMD = 1024              # 256 CUs x 4 SIMDs
 
 
 def kernel_model(kde_obj, dc, du):
-    """Name and per-256-pair cost model of the scoring kernel a prepared KDE runs (hbx_score_h.hip).
+    """Name and per-256-pair cost model of the scoring kernel a prepared KDE runs.
 
-    One 16x16 output tile = 16 candidates x 16 observations = 256 pairs per SIMD:
+    hbx_score_h.hip (16x16 tiles, variant bit 4): one output tile = 16 candidates x 16 observations =
+    256 pairs per SIMD:
       matrix pipe: NSC dense 16x16x32 f16 MFMAs + KC/2 sparse 16x16x64 (16 cycles each)
       issue:       8 cycles held per matrix instruction + 4 v_exp_f32 (8 each) + 4 v_add_f32 (4 each)
-    (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost').  Dense-equivalent matrix work: 2 x 32 x
-    (NSC + KC) flops per pair."""
+    hbx_score_h32.hip (32x32 tiles, variant bit 6): one tile = 1024 pairs:
+      matrix pipe: 2 NSC dense 32x32x16 f16 MFMAs + KC sparse 32x32x32 (32 cycles each)
+      issue:       8 cycles held per matrix instruction + 16 v_exp_f32 + 16 v_add_f32
+    both quoted per 256 pairs (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost').  Dense-equivalent
+    matrix work: 2 x 32 x (NSC + KC) flops per pair either way."""
     v = kde_obj.variant
-    signed, kc, hmode = v & 1, (v >> 1) & 7, (v >> 4) & 1
+    signed, kc, hmode, h32 = v & 1, (v >> 1) & 7, (v >> 4) & 1, (v >> 6) & 1
     if not hmode:
         return {"kernel": "kde_logpdf_%s_kernel (f32 MFMA fallback)" % ("oh" if kc else ""), "model": None}
     nsc = (4 * kde_obj.dc_pad + 31) // 32
+    if h32:
+        n_mat = 2 * nsc + kc  # per 1024 pairs
+        return {"kernel": "kde_logpdf_h32_kernel<%d,%d>" % (nsc, kc),
+                "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
+                          "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + 16 * 8 + 16 * 4) / 4,
+                          "bound_cycles": max(32 * n_mat, 8 * n_mat + 16 * 8 + 16 * 4) / 4,
+                          "dense_equiv_flops_per_pair": 2 * 32 * (nsc + kc)}}
     sparse = (not signed) and kc > 0 and kc % 2 == 0
     n_mat = nsc + (kc // 2 if sparse else kc)
     pipe = 16 * n_mat
@@ -612,7 +623,7 @@ def main():
     traffic = load_traffic(workload)
     km = kernel_model(pair.bad, a.dc, a.du)
     if fused:
-        km["kernel"] = km["kernel"].replace("kde_logpdf_h_kernel", "kde_logpdf_h_pair_kernel")
+        km["kernel"] = km["kernel"].replace("_kernel<", "_pair_kernel<")
     mfma_util = issue_bound = None
     if km["model"]:
         m = km["model"]

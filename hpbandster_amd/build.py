@@ -42,7 +42,7 @@ def _flags():
 
 # per-file extra flags: the scoring loops interleave MFMAs with scalar f32 adds; SLP packing them into
 # v_pk_add_f32 costs more issue cycles beside MFMAs than the plain adds (MI355X_MICROARCH.md)
-EXTRA_FLAGS = {"hbx_score_h.hip": ["-fno-slp-vectorize"], "hbx_score_oh.hip": ["-fno-slp-vectorize"],
+EXTRA_FLAGS = {"hbx_score_h.hip": ["-fno-slp-vectorize"], "hbx_score_h32.hip": ["-fno-slp-vectorize"], "hbx_score_oh.hip": ["-fno-slp-vectorize"],
                "hbx_score_f32.hip": ["-fno-slp-vectorize"]}
 
 

@@ -43,8 +43,9 @@ static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
   if (dc_pad < 0 || du_pad < 0) return 1;
   int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
-  const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1);
+  const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1), d = h32_chunk_floats(nsc_of(dc_pad), OH_MAX_KC);
   a = a > b ? a : b;
+  a = a > d ? a : d;
   return n_chunks(n) * (int64_t)(a > c ? a : c);
 }
 
@@ -60,6 +61,7 @@ struct PrepArgs {
   int32_t* info;        // device i32[8]
   int32_t n, D;
   int32_t hm_allowed;   // HBX_HMODE not 0
+  int32_t h32_allowed;  // HBX_H32 not 0
   int32_t nblk_table;   // blocks of this KDE in the table launches
   uint32_t vt[HBX_MAX_D / 32];  // bit d: dim d categorical ('u')
 };
@@ -269,10 +271,13 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
   // otherwise the exact f32 MFMA product.  |C_j| beyond the f16 range is caught after the table.
   const bool hm_ok = (du == 0 || kc > 0) && dcp >= 8;
-  const int hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
+  int hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
+  // the 32x32-tile kernel (hbx_score_h32.hip) for unsigned sums in the buckets it is built for
+  if (hmode && A.h32_allowed && !has_neg && h32_ok(nsc_of(dcp), kc)) hmode = 2;
   P->hmode = hmode;
   P->nsc = nsc_of(dcp);
-  P->chunk_floats = hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0);
+  P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), kc)
+                               : (hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0));
 }
 
 // Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
@@ -281,7 +286,8 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
 // layout; |C_j| and |X'| maxima go to *cmax_acc / P->xmax.
 __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, const KdeParams* __restrict__ P,
                                                KdeParams* __restrict__ Pw, float* __restrict__ table, int j,
-                                               bool hm, int chunk_f, float* cmax_acc) {
+                                               int hm, int chunk_f, float* cmax_acc, _Float16* hst) {
+  // hst: this thread's LDS row (H32_ROW_MAX halves) where the h32 layout's dense slots are assembled
   // P: the parameters as read (an LDS copy); Pw: the global block, written (xmax, cmax / cmax2,
   // const_level) -- fields disjoint from every one read here
   const int n = P->n;
@@ -292,19 +298,30 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   const int KP = kp_of(dcp);
   float* ch = table + (int64_t)(j / OBS_CHUNK) * chunk_f;
   const int jj = j % OBS_CHUNK;
-  const int KTP = h_ktp(dcp, P->kc);
-  _Float16* hrow = (_Float16*)(ch + OBS_CHUNK) + jj * KTP;
+  // hm: 0 = f32 layout, 1 = hmode (16x16 kernel), 2 = h32 (32x32 kernel, no chunk header)
+  const int KTP = hm == 2 ? h32_ktp(P->nsc, P->kc) : h_ktp(dcp, P->kc);
+  _Float16* hrow = (_Float16*)(hm == 2 ? ch : ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
   // hmode rows are written 16 bytes (8 halves) at a time: two dims' h, l, h, l per store
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   h8 grp = {};
+  const int nd32 = h32_nd(P->nsc);
+  if (hm == 2)
+    for (int q = 0; q < 2 * nd32; ++q) *(h8*)(hst + 8 * q) = h8{};
 #pragma unroll 8
   for (int k = 0; k < (hm ? dcp : KP - 2); ++k) {
     float v = 0.f;
     if (ok && k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
     C -= (double)v * (double)v;
     if (slot) {
-      if (hm) {
+      if (hm == 2) {  // slots 6 + 3k: Xh, Xl, Xh
+        const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
+        const _Float16 h = (_Float16)vc;
+        const _Float16 l = (_Float16)(vc - (float)h);
+        hst[6 + 3 * k] = h;
+        hst[7 + 3 * k] = l;
+        hst[8 + 3 * k] = h;
+      } else if (hm) {
         const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
         const _Float16 h = (_Float16)vc;
         const _Float16 l = (_Float16)(vc - (float)h);
@@ -323,20 +340,52 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&Pw->xmax[k], a);
   }
   const h8 z8 = {};
-  if (hm && slot) {  // dc_pad is a multiple of 8: the dims filled whole groups
+  if (hm == 1 && slot) {  // dc_pad is a multiple of 8: the dims filled whole groups
     for (int k = 4 * dcp; k < 32 * P->nsc; k += 8) *(h8*)(hrow + k) = z8;
     for (int k = 32 * (P->nsc + P->kc); k < KTP; k += 8) *(h8*)(hrow + k) = z8;
   }
+  if (hm == 2 && slot)  // row padding past the index words (rows are 16-byte aligned, KTP % 8 == 0)
+    for (int k = (16 * nd32 + 16 * P->kc + 4 * h32_ksp(P->kc)) & ~7; k < KTP; k += 8) *(h8*)(hrow + k) = z8;
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
       const float v = (ok && u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
       if (slot) ch[KP * KROW + jj * dup + u] = v;
     }
+  } else if (slot && hm == 2) {
+    // 2:4-compressed one-hot (h32 layout): per step s and group g (positions t0 = 16s + 2g and t0 + 1, a
+    // dim's positions never straddle a group) the observation's (delta hi, lo) when its level is t0 or
+    // t0 + 1, and the index nibble (slots 0,1: 0x4; slots 2,3: 0xE); index dword ksp h + s holds groups
+    // 4h..4h+3 of step s
+    _Float16* cz = hrow + 16 * nd32;
+    const int ksp = h32_ksp(P->kc);
+    uint32_t iw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (int s = 0; s < P->kc; ++s) {
+      h8 v[2] = {{}, {}};
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const int t0 = 16 * s + 2 * g;
+        bool m0 = false, m1 = false;
+        if (ok && t0 < P->oh_total) m0 = x[P->oh_col[t0]] == P->oh_val[t0];
+        if (ok && t0 + 1 < P->oh_total) m1 = x[P->oh_col[t0 + 1]] == P->oh_val[t0 + 1];
+        if (m0 || m1) {
+          const int u = P->oh_dim[m1 ? t0 + 1 : t0];
+          const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
+          const float hi = (float)(_Float16)dl;
+          v[g >> 2][2 * (g & 3)] = (_Float16)hi;
+          v[g >> 2][2 * (g & 3) + 1] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
+        }
+        iw[ksp * (g >> 2) + s] |= (m1 ? 0xEu : 0x4u) << (4 * (g & 3));
+      }
+      *(h8*)(cz + 16 * s) = v[0];
+      *(h8*)(cz + 16 * s + 8) = v[1];
+    }
+    uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 16 * P->kc);
+    for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
   } else if (slot) {
     const int W = P->kc * 32;  // one-hot halves per observation
     _Float16* oh;
     _Float16* par;
-    if (hm) {
+    if (hm == 1) {
       oh = hrow + 32 * P->nsc;
       par = (_Float16*)(ch + OBS_CHUNK + OBS_CHUNK * KTP / 2) + jj * h_kpp(P->kc);
     } else {
@@ -364,24 +413,33 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
         if (P->has_neg) *(h8*)(par + k - 7) = pg;
       }
     }
-    if (hm && P->has_neg)
+    if (hm == 1 && P->has_neg)
       for (int k = W; k < h_kpp(P->kc); k += 8) *(h8*)(par + k) = z8;
   }
   C += P->lb_sum - P->m0_log2;
   const float Cf = ok ? (float)C : -1e30f;
   if (slot) {
     if (hm) {
-      ch[jj] = Cf;
+      if (hm == 1) ch[jj] = Cf;
       // C_j as three f16 pieces in the lo.lo slots 4c+3 of dims c = 0, 1, 2 (A side = 1 there);
-      // padding rows get -60000, so their terms underflow to 0 (c_i <= 0, the rest of the row is 0)
+      // padding rows get -60000, so their terms underflow to 0 (c_i <= 0, the rest of the row is 0;
+      // h32: the shifted c_i stays below H32_CMAX = 30000)
       const float cv = ok ? fmaxf(Cf, -H_CMAX) : -H_CMAX;
       const _Float16 c0 = (_Float16)cv;
       const float r1 = cv - (float)c0;
       const _Float16 c1 = (_Float16)r1;
       const _Float16 c2 = (_Float16)(r1 - (float)c1);
-      hrow[3] = c0;
-      hrow[7] = c1;
-      hrow[11] = c2;
+      if (hm == 2) {  // slots 0-2: the C_j pieces; 3-5: 1 against the candidate's c_i pieces
+        hst[0] = c0;
+        hst[1] = c1;
+        hst[2] = c2;
+        hst[3] = hst[4] = hst[5] = (_Float16)1.f;
+        for (int q = 0; q < 2 * nd32; ++q) *(h8*)(hrow + 8 * q) = *(const h8*)(hst + 8 * q);
+      } else {
+        hrow[3] = c0;
+        hrow[7] = c1;
+        hrow[11] = c2;
+      }
     } else {
       ch[0 * KROW + jj] = Cf;
       ch[1 * KROW + jj] = 1.f;
@@ -416,6 +474,7 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
   __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
   for (int i = threadIdx.x; i < (int)((sizeof(KdeParams) + 15) / 16); i += 64) pl[i] = ((const uint4*)P)[i];
   __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
+  __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_MAX];  // h32 rows assembled here
   const int D = A.D, n = A.n;
   const KdeParams* Pl = (const KdeParams*)pl;
   float* tab = second ? table1 : table0;
@@ -423,10 +482,10 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
   // (a generic pointer would make each row read wait for the outstanding table stores as well)
   auto run = [&](const double* x) {
     if (pass == 0)
-      kde_table_body(x, Pl, P, tab, j, Pl->hmode != 0, Pl->chunk_floats, &P->cmax);
+      kde_table_body(x, Pl, P, tab, j, Pl->hmode, Pl->chunk_floats, &P->cmax, h32s + threadIdx.x * H32_ROW_MAX);
     else
-      kde_table_body(x, Pl, P, tab, j, false, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
-                     &P->cmax2);
+      kde_table_body(x, Pl, P, tab, j, 0, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
+                     &P->cmax2, h32s + threadIdx.x * H32_ROW_MAX);
   };
   if (D <= TABLE_STAGE_D) {
     const int DS = D | 1;  // odd row stride: the 64 threads' reads of one dim hit distinct banks
@@ -458,7 +517,8 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
 }
 
 // Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
-// du_pad}; variant = has_neg | kc << 1 | hmode << 4 selects the scoring kernel.
+// du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6
+// selects the scoring kernel.
 __global__ void kde_prep_finish_kernel(PrepSet ps) {
   const int k = threadIdx.x;
   if (k >= ps.nk) return;
@@ -470,7 +530,7 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
     P->cmax = P->cmax2;
   }
   int32_t* info = A.info;
-  info[0] = P->has_neg | (P->kc << 1) | (P->hmode << 4) | (P->exact_only << 5);
+  info[0] = P->has_neg | (P->kc << 1) | ((P->hmode != 0) << 4) | (P->exact_only << 5) | ((P->hmode == 2) << 6);
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
@@ -512,6 +572,8 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
   A->n = n;
   A->D = D;
   A->hm_allowed = !(hm_env && hm_env[0] == '0');
+  const char* h32_env = getenv("HBX_H32");  // 0: the 16x16-tile hmode kernel instead of the 32x32 one
+  A->h32_allowed = !(h32_env && h32_env[0] == '0');
   A->nblk_table = (dcp < 0 || dup < 0) ? 0 : (int32_t)prep_table_blocks(n);
   return HBX_OK;
 }
@@ -1330,7 +1392,7 @@ static logpdf_fn pick_rescue(int dc_pad) {
 }
 
 // variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
-// bit 4 = hmode (whole exponent on the f16 matrix cores)
+// bit 4 = hmode (whole exponent on the f16 matrix cores), bit 6 = its 32x32-tile kernel (h32 table)
 static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const bool sg = variant & 1;
   const int kc = du_pad == 0 ? 0 : (variant >> 1) & 7;  // no categorical dims: kc irrelevant
@@ -1339,6 +1401,11 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   bucket_dims(dc_pad, du_pad, &dcp, &dup);
   if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr, nullptr};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
+  if (hm && ((variant >> 6) & 1)) {
+    if (dc_pad < 8 || sg) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
+    return {hbx_pick_h32(nsc_of(dc_pad), kc), r, 32 * H16_WAVES, 64 * H16_WAVES, hbx_pick_h32_pair(nsc_of(dc_pad), kc),
+            pick_rescue_pair<false>(dc_pad)};
+  }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
     return {hbx_pick_h(nsc_of(dc_pad), kc, sg), r, 16 * H16_WAVES * H_ROW_TILES, 64 * H16_WAVES,

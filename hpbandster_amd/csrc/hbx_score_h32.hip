@@ -1,0 +1,424 @@
+// hbx_score_h32.hip -- hmode scoring on 32x32 matrix tiles, observations on the A side (hmode 2).
+//
+// Same exponent as hbx_score_h.hip (continuous hi/lo f16 products, C_j as three exact f16 pieces, the
+// one-hot product on the sparse matrix cores), on v_mfma_f32_32x32x16_f16 / v_smfmac_f32_32x32x32_f16.
+// Why: the 16x16 kernel is bound by the SIMD's vector ISSUE port, not by the matrix pipe.  Per 1024
+// pairs it spends 16 MFMAs x 8 issue cycles + 16 v_exp_f32 x 8 + 16 v_add_f32 x 4 = 320 cycles against
+// 256 cycles of matrix pipe; a 32x32x16 MFMA holds the issue port for 8 of its 32 cycles, so the same
+// work costs 8 x 8 + 128 + 64 = 256: two exp2 and two adds (24 cycles) hide in each MFMA's gap
+// (MI355X_MICROARCH, 'vector-instruction ISSUE cost').
+//
+// Roles: A = observations (32 rows per tile, read from the LDS ring; the one-hot part 2:4-compressed
+// in the table, hbx_kde_impl.h h32 layout), B = candidates (32 columns per wave, resident in registers).
+// The output column of a lane is ONE candidate, so a lane's 16 accumulator registers are 16
+// observations of the same candidate: the exp2 sum is an in-register tree and a lane carries one
+// running sum (the 16x16 kernel's A = candidates layout needs 16 per lane here).  The candidate's
+// c_i cannot then be the accumulator input (it would take 16 registers): it rides as three exact f16
+// pieces in the lo.lo slots of dims 3-5 against 1 on the observation side, like C_j in dims 0-2.
+//
+// Operand layouts (gfx950, tools/mfma32_probe.hip, profiles/r01/mfma32_probe.txt):
+//   dense A: lane l holds row l%32, K = 8(l/32) + 0..7;  dense B: K = 8(l/32) + 0..7 of column l%32;
+//   D: register r of lane l = row 8(r/4) + 4(l/32) + r%4, column l%32;
+//   sparse A: lane l covers row l%32, dense K [16(l/32), +16) as four 2-of-4 groups (index nibbles);
+//   sparse B: lane half h holds K = 8h..8h+7 and 16+8h..16+8h+7 of column l%32.
+//
+// Pipeline per 64-observation chunk c (tiles T0, T1 of 32 observations), one basic block per phase:
+//   LDS-DMA of chunk c+3 (part 0) | MFMAs of T0(c), each A fragment re-read for T1(c) right behind
+//   its MFMA | exp2/sum of T1(c-1) beside them | LDS-DMA part 1 | wait chunk c+1 + barrier |
+//   MFMAs of T1(c), fragments re-read for T0(c+1) | exp2/sum of T0(c) beside them.
+#include "hbx_common.h"
+#include "hbx_kde_impl.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef HBX_H32_ABL
+#define HBX_H32_ABL 0  // TEMP ablation bits: 1 no loop DMA, 2 no loop barrier, 4 no duplicate pieces, 8 no exp2
+#endif
+#define H32_CMAX 30000.f    // |shifted c_i| limit of the three-piece split (else: rescue pass)
+
+// sparse index words of one tile: KS dwords (one ds_read)
+template <int KS> struct H32Idx { typedef u32x4 T; };
+template <> struct H32Idx<1> { typedef uint32_t T; };
+template <> struct H32Idx<2> { typedef u32x2 T; };
+template <int KS, typename T> __device__ __forceinline__ int h32_idx(const T& v, int s) {
+  if constexpr (KS == 1) return (int)v;
+  else return (int)v[s];
+}
+
+// sched_group_barrier pattern of one phase: NM times {1 MFMA, its fragment re-read(s), a share of the
+// NV VALU ops} (the last matrix instruction re-reads its fragment and the index words)
+template <int I, int NM, int NV, int NRL>
+struct SgbH32 {
+  static __device__ __forceinline__ void run() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, I == NM - 1 ? NRL : 1, 0);
+    constexpr int n = NV / NM + (I < NV % NM ? 1 : 0);
+    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x002, n, 0);
+    SgbH32<I + 1, NM, NV, NRL>::run();
+  }
+};
+template <int NM, int NV, int NRL>
+struct SgbH32<NM, NM, NV, NRL> {
+  static __device__ __forceinline__ void run() {}
+};
+
+template <int NSC, int KC>
+__device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                    const KdeParams* __restrict__ P,
+                                                    const float* __restrict__ table, KdeEst* __restrict__ out,
+                                                    const unsigned blk) {
+  constexpr int ND = h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + 3 slots per continuous dim)
+  constexpr int KS = KC;       // sparse 32-wide K-steps (one-hot)
+  constexpr int NMT = ND + KS; // matrix instructions per 32x32 tile
+  constexpr int KTP = h32_ktp(NSC, KC);
+  constexpr int CHF = h32_chunk_floats(NSC, KC);
+  constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
+  constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
+  // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
+  constexpr int NBUF = 2 * (4 * CHF + AUXF) * 4 <= 160 * 1024 ? 4 : 3;
+  static_assert(2 * (NBUF * CHF + AUXF) * 4 <= 160 * 1024, "two blocks per CU");
+  constexpr int GP = CHF * 4 / 1024;  // 1-KB LDS-DMA pieces per chunk: GL per wave, one more for NX waves
+  constexpr int GL = GP / HW, NX = GP % HW;
+  static_assert(GP * 1024 == CHF * 4, "chunk must be a multiple of 1 KB");
+  __shared__ __align__(16) float lds[NBUF * CHF + AUXF];  // the kernel's only LDS object
+  float* aux = lds + NBUF * CHF;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t cbase = ((int64_t)blk * HW + wave) * 32;
+  const bool xpiece = wave < NX;
+  const int n = P->n, dc = P->dc;
+
+  // per-dim parameters and the block's candidate rows staged in the (not yet used) ring
+  struct ContPrm { double scale, center; float xmax; int32_t col; };
+  struct OhPrm { double val; int32_t col, pad; };
+  constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 16 * (KC > 0 ? KC : 1) * (int)sizeof(OhPrm);
+  static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
+  const int DS = D | 1;  // odd row stride in doubles: conflict-free
+  const int64_t rows_bytes = (int64_t)HW * 32 * DS * 8;
+  const bool rows_fit = rows_bytes + PRM_BYTES <= (int64_t)NBUF * CHF * 4;
+  ContPrm* cprm = (ContPrm*)((char*)lds + (rows_fit ? rows_bytes : 0));
+  OhPrm* oprm = (OhPrm*)(cprm + 8 * NSC);
+  const int tid = threadIdx.x;
+  if (tid < 8 * NSC) {
+    const bool act = tid < dc;  // padding: never read unmasked
+    cprm[tid] = ContPrm{act ? P->cont_scale[tid] : 0.0, act ? P->center[tid] : 0.0, act ? P->xmax[tid] : 0.f,
+                        act ? P->cont_dim[tid] : 0};
+  }
+  if (tid < 16 * KC) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
+  const bool staged = rows_fit && cbase < Nc;
+  const int64_t nv = (Nc - cbase) < 32 ? (Nc - cbase) : 32;  // valid rows of this wave
+  double* xs = (double*)lds + (int64_t)wave * 32 * DS;
+  if (staged) {
+    const double* src = cand + cbase * (int64_t)D;
+    if (D <= 64) {  // 64 / D rows per pass, coalesced
+      const int rpi = 64 / D, lr = lane / D, lcl = lane - lr * D;
+      if (lr < rpi)
+        for (int row = lr; row < nv; row += rpi) xs[row * DS + lcl] = src[row * D + lcl];
+    } else {
+      for (int row = 0; row < nv; ++row)
+        for (int k = lane; k < D; k += 64) xs[row * DS + k] = src[row * D + k];
+    }
+  }
+  __syncthreads();
+
+  // B operands of candidate column c.  Dense step s, half j of the lane: slot k = 16s + 8h + j -- slots
+  // 0-2: 1 (against the C_j pieces), 3-5: the pieces of the shifted c_i (against 1; 0 in the probe),
+  // 6 + 3d + {0,1,2}: (hi, hi, lo) of x''_d against the observation's (Xh, Xl, Xh).  Sparse step s:
+  // one-hot positions 16s + 4h + q (halves 2q, 2q+1) and 16s + 8 + 4h + q (halves 8 + 2q, +1), both
+  // halves 1 on a match.
+  f16x8 bd[ND];
+  f16x16 bsp[KS > 0 ? KS : 1];
+  float ci = 0.f, bnd = 0.f;
+  auto build = [&](const double* x) {
+    auto coord = [&](int d) {  // 2 x'_d (0 past the continuous dims), clamped to the f16 range
+      const ContPrm q = cprm[d];
+      const float v0 = (float)(q.scale * (x[q.col] - q.center));
+      return d < dc ? v0 : 0.f;
+    };
+#pragma unroll
+    for (int s = 0; s < ND; ++s) bd[s] = f16x8{};
+    if (h == 0) bd[0][0] = bd[0][1] = bd[0][2] = (_Float16)1.f;
+    // every lane walks all dims (compile-time slot positions; each lane keeps its half's slots)
+#pragma unroll
+    for (int d = 0; d < 8 * NSC; ++d) {
+      const float v = coord(d);
+      ci = fmaf(-v, v, ci);
+      bnd = fmaf(2.f * fabsf(v), cprm[d].xmax, bnd);
+      const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
+      const _Float16 hi = (_Float16)xc;
+      const _Float16 lo = (_Float16)(xc - (float)hi);
+#pragma unroll
+      for (int comp = 0; comp < 3; ++comp) {
+        const int k = 6 + 3 * d + comp;
+        if (h == ((k >> 3) & 1)) bd[k >> 4][k & 7] = comp < 2 ? hi : lo;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const OhPrm o0 = oprm[16 * s + 4 * h + q], o1 = oprm[16 * s + 8 + 4 * h + q];
+        const _Float16 m0 = (x[o0.col] == o0.val) ? (_Float16)1.f : (_Float16)0.f;
+        const _Float16 m1 = (x[o1.col] == o1.val) ? (_Float16)1.f : (_Float16)0.f;
+        bsp[s][2 * q] = m0;
+        bsp[s][2 * q + 1] = m0;
+        bsp[s][8 + 2 * q] = m1;
+        bsp[s][8 + 2 * q + 1] = m1;
+      }
+    }
+  };
+  {
+    const int loc = c < nv ? c : (int)nv - 1;
+    if (staged) {
+      build(xs + loc * DS);
+    } else {
+      int64_t ii = cbase + c;
+      if (ii >= Nc) ii = Nc - 1;
+      build(cand + ii * (int64_t)D);
+    }
+  }
+
+  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
+  // LDS-DMA of chunk cc into ring slot `slot`; part p issues the pieces g with g % 2 == p.  Every wave
+  // issues GL + 1 pieces when GP is not a multiple of HW: the waves without an extra piece load their
+  // first one again (same bytes to the same place), so the loop body has no branch -- a branch would
+  // split the phases' scheduling regions -- and every wave's counted vmcnt is the same.
+  auto issue = [&](int cc, int slot, int part) {
+    const float* src = table + (int64_t)(cc < nchunks ? cc : nchunks - 1) * CHF;
+    float* dst = lds + slot * CHF;
+#pragma unroll
+    for (int g = 0; g < GL + (NX ? 1 : 0); ++g) {
+      const int piece = (g < GL || xpiece) ? wave + g * HW : wave % GP;
+      if ((HBX_H32_ABL & 4) && !(g < GL || xpiece)) continue;
+      if (g % 2 == part)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
+    }
+  };
+  constexpr int GW = GL + (NX ? 1 : 0);  // pieces per wave per chunk
+  constexpr int PD = NBUF - 1;  // chunks in flight ahead of the one being read
+  __syncthreads();  // every wave has read its staged rows and the parameters: the ring may be overwritten
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    issue(i, i, 0);
+    issue(i, i, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GW * (PD - 1)) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // A fragments of one 32-observation tile: row 32 jt + c, halves 8h.. of every step, and the lane
+  // half's index words (at 2 ksp h halves past the compressed one-hot part)
+  f16x8 ad[ND];
+  f16x8 asp[KS > 0 ? KS : 1];
+  typename H32Idx<KS>::T aix;
+  const int ixo = 16 * ND + 16 * KC + 2 * h32_ksp(KC) * h - 8 * h;  // index words relative to arow
+  auto arow = [&](const float* buf, int jt) { return (const _Float16*)buf + (32 * jt + c) * KTP + 8 * h; };
+  auto readA = [&](const float* buf, int jt) {
+    const _Float16* a = arow(buf, jt);
+#pragma unroll
+    for (int s = 0; s < ND; ++s) ad[s] = *(const f16x8*)(a + 16 * s);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
+    if constexpr (KS > 0) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+  };
+  const f32x16 zero16 = {};
+  // the tile's matrix instructions
+  auto mma = [&](f32x16& acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[0], zero16, 0, 0, 0);
+#pragma unroll
+    for (int s = 1; s < ND; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+  };
+  // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it
+  auto mma_rd = [&](f32x16& acc, const float* nb, int jt) {
+    const _Float16* a = arow(nb, jt);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[0], zero16, 0, 0, 0);
+    ad[0] = *(const f16x8*)a;
+#pragma unroll
+    for (int s = 1; s < ND; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[s], acc, 0, 0, 0);
+      ad[s] = *(const f16x8*)(a + 16 * s);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
+      if (s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+    }
+  };
+
+  // Per-candidate shift (see hbx_score_h.hip): the exponent's maximum over chunk 0 is moved to 0.  The
+  // probe runs without c_i (its B slots are 0); the maximum with it is c_i + the probe's maximum.
+  {
+    f32x16 a0, a1;
+    readA(lds, 0);
+    mma(a0);
+    readA(lds, 1);
+    mma(a1);
+    float mx = fmaxf(a0[0], a1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(a0[r], a1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float d = rintf(-(ci + mx));
+    const float dl = (d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
+    const float cs = ci + dl;                           // the shifted c_i (its rounding is in the bound)
+    const bool big = fabsf(cs) > H32_CMAX;              // beyond the split: the rescue pass
+    const float cv = big ? 0.f : cs;
+    const _Float16 p0 = (_Float16)cv;
+    const float r1 = cv - (float)p0;
+    const _Float16 p1 = (_Float16)r1;
+    const _Float16 p2 = (_Float16)(r1 - (float)p1);
+    // slots 3-5 = step 0, lane half 0, halves 3-5
+    if (h == 0) {
+      bd[0][3] = p0;
+      bd[0][4] = p1;
+      bd[0][5] = p2;
+    }
+    if (h == 0) {
+      float* ax = aux + (wave * 32 + c) * 4;
+      ax[0] = ci;
+      ax[1] = bnd;
+      ax[2] = dl;
+      ax[3] = big ? 1.f : 0.f;
+    }
+  }
+
+  // exp2 of a tile's 16 terms and their pairwise sum (depth 4)
+  auto tile_sum = [&](const f32x16& a) -> float {
+    float e[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) e[r] = (HBX_H32_ABL & 8) ? a[r] : __builtin_amdgcn_exp2f(a[r]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int r = 0; r < w; ++r) e[r] = e[2 * r] + e[2 * r + 1];
+    return e[0];
+  };
+  auto schedule = [&]() {
+    SgbH32<0, NMT, 32, (KS > 0 ? 2 : 1)>::run();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // Main loop.  Sums: a tile's 16 terms pairwise (depth 4), the chunk's two tiles (1), the chunks in
+  // order (nchunks), the two lane halves (1).
+  float S = 0.f, Sb = 0.f;
+  f32x16 accA, accB;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accB[r] = -INFINITY;  // "T1(-1)": exp2 -> 0
+  readA(lds, 0);
+  for (int cc = 0; cc < nchunks; ++cc) {
+    const float* buf = lds + (cc % NBUF) * CHF;
+    const float* nbuf = lds + ((cc + 1) % NBUF) * CHF;
+    // chunk cc+PD's buffer was last read before the previous iteration's barrier
+    if (!(HBX_H32_ABL & 1)) issue(cc + PD, (cc + PD) % NBUF, 0);
+    mma_rd(accA, buf, 1);  // T0(cc); fragments of T1(cc)
+    Sb += tile_sum(accB);  // T1(cc-1): chunk cc-1 complete
+    S += Sb;
+    schedule();
+    if (!(HBX_H32_ABL & 1)) issue(cc + PD, (cc + PD) % NBUF, 1);
+    // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
+    // the barrier makes chunk cc+1 visible to every wave
+    if (!(HBX_H32_ABL & 2)) {
+      if (HBX_H32_ABL & 4) {
+        if (xpiece) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    mma_rd(accB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
+    Sb = tile_sum(accA);  // T0(cc)
+    schedule();
+  }
+  Sb += tile_sum(accB);
+  S += Sb;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+  S += __shfl_xor(S, 32);
+  if (h == 0) {
+    const int64_t ii = cbase + c;
+    if (ii < Nc) {
+      const float* ax = aux + (wave * 32 + c) * 4;
+      const float ci_q = ax[0], bnd_q = ax[1], dq = ax[2];
+      const bool big = ax[3] != 0.f;
+      const double* x = cand + ii * (int64_t)D;
+      bool nq = P->nan_all != 0;
+      for (int k = 0; k < P->nconst; ++k)
+        if (x[P->const_dim[k]] != P->const_level[k]) nq = true;
+      // S carries the factor 2^dq; |c_i| + dq bounds the rounding of the shifted c_i
+      KdeEst o = finish_est_terms(P, S, 0.f, -dq, nq, ci_q - dq, bnd_q, false, (float)(nchunks + 6 + 24));
+      // f16 hi/lo representation error of both coordinates and the six lo.lo products given up to the
+      // C_j / c_i pieces (together <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
+      if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-19f) * HBX_LN2f;
+      if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) o.err = -1.f;  // rescue marker
+      out[ii] = o;
+    }
+  }
+}
+
+template <int NSC, int KC>
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
+    const float* __restrict__ table, KdeEst* __restrict__ out) {
+  kde_logpdf_h32_body<NSC, KC>(cand, Nc, D, P, table, out, blockIdx.x);
+}
+
+// both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
+template <int NSC, int KC>
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_pair_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+  const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
+  kde_logpdf_h32_body<NSC, KC>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                               second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+}
+
+template <int NSC, int KC>
+static constexpr bool h32_built() { return h32_ok(NSC, KC); }
+
+template <int NSC>
+static logpdf_fn pick32_kc(int kc) {
+  switch (kc) {
+    case 0: if constexpr (h32_built<NSC, 0>()) return kde_logpdf_h32_kernel<NSC, 0>; break;
+    case 1: if constexpr (h32_built<NSC, 1>()) return kde_logpdf_h32_kernel<NSC, 1>; break;
+    case 2: if constexpr (h32_built<NSC, 2>()) return kde_logpdf_h32_kernel<NSC, 2>; break;
+    case 3: if constexpr (h32_built<NSC, 3>()) return kde_logpdf_h32_kernel<NSC, 3>; break;
+    case 4: if constexpr (h32_built<NSC, 4>()) return kde_logpdf_h32_kernel<NSC, 4>; break;
+  }
+  return nullptr;
+}
+template <int NSC>
+static logpdf_pair_fn pick32_pair_kc(int kc) {
+  switch (kc) {
+    case 0: if constexpr (h32_built<NSC, 0>()) return kde_logpdf_h32_pair_kernel<NSC, 0>; break;
+    case 1: if constexpr (h32_built<NSC, 1>()) return kde_logpdf_h32_pair_kernel<NSC, 1>; break;
+    case 2: if constexpr (h32_built<NSC, 2>()) return kde_logpdf_h32_pair_kernel<NSC, 2>; break;
+    case 3: if constexpr (h32_built<NSC, 3>()) return kde_logpdf_h32_pair_kernel<NSC, 3>; break;
+    case 4: if constexpr (h32_built<NSC, 4>()) return kde_logpdf_h32_pair_kernel<NSC, 4>; break;
+  }
+  return nullptr;
+}
+
+logpdf_fn hbx_pick_h32(int nsc, int kc) {
+  switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {8, 16, 24, 32}
+    case 1: return pick32_kc<1>(kc);
+    case 2: return pick32_kc<2>(kc);
+    case 3: return pick32_kc<3>(kc);
+    case 4: return pick32_kc<4>(kc);
+  }
+  return nullptr;
+}
+
+logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kc) {
+  switch (nsc) {
+    case 1: return pick32_pair_kc<1>(kc);
+    case 2: return pick32_pair_kc<2>(kc);
+    case 3: return pick32_pair_kc<3>(kc);
+    case 4: return pick32_pair_kc<4>(kc);
+  }
+  return nullptr;
+}
