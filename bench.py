@@ -46,7 +46,8 @@ def kernel_model(kde_obj, dc, du):
       matrix pipe: NSC dense 16x16x32 f16 MFMAs + KC/2 sparse 16x16x64 (16 cycles each)
       issue:       8 cycles held per matrix instruction + 4 v_exp_f32 (8 each) + 4 v_add_f32 (4 each)
     hbx_score_h32.hip (32x32 tiles, variant bit 6): one tile = 1024 pairs:
-      matrix pipe: 2 NSC dense 32x32x16 f16 MFMAs + KC sparse 32x32x32 (32 cycles each)
+      matrix pipe: h32_nd(NSC) = ceil((6 + 24 NSC) / 16) dense 32x32x16 f16 MFMAs (3 slots per
+                   continuous dim, 6 for the C_j / c_i pieces) + KC sparse 32x32x32 (32 cycles each)
       issue:       8 cycles held per matrix instruction + 16 v_exp_f32 + 16 v_add_f32
     both quoted per 256 pairs (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost').  Dense-equivalent
     matrix work: 2 x 32 x (NSC + KC) flops per pair either way."""
@@ -56,12 +57,12 @@ def kernel_model(kde_obj, dc, du):
         return {"kernel": "kde_logpdf_%s_kernel (f32 MFMA fallback)" % ("oh" if kc else ""), "model": None}
     nsc = (4 * kde_obj.dc_pad + 31) // 32
     if h32:
-        n_mat = 2 * nsc + kc  # per 1024 pairs
+        n_mat = (6 + 24 * nsc + 15) // 16 + kc  # per 1024 pairs: h32_nd(nsc) dense + kc sparse
         return {"kernel": "kde_logpdf_h32_kernel<%d,%d>" % (nsc, kc),
                 "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
                           "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + 16 * 8 + 16 * 4) / 4,
                           "bound_cycles": max(32 * n_mat, 8 * n_mat + 16 * 8 + 16 * 4) / 4,
-                          "dense_equiv_flops_per_pair": 2 * 32 * (nsc + kc)}}
+                          "dense_equiv_flops_per_pair": 2 * (16 * (n_mat - kc) + 32 * kc)}}
     sparse = (not signed) and kc > 0 and kc % 2 == 0
     n_mat = nsc + (kc // 2 if sparse else kc)
     pipe = 16 * n_mat
@@ -642,7 +643,7 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f16 hi/lo MFMA, f32 accumulate, f64 re-score", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f16 hi/lo MFMA (3 products per dim), f32 accumulate, f64 re-score", "data": "synthetic",
         "config": {"workload": workload, "candidates_per_gpu": Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,
                    "parallelism": "candidate-sharded x%d, %s" % (
@@ -659,8 +660,8 @@ def main():
                      "flops_per_pair": W,
                      "basis": "SURVEY 8d: W = 3 Dc + 2 Du + 4 algorithmic flops per pair x pairs per launch / "
                               "launch time vs the dense f16 MFMA peak; the exact hi/lo f16 formulation does "
-                              "320 dense-equivalent flops per pair (mfma_util); vs the fp32 VALU peak "
-                              "(valu_basis) frac > 1",
+                              "%s dense-equivalent flops per pair (mfma_util); vs the fp32 VALU peak "
+                              "(valu_basis) frac > 1" % (km["model"] or {}).get("dense_equiv_flops_per_pair", "-"),
                      "ms_per_launch": ({"l+g": avg_l + avg_g, "pairs_per_launch": Nc * (Ng + Nb)} if fused else
                                        {"l": avg_l, "g": avg_g, "mean": (avg_l + avg_g) / 2}),
                      "mfma_util": mfma_util, "issue_bound": issue_bound},

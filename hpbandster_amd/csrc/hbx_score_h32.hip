@@ -33,9 +33,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef HBX_H32_ABL
-#define HBX_H32_ABL 0  // TEMP ablation bits: 1 no loop DMA, 2 no loop barrier, 4 no duplicate pieces, 8 no exp2
-#endif
 #define H32_CMAX 30000.f    // |shifted c_i| limit of the three-piece split (else: rescue pass)
 
 // sparse index words of one tile: KS dwords (one ds_read)
@@ -53,7 +50,8 @@ template <int I, int NM, int NV, int NRL>
 struct SgbH32 {
   static __device__ __forceinline__ void run() {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, I == NM - 1 ? NRL : 1, 0);
+    constexpr int nr = I == NM - 1 ? NRL : 1;
+    if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
     constexpr int n = NV / NM + (I < NV % NM ? 1 : 0);
     if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x002, n, 0);
     SgbH32<I + 1, NM, NV, NRL>::run();
@@ -192,7 +190,6 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
     for (int g = 0; g < GL + (NX ? 1 : 0); ++g) {
       const int piece = (g < GL || xpiece) ? wave + g * HW : wave % GP;
-      if ((HBX_H32_ABL & 4) && !(g < GL || xpiece)) continue;
       if (g % 2 == part)
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(src + piece * 256 + lane * 4),
                                          (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
@@ -292,7 +289,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   auto tile_sum = [&](const f32x16& a) -> float {
     float e[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) e[r] = (HBX_H32_ABL & 8) ? a[r] : __builtin_amdgcn_exp2f(a[r]);
+    for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(a[r]);
 #pragma unroll
     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
@@ -315,23 +312,16 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     const float* buf = lds + (cc % NBUF) * CHF;
     const float* nbuf = lds + ((cc + 1) % NBUF) * CHF;
     // chunk cc+PD's buffer was last read before the previous iteration's barrier
-    if (!(HBX_H32_ABL & 1)) issue(cc + PD, (cc + PD) % NBUF, 0);
+    issue(cc + PD, (cc + PD) % NBUF, 0);
     mma_rd(accA, buf, 1);  // T0(cc); fragments of T1(cc)
     Sb += tile_sum(accB);  // T1(cc-1): chunk cc-1 complete
     S += Sb;
     schedule();
-    if (!(HBX_H32_ABL & 1)) issue(cc + PD, (cc + PD) % NBUF, 1);
+    issue(cc + PD, (cc + PD) % NBUF, 1);
     // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
     // the barrier makes chunk cc+1 visible to every wave
-    if (!(HBX_H32_ABL & 2)) {
-      if (HBX_H32_ABL & 4) {
-        if (xpiece) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL * (PD - 1)) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-    }
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+    __builtin_amdgcn_s_barrier();
     mma_rd(accB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
     Sb = tile_sum(accA);  // T0(cc)
     schedule();

@@ -48,12 +48,23 @@ def test_fit_bit_exact(device, name):
     np.testing.assert_array_equal(pair.bad.nlev, c["nlev_bad"])
 
 
-@pytest.mark.parametrize("hmode", ["1", "0"])
+# scoring kernel families, chosen when a KDE is prepared: "h32" the default (f16 matrix-core exponent
+# on 32x32 tiles where the shape allows it, hbx_score_h32.hip), "h16" its 16x16-tile form
+# (hbx_score_h.hip, HBX_H32=0), "f32" the f32-MFMA fallback kernels everywhere (HBX_HMODE=0)
+KERNELS = {"h32": {"HBX_HMODE": "1", "HBX_H32": "1"}, "h16": {"HBX_HMODE": "1", "HBX_H32": "0"},
+           "f32": {"HBX_HMODE": "0", "HBX_H32": "1"}}
+
+
+def _kernel_env(monkeypatch, kernel):
+    for k, v in KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
 @pytest.mark.parametrize("name", G.kde_case_names())
-def test_logpdf_fp32_within_tolerance(device, name, hmode, monkeypatch):
-    """hmode "1": the default kernel choice (f16 matrix-core exponent where the shape allows it);
-    "0" (HBX_HMODE=0, read when the KDE is prepared): the f32-MFMA fallback kernels everywhere."""
-    monkeypatch.setenv("HBX_HMODE", hmode)
+def test_logpdf_fp32_within_tolerance(device, name, kernel, monkeypatch):
+    """Every kernel family's fp32 ln-pdf estimates within the north-star 1e-5 of the reference."""
+    _kernel_env(monkeypatch, kernel)
     c = G.load_kde_case(name)
     pair = _pair_from_fixture(c)
     C = c["cands"]
@@ -120,10 +131,10 @@ def test_np_exp_known_answers(device):
     np.testing.assert_array_equal(y.cpu().numpy().view(np.uint64), z["y"].view(np.uint64))
 
 
-@pytest.mark.parametrize("hmode", ["1", "0"])
+@pytest.mark.parametrize("kernel", list(KERNELS))
 @pytest.mark.parametrize("name", G.kde_case_names())
-def test_acquire_chosen_index_bit_exact(device, name, hmode, monkeypatch):
-    monkeypatch.setenv("HBX_HMODE", hmode)
+def test_acquire_chosen_index_bit_exact(device, name, kernel, monkeypatch):
+    _kernel_env(monkeypatch, kernel)
     c = G.load_kde_case(name)
     pair = _pair_from_fixture(c)
     res = pair.acquire(c["cands"])
@@ -271,10 +282,13 @@ def test_hmode_falls_back_when_cj_exceeds_f16_range(device):
     (30, [4] * 16),             # 64 positions -> kc = 4, two sparse steps
     (17, []),                   # continuous only on the f16 kernel
 ])
-def test_hmode_categorical_layouts_match_oracle(device, dc, levels):
-    """The f16 matrix-core kernel over one-hot layouts the bench shape does not use."""
+@pytest.mark.parametrize("kernel", ["h32", "h16"])
+def test_hmode_categorical_layouts_match_oracle(device, dc, levels, kernel, monkeypatch):
+    """The f16 matrix-core kernels over one-hot layouts the bench shape does not use (kc = 4 at
+    dc_pad = 32 is beyond the 32x32 kernel's register budget: the 16x16 kernel runs it either way)."""
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
+    _kernel_env(monkeypatch, kernel)
     du = len(levels)
     n = 2000
     X = S.make_observations(n, dc, du, levels if du else 2, seed=21)
@@ -282,6 +296,9 @@ def test_hmode_categorical_layouts_match_oracle(device, dc, levels):
     vt = S.var_type_string(dc, du)
     pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
     assert (pair.good.variant >> 4) & 1 == 1 and (pair.bad.variant >> 4) & 1 == 1
+    want32 = kernel == "h32" and not (dc == 30 and du == 16)
+    for k in (pair.good, pair.bad):  # signed sums (a factor 1 - h < 0) stay on the 16x16 kernel
+        assert (k.variant >> 6) & 1 == (want32 and not k.has_neg)
     C = S.make_candidates(384, dc, du, levels if du else 2, seed=23)
     res, logl, logg = pair.acquire(C, logs=True)
     for est, k in ((logl, pair.good), (logg, pair.bad)):
@@ -330,14 +347,16 @@ def test_clamped_ties_score_one_first_index(device):
     assert rb[1].index == O.py_argmin(scores[800:1300])
 
 
+@pytest.mark.parametrize("kernel", ["h32", "h16"])
 @pytest.mark.parametrize("shape", [(24, 8, 4, 3000, 20011), (32, 0, 0, 1000, 777), (16, 8, 3, 400, 65)])
-def test_pair_launch_identical_to_two_launches(device, shape, monkeypatch):
+def test_pair_launch_identical_to_two_launches(device, shape, kernel, monkeypatch):
     """l and g scored by one pair launch (the default) against two single launches
     (HBX_SCORE_PAIR=0): the same kernel body per block, so the ln-pdf estimates and the acquisition
     record are bit-identical; the chosen index is the oracle's."""
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
     dc, du, lev, n_obs, n_cand = shape
+    _kernel_env(monkeypatch, kernel)
     X = S.make_observations(n_obs, dc, du, lev)
     L = S.make_losses(n_obs)
     vt = S.var_type_string(dc, du)
@@ -410,3 +429,38 @@ def test_exact_only_outside_scoring_buckets(device, dc, du, lev):
     rb = pair.acquire_batch(C, 100)
     for b in range(3):
         assert rb[b].index == O.py_argmin(scores[100 * b:100 * b + 100])
+
+
+def test_h32_kernel_choice_and_large_shift_rescue(device, monkeypatch):
+    """The bench shape (24c + 8u, 4 levels) runs the 32x32-tile kernel (variant bit 6) and, with
+    HBX_H32=0, the 16x16 one.  Candidates thousands of bandwidths out have a shifted c_i beyond the
+    range of its three f16 pieces (H32_CMAX): they take the rescue pass and still match the oracle's
+    log-space pdf; both kernels pick the oracle's winner."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    vt = S.var_type_string(24, 8)
+    X = S.make_observations(3000, 24, 8, 4, seed=31)
+    L = S.make_losses(3000, seed=32)
+    C = S.make_candidates(512, 24, 8, 4, seed=33)
+    C[5, 0] = 1000.0
+    C[77, 3] = -400.0
+    C[300, 23] = 2500.0
+    for kernel, bit in (("h32", 1), ("h16", 0)):
+        _kernel_env(monkeypatch, kernel)
+        pair = kde.fit_pair(X, L, vt, 33, device=device)
+        assert (pair.good.variant >> 4) & 1 == 1 and (pair.bad.variant >> 4) & 1 == 1
+        assert not pair.bad.has_neg
+        for k in (pair.good, pair.bad):  # signed sums (a factor 1 - h < 0) run the 16x16 kernel
+            assert (k.variant >> 6) & 1 == (bit and not k.has_neg)
+        res, logl, logg = pair.acquire(C, logs=True)
+        for est, k in ((logl, pair.good), (logg, pair.bad)):
+            lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+            fin = np.isfinite(lref)
+            if not k.has_neg:  # (a signed KDE's far pdf may be <= 0: -inf)
+                assert fin[[5, 77, 300]].all()
+            assert np.array_equal(np.isfinite(est), fin)
+            err = np.abs(est[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+            assert err.max() <= 1e-5, (kernel, err.max())
+        l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+        g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+        assert res.index == O.select(l, g)[0]
