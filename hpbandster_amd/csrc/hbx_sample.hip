@@ -5,15 +5,18 @@
 //     (bohb.py:141).  The bounds are in units of bw while the scale is bw_factor*bw, so the sample
 //     lies in [m - bw_factor*m, m + bw_factor*(1-m)] -- the reference's quirk, kept as is;
 //   categorical (levels[d] = t): keep m with probability 1 - bw, else U{0..t-1} (bohb.py:143-146).
-// The truncated normal is drawn by inversion, z = Phi^-1(Phi(a) + u (Phi(b) - Phi(a))), evaluated on
-// the lower side (a > 0 is mirrored) so the tail probabilities keep their relative precision.
-// Random numbers: Philox4x32-10 keyed by the seed; counter = (candidate index, dim, stream) -- the
-// reference draws from numpy's global RNG, so parity is distributional (tests/test_gpu_sample.py).
+// The truncated normal is drawn by inversion, z = Phi^-1(p), p = Phi(a) + u (Phi(b) - Phi(a)) (Phi at
+// the bounds in fp64; a > 0 is mirrored), Phi^-1 on the smaller tail min(p, 1 - p) in fp32
+// (-sqrt(2) erfcinv(2 min(p, 1 - p)): ~1e-7 relative in z, far below what a distributional test can see).
+// Random numbers: Philox4x32-10 keyed by the seed; counter = (candidate index, pair of dims, stream),
+// 32-bit words (dim 2k: words 0, 1; dim 2k + 1: words 2, 3 -- the uniform, then the categorical level
+// draw) -- the reference draws from numpy's global RNG, so parity is distributional
+// (tests/test_gpu_sample.py).
 //
-// One thread per (candidate, dim) element: the writes of a wave are contiguous (8 B per element).
-// The datum draws of a block's candidates go through LDS; Phi at the bounds comes from a per-model
-// table when many candidates are drawn (hbx_kde_sample_table), so a draw costs one Philox block and
-// one inverse normal CDF (AS 241).
+// One thread per (candidate, pair of dims): one Philox block and one 16-byte store per thread (even D),
+// the writes of a wave contiguous.  The datum draws of a block's candidates go through LDS; Phi at the
+// bounds comes from a per-model table when many candidates are drawn (hbx_kde_sample_table).
+// hbx_norm_ppf keeps the fp64 inverse normal CDF (Wichura's AS 241) as a library function.
 #include <math.h>
 
 #include "hbx_common.h"
@@ -32,9 +35,11 @@ __device__ __forceinline__ HbxU32x4 draw(uint64_t seed, uint64_t i, uint32_t wor
 }
 
 // Standardised bounds of a continuous dim around datum m, mirrored so that lo <= 0 side is used
-// (a > 0 -> sample -z from [-b, -a]); false when scipy's a < b check fails.
-__device__ __forceinline__ bool tn_bounds(double m, double h, double* lo, double* hi, bool* flip) {
-  const double a = -m / h, b = (1.0 - m) / h;
+// (a > 0 -> sample -z from [-b, -a]); false when scipy's a < b check fails.  rh = 1 / h: the bounds are
+// within an ulp or two of scipy's -m / h, (1 - m) / h (a distributional difference of nothing), and the
+// domain check agrees exactly (h = 0: +-inf, or NaN where m is 0 or 1, as with the divisions).
+__device__ __forceinline__ bool tn_bounds(double m, double rh, double* lo, double* hi, bool* flip) {
+  const double a = -m * rh, b = (1.0 - m) * rh;
   if (!(a < b)) return false;
   *flip = a > 0.0;
   *lo = *flip ? -b : a;
@@ -92,12 +97,6 @@ __device__ __forceinline__ double norm_ppf(double p) {
   return q < 0.0 ? -v : v;
 }
 
-// z = Phi^-1(Phi(lo) + u (Phi(hi) - Phi(lo))) clamped to [lo, hi]
-__device__ __forceinline__ double tn_invert(double plo, double phi, double lo, double hi, double u) {
-  const double z = norm_ppf(fma(u, phi - plo, plo));
-  return fmin(fmax(z, lo), hi);
-}
-
 __global__ void norm_ppf_kernel(const double* __restrict__ p, int64_t n, double* __restrict__ z) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) z[i] = norm_ppf(p[i]);
@@ -118,7 +117,7 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_table_kernel(
     if (levels[d] == 0) {
       double lo, hi;
       bool flip;
-      if (tn_bounds(X[rows[j] * (int64_t)D + d], bw[d], &lo, &hi, &flip))
+      if (tn_bounds(X[rows[j] * (int64_t)D + d], 1.0 / bw[d], &lo, &hi, &flip))
         r = make_double2(normcdf(lo), normcdf(hi));
       else
         r = make_double2(NAN, NAN);
@@ -127,9 +126,49 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_table_kernel(
   }
 }
 
-// One thread per (candidate, dim) element; a block covers SAMPLE_BLOCK consecutive elements and first
-// draws the datum of each candidate they touch into LDS (one Philox call per candidate, not per
-// element).  IDX is uint32_t when Nc * D < 2^32 (cheap index division) else uint64_t.
+// z = Phi^-1(p) on the smaller tail in fp32, p = Phi(lo) + u (Phi(hi) - Phi(lo)) in fp64, clamped to [lo, hi]
+__device__ __forceinline__ double tn_invert_f32(double plo, double phi, double lo, double hi, double u) {
+  const double p = fma(u, phi - plo, plo);
+  const bool up = p > 0.5;
+  const float t = (float)(2.0 * (up ? 1.0 - p : p));        // in (0, 1]
+  const float zt = -1.41421356237309505f * erfcinvf(t);    // Phi^-1(min(p, 1 - p)) <= 0
+  const double z = (double)(up ? -zt : zt);
+  return fmin(fmax(z, lo), hi);
+}
+
+// One draw of dim d of a candidate whose datum row is xr: w0 the uniform, w1 the categorical level draw
+__device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int d, int32_t idx, int32_t D,
+                                             const double* __restrict__ bw, const double* __restrict__ rbw,
+                                             const int32_t* __restrict__ levels,
+                                             const double2* __restrict__ tab, double bw_factor, uint32_t w0,
+                                             uint32_t w1, bool* derr) {
+  const double m = xr[d];
+  const double h = bw[d];
+  const int t = levels[d];
+  const double u = ((double)w0 + 0.5) * 0x1p-32;  // open (0, 1)
+  if (t != 0) return (u < 1.0 - h) ? m : (double)(uint32_t)(((uint64_t)w1 * (uint64_t)t) >> 32);
+  double lo, hi;
+  bool flip;
+  if (!tn_bounds(m, rbw[d], &lo, &hi, &flip)) {  // scipy's argcheck fails: the reference call raises
+    *derr = true;
+    return NAN;
+  }
+  double plo, phi;
+  if (tab) {
+    const double2 p = tab[(int64_t)idx * D + d];
+    plo = p.x;
+    phi = p.y;
+  } else {
+    plo = normcdf(lo);
+    phi = normcdf(hi);
+  }
+  const double z = tn_invert_f32(plo, phi, lo, hi, u);
+  return fma(bw_factor * h, flip ? -z : z, m);
+}
+
+// One thread per (candidate, pair of dims); a block covers SAMPLE_BLOCK consecutive pairs and first
+// draws the datum of each candidate they touch into LDS (one Philox call per candidate).  IDX is
+// uint32_t when Nc * ceil(D/2) < 2^32 (cheap index division) else uint64_t.
 template <typename IDX>
 __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
@@ -137,11 +176,14 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
     double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
     double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
   __shared__ int32_t sdat[SAMPLE_BLOCK + 1];
-  const IDX total = (IDX)(Nc * (int64_t)D), Dd = (IDX)D;
+  __shared__ double srh[HBX_MAX_D];  // 1 / bw per dim
+  for (int t = threadIdx.x; t < D; t += SAMPLE_BLOCK) srh[t] = 1.0 / bw[t];
+  const int D2 = (D + 1) >> 1;
+  const IDX total = (IDX)(Nc * (int64_t)D2), Pd = (IDX)D2;
   for (IDX base = (IDX)blockIdx.x * SAMPLE_BLOCK; base < total; base += (IDX)gridDim.x * SAMPLE_BLOCK) {
-    const IDX c0 = base / Dd;
+    const IDX c0 = base / Pd;
     const IDX last = (base + SAMPLE_BLOCK < total ? base + SAMPLE_BLOCK : total) - 1;
-    const int nc = (int)(last / Dd - c0) + 1;
+    const int nc = (int)(last / Pd - c0) + 1;
     for (int t = threadIdx.x; t < nc; t += SAMPLE_BLOCK) {
       const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)(c0 + t), DATUM_WORD, stream_id), 0);
       const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
@@ -151,38 +193,26 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
     __syncthreads();
     const IDX e = base + threadIdx.x;
     if (e < total) {
-      const IDX i = e / Dd;
-      const int d = (int)(e - i * Dd);
+      const IDX i = e / Pd;
+      const int k = (int)(e - i * Pd), d = 2 * k;
       const int32_t idx = sdat[i - c0];
-      const double m = X[rows[idx] * (int64_t)D + d];
-      const double h = bw[d];
-      const int t = levels[d];
-      const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)d, stream_id);
-      const double u = hbx_u01_open(hbx_bits64(r, 0));
-      double v;
-      if (t == 0) {
-        double lo, hi;
-        bool flip;
-        if (!tn_bounds(m, h, &lo, &hi, &flip)) {  // scipy's argcheck fails: the reference call raises
-          v = NAN;
-          if (domain_err) domain_err[i] = 1;
+      const double* xr = X + rows[idx] * (int64_t)D;
+      const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
+      bool derr = false;
+      const double v0 = sample_dim(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
+      double* out = cands + (int64_t)i * D + d;
+      if (d + 1 < D) {
+        const double v1 = sample_dim(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
+        if ((D & 1) == 0) {
+          *(double2*)out = make_double2(v0, v1);  // 16-byte aligned: even offset, 16-byte aligned base
         } else {
-          double plo, phi;
-          if (tab) {
-            const double2 p = tab[(int64_t)idx * D + d];
-            plo = p.x;
-            phi = p.y;
-          } else {
-            plo = normcdf(lo);
-            phi = normcdf(hi);
-          }
-          const double z = tn_invert(plo, phi, lo, hi, u);
-          v = fma(bw_factor * h, flip ? -z : z, m);
+          out[0] = v0;
+          out[1] = v1;
         }
       } else {
-        v = (u < 1.0 - h) ? m : (double)(int64_t)__umul64hi(hbx_bits64(r, 1), (uint64_t)t);
+        out[0] = v0;
       }
-      cands[e] = v;
+      if (derr && domain_err) domain_err[i] = 1;
     }
     __syncthreads();
   }
@@ -229,7 +259,8 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   if (n < 1 || n > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: n=%lld observations", (long long)n);
   hipStream_t s = (hipStream_t)stream;
   if (domain_err) HBX_HIP(hipMemsetAsync(domain_err, 0, (size_t)Nc, s));
-  const int64_t total = Nc * (int64_t)D;
+  if ((D & 1) == 0 && ((uintptr_t)cands & 15)) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: cands not 16-byte aligned");
+  const int64_t total = Nc * (int64_t)((D + 1) / 2);
   const int64_t blocks = (total + SAMPLE_BLOCK - 1) / SAMPLE_BLOCK;
   const unsigned grid = (unsigned)(blocks < 65536 ? blocks : 65536);
   if (total + SAMPLE_BLOCK < (int64_t)UINT32_MAX)

@@ -194,16 +194,18 @@ int hbx_philox4x32_10(const uint32_t* counter, const uint32_t* key, uint32_t* ou
 /* Nc candidates around the good KDE's observations, BOHB's rule: datum = rows[U{0..n-1}], then per
  * dim truncnorm(-m/bw, (1-m)/bw, loc=m, scale=bw_factor*bw) (levels[d] == 0) or keep-with-prob-(1-bw)
  * / U{0..t-1} (levels[d] = t).  X: device f64[*][D]; rows: device i64[n] (the good KDE's rows);
- * bw: device f64[D]; levels: device i32[D].  Candidate i uses Philox counter (counter_base + i, dim,
- * stream_id) under key = seed, so consecutive calls with advancing counter_base equal one call over
- * the union.  cands: device f64[Nc][D]; datum: nullable device i64[Nc] (drawn row positions);
+ * bw: device f64[D]; levels: device i32[D].  Dims 2k, 2k+1 of candidate i use Philox counter
+ * (counter_base + i, k, stream_id) under key = seed (32-bit words: the uniform, the categorical level
+ * draw), so consecutive calls with advancing counter_base equal one call over the union; the truncnorm
+ * inversion is fp32 on the smaller tail (distributional parity).  cands: device f64[Nc][D], 16-byte
+ * aligned when D is even; datum: nullable device i64[Nc] (drawn row positions);
  * domain_err: nullable device u8[Nc], 1 where a continuous dim's bounds fail scipy's a < b check
  * (the reference's call raises and falls back to a random configuration). */
 int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, const double* bw,
                    const int32_t* levels, const double* tab, double bw_factor, uint64_t seed, uint64_t counter_base,
                    uint32_t stream_id, int64_t Nc, double* cands, int64_t* datum, uint8_t* domain_err, void* stream);
-/* Standard normal quantile Phi^-1 (device f64[n] -> device f64[n]), the sampler's inversion
- * routine (scipy.special.ndtri semantics on (0, 1)). */
+/* Standard normal quantile Phi^-1 (device f64[n] -> device f64[n]) in fp64 (Wichura's AS 241,
+ * scipy.special.ndtri semantics on (0, 1)). */
 int hbx_norm_ppf(const double* p, int64_t n, double* z, void* stream);
 /* Optional per-model table for hbx_kde_sample (`tab`, nullable): Phi at the standardised truncnorm
  * bounds of every (good row, continuous dim), device f64[hbx_kde_sample_table_bytes(n, D) / 8].  Same
