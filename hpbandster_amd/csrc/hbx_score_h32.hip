@@ -308,16 +308,18 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
   for (int r = 0; r < 16; ++r) accB[r] = -INFINITY;  // "T1(-1)": exp2 -> 0
   readA(lds, 0);
-  for (int cc = 0; cc < nchunks; ++cc) {
-    const float* buf = lds + (cc % NBUF) * CHF;
-    const float* nbuf = lds + ((cc + 1) % NBUF) * CHF;
+  // one chunk; b = cc % NBUF.  The main loop is unrolled over the ring so that b is a constant there: the
+  // fragment addresses are then one lane base plus ds_read immediates (no address arithmetic per tile)
+  auto chunk = [&](int cc, int b) {
+    const float* buf = lds + b * CHF;
+    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
     // chunk cc+PD's buffer was last read before the previous iteration's barrier
-    issue(cc + PD, (cc + PD) % NBUF, 0);
+    issue(cc + PD, (b + PD) % NBUF, 0);
     mma_rd(accA, buf, 1);  // T0(cc); fragments of T1(cc)
     Sb += tile_sum(accB);  // T1(cc-1): chunk cc-1 complete
     S += Sb;
     schedule();
-    issue(cc + PD, (cc + PD) % NBUF, 1);
+    issue(cc + PD, (b + PD) % NBUF, 1);
     // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
     // the barrier makes chunk cc+1 visible to every wave
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
@@ -325,7 +327,15 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     mma_rd(accB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
     Sb = tile_sum(accA);  // T0(cc)
     schedule();
+  };
+  int cc = 0;
+  for (; cc + NBUF <= nchunks; cc += NBUF) {
+    chunk(cc, 0);
+    chunk(cc + 1, 1);
+    chunk(cc + 2, 2);
+    if constexpr (NBUF == 4) chunk(cc + 3, 3);
   }
+  for (; cc < nchunks; ++cc) chunk(cc, cc % NBUF);
   Sb += tile_sum(accB);
   S += Sb;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
