@@ -44,7 +44,7 @@ if a.traffic_out:
            "bytes_per_launch": 2 * fetch * 1024 + write * 1024,
            "note": "HBM-side bytes per launch (%s) = 2 x FETCH_SIZE + WRITE_SIZE "
                    "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md); from tools/profile_round.sh"
-                   % ("l and g in one launch" if "pair" in a.kernel else "mean over the l and g launches")}
+                   % ("l and g in one launch" if any("pair" in k for k in ks) else "mean over the l and g launches")}
     if a.trace:
         import statistics
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in csv.DictReader(open(a.trace))
