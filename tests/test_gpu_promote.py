@@ -87,6 +87,27 @@ def test_config5_shape_with_fit(device):
         np.testing.assert_array_equal(bwb[b], O.normal_reference_bw(Xb[bad]))
 
 
+def test_config5_full_shape_every_mask(device):
+    """Config #5 at its full shape: 1e4 brackets x 1e3 configs, eta = 3 (k = 333): every one of the 1e7
+    mask bytes against argsort(argsort(losses)) < k per bracket (HB_iteration.py:179-182; numpy's
+    stable argsort, vectorised over the brackets -- the synthetic losses have no ties, so any argsort
+    ranks them alike); and the same brackets sharded over two 'ranks' (independent calls on the two
+    halves, no collective) give the same masks."""
+    from hpbandster_amd import promote
+    from hpbandster_amd import synthetic as S
+    B, n, k = 10000, 1000, 333
+    losses = S.make_bracket_losses(B, n)
+    assert all(len(np.unique(r)) == n for r in losses[:50])
+    want = np.argsort(np.argsort(losses, axis=1, kind="stable"), axis=1, kind="stable") < k
+    seg = np.arange(B + 1, dtype=np.int64) * n
+    adv = promote.promote_segments(losses.reshape(-1), seg, np.full(B, float(k)), device=device)
+    np.testing.assert_array_equal(adv.reshape(B, n), want)
+    h = B // 2
+    a0 = promote.promote_segments(losses[:h].reshape(-1), seg[:h + 1], np.full(h, float(k)), device=device)
+    a1 = promote.promote_segments(losses[h:].reshape(-1), seg[:B - h + 1], np.full(B - h, float(k)), device=device)
+    np.testing.assert_array_equal(np.concatenate([a0, a1]), adv)
+
+
 @pytest.mark.parametrize("B,n", [(300, 1024), (97, 200), (5, 1), (64, 3)])
 def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
     """Brackets of <= 1024 configurations run the register-resident wave kernel; HBX_PROMOTE_WAVE=0
