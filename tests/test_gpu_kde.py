@@ -464,3 +464,31 @@ def test_h32_kernel_choice_and_large_shift_rescue(device, monkeypatch):
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
         assert res.index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("dc,du", [(8, 4), (6, 8), (8, 12), (16, 0), (12, 4), (16, 8), (24, 4), (32, 0)])
+def test_h32_every_instance_matches_oracle(device, dc, du):
+    """Every (continuous K-steps, one-hot K-steps) instance of the 32x32-tile kernel the bench shape does
+    not use -- nsc = dc_pad / 8, kc = ceil(one-hot positions / 16) with 3-level dims padded to 4
+    positions -- on 2000 observations (chunks partly filled) and 700 candidates (a partial block):
+    ln-pdf estimates within 1e-5 of the oracle's log-space restatement, the oracle's winner."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    n, lev = 2000, 3
+    X = S.make_observations(n, dc, du, lev, seed=41)
+    L = S.make_losses(n, seed=42)
+    vt = S.var_type_string(dc, du)
+    pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    assert not pair.bad.has_neg
+    assert (pair.bad.variant >> 6) & 1 == 1  # the 32x32 kernel
+    C = S.make_candidates(700, dc, du, lev, seed=43)
+    res, logl, logg = pair.acquire(C, logs=True)
+    for est, k in ((logl, pair.good), (logg, pair.bad)):
+        lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        fin = np.isfinite(lref)
+        assert np.array_equal(np.isfinite(est), fin)
+        err = np.abs(est[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        assert err.max() <= 1e-5, err.max()
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+    assert res.index == O.select(l, g)[0]
