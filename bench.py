@@ -57,12 +57,14 @@ def kernel_model(kde_obj, dc, du):
         return {"kernel": "kde_logpdf_%s_kernel (f32 MFMA fallback)" % ("oh" if kc else ""), "model": None}
     nsc = (4 * kde_obj.dc_pad + 31) // 32
     if h32:
-        n_mat = (6 + 24 * nsc + 15) // 16 + kc  # per 1024 pairs: h32_nd(nsc) dense + kc sparse
-        return {"kernel": "kde_logpdf_h32_kernel<%d,%d>" % (nsc, kc),
+        nd = (6 + 24 * nsc + 15) // 16  # h32_nd(nsc) dense steps
+        n_mat = nd + kc * (2 if signed else 1)  # per 1024 pairs (+ the parity product when signed)
+        valu = 16 * 8 + 16 * 4 + (32 * 4 if signed else 0)  # exp2, add (+ fract, fma when signed)
+        return {"kernel": "kde_logpdf_h32%s_kernel<%d,%d>" % ("s" if signed else "", nsc, kc),
                 "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
-                          "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + 16 * 8 + 16 * 4) / 4,
-                          "bound_cycles": max(32 * n_mat, 8 * n_mat + 16 * 8 + 16 * 4) / 4,
-                          "dense_equiv_flops_per_pair": 2 * (16 * (n_mat - kc) + 32 * kc)}}
+                          "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + valu) / 4,
+                          "bound_cycles": max(32 * n_mat, 8 * n_mat + valu) / 4,
+                          "dense_equiv_flops_per_pair": 2 * (16 * nd + 32 * (n_mat - nd))}}
     sparse = (not signed) and kc > 0 and kc % 2 == 0
     n_mat = nsc + (kc // 2 if sparse else kc)
     pipe = 16 * n_mat

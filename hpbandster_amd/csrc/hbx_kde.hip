@@ -43,7 +43,7 @@ static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
   if (dc_pad < 0 || du_pad < 0) return 1;
   int a = chunk_floats(dc_pad, du_pad, 0, 0), b = chunk_floats(dc_pad, du_pad, OH_MAX_KC, 1);
-  const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1), d = h32_chunk_floats(nsc_of(dc_pad), OH_MAX_KC);
+  const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1), d = h32_chunk_floats(nsc_of(dc_pad), OH_MAX_KC, 1);
   a = a > b ? a : b;
   a = a > d ? a : d;
   return n_chunks(n) * (int64_t)(a > c ? a : c);
@@ -272,11 +272,11 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // otherwise the exact f32 MFMA product.  |C_j| beyond the f16 range is caught after the table.
   const bool hm_ok = (du == 0 || kc > 0) && dcp >= 8;
   int hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
-  // the 32x32-tile kernel (hbx_score_h32.hip) for unsigned sums in the buckets it is built for
-  if (hmode && A.h32_allowed && !has_neg && h32_ok(nsc_of(dcp), kc)) hmode = 2;
+  // the 32x32-tile kernel (hbx_score_h32.hip) in the buckets it is built for
+  if (hmode && A.h32_allowed && h32_ok(nsc_of(dcp), kc, has_neg)) hmode = 2;
   P->hmode = hmode;
   P->nsc = nsc_of(dcp);
-  P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), kc)
+  P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), kc, has_neg)
                                : (hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0));
 }
 
@@ -299,7 +299,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   float* ch = table + (int64_t)(j / OBS_CHUNK) * chunk_f;
   const int jj = j % OBS_CHUNK;
   // hm: 0 = f32 layout, 1 = hmode (16x16 kernel), 2 = h32 (32x32 kernel, no chunk header)
-  const int KTP = hm == 2 ? h32_ktp(P->nsc, P->kc) : h_ktp(dcp, P->kc);
+  const int KTP = hm == 2 ? h32_ktp(P->nsc, P->kc, P->has_neg) : h_ktp(dcp, P->kc);
   _Float16* hrow = (_Float16*)(hm == 2 ? ch : ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
   // hmode rows are written 16 bytes (8 halves) at a time: two dims' h, l, h, l per store
@@ -344,7 +344,8 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     for (int k = 4 * dcp; k < 32 * P->nsc; k += 8) *(h8*)(hrow + k) = z8;
     for (int k = 32 * (P->nsc + P->kc); k < KTP; k += 8) *(h8*)(hrow + k) = z8;
   }
-  if (hm == 2 && slot)  // row padding past the index words (rows are 16-byte aligned, KTP % 8 == 0)
+  if (hm == 2 && slot)  // row padding past the index words (rows are 16-byte aligned, KTP % 8 == 0); the
+    // parity block of a signed KDE is rewritten below
     for (int k = (16 * nd32 + 16 * P->kc + 4 * h32_ksp(P->kc)) & ~7; k < KTP; k += 8) *(h8*)(hrow + k) = z8;
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
@@ -357,10 +358,11 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     // t0 + 1, and the index nibble (slots 0,1: 0x4; slots 2,3: 0xE); index dword ksp h + s holds groups
     // 4h..4h+3 of step s
     _Float16* cz = hrow + 16 * nd32;
+    _Float16* cp = hrow + h32_par(P->nsc, P->kc);  // parity block (signed KDEs)
     const int ksp = h32_ksp(P->kc);
     uint32_t iw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     for (int s = 0; s < P->kc; ++s) {
-      h8 v[2] = {{}, {}};
+      h8 v[2] = {{}, {}}, pv[2] = {{}, {}};
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         const int t0 = 16 * s + 2 * g;
@@ -373,11 +375,16 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
           const float hi = (float)(_Float16)dl;
           v[g >> 2][2 * (g & 3)] = (_Float16)hi;
           v[g >> 2][2 * (g & 3) + 1] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
+          if (P->cat_negf[u] != 0.f) pv[g >> 2][2 * (g & 3)] = (_Float16)0.5f;
         }
         iw[ksp * (g >> 2) + s] |= (m1 ? 0xEu : 0x4u) << (4 * (g & 3));
       }
       *(h8*)(cz + 16 * s) = v[0];
       *(h8*)(cz + 16 * s + 8) = v[1];
+      if (P->has_neg) {
+        *(h8*)(cp + 16 * s) = pv[0];
+        *(h8*)(cp + 16 * s + 8) = pv[1];
+      }
     }
     uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 16 * P->kc);
     for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
@@ -1402,9 +1409,9 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   if (dcp != dc_pad || dup != du_pad) return {nullptr, nullptr, 0, 0, nullptr, nullptr};  // not a bucket
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm && ((variant >> 6) & 1)) {
-    if (dc_pad < 8 || sg) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
-    return {hbx_pick_h32(nsc_of(dc_pad), kc), r, 32 * H16_WAVES, 64 * H16_WAVES, hbx_pick_h32_pair(nsc_of(dc_pad), kc),
-            pick_rescue_pair<false>(dc_pad)};
+    if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
+    return {hbx_pick_h32(nsc_of(dc_pad), kc, sg), r, 32 * H16_WAVES, 64 * H16_WAVES,
+            hbx_pick_h32_pair(nsc_of(dc_pad), kc, sg), sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};

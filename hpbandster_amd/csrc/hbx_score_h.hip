@@ -116,17 +116,7 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
   const bool staged = rows_fit && cbase < Nc;
   const int64_t nv = (Nc - cbase) < 16 * RT ? (Nc - cbase) : 16 * RT;  // valid rows of this wave
   double* xs = (double*)lds + (int64_t)wave * 16 * RT * DS;
-  if (staged) {
-    const double* src = cand + cbase * (int64_t)D;
-    if (D <= 64) {  // 64 / D rows per pass, coalesced
-      const int rpi = 64 / D, lr = lane / D, lc = lane - lr * D;
-      if (lr < rpi)
-        for (int row = lr; row < nv; row += rpi) xs[row * DS + lc] = src[row * D + lc];
-    } else {
-      for (int row = 0; row < nv; ++row)
-        for (int c = lane; c < D; c += 64) xs[row * DS + c] = src[row * D + c];
-    }
-  }
+  if (staged) stage_rows(cand + cbase * (int64_t)D, nv, D, DS, xs, lane);
   __syncthreads();
   f16x8 ah[RT][NSH];
   f16x8 asp[RT][KS];  // SP: compressed one-hot A (two nonzeros per group of four K slots)

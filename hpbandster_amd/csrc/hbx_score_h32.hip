@@ -62,7 +62,7 @@ struct SgbH32<NM, NM, NV, NRL> {
   static __device__ __forceinline__ void run() {}
 };
 
-template <int NSC, int KC>
+template <int NSC, int KC, bool SG>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
@@ -70,8 +70,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   constexpr int ND = h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + 3 slots per continuous dim)
   constexpr int KS = KC;       // sparse 32-wide K-steps (one-hot)
   constexpr int NMT = ND + KS; // matrix instructions per 32x32 tile
-  constexpr int KTP = h32_ktp(NSC, KC);
-  constexpr int CHF = h32_chunk_floats(NSC, KC);
+  constexpr int KTP = h32_ktp(NSC, KC, SG);
+  constexpr int CHF = h32_chunk_floats(NSC, KC, SG);
+  constexpr int PAR = h32_par(NSC, KC);  // signed: the parity block (halves into the row)
+  static_assert(!SG || KC > 0, "signed sums come from categorical dims");
   constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
   constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -109,17 +111,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   const bool staged = rows_fit && cbase < Nc;
   const int64_t nv = (Nc - cbase) < 32 ? (Nc - cbase) : 32;  // valid rows of this wave
   double* xs = (double*)lds + (int64_t)wave * 32 * DS;
-  if (staged) {
-    const double* src = cand + cbase * (int64_t)D;
-    if (D <= 64) {  // 64 / D rows per pass, coalesced
-      const int rpi = 64 / D, lr = lane / D, lcl = lane - lr * D;
-      if (lr < rpi)
-        for (int row = lr; row < nv; row += rpi) xs[row * DS + lcl] = src[row * D + lcl];
-    } else {
-      for (int row = 0; row < nv; ++row)
-        for (int k = lane; k < D; k += 64) xs[row * DS + k] = src[row * D + k];
-    }
-  }
+  if (staged) stage_rows(cand + cbase * (int64_t)D, nv, D, DS, xs, lane);
   __syncthreads();
 
   // B operands of candidate column c.  Dense step s, half j of the lane: slot k = 16s + 8h + j -- slots
@@ -210,6 +202,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // half's index words (at 2 ksp h halves past the compressed one-hot part)
   f16x8 ad[ND];
   f16x8 asp[KS > 0 ? KS : 1];
+  f16x8 apar[SG ? KS : 1];  // signed: parity fragments (the one-hot part's positions, 0.5 per negative dim)
   typename H32Idx<KS>::T aix;
   const int ixo = 16 * ND + 16 * KC + 2 * h32_ksp(KC) * h - 8 * h;  // index words relative to arow
   auto arow = [&](const float* buf, int jt) { return (const _Float16*)buf + (32 * jt + c) * KTP + 8 * h; };
@@ -219,6 +212,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 0; s < ND; ++s) ad[s] = *(const f16x8*)(a + 16 * s);
 #pragma unroll
     for (int s = 0; s < KS; ++s) asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
+    if constexpr (SG)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) apar[s] = *(const f16x8*)(a + PAR + 16 * s);
     if constexpr (KS > 0) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
   };
   const f32x16 zero16 = {};
@@ -231,8 +227,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 0; s < KS; ++s)
       acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
   };
-  // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it
-  auto mma_rd = [&](f32x16& acc, const float* nb, int jt) {
+  // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it; a
+  // signed KDE's parity product (the same index words) follows into accp
+  auto mma_rd = [&](f32x16& acc, f32x16& accp, const float* nb, int jt) {
     const _Float16* a = arow(nb, jt);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[0], zero16, 0, 0, 0);
     ad[0] = *(const f16x8*)a;
@@ -245,10 +242,18 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 0; s < KS; ++s) {
       acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
       asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
-      if (s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+      if (!SG && s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+    }
+    if constexpr (SG) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        accp = __builtin_amdgcn_smfmac_f32_32x32x32_f16(apar[s], bsp[s], s == 0 ? zero16 : accp, h32_idx<KS>(aix, s),
+                                                        0, 0);
+        apar[s] = *(const f16x8*)(a + PAR + 16 * s);
+        if (s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+      }
     }
   };
-
   // Per-candidate shift (see hbx_score_h.hip): the exponent's maximum over chunk 0 is moved to 0.  The
   // probe runs without c_i (its B slots are 0); the maximum with it is c_i + the probe's maximum.
   {
@@ -285,11 +290,17 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     }
   }
 
-  // exp2 of a tile's 16 terms and their pairwise sum (depth 4)
-  auto tile_sum = [&](const f32x16& a) -> float {
+  // exp2 of a tile's 16 terms and their pairwise sum (depth 4); signed: also the odd-parity terms'
+  // sum, halved (fract of 0.5 x count is 0.5 for an odd count, else 0), in register order
+  auto tile_sum = [&](const f32x16& a, const f32x16& ap, float& sn) -> float {
     float e[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(a[r]);
+    if constexpr (SG) {
+      sn = __builtin_amdgcn_fractf(ap[0]) * e[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) sn = fmaf(__builtin_amdgcn_fractf(ap[r]), e[r], sn);
+    }
 #pragma unroll
     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
@@ -303,10 +314,13 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 
   // Main loop.  Sums: a tile's 16 terms pairwise (depth 4), the chunk's two tiles (1), the chunks in
   // order (nchunks), the two lane halves (1).
-  float S = 0.f, Sb = 0.f;
-  f32x16 accA, accB;
+  float S = 0.f, Sb = 0.f, Sn = 0.f, Snb = 0.f;
+  f32x16 accA, accB, accpA, accpB;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) accB[r] = -INFINITY;  // "T1(-1)": exp2 -> 0
+  for (int r = 0; r < 16; ++r) {
+    accB[r] = -INFINITY;  // "T1(-1)": exp2 -> 0
+    accpB[r] = 0.f;
+  }
   readA(lds, 0);
   // one chunk; b = cc % NBUF.  The main loop is unrolled over the ring so that b is a constant there: the
   // fragment addresses are then one lane base plus ds_read immediates (no address arithmetic per tile)
@@ -315,17 +329,23 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
     // chunk cc+PD's buffer was last read before the previous iteration's barrier
     issue(cc + PD, (b + PD) % NBUF, 0);
-    mma_rd(accA, buf, 1);  // T0(cc); fragments of T1(cc)
-    Sb += tile_sum(accB);  // T1(cc-1): chunk cc-1 complete
+    mma_rd(accA, accpA, buf, 1);  // T0(cc); fragments of T1(cc)
+    float tn;
+    Sb += tile_sum(accB, accpB, tn);  // T1(cc-1): chunk cc-1 complete
     S += Sb;
+    if constexpr (SG) {
+      Snb += tn;
+      Sn += Snb;
+    }
     schedule();
     issue(cc + PD, (b + PD) % NBUF, 1);
     // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
     // the barrier makes chunk cc+1 visible to every wave
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
     __builtin_amdgcn_s_barrier();
-    mma_rd(accB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
-    Sb = tile_sum(accA);  // T0(cc)
+    mma_rd(accB, accpB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
+    Sb = tile_sum(accA, accpA, tn);  // T0(cc)
+    if constexpr (SG) Snb = tn;
     schedule();
   };
   int cc = 0;
@@ -336,10 +356,15 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     if constexpr (NBUF == 4) chunk(cc + 3, 3);
   }
   for (; cc < nchunks; ++cc) chunk(cc, cc % NBUF);
-  Sb += tile_sum(accB);
-  S += Sb;
+  {
+    float tn;
+    Sb += tile_sum(accB, accpB, tn);  // T1(last)
+    S += Sb;
+    if constexpr (SG) Sn += Snb + tn;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
   S += __shfl_xor(S, 32);
+  if constexpr (SG) Sn = 2.f * (Sn + __shfl_xor(Sn, 32));  // the odd-parity terms' sum (exact doubling)
   if (h == 0) {
     const int64_t ii = cbase + c;
     if (ii < Nc) {
@@ -351,9 +376,11 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       for (int k = 0; k < P->nconst; ++k)
         if (x[P->const_dim[k]] != P->const_level[k]) nq = true;
       // S carries the factor 2^dq; |c_i| + dq bounds the rounding of the shifted c_i
-      KdeEst o = finish_est_terms(P, S, 0.f, -dq, nq, ci_q - dq, bnd_q, false, (float)(nchunks + 6 + 24));
-      // f16 hi/lo representation error of both coordinates and the six lo.lo products given up to the
-      // C_j / c_i pieces (together <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
+      // sums: a tile's terms pairwise (depth 4; signed: its odd-parity terms in order, 16), the chunk's
+      // two tiles, the chunks in order, the two lane halves
+      KdeEst o = finish_est_terms(P, S, Sn, -dq, nq, ci_q - dq, bnd_q, SG, (float)(nchunks + (SG ? 18 : 6) + 24));
+      // f16 hi/lo representation error of both coordinates (2 x 2^-22 sum|x''X'|) and the lo.lo products
+      // given up (together <= 2^-22 sum|x''X'|), plus the C_j / c_i pieces' subnormal rounding
       if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-19f) * HBX_LN2f;
       if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) o.err = -1.f;  // rescue marker
       out[ii] = o;
@@ -361,11 +388,12 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   }
 }
 
+// unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU)
 template <int NSC, int KC>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KC>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KC, false>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
 // both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
@@ -373,52 +401,66 @@ template <int NSC, int KC>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
-  kde_logpdf_h32_body<NSC, KC>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                               second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+  kde_logpdf_h32_body<NSC, KC, false>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                      second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+}
+
+// signed sums (the parity product and its accumulators: 130-170 VGPRs): one 8-wave block per CU, so
+// 2 waves per SIMD and a 256-register budget
+template <int NSC, int KC>
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
+    const float* __restrict__ table, KdeEst* __restrict__ out) {
+  kde_logpdf_h32_body<NSC, KC, true>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
 template <int NSC, int KC>
-static constexpr bool h32_built() { return h32_ok(NSC, KC); }
-
-template <int NSC>
-static logpdf_fn pick32_kc(int kc) {
-  switch (kc) {
-    case 0: if constexpr (h32_built<NSC, 0>()) return kde_logpdf_h32_kernel<NSC, 0>; break;
-    case 1: if constexpr (h32_built<NSC, 1>()) return kde_logpdf_h32_kernel<NSC, 1>; break;
-    case 2: if constexpr (h32_built<NSC, 2>()) return kde_logpdf_h32_kernel<NSC, 2>; break;
-    case 3: if constexpr (h32_built<NSC, 3>()) return kde_logpdf_h32_kernel<NSC, 3>; break;
-    case 4: if constexpr (h32_built<NSC, 4>()) return kde_logpdf_h32_kernel<NSC, 4>; break;
-  }
-  return nullptr;
-}
-template <int NSC>
-static logpdf_pair_fn pick32_pair_kc(int kc) {
-  switch (kc) {
-    case 0: if constexpr (h32_built<NSC, 0>()) return kde_logpdf_h32_pair_kernel<NSC, 0>; break;
-    case 1: if constexpr (h32_built<NSC, 1>()) return kde_logpdf_h32_pair_kernel<NSC, 1>; break;
-    case 2: if constexpr (h32_built<NSC, 2>()) return kde_logpdf_h32_pair_kernel<NSC, 2>; break;
-    case 3: if constexpr (h32_built<NSC, 3>()) return kde_logpdf_h32_pair_kernel<NSC, 3>; break;
-    case 4: if constexpr (h32_built<NSC, 4>()) return kde_logpdf_h32_pair_kernel<NSC, 4>; break;
-  }
-  return nullptr;
+__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_pair_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+  const bool second = blockIdx.x >= a.nblk0;
+  kde_logpdf_h32_body<NSC, KC, true>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                     second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
 }
 
-logpdf_fn hbx_pick_h32(int nsc, int kc) {
+// instances: h32_ok (hbx_kde_impl.h)
+template <int NSC, int KC, bool SG, bool PAIR>
+static constexpr auto h32_inst() {
+  if constexpr (PAIR) {
+    if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KC>;
+    else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KC>;
+  } else {
+    if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KC>;
+    else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KC>;
+  }
+}
+
+template <int NSC, bool SG, bool PAIR>
+static auto pick32_kc(int kc) {
+  switch (kc) {
+    case 0: if constexpr (h32_ok(NSC, 0, SG)) return h32_inst<NSC, 0, SG, PAIR>(); break;
+    case 1: if constexpr (h32_ok(NSC, 1, SG)) return h32_inst<NSC, 1, SG, PAIR>(); break;
+    case 2: if constexpr (h32_ok(NSC, 2, SG)) return h32_inst<NSC, 2, SG, PAIR>(); break;
+    case 3: if constexpr (h32_ok(NSC, 3, SG)) return h32_inst<NSC, 3, SG, PAIR>(); break;
+    case 4: if constexpr (h32_ok(NSC, 4, SG)) return h32_inst<NSC, 4, SG, PAIR>(); break;
+  }
+  return decltype(h32_inst<NSC, 1, SG, PAIR>())(nullptr);
+}
+
+template <bool SG, bool PAIR>
+static auto pick32(int nsc, int kc) {
   switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {8, 16, 24, 32}
-    case 1: return pick32_kc<1>(kc);
-    case 2: return pick32_kc<2>(kc);
-    case 3: return pick32_kc<3>(kc);
-    case 4: return pick32_kc<4>(kc);
+    case 1: return pick32_kc<1, SG, PAIR>(kc);
+    case 2: return pick32_kc<2, SG, PAIR>(kc);
+    case 3: return pick32_kc<3, SG, PAIR>(kc);
+    case 4: return pick32_kc<4, SG, PAIR>(kc);
   }
-  return nullptr;
+  return decltype(pick32_kc<1, SG, PAIR>(0))(nullptr);
 }
 
-logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kc) {
-  switch (nsc) {
-    case 1: return pick32_pair_kc<1>(kc);
-    case 2: return pick32_pair_kc<2>(kc);
-    case 3: return pick32_pair_kc<3>(kc);
-    case 4: return pick32_pair_kc<4>(kc);
-  }
-  return nullptr;
+logpdf_fn hbx_pick_h32(int nsc, int kc, bool sg) {
+  return sg ? pick32<true, false>(nsc, kc) : pick32<false, false>(nsc, kc);
+}
+
+logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kc, bool sg) {
+  return sg ? pick32<true, true>(nsc, kc) : pick32<false, true>(nsc, kc);
 }

@@ -297,8 +297,8 @@ def test_hmode_categorical_layouts_match_oracle(device, dc, levels, kernel, monk
     pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
     assert (pair.good.variant >> 4) & 1 == 1 and (pair.bad.variant >> 4) & 1 == 1
     want32 = kernel == "h32" and not (dc == 30 and du == 16)
-    for k in (pair.good, pair.bad):  # signed sums (a factor 1 - h < 0) stay on the 16x16 kernel
-        assert (k.variant >> 6) & 1 == (want32 and not k.has_neg)
+    for k in (pair.good, pair.bad):  # signed sums (a factor 1 - h < 0) included
+        assert (k.variant >> 6) & 1 == want32
     C = S.make_candidates(384, dc, du, levels if du else 2, seed=23)
     res, logl, logg = pair.acquire(C, logs=True)
     for est, k in ((logl, pair.good), (logg, pair.bad)):
@@ -449,9 +449,9 @@ def test_h32_kernel_choice_and_large_shift_rescue(device, monkeypatch):
         _kernel_env(monkeypatch, kernel)
         pair = kde.fit_pair(X, L, vt, 33, device=device)
         assert (pair.good.variant >> 4) & 1 == 1 and (pair.bad.variant >> 4) & 1 == 1
-        assert not pair.bad.has_neg
-        for k in (pair.good, pair.bad):  # signed sums (a factor 1 - h < 0) run the 16x16 kernel
-            assert (k.variant >> 6) & 1 == (bit and not k.has_neg)
+        assert not pair.bad.has_neg and pair.good.has_neg  # one KDE of each kind
+        for k in (pair.good, pair.bad):
+            assert (k.variant >> 6) & 1 == bit
         res, logl, logg = pair.acquire(C, logs=True)
         for est, k in ((logl, pair.good), (logg, pair.bad)):
             lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
