@@ -12,21 +12,17 @@ struct HbxU32x4 {
   uint32_t x[4];
 };
 
-__host__ __device__ __forceinline__ uint32_t hbx_mulhi32(uint32_t a, uint32_t b) {
-  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
-}
-
 __host__ __device__ __forceinline__ HbxU32x4 hbx_philox4x32_10_impl(HbxU32x4 c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = hbx_mulhi32(M0, c.x[0]), lo0 = M0 * c.x[0];
-    const uint32_t hi1 = hbx_mulhi32(M1, c.x[2]), lo1 = M1 * c.x[2];
+    // one 32x32 -> 64-bit product per multiplier (v_mad_u64_u32: hi and lo in one instruction)
+    const uint64_t p0 = (uint64_t)M0 * c.x[0], p1 = (uint64_t)M1 * c.x[2];
     HbxU32x4 n;
-    n.x[0] = hi1 ^ c.x[1] ^ k0;
-    n.x[1] = lo1;
-    n.x[2] = hi0 ^ c.x[3] ^ k1;
-    n.x[3] = lo0;
+    n.x[0] = (uint32_t)(p1 >> 32) ^ c.x[1] ^ k0;
+    n.x[1] = (uint32_t)p1;
+    n.x[2] = (uint32_t)(p0 >> 32) ^ c.x[3] ^ k1;
+    n.x[3] = (uint32_t)p0;
     c = n;
     k0 += W0;
     k1 += W1;

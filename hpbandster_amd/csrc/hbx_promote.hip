@@ -4,8 +4,8 @@
 //     ranks = np.argsort(np.argsort(losses)); advance = ranks < num_configs[SH_iter]
 // and HB_iteration.py:240-242 (SuccessiveResampling: ranks < max(1, n * (1 - 0.5))).
 // Only REVIEW configurations (finite losses) are ranked; CRASHED ones (non-finite, register_result
-// HB_iteration.py:102-106) never advance.  Mask only (the drop-in's need): a radix select of the k-th
-// (key, position) per bracket (sh_select_kernel).  With the sorted order requested: a stable sort of
+// HB_iteration.py:102-106) never advance.  Mask only (the drop-in's need): a selection of the k-th
+// (key, position) per bracket (sh_select_kernel: interpolation, then bisection of the key range).  With the sorted order requested: a stable sort of
 // the losses (hbx_sort.h; one wave per bracket <= 1024, else one workgroup), then
 // advance[position] = (rank < k).  Ties are ranked by position (stable);
 // numpy's argsort is unstable, so on tied losses the reference's choice is platform dependent.
@@ -77,27 +77,48 @@ __global__ __launch_bounds__(256) void sh_promote_wave_kernel(const double* __re
 }
 
 // Brackets of up to 1024 configurations without a sorted order requested: the mask needs only the
-// k-th smallest (key, position) of the bracket, found by a bitwise radix select -- O(n) per bracket
-// instead of the O(n log^2 n) sort.  One wave per bracket; element i = 64 r + lane sits in register r
-// of lane `lane` (coalesced buffer loads issued together, 64 consecutive mask bytes per store).
-//   Bits are resolved from the highest bit where the finite keys differ downwards: a pass counts the
-// bucket's elements (those matching every bit resolved so far) with a 0 at the bit and keeps the half
-// holding the k-th.  While the bucket is large each lane tracks its 16 elements as a bit mask and a
-// pass costs 16 bit extractions and one DPP wave sum; once it holds <= 64 keys they are compacted into
-// one per lane (LDS, position order) and a pass is one compare and one ballot.  It stops as soon as
-// the whole bucket advances.  The mask is then one masked 64-bit compare per element against the
-// resolved prefix; keys equal in all 64 bits are ranked by position (stable), as sh_promote_wave_kernel
-// and sh_promote_kernel rank them.
+// k-th smallest (loss, position) of the bracket -- a selection, O(n) per bracket instead of a sort.
+// One wave per bracket; element i = 64 r + lane sits in register r of lane `lane` (coalesced buffer
+// loads issued together, 64 consecutive mask bytes per store).  Non-finite losses (CRASHED) and lanes
+// past n hold NaN, which no comparison counts.
+//   The search keeps a bracket [Lk, Hk) of order-preserving 64-bit keys (hbx_d2ord's order, -0.0 and
+// 0.0 one key) with cL = #{keys < Lk} < kk <= cH = #{keys < Hk}; it starts from the high key words of
+// the minimum and the maximum, and its ends live in scalar registers.  A key threshold K is compared in
+// the loss domain (key(x) < K  <=>  x < val(K) for finite x), so counting the losses below it is one
+// f64 compare and one carry-add per register plus one wave sum.  Rounds: (1) up to two interpolation
+// rounds -- two thresholds around the k-th loss's position estimated linearly between the bracket ends
+// (+-1.5 sigma of its rank, + 2), which isolate <= 64 keys in one round on smooth data; (2) bisection of
+// the key range at its highest differing bit while the bracket holds > 64 keys (any data: at most 64
+// rounds); (3) the <= 64 bracket losses compacted into one key per lane (LDS, position order) and the
+// bisection finished with one compare and one ballot per round.  It ends when kk losses lie below one
+// end of the bracket -- the mask is then one compare per element -- or when the bracket is a single key
+// value: its copies are ranked by position (stable), as sh_promote_wave_kernel / sh_promote_kernel
+// rank them.
 
 constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (raw 32-bit data, range checked)
 
-__global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict__ loss,
+// finite x -> order-preserving key (-0.0 and 0.0 map to one key); val() inverts it on keys of finite
+// values and of the thresholds between them (key(x) < K  <=>  x < val(K))
+__device__ __forceinline__ uint64_t sel_key(double x) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x + 0.0);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double sel_val(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k ^ 0x8000000000000000ull) : ~k));
+}
+// a uniform 64-bit value into scalar registers (the bracket ends: the loops over them run in SALU)
+__device__ __forceinline__ uint64_t sel_uniform(uint64_t x) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void sh_select_kernel(const double* __restrict__ loss,
                                                         const int64_t* __restrict__ seg_off, int64_t B,
                                                         const double* __restrict__ k,
                                                         uint8_t* __restrict__ advance,
                                                         int64_t* __restrict__ n_advance) {
   constexpr int R = PW_PER_LANE;  // 16 registers x 64 lanes = 1024 elements
-  __shared__ uint64_t cbuf[4][64];  // per wave: the compacted bucket
+  __shared__ double cbuf[4][64];  // per wave: the compacted bracket
   // the wave index made visibly uniform: the bracket's bounds, k and buffer resources live in SGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t b = (int64_t)blockIdx.x * 4 + wv;
@@ -115,172 +136,160 @@ __global__ __launch_bounds__(256) void sh_select_kernel(const double* __restrict
   double v[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane, 512 * r, 0));
-  // order-preserving keys (hbx_d2ord; -0.0 + 0.0 = +0.0 merges the zeros) and the min / max of the
-  // high words over the bracket (rows past n skipped, the partial row masked: uniform branches).
-  // Finite keys have high words in [0x00100000, 0xFFEFFFFF]; a bracket without CRASHED (non-finite)
-  // entries -- the common case -- then needs no per-element finite mask at all.
-  const int nrow = (n + 63) >> 6;  // rows holding elements
-  uint64_t key[R];
-  uint32_t mnh = ~0u, mxh = 0u;
+  // fz = sum of x * 0: NaN iff some loss is not finite (the loads past n returned 0.0)
+  double fz = 0.0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) fz = fma(v[r], 0.0, fz);
+  // lanes past n become NaN (the partial row and the absent rows), then min / max
+  const int nfull = n >> 6;
+  const bool inpart = lane < (n & 63);
+  const double qnan = __builtin_nan("");
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (r >= nfull) v[r] = (r == nfull && inpart) ? v[r] : qnan;
+  double mn = __builtin_inf(), mx = -__builtin_inf();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const double z = v[r] + 0.0;
-    const uint32_t hi = (uint32_t)(__double_as_longlong(z) >> 32), lo = (uint32_t)__double_as_longlong(z);
-    const uint32_t sg = (uint32_t)((int32_t)hi >> 31);
-    const uint32_t kh = hi ^ (sg | 0x80000000u);
-    key[r] = ((uint64_t)kh << 32) | (lo ^ sg);
-    if (64 * r + 64 <= n) {
-      mnh = min(mnh, kh);
-      mxh = max(mxh, kh);
-    } else if (r < nrow) {
-      const bool ok = 64 * r + lane < n;
-      mnh = min(mnh, ok ? kh : ~0u);
-      mxh = max(mxh, ok ? kh : 0u);
-    }
+    mn = fmin(mn, v[r]);
+    mx = fmax(mx, v[r]);
   }
-  mnh = ~wave_reduce_dpp(~mnh, OpMax());
-  mxh = wave_reduce_dpp(mxh, OpMax());
-  const bool allfin = mnh >= 0x00100000u && mxh <= 0xFFEFFFFFu;  // uniform
-  // per-lane element mask: bit r = element 64 r + lane exists (and, with CRASHED entries, is finite)
-  const int nr = min(max((n - lane + 63) >> 6, 0), R);
-  uint32_t fin = (1u << nr) - 1u;
   int nfin = n;
-  uint32_t ph, pl = 0u, dh, dl = 0u;  // resolved prefix of the k-th key; bits where the keys differ
-  if (allfin) {
-    dh = mnh ^ mxh;
-    ph = mnh;
-    if (dh == 0u) {  // equal high words: the low words decide (rare)
-      uint32_t mnl = ~0u, mxl = 0u;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const bool f = (fin >> r) & 1u;
-        mnl = min(mnl, f ? (uint32_t)key[r] : ~0u);
-        mxl = max(mxl, f ? (uint32_t)key[r] : 0u);
-      }
-      mnl = ~wave_reduce_dpp(~mnl, OpMax());
-      mxl = wave_reduce_dpp(mxl, OpMax());
-      dl = mnl ^ mxl;
-      pl = mnl;
-    }
-  } else {  // CRASHED entries present: finite mask, AND / OR of the finite keys
-    uint32_t andh = ~0u, orh = 0u;
+  if (__builtin_amdgcn_ballot_w64(fz != fz)) {  // CRASHED entries present (uniform): they become NaN
+    mn = __builtin_inf();
+    mx = -__builtin_inf();
+    nfin = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint32_t kh = (uint32_t)(key[r] >> 32);
-      const bool f = ((fin >> r) & 1u) && kh >= 0x00100000u && kh <= 0xFFEFFFFFu;  // finite
-      fin &= ~((f ? 0u : 1u) << r);
-      andh &= f ? kh : ~0u;
-      orh |= f ? kh : 0u;
-    }
-    nfin = (int)wave_reduce_dpp((uint32_t)__popc(fin), OpAdd());
-    ph = wave_reduce_dpp(andh, OpAnd());
-    dh = wave_reduce_dpp(orh, OpOr()) ^ ph;
-    if (dh == 0u) {
-      uint32_t andl = ~0u, orl = 0u;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const bool f = (fin >> r) & 1u;
-        andl &= f ? (uint32_t)key[r] : ~0u;
-        orl |= f ? (uint32_t)key[r] : 0u;
-      }
-      pl = wave_reduce_dpp(andl, OpAnd());
-      dl = wave_reduce_dpp(orl, OpOr()) ^ pl;
+      const bool f = v[r] - v[r] == 0.0;
+      v[r] = f ? v[r] : qnan;
+      mn = fmin(mn, v[r]);
+      mx = fmax(mx, v[r]);
+      nfin += (int)__popcll(__builtin_amdgcn_ballot_w64(f));
     }
   }
   // rank < k advances: the first kk ranks, kk = min(nfin, ceil(k)) (k > 0; NaN or k <= 0: none)
   const double kb = k[b];
-  const int kk = kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0;
+  const int kk = __builtin_amdgcn_readfirstlane(kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0);
   if (kk == nfin || kk == 0) {  // all the finite entries, or none
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk ? (fin >> r) & 1u : 0u), ars, lane, 64 * r, 0);
+    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk && v[r] == v[r] ? 1u : 0u), ars, lane, 64 * r, 0);
     if (lane == 0 && n_advance) n_advance[b] = kk;
     return;
   }
-  // bits above the highest one where the finite keys differ are common to all of them: resolved
-  int bit = dh ? 63 - __clz((int)dh) : (dl ? 31 - __clz((int)dl) : -1);
-  if (bit >= 32) {  // the prefix keeps only the bits above `bit`
-    ph &= ~((2u << (bit - 32)) - 1u);
-    pl = 0u;
-  } else if (bit >= 0) {
-    pl &= ~((2u << bit) - 1u);
+  // the bracket: the high key words of the minimum and the maximum (a lane without a finite loss
+  // contributes key(+inf) / key(-inf)); exact bounds only when the two coincide
+  const uint32_t mnh = ~wave_reduce_dpp(~(uint32_t)(sel_key(mn) >> 32), OpMax());
+  const uint32_t mxh = wave_reduce_dpp((uint32_t)(sel_key(mx) >> 32), OpMax());
+  uint64_t Lk = (uint64_t)mnh << 32, Hk = ((uint64_t)mxh + 1ull) << 32;
+  if (mnh == mxh) {
+    Lk = ((uint64_t)mnh << 32) | ~wave_reduce_dpp(~(uint32_t)sel_key(mn), OpMax());
+    Hk = (((uint64_t)mxh << 32) | wave_reduce_dpp((uint32_t)sel_key(mx), OpMax())) + 1ull;
   }
-  int need = kk, cnt = nfin;
-  uint32_t alive = fin;
-  // phase 1: the bucket as per-lane bit masks
-  for (; bit >= 0 && cnt != need && cnt > 64; --bit) {
-    uint32_t ones = 0u;
-    if (bit >= 32) {
+  int cL = 0, cH = nfin;
+#define HBX_SEL_OPEN (cL != kk && cH != kk && ((Hk - Lk) >> 1) != 0ull)
+  // (1) interpolation rounds
+  for (int it = 0; it < 2 && HBX_SEL_OPEN && cH - cL > 64; ++it) {
+    const double Ld = sel_val(Lk), Hd = sel_val(Hk), rng = Hd - Ld;
+    if (!(rng - rng == 0.0)) break;  // range beyond the doubles: bisection only
+    const double span = (double)(cH - cL);
+    const double tm = fma(((double)(kk - cL) - 0.5) / span, rng, Ld);
+    const double de = (1.5 * sqrt((double)(kk - cL) * (double)(cH - kk) / span) + 2.0) / span * rng;
+    uint64_t klo = sel_key(tm - de), khi = sel_key(tm + de);
+    klo = klo < Lk ? Lk : (klo > Hk ? Hk : klo);
+    khi = khi < Lk ? Lk : (khi > Hk ? Hk : khi);
+    if (klo <= Lk && khi >= Hk) break;  // the window covers the bracket
+    const double lo = sel_val(klo), hi = sel_val(khi);
+    uint32_t alo = 0, ahi = 0;
 #pragma unroll
-      for (int r = 0; r < R; ++r) ones |= __builtin_amdgcn_ubfe((uint32_t)(key[r] >> 32), (uint32_t)(bit - 32), 1u) << r;
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) ones |= __builtin_amdgcn_ubfe((uint32_t)key[r], (uint32_t)bit, 1u) << r;
+    for (int r = 0; r < R; ++r) {
+      alo += v[r] < lo;
+      ahi += v[r] < hi;
     }
-    const uint32_t zero = alive & ~ones;
-    const int c0 = (int)wave_reduce_dpp((uint32_t)__popc(zero), OpAdd());
-    if (need <= c0) {
-      alive = zero;
-      cnt = c0;
+    const uint32_t both = wave_reduce_dpp(alo | (ahi << 16), OpAdd());  // counts <= 1024
+    const int clo = (int)(both & 0xffffu), chi = (int)(both >> 16);
+    if (clo >= kk) {
+      Hk = klo;
+      cH = clo;
+    } else if (chi < kk) {
+      Lk = khi;
+      cL = chi;
     } else {
-      alive &= ones;
-      need -= c0;
-      cnt -= c0;
-      if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
+      Lk = klo;
+      cL = clo;
+      Hk = khi;
+      cH = chi;
+    }
+    Lk = sel_uniform(Lk);
+    Hk = sel_uniform(Hk);
+  }
+  // (2) bisection at the highest bit where the bracket's keys can differ, while it holds > 64 keys
+  while (HBX_SEL_OPEN && cH - cL > 64) {
+    Lk = sel_uniform(Lk);
+    Hk = sel_uniform(Hk);
+    const int bt = 63 - __clzll((long long)(Lk ^ (Hk - 1ull)));
+    const uint64_t M = (Lk & ~((2ull << bt) - 1ull)) | (1ull << bt);  // bt = 63: 2 << 63 = 0
+    const double Md = sel_val(M);
+    uint32_t a = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) a += v[r] < Md;
+    const int cM = (int)wave_reduce_dpp(a, OpAdd());
+    if (cM >= kk) {
+      Hk = M;
+      cH = cM;
+    } else {
+      Lk = M;
+      cL = cM;
     }
   }
-  if (bit >= 0 && cnt != need) {
-    // phase 2: compact the <= 64 bucket keys into one per lane, in position order
+  if (HBX_SEL_OPEN) {
+    // (3) compact the <= 64 bracket losses into one per lane, in position order, and finish there
+    const double Ld = sel_val(Lk), Hd = sel_val(Hk);
     int base = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const bool a = (alive >> r) & 1u;
-      const uint64_t m = __ballot(a);
-      if (a) cbuf[wv][base + __popcll(m & ((1ull << lane) - 1ull))] = key[r];
-      base += __popcll(m);
+      const bool a = !(v[r] < Ld) && v[r] < Hd;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(v[r] < Hd) & ~__builtin_amdgcn_ballot_w64(v[r] < Ld);
+      const int at = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (a) cbuf[wv][at] = v[r];
+      base += (int)__popcll(m);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t key1 = cbuf[wv][lane < cnt ? lane : 0];
-    bool a1 = lane < cnt;
-    for (; bit >= 0 && cnt != need; --bit) {
-      const bool one = (key1 >> bit) & 1ull;
-      const int c0 = __popcll(__ballot(a1 && !one));
-      if (need <= c0) {
-        a1 = a1 && !one;
-        cnt = c0;
+    const int c0 = cL;
+    const uint64_t key1 = lane < cH - cL ? sel_key(cbuf[wv][lane]) : ~0ull;
+    while (HBX_SEL_OPEN) {
+      Lk = sel_uniform(Lk);
+      Hk = sel_uniform(Hk);
+      const int bt = 63 - __clzll((long long)(Lk ^ (Hk - 1ull)));
+      const uint64_t M = (Lk & ~((2ull << bt) - 1ull)) | (1ull << bt);
+      const int cM = c0 + (int)__popcll(__builtin_amdgcn_ballot_w64(key1 < M));
+      if (cM >= kk) {
+        Hk = M;
+        cH = cM;
       } else {
-        a1 = a1 && one;
-        need -= c0;
-        cnt -= c0;
-        if (bit >= 32) ph |= 1u << (bit - 32); else pl |= 1u << bit;
+        Lk = M;
+        cL = cM;
       }
     }
   }
-  // bits > bit are resolved (prefix P): an element advances iff its key's resolved part is below P,
-  // or equal and either the whole bucket advances (cnt == need: key < P + 2^(bit+1), one 64-bit
-  // compare) or -- keys equal in all 64 bits -- it is among the first `need` of them by position
-  const uint64_t P = ((uint64_t)ph << 32) | pl;
-  if (cnt == need) {
-    // bit <= 62 (at least one pass ran); -1 when all 64 bits were resolved.  No overflow: finite keys
-    // stay below 0xFFF0000000000000
-    const uint64_t T = P + (bit >= 0 ? (2ull << bit) : 1ull);
+#undef HBX_SEL_OPEN
+  if (cL == kk || cH == kk) {  // exactly kk keys below T
+    const double T = sel_val(cL == kk ? Lk : Hk);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool adv = key[r] < T && (allfin || ((fin >> r) & 1u));
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(adv ? 1 : 0), ars, lane, 64 * r, 0);
-    }
-  } else {
+    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[r] < T ? 1u : 0u), ars, lane, 64 * r, 0);
+  } else {  // Hk = Lk + 1: the bracket holds copies of one key, the first kk - cL of them by position advance
+    const double P = sel_val(Lk);
+    const int need = kk - cL;
     int taken = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const bool f = (fin >> r) & 1u;
-      const bool eq = f && key[r] == P;
-      const uint64_t m = __ballot(eq);
-      const bool take = (f && key[r] < P) || (eq && taken + __popcll(m & ((1ull << lane) - 1ull)) < need);
-      taken += __popcll(m);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1 : 0), ars, lane, 64 * r, 0);
+      const bool eq = v[r] == P;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(eq);
+      const int at = taken + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const bool take = v[r] < P || (eq && at < need);
+      taken += (int)__popcll(m);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1u : 0u), ars, lane, 64 * r, 0);
     }
   }
   if (lane == 0 && n_advance) n_advance[b] = kk;

@@ -228,3 +228,34 @@ def test_select_kernel_counts_and_extreme_keys(device):
             want = O.sh_advance(loss, kk)
             np.testing.assert_array_equal(adv.cpu().numpy().astype(bool), want, err_msg="k=%d" % kk)
             assert int(cnt.item()) == int(want.sum())
+
+
+@pytest.mark.parametrize("dist", ["lognormal", "exponents", "signed", "lowbits", "clustered", "uniform"])
+def test_select_kernel_search_paths(device, dist):
+    """The select kernel's three search stages on 1024-config brackets: interpolation hits (uniform),
+    misses on skewed or clustered losses, bisection across exponents and signs, and brackets whose
+    losses differ only in their lowest mantissa bits.  Masks equal argsort(argsort(losses)) < k."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(len(dist))
+    B, n = 96, 1024
+    lens = rs.randint(n // 2, n + 1, size=B)
+    lens[0] = n
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    N = int(seg[-1])
+    if dist == "lognormal":
+        loss = np.exp(rs.randn(N) * 4)
+    elif dist == "exponents":
+        loss = 10.0 ** rs.uniform(-300, 300, N)
+    elif dist == "signed":
+        loss = rs.randn(N) * 10.0 ** rs.randint(-5, 5, N)
+    elif dist == "lowbits":
+        loss = 0.75 + rs.randint(0, 4096, N) * np.spacing(0.75)
+    elif dist == "clustered":
+        loss = np.round(rs.rand(N) * 7) + rs.rand(N) * 1e-9
+    else:
+        loss = rs.rand(N)
+    k = np.floor(lens * rs.uniform(0.01, 0.99, size=B))
+    a_sel = promote.promote_segments(loss, seg, k, device=device)
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(a_sel[s:e], O.sh_advance(loss[s:e], k[b]), err_msg="bracket %d" % b)
