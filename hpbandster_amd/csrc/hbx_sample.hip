@@ -13,9 +13,10 @@
 // draw) -- the reference draws from numpy's global RNG, so parity is distributional
 // (tests/test_gpu_sample.py).
 //
-// One thread per (candidate, pair of dims): one Philox block and one 16-byte store per thread (even D),
-// the writes of a wave contiguous.  The datum draws of a block's candidates go through LDS; Phi at the
-// bounds comes from a per-model table when many candidates are drawn (hbx_kde_sample_table).
+// One Philox block per (candidate, pair of dims); a wave draws one pair of dims for 64 candidates (the
+// dim's branch and parameters uniform), the block's 64 rows leave through an LDS tile as contiguous
+// 16-byte stores.  Phi at the bounds comes from a per-model table when many candidates are drawn
+// (hbx_kde_sample_table).
 // hbx_norm_ppf keeps the fp64 inverse normal CDF (Wichura's AS 241) as a library function.
 #include <math.h>
 
@@ -166,55 +167,69 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
   return fma(bw_factor * h, flip ? -z : z, m);
 }
 
-// One thread per (candidate, pair of dims); a block covers SAMPLE_BLOCK consecutive pairs and first
-// draws the datum of each candidate they touch into LDS (one Philox call per candidate).  IDX is
-// uint32_t when Nc * ceil(D/2) < 2^32 (cheap index division) else uint64_t.
-template <typename IDX>
-__global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_kernel(
+// A block draws 64 candidates: lane l of every wave is candidate c0 + l, and wave w draws the pairs of
+// dims w, w + W, ... (W waves), so a wave's dims -- continuous or categorical, their bandwidths and
+// levels -- are uniform and the branches of sample_dim never split a wave.  Counter (candidate, pair of
+// dims, stream) and arithmetic as before: the draws do not depend on the launch shape.  Results go
+// through an LDS tile (row stride S doubles, even) and leave as contiguous 16-byte stores of the block's
+// 64 rows.  The datum draw of each candidate is made once (wave 0) and shared through LDS.
+__global__ __launch_bounds__(512) void kde_sample_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
     const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
     double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
     double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
-  __shared__ int32_t sdat[SAMPLE_BLOCK + 1];
+  extern __shared__ __align__(16) double tile[];  // [64][S]
+  __shared__ int32_t sdat[64];
   __shared__ double srh[HBX_MAX_D];  // 1 / bw per dim
-  for (int t = threadIdx.x; t < D; t += SAMPLE_BLOCK) srh[t] = 1.0 / bw[t];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const int S = (D + 2) & ~1;
   const int D2 = (D + 1) >> 1;
-  const IDX total = (IDX)(Nc * (int64_t)D2), Pd = (IDX)D2;
-  for (IDX base = (IDX)blockIdx.x * SAMPLE_BLOCK; base < total; base += (IDX)gridDim.x * SAMPLE_BLOCK) {
-    const IDX c0 = base / Pd;
-    const IDX last = (base + SAMPLE_BLOCK < total ? base + SAMPLE_BLOCK : total) - 1;
-    const int nc = (int)(last / Pd - c0) + 1;
-    for (int t = threadIdx.x; t < nc; t += SAMPLE_BLOCK) {
-      const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)(c0 + t), DATUM_WORD, stream_id), 0);
-      const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
-      sdat[t] = idx;
-      if (datum) datum[c0 + t] = idx;
-    }
-    __syncthreads();
-    const IDX e = base + threadIdx.x;
-    if (e < total) {
-      const IDX i = e / Pd;
-      const int k = (int)(e - i * Pd), d = 2 * k;
-      const int32_t idx = sdat[i - c0];
-      const double* xr = X + rows[idx] * (int64_t)D;
+  const int64_t c0 = (int64_t)blockIdx.x * 64;
+  const int nc = (int)(Nc - c0 < 64 ? Nc - c0 : 64);  // candidates of this block
+  const int64_t i = c0 + lane;
+  for (int t = threadIdx.x; t < D; t += blockDim.x) srh[t] = 1.0 / bw[t];
+  if (wave == 0 && lane < nc) {
+    const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)i, DATUM_WORD, stream_id), 0);
+    const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
+    sdat[lane] = idx;
+    if (datum) datum[i] = idx;
+  }
+  __syncthreads();
+  if (lane < nc) {
+    const int32_t idx = sdat[lane];
+    const double* xr = X + rows[idx] * (int64_t)D;
+    bool derr = false;
+    for (int k = wave; k < D2; k += W) {
+      const int d = 2 * k;
       const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
-      bool derr = false;
       const double v0 = sample_dim(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
-      double* out = cands + (int64_t)i * D + d;
       if (d + 1 < D) {
         const double v1 = sample_dim(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
-        if ((D & 1) == 0) {
-          *(double2*)out = make_double2(v0, v1);  // 16-byte aligned: even offset, 16-byte aligned base
-        } else {
-          out[0] = v0;
-          out[1] = v1;
-        }
+        *(double2*)(tile + lane * S + d) = make_double2(v0, v1);
       } else {
-        out[0] = v0;
+        tile[lane * S + d] = v0;
       }
-      if (derr && domain_err) domain_err[i] = 1;
     }
-    __syncthreads();
+    if (derr && domain_err) domain_err[i] = 1;
+  }
+  __syncthreads();
+  // the block's rows are contiguous in HBM: nc * D doubles from cands + c0 * D
+  double* out = cands + c0 * (int64_t)D;
+  if ((D & 1) == 0) {
+    const int h = D >> 1;  // 16-byte pieces per row
+    const float rh = 1.f / (float)h;
+    for (int j = threadIdx.x; j < nc * h; j += blockDim.x) {
+      const int row = (int)(((float)j + 0.5f) * rh);  // exact: (j + 1/2) / h is >= 1/(2h) from an integer
+      const int col = 2 * (j - row * h);
+      *(double2*)(out + 2 * j) = *(const double2*)(tile + row * S + col);
+    }
+  } else {
+    const float rd = 1.f / (float)D;
+    for (int j = threadIdx.x; j < nc * D; j += blockDim.x) {
+      const int row = (int)(((float)j + 0.5f) * rd);
+      out[j] = tile[row * S + (j - row * D)];
+    }
   }
 }
 
@@ -260,15 +275,14 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   hipStream_t s = (hipStream_t)stream;
   if (domain_err) HBX_HIP(hipMemsetAsync(domain_err, 0, (size_t)Nc, s));
   if ((D & 1) == 0 && ((uintptr_t)cands & 15)) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: cands not 16-byte aligned");
-  const int64_t total = Nc * (int64_t)((D + 1) / 2);
-  const int64_t blocks = (total + SAMPLE_BLOCK - 1) / SAMPLE_BLOCK;
-  const unsigned grid = (unsigned)(blocks < 65536 ? blocks : 65536);
-  if (total + SAMPLE_BLOCK < (int64_t)UINT32_MAX)
-    hipLaunchKernelGGL(kde_sample_kernel<uint32_t>, dim3(grid), dim3(SAMPLE_BLOCK), 0, s, X, D, rows, n, bw, levels,
-                       (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
-  else
-    hipLaunchKernelGGL(kde_sample_kernel<uint64_t>, dim3(grid), dim3(SAMPLE_BLOCK), 0, s, X, D, rows, n, bw, levels,
-                       (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
+  const int D2 = (D + 1) / 2, W = D2 < 8 ? D2 : 8;  // waves per block: pairs of dims drawn side by side
+  const size_t lds = (size_t)64 * ((D + 2) & ~1) * sizeof(double);
+  const int64_t blocks = (Nc + 63) / 64;
+  if (blocks > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
+  if (lds > 65536)  // D > 126: the tile needs more than the default dynamic LDS limit (<= 132 KB at D = 256)
+    HBX_HIP(hipFuncSetAttribute((const void*)kde_sample_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kde_sample_kernel, dim3((unsigned)blocks), dim3(64 * W), lds, s, X, D, rows, n, bw, levels,
+                     (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
