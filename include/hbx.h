@@ -251,7 +251,7 @@ int hbx_argmax_records(const void* all, int32_t nranks, void* out, void* stream)
 /* advance[i] = rank_i < k[b] among the finite losses of bracket b (non-finite = CRASHED, never
  * advance; ties ranked by position).  loss: device f64[N]; seg_off: device i64[B+1]; k: device f64[B];
  * order: device i64[N] (sorted positions per bracket, output) or NULL when only the mask is wanted --
- * brackets of <= 1024 configurations then take an O(n) radix select of the k-th loss and need no
+ * brackets of <= 1024 configurations then take an O(n) selection of the k-th loss and need no
  * scratch (scratch may be NULL); advance: device u8[N]; n_advance: device i64[B], nullable.
  * scratch: hbx_sort_scratch_bytes(N) bytes when order is requested or a bracket exceeds 1024. */
 int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
