@@ -47,7 +47,9 @@ def kernel_model(kde_obj, dc, du):
       issue:       8 cycles held per matrix instruction + 4 v_exp_f32 (8 each) + 4 v_add_f32 (4 each)
     hbx_score_h32.hip (32x32 tiles, variant bit 6): one tile = 1024 pairs:
       matrix pipe: h32_nd(NSC) = ceil((6 + 24 NSC) / 16) dense 32x32x16 f16 MFMAs (3 slots per
-                   continuous dim, 6 for the C_j / c_i pieces) + KC sparse 32x32x32 (32 cycles each)
+                   continuous dim, 6 for the C_j / c_i pieces) + KP = ceil(KC / 2) sparse 32x32x32 (32
+                   cycles each; the acquisition's FAST instance multiplies the one-hot hi parts only, the
+                   precise one adds KP for the lo parts)
       issue:       8 cycles held per matrix instruction + 16 v_exp_f32 + 16 v_add_f32
     both quoted per 256 pairs (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost').  Dense-equivalent
     matrix work: 2 x 32 x (NSC + KC) flops per pair either way."""
@@ -58,9 +60,13 @@ def kernel_model(kde_obj, dc, du):
     nsc = (4 * kde_obj.dc_pad + 31) // 32
     if h32:
         nd = (6 + 24 * nsc + 15) // 16  # h32_nd(nsc) dense steps
-        n_mat = nd + kc * (2 if signed else 1)  # per 1024 pairs (+ the parity product when signed)
+        kp = (kc + 1) // 2  # 32-position one-hot steps
+        fast = (not signed) and kp > 0  # the acquisition's instance
+        n_mat = nd + kp * (1 if fast else 2) + (kp if signed else 0)  # per 1024 pairs (+ signed parity)
         valu = 16 * 8 + 16 * 4 + (32 * 4 if signed else 0)  # exp2, add (+ fract, fma when signed)
-        return {"kernel": "kde_logpdf_h32%s_kernel<%d,%d>" % ("s" if signed else "", nsc, kc),
+        name = ("kde_logpdf_h32s_kernel<%d,%d>" % (nsc, kp) if signed else
+                "kde_logpdf_h32_kernel<%d,%d,%s>" % (nsc, kp, "true" if fast else "false"))
+        return {"kernel": name,
                 "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
                           "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + valu) / 4,
                           "bound_cycles": max(32 * n_mat, 8 * n_mat + valu) / 4,

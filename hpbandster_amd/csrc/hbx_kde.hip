@@ -273,10 +273,10 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   const bool hm_ok = (du == 0 || kc > 0) && dcp >= 8;
   int hmode = (hm_ok && A.hm_allowed) ? 1 : 0;
   // the 32x32-tile kernel (hbx_score_h32.hip) in the buckets it is built for
-  if (hmode && A.h32_allowed && h32_ok(nsc_of(dcp), kc, has_neg)) hmode = 2;
+  if (hmode && A.h32_allowed && h32_ok(nsc_of(dcp), h32_kp(kc), has_neg)) hmode = 2;
   P->hmode = hmode;
   P->nsc = nsc_of(dcp);
-  P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), kc, has_neg)
+  P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), h32_kp(kc), has_neg)
                                : (hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0));
 }
 
@@ -299,7 +299,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   float* ch = table + (int64_t)(j / OBS_CHUNK) * chunk_f;
   const int jj = j % OBS_CHUNK;
   // hm: 0 = f32 layout, 1 = hmode (16x16 kernel), 2 = h32 (32x32 kernel, no chunk header)
-  const int KTP = hm == 2 ? h32_ktp(P->nsc, P->kc, P->has_neg) : h_ktp(dcp, P->kc);
+  const int KTP = hm == 2 ? h32_ktp(P->nsc, h32_kp(P->kc), P->has_neg) : h_ktp(dcp, P->kc);
   _Float16* hrow = (_Float16*)(hm == 2 ? ch : ch + OBS_CHUNK) + jj * KTP;
   double C = 0.0;
   // hmode rows are written 16 bytes (8 halves) at a time: two dims' h, l, h, l per store
@@ -346,47 +346,56 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   }
   if (hm == 2 && slot)  // row padding past the index words (rows are 16-byte aligned, KTP % 8 == 0); the
     // parity block of a signed KDE is rewritten below
-    for (int k = (16 * nd32 + 16 * P->kc + 4 * h32_ksp(P->kc)) & ~7; k < KTP; k += 8) *(h8*)(hrow + k) = z8;
+    for (int k = (16 * nd32 + 32 * h32_kp(P->kc) + 4 * h32_ksp(h32_kp(P->kc))) & ~7; k < KTP; k += 8)
+      *(h8*)(hrow + k) = z8;
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
       const float v = (ok && u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
       if (slot) ch[KP * KROW + jj * dup + u] = v;
     }
   } else if (slot && hm == 2) {
-    // 2:4-compressed one-hot (h32 layout): per step s and group g (positions t0 = 16s + 2g and t0 + 1, a
-    // dim's positions never straddle a group) the observation's (delta hi, lo) when its level is t0 or
-    // t0 + 1, and the index nibble (slots 0,1: 0x4; slots 2,3: 0xE); index dword ksp h + s holds groups
-    // 4h..4h+3 of step s
+    // 2:4-compressed one-hot (h32 layout, hbx_kde_impl.h): per step s and group g (positions t0 = 32s + 4g
+    // .. t0 + 3) the f16 hi / lo of delta_u for the observation's level in the pair (t0, t0+1) and in
+    // (t0+2, t0+3), and the index nibble i0 | i1 << 2 (i0: 0 or 1, i1: 2 or 3); index dword ksp h + s
+    // holds groups 4h..4h+3 of step s
+    const int kp = h32_kp(P->kc);
     _Float16* cz = hrow + 16 * nd32;
-    _Float16* cp = hrow + h32_par(P->nsc, P->kc);  // parity block (signed KDEs)
-    const int ksp = h32_ksp(P->kc);
+    _Float16* cp = hrow + h32_par(P->nsc, kp);  // parity block (signed KDEs)
+    const int ksp = h32_ksp(kp);
     uint32_t iw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    for (int s = 0; s < P->kc; ++s) {
-      h8 v[2] = {{}, {}}, pv[2] = {{}, {}};
+    for (int s = 0; s < kp; ++s) {
+      h8 vh[2] = {{}, {}}, vl[2] = {{}, {}}, pv[2] = {{}, {}};
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
-        const int t0 = 16 * s + 2 * g;
-        bool m0 = false, m1 = false;
-        if (ok && t0 < P->oh_total) m0 = x[P->oh_col[t0]] == P->oh_val[t0];
-        if (ok && t0 + 1 < P->oh_total) m1 = x[P->oh_col[t0 + 1]] == P->oh_val[t0 + 1];
-        if (m0 || m1) {
-          const int u = P->oh_dim[m1 ? t0 + 1 : t0];
-          const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
-          const float hi = (float)(_Float16)dl;
-          v[g >> 2][2 * (g & 3)] = (_Float16)hi;
-          v[g >> 2][2 * (g & 3) + 1] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
-          if (P->cat_negf[u] != 0.f) pv[g >> 2][2 * (g & 3)] = (_Float16)0.5f;
+        uint32_t nib = 0u;
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int t0 = 32 * s + 4 * g + 2 * pr;
+          bool m0 = false, m1 = false;
+          if (ok && t0 < P->oh_total) m0 = x[P->oh_col[t0]] == P->oh_val[t0];
+          if (ok && t0 + 1 < P->oh_total) m1 = x[P->oh_col[t0 + 1]] == P->oh_val[t0 + 1];
+          if (m0 || m1) {
+            const int u = P->oh_dim[m1 ? t0 + 1 : t0];
+            const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
+            const float hi = (float)(_Float16)dl;
+            vh[g >> 2][2 * (g & 3) + pr] = (_Float16)hi;
+            vl[g >> 2][2 * (g & 3) + pr] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
+            if (P->cat_negf[u] != 0.f) pv[g >> 2][2 * (g & 3) + pr] = (_Float16)0.5f;
+          }
+          nib |= (uint32_t)(2 * pr + (m1 ? 1 : 0)) << (2 * pr);
         }
-        iw[ksp * (g >> 2) + s] |= (m1 ? 0xEu : 0x4u) << (4 * (g & 3));
+        iw[ksp * (g >> 2) + s] |= nib << (4 * (g & 3));
       }
-      *(h8*)(cz + 16 * s) = v[0];
-      *(h8*)(cz + 16 * s + 8) = v[1];
+      *(h8*)(cz + 16 * s) = vh[0];
+      *(h8*)(cz + 16 * s + 8) = vh[1];
+      *(h8*)(cz + 16 * kp + 16 * s) = vl[0];
+      *(h8*)(cz + 16 * kp + 16 * s + 8) = vl[1];
       if (P->has_neg) {
         *(h8*)(cp + 16 * s) = pv[0];
         *(h8*)(cp + 16 * s + 8) = pv[1];
       }
     }
-    uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 16 * P->kc);
+    uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 32 * kp);
     for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
   } else if (slot) {
     const int W = P->kc * 32;  // one-hot halves per observation
@@ -1400,7 +1409,9 @@ static logpdf_fn pick_rescue(int dc_pad) {
 
 // variant code of a prepared KDE (hbx_kde_prepare info[0]): bit 0 = signed sums, bits 1-3 = kc,
 // bit 4 = hmode (whole exponent on the f16 matrix cores), bit 6 = its 32x32-tile kernel (h32 table)
-static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
+// fast: the acquisition's instance where one exists (the 32x32 kernel without the one-hot lo steps,
+// their bound added) -- its ln-pdf estimates are looser than 1e-5, so calls that report them do not use it
+static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = false) {
   const bool sg = variant & 1;
   const int kc = du_pad == 0 ? 0 : (variant >> 1) & 7;  // no categorical dims: kc irrelevant
   const bool hm = (variant >> 4) & 1;
@@ -1410,8 +1421,11 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant) {
   const logpdf_fn r = sg ? pick_rescue<true>(dc_pad) : pick_rescue<false>(dc_pad);
   if (hm && ((variant >> 6) & 1)) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
-    return {hbx_pick_h32(nsc_of(dc_pad), kc, sg), r, 32 * H16_WAVES, 64 * H16_WAVES,
-            hbx_pick_h32_pair(nsc_of(dc_pad), kc, sg), sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
+    const int kp = h32_kp(kc);
+    const bool fa = fast && !sg && kp > 0;
+    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa), r, 32 * H16_WAVES, 64 * H16_WAVES,
+            hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa),
+            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1715,8 +1729,11 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     return hbx_fail(HBX_ERR_ARG, "workspace too small: %lld < %lld bytes", (long long)ws_bytes,
                     (long long)w.total);
   const bool exact_only = ((variant_good | variant_bad) >> 5) & 1;
-  ScoreFns fg = pick_logpdf(dc_pad, du_pad, variant_good);
-  ScoreFns fb = pick_logpdf(dc_pad, du_pad, variant_bad);
+  // no ln-pdf estimates returned: the fast scoring instances (their looser bounds only widen the shortlist
+  // the exact re-score resolves)
+  const bool fast = !logl_out && !logg_out;
+  ScoreFns fg = pick_logpdf(dc_pad, du_pad, variant_good, fast);
+  ScoreFns fb = pick_logpdf(dc_pad, du_pad, variant_bad, fast);
   if (!exact_only && (!fg.main || !fb.main))
     return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
   char* ws = (char*)workspace;

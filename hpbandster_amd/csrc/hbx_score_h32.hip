@@ -10,6 +10,9 @@
 //
 // Roles: A = observations (32 rows per tile, read from the LDS ring; the one-hot part 2:4-compressed
 // in the table, hbx_kde_impl.h h32 layout), B = candidates (32 columns per wave, resident in registers).
+// One-hot part: KP steps of 32 positions, the deltas' f16 hi parts then their lo parts against the same
+// candidate fragments and index words; the FAST instance (acquisition) multiplies the hi parts only and
+// adds the lo parts' bound: 6 matrix instructions per 1024 pairs at 24c + 8u instead of 7.
 // The output column of a lane is ONE candidate, so a lane's 16 accumulator registers are 16
 // observations of the same candidate: the exp2 sum is an in-register tree and a lane carries one
 // running sum (the 16x16 kernel's A = candidates layout needs 16 per lane here).  The candidate's
@@ -62,18 +65,20 @@ struct SgbH32<NM, NM, NV, NRL> {
   static __device__ __forceinline__ void run() {}
 };
 
-template <int NSC, int KC, bool SG>
+template <int NSC, int KP, bool SG, bool FAST>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
                                                     const unsigned blk) {
   constexpr int ND = h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + 3 slots per continuous dim)
-  constexpr int KS = KC;       // sparse 32-wide K-steps (one-hot)
-  constexpr int NMT = ND + KS; // matrix instructions per 32x32 tile
-  constexpr int KTP = h32_ktp(NSC, KC, SG);
-  constexpr int CHF = h32_chunk_floats(NSC, KC, SG);
-  constexpr int PAR = h32_par(NSC, KC);  // signed: the parity block (halves into the row)
-  static_assert(!SG || KC > 0, "signed sums come from categorical dims");
+  constexpr int KS = KP;                     // sparse 32-wide K-steps (one-hot positions), hi parts
+  constexpr int KL = FAST ? 0 : KP;          // ... and lo parts
+  constexpr int NMT = ND + KS + KL;          // matrix instructions per 32x32 tile
+  constexpr int KTP = h32_ktp(NSC, KP, SG);
+  constexpr int CHF = h32_chunk_floats(NSC, KP, SG);
+  constexpr int PAR = h32_par(NSC, KP);  // signed: the parity block (halves into the row)
+  static_assert(!SG || KP > 0, "signed sums come from categorical dims");
+  static_assert(!FAST || (KP > 0 && !SG), "the fast instance drops one-hot lo parts of unsigned sums");
   constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
   constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -94,7 +99,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // per-dim parameters and the block's candidate rows staged in the (not yet used) ring
   struct ContPrm { double scale, center; float xmax; int32_t col; };
   struct OhPrm { double val; int32_t col, pad; };
-  constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 16 * (KC > 0 ? KC : 1) * (int)sizeof(OhPrm);
+  constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 32 * (KP > 0 ? KP : 1) * (int)sizeof(OhPrm);
   static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
   const int DS = D | 1;  // odd row stride in doubles: conflict-free
   const int64_t rows_bytes = (int64_t)HW * 32 * DS * 8;
@@ -107,7 +112,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     cprm[tid] = ContPrm{act ? P->cont_scale[tid] : 0.0, act ? P->center[tid] : 0.0, act ? P->xmax[tid] : 0.f,
                         act ? P->cont_dim[tid] : 0};
   }
-  if (tid < 16 * KC) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
+  if (tid < 32 * KP) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
   const bool staged = rows_fit && cbase < Nc;
   const int64_t nv = (Nc - cbase) < 32 ? (Nc - cbase) : 32;  // valid rows of this wave
   double* xs = (double*)lds + (int64_t)wave * 32 * DS;
@@ -117,8 +122,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // B operands of candidate column c.  Dense step s, half j of the lane: slot k = 16s + 8h + j -- slots
   // 0-2: 1 (against the C_j pieces), 3-5: the pieces of the shifted c_i (against 1; 0 in the probe),
   // 6 + 3d + {0,1,2}: (hi, hi, lo) of x''_d against the observation's (Xh, Xl, Xh).  Sparse step s:
-  // one-hot positions 16s + 4h + q (halves 2q, 2q+1) and 16s + 8 + 4h + q (halves 8 + 2q, +1), both
-  // halves 1 on a match.
+  // one-hot positions 32s + 8h + j (half j) and 32s + 16 + 8h + j (half 8 + j), 1 on a match.
   f16x8 bd[ND];
   f16x16 bsp[KS > 0 ? KS : 1];
   float ci = 0.f, bnd = 0.f;
@@ -149,14 +153,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const OhPrm o0 = oprm[16 * s + 4 * h + q], o1 = oprm[16 * s + 8 + 4 * h + q];
-        const _Float16 m0 = (x[o0.col] == o0.val) ? (_Float16)1.f : (_Float16)0.f;
-        const _Float16 m1 = (x[o1.col] == o1.val) ? (_Float16)1.f : (_Float16)0.f;
-        bsp[s][2 * q] = m0;
-        bsp[s][2 * q + 1] = m0;
-        bsp[s][8 + 2 * q] = m1;
-        bsp[s][8 + 2 * q + 1] = m1;
+      for (int j = 0; j < 8; ++j) {
+        const OhPrm o0 = oprm[32 * s + 8 * h + j], o1 = oprm[32 * s + 16 + 8 * h + j];
+        bsp[s][j] = (x[o0.col] == o0.val) ? (_Float16)1.f : (_Float16)0.f;
+        bsp[s][8 + j] = (x[o1.col] == o1.val) ? (_Float16)1.f : (_Float16)0.f;
       }
     }
   };
@@ -202,9 +202,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // half's index words (at 2 ksp h halves past the compressed one-hot part)
   f16x8 ad[ND];
   f16x8 asp[KS > 0 ? KS : 1];
+  f16x8 asl[KL > 0 ? KL : 1];  // the lo parts (precise instance)
   f16x8 apar[SG ? KS : 1];  // signed: parity fragments (the one-hot part's positions, 0.5 per negative dim)
   typename H32Idx<KS>::T aix;
-  const int ixo = 16 * ND + 16 * KC + 2 * h32_ksp(KC) * h - 8 * h;  // index words relative to arow
+  const int ixo = 16 * ND + 32 * KP + 2 * h32_ksp(KP) * h - 8 * h;  // index words relative to arow
   auto arow = [&](const float* buf, int jt) { return (const _Float16*)buf + (32 * jt + c) * KTP + 8 * h; };
   auto readA = [&](const float* buf, int jt) {
     const _Float16* a = arow(buf, jt);
@@ -212,6 +213,8 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 0; s < ND; ++s) ad[s] = *(const f16x8*)(a + 16 * s);
 #pragma unroll
     for (int s = 0; s < KS; ++s) asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
+#pragma unroll
+    for (int s = 0; s < KL; ++s) asl[s] = *(const f16x8*)(a + 16 * ND + 16 * KP + 16 * s);
     if constexpr (SG)
 #pragma unroll
       for (int s = 0; s < KS; ++s) apar[s] = *(const f16x8*)(a + PAR + 16 * s);
@@ -226,6 +229,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+#pragma unroll
+    for (int s = 0; s < KL; ++s)
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
   };
   // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it; a
   // signed KDE's parity product (the same index words) follows into accp
@@ -242,7 +248,13 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 0; s < KS; ++s) {
       acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
       asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
-      if (!SG && s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+      if (!SG && KL == 0 && s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
+    }
+#pragma unroll
+    for (int s = 0; s < KL; ++s) {
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      asl[s] = *(const f16x8*)(a + 16 * ND + 16 * KP + 16 * s);
+      if (!SG && s == KL - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
     }
     if constexpr (SG) {
 #pragma unroll
@@ -382,6 +394,14 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       // f16 hi/lo representation error of both coordinates (2 x 2^-22 sum|x''X'|) and the lo.lo products
       // given up (together <= 2^-22 sum|x''X'|), plus the C_j / c_i pieces' subnormal rounding
       if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-19f) * HBX_LN2f;
+      if constexpr (FAST) {  // the one-hot lo parts left out: |sum_u lo_u m_u| <= sum_u |lo_u| (log2 units)
+        float lo_err = 0.f;
+        for (int u = 0; u < P->du; ++u) {
+          const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
+          if (fabsf(dl) < 60000.f) lo_err += fabsf(dl - (float)(_Float16)dl);
+        }
+        if (o.err > 0.f) o.err += 2.f * lo_err * HBX_LN2f;
+      }
       if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) o.err = -1.f;  // rescue marker
       out[ii] = o;
     }
@@ -389,78 +409,83 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 }
 
 // unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU)
-template <int NSC, int KC>
+template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KC, false>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, false, FAST>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
 // both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
-template <int NSC, int KC>
+template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
-  kde_logpdf_h32_body<NSC, KC, false>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                      second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, false, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
 }
 
-// signed sums (the parity product and its accumulators: 130-170 VGPRs): one 8-wave block per CU, so
-// 2 waves per SIMD and a 256-register budget
-template <int NSC, int KC>
+// signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
+// and a 256-register budget
+template <int NSC, int KP>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KC, true>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, true, false>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
-template <int NSC, int KC>
+template <int NSC, int KP>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;
-  kde_logpdf_h32_body<NSC, KC, true>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                     second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, true, false>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
 }
 
-// instances: h32_ok (hbx_kde_impl.h)
-template <int NSC, int KC, bool SG, bool PAIR>
+// instances: h32_ok (hbx_kde_impl.h); FAST for unsigned sums with a one-hot part
+template <int NSC, int KP, bool SG, bool PAIR, bool FAST>
 static constexpr auto h32_inst() {
   if constexpr (PAIR) {
-    if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KC>;
-    else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KC>;
+    if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KP>;
+    else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KP, FAST>;
   } else {
-    if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KC>;
-    else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KC>;
+    if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KP>;
+    else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KP, FAST>;
   }
+}
+
+template <int NSC, int KP, bool SG, bool PAIR>
+static auto pick32_fast(bool fast) {
+  if constexpr (!SG && KP > 0)
+    if (fast) return h32_inst<NSC, KP, SG, PAIR, true>();
+  return h32_inst<NSC, KP, SG, PAIR, false>();
 }
 
 template <int NSC, bool SG, bool PAIR>
-static auto pick32_kc(int kc) {
-  switch (kc) {
-    case 0: if constexpr (h32_ok(NSC, 0, SG)) return h32_inst<NSC, 0, SG, PAIR>(); break;
-    case 1: if constexpr (h32_ok(NSC, 1, SG)) return h32_inst<NSC, 1, SG, PAIR>(); break;
-    case 2: if constexpr (h32_ok(NSC, 2, SG)) return h32_inst<NSC, 2, SG, PAIR>(); break;
-    case 3: if constexpr (h32_ok(NSC, 3, SG)) return h32_inst<NSC, 3, SG, PAIR>(); break;
-    case 4: if constexpr (h32_ok(NSC, 4, SG)) return h32_inst<NSC, 4, SG, PAIR>(); break;
+static auto pick32_kp(int kp, bool fast) {
+  switch (kp) {
+    case 0: if constexpr (h32_ok(NSC, 0, SG)) return pick32_fast<NSC, 0, SG, PAIR>(fast); break;
+    case 1: if constexpr (h32_ok(NSC, 1, SG)) return pick32_fast<NSC, 1, SG, PAIR>(fast); break;
+    case 2: if constexpr (h32_ok(NSC, 2, SG)) return pick32_fast<NSC, 2, SG, PAIR>(fast); break;
   }
-  return decltype(h32_inst<NSC, 1, SG, PAIR>())(nullptr);
+  return decltype(h32_inst<NSC, 1, SG, PAIR, false>())(nullptr);
 }
 
 template <bool SG, bool PAIR>
-static auto pick32(int nsc, int kc) {
+static auto pick32(int nsc, int kp, bool fast) {
   switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {8, 16, 24, 32}
-    case 1: return pick32_kc<1, SG, PAIR>(kc);
-    case 2: return pick32_kc<2, SG, PAIR>(kc);
-    case 3: return pick32_kc<3, SG, PAIR>(kc);
-    case 4: return pick32_kc<4, SG, PAIR>(kc);
+    case 1: return pick32_kp<1, SG, PAIR>(kp, fast);
+    case 2: return pick32_kp<2, SG, PAIR>(kp, fast);
+    case 3: return pick32_kp<3, SG, PAIR>(kp, fast);
+    case 4: return pick32_kp<4, SG, PAIR>(kp, fast);
   }
-  return decltype(pick32_kc<1, SG, PAIR>(0))(nullptr);
+  return decltype(pick32_kp<1, SG, PAIR>(0, false))(nullptr);
 }
 
-logpdf_fn hbx_pick_h32(int nsc, int kc, bool sg) {
-  return sg ? pick32<true, false>(nsc, kc) : pick32<false, false>(nsc, kc);
+logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast) {
+  return sg ? pick32<true, false>(nsc, kp, fast) : pick32<false, false>(nsc, kp, fast);
 }
 
-logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kc, bool sg) {
-  return sg ? pick32<true, true>(nsc, kc) : pick32<false, true>(nsc, kc);
+logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast) {
+  return sg ? pick32<true, true>(nsc, kp, fast) : pick32<false, true>(nsc, kp, fast);
 }

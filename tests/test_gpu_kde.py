@@ -466,12 +466,15 @@ def test_h32_kernel_choice_and_large_shift_rescue(device, monkeypatch):
         assert res.index == O.select(l, g)[0]
 
 
-@pytest.mark.parametrize("dc,du", [(8, 4), (6, 8), (8, 12), (16, 0), (12, 4), (16, 8), (24, 4), (32, 0)])
+@pytest.mark.parametrize("dc,du", [(8, 4), (6, 8), (8, 12), (16, 0), (12, 4), (16, 8), (24, 4), (32, 0), (16, 12),
+                                   (32, 4)])
 def test_h32_every_instance_matches_oracle(device, dc, du):
-    """Every (continuous K-steps, one-hot K-steps) instance of the 32x32-tile kernel the bench shape does
-    not use -- nsc = dc_pad / 8, kc = ceil(one-hot positions / 16) with 3-level dims padded to 4
+    """Every (continuous K-steps, one-hot steps) instance of the 32x32-tile kernel the bench shape does
+    not use -- nsc = dc_pad / 8, kp = ceil(one-hot positions / 32) with 3-level dims padded to 4
     positions -- on 2000 observations (chunks partly filled) and 700 candidates (a partial block):
-    ln-pdf estimates within 1e-5 of the oracle's log-space restatement, the oracle's winner."""
+    the precise instance's ln-pdf estimates within 1e-5 of the oracle's log-space restatement, the
+    oracle's winner from it and from the acquisition's FAST instance (one-hot lo parts in the bound),
+    whose result record equals the precise one's in index, score and pdfs."""
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
     n, lev = 2000, 3
@@ -492,3 +495,6 @@ def test_h32_every_instance_matches_oracle(device, dc, du):
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
     assert res.index == O.select(l, g)[0]
+    fast = pair.acquire(C)  # no ln-pdf estimates requested: the FAST scoring instance
+    assert fast.index == res.index
+    assert (fast.score, fast.pdf_l, fast.pdf_g) == (res.score, res.pdf_l, res.pdf_g)
