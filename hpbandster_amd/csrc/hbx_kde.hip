@@ -346,7 +346,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   }
   if (hm == 2 && slot)  // row padding past the index words (rows are 16-byte aligned, KTP % 8 == 0); the
     // parity block of a signed KDE is rewritten below
-    for (int k = (16 * nd32 + 32 * h32_kp(P->kc) + 4 * h32_ksp(h32_kp(P->kc))) & ~7; k < KTP; k += 8)
+    for (int k = (16 * nd32 + 32 * h32_kp(P->kc) + 2 * h32_ixw(h32_kp(P->kc))) & ~7; k < KTP; k += 8)
       *(h8*)(hrow + k) = z8;
   if (P->kc == 0) {
     for (int u = 0; u < dup; ++u) {
@@ -396,7 +396,12 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
       }
     }
     uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 32 * kp);
-    for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
+    if (kp == 1) {  // dwords 2b + h, b = bit 4 of the row (bank spread of the kernel's b64 reads)
+      const int b = (jj >> 4) & 1;
+      for (int q = 0; q < 4; ++q) ix[q] = (q >> 1) == b ? iw[q & 1] : 0u;
+    } else {
+      for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
+    }
   } else if (slot) {
     const int W = P->kc * 32;  // one-hot halves per observation
     _Float16* oh;

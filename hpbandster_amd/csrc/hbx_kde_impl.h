@@ -84,8 +84,11 @@ __host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
 //                          halves 16s + 2g, +1 = the f16 hi of delta_u for the observation's level in
 //                          (t0, t0+1) and in (t0+2, t0+3), 0 where it has none
 //   [16 nd + 16 kp, +16 kp) the lo parts of the same deltas, same places
-//   [16 nd + 32 kp, ...)   sparse index words, shared by both parts: 2 x h32_ksp dwords, dword ksp h + s =
-//                          the index nibbles (i0 in {0,1}, i1 in {2,3}) of groups 4h..4h+3 of step s
+//   [16 nd + 32 kp, ...)   sparse index words, shared by both parts: h32_ixw dwords; dword ksp h + s = the
+//                          index nibbles (i0 in {0,1}, i1 in {2,3}) of groups 4h..4h+3 of step s -- for kp = 1
+//                          at dword 2b + h with b = bit 4 of the row: the lanes read them as ds_read_b64
+//                          (banks (a/4) mod 64 over 32-lane groups), and rows c, c + 16 of a tile, 16 x 4*odd
+//                          dwords apart, would otherwise share banks
 // The precise instance runs the hi and the lo steps (2 kp sparse instructions); the FAST one (the
 // acquisition) only the hi steps, the lo part -- at most sum_u |delta_u - f16(delta_u)| in the exponent
 // -- going into its bound.
@@ -103,8 +106,9 @@ __host__ __device__ constexpr bool h32_ok(int nsc, int kp, int sgn = 0) {
   return kp <= 2 && (h32_nd(nsc) + 2 * kp <= 8 || (nsc == 4 && kp == 1)) && (!sgn || kp >= 1);
 }
 __host__ __device__ constexpr int h32_ksp(int kp) { return kp == 3 ? 4 : kp; }  // index dwords per lane half
+__host__ __device__ constexpr int h32_ixw(int kp) { return kp == 1 ? 4 : 2 * h32_ksp(kp); }  // index dwords per row
 __host__ __device__ constexpr int h32_par(int nsc, int kp) {  // parity block offset (halves, 16-byte aligned)
-  return (16 * h32_nd(nsc) + 32 * kp + 4 * h32_ksp(kp) + 7) & ~7;
+  return (16 * h32_nd(nsc) + 32 * kp + 2 * h32_ixw(kp) + 7) & ~7;
 }
 __host__ __device__ constexpr int h32_ktp(int nsc, int kp, int sgn = 0) {
   return 8 * (((h32_par(nsc, kp) + (sgn ? 16 * kp : 0) + 7) / 8) | 1);

@@ -38,12 +38,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define H32_CMAX 30000.f    // |shifted c_i| limit of the three-piece split (else: rescue pass)
 
-// sparse index words of one tile: KS dwords (one ds_read)
+// sparse index words of one tile: KS dwords (one ds_read).  KS = 1: both lane halves read the row's two
+// dwords and take theirs (ds_read_b64 banks over 64 dwords, b32 over 32: 4-way on these rows)
 template <int KS> struct H32Idx { typedef u32x4 T; };
-template <> struct H32Idx<1> { typedef uint32_t T; };
+template <> struct H32Idx<1> { typedef u32x2 T; };
 template <> struct H32Idx<2> { typedef u32x2 T; };
-template <int KS, typename T> __device__ __forceinline__ int h32_idx(const T& v, int s) {
-  if constexpr (KS == 1) return (int)v;
+template <int KS, typename T> __device__ __forceinline__ int h32_idx(const T& v, int s, int h) {
+  if constexpr (KS == 1) return (int)(h ? v[1] : v[0]);
   else return (int)v[s];
 }
 
@@ -205,7 +206,8 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   f16x8 asl[KL > 0 ? KL : 1];  // the lo parts (precise instance)
   f16x8 apar[SG ? KS : 1];  // signed: parity fragments (the one-hot part's positions, 0.5 per negative dim)
   typename H32Idx<KS>::T aix;
-  const int ixo = 16 * ND + 32 * KP + 2 * h32_ksp(KP) * h - 8 * h;  // index words relative to arow
+  // index words relative to arow (KP = 1: dwords 2b, 2b + 1, b = bit 4 of the row -- hbx_kde_impl.h)
+  const int ixo = 16 * ND + 32 * KP + (KP == 1 ? 4 * ((c >> 4) & 1) : 2 * h32_ksp(KP) * h) - 8 * h;
   auto arow = [&](const float* buf, int jt) { return (const _Float16*)buf + (32 * jt + c) * KTP + 8 * h; };
   auto readA = [&](const float* buf, int jt) {
     const _Float16* a = arow(buf, jt);
@@ -228,10 +230,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     for (int s = 1; s < ND; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[s], acc, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
 #pragma unroll
     for (int s = 0; s < KL; ++s)
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
   };
   // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it; a
   // signed KDE's parity product (the same index words) follows into accp
@@ -246,20 +248,20 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
       asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
       if (!SG && KL == 0 && s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
     }
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
       asl[s] = *(const f16x8*)(a + 16 * ND + 16 * KP + 16 * s);
       if (!SG && s == KL - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
     }
     if constexpr (SG) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        accp = __builtin_amdgcn_smfmac_f32_32x32x32_f16(apar[s], bsp[s], s == 0 ? zero16 : accp, h32_idx<KS>(aix, s),
+        accp = __builtin_amdgcn_smfmac_f32_32x32x32_f16(apar[s], bsp[s], s == 0 ? zero16 : accp, h32_idx<KS>(aix, s, h),
                                                         0, 0);
         apar[s] = *(const f16x8*)(a + PAR + 16 * s);
         if (s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
