@@ -903,6 +903,7 @@ __device__ void exact_setup(const KdeParams* __restrict__ P, int32_t D, const do
 
 // Sum of the per-observation terms Kval.prod(1) / prod(bw_c) (SM:_kernel_base.py:509-516) over
 // the observations [first, first+len) -- one unit of one buffer, pairwise order; whole block.
+template <int LEVELS = PW_LEVELS>
 __device__ double exact_unit(const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows,
                              const KdeParams* __restrict__ P, int first, int len, ExactShared* sh) {
   const double pbc = P->prod_bw_c;
@@ -924,7 +925,7 @@ __device__ double exact_unit(const double* __restrict__ X, int32_t D, const int6
     sh->dens[j] = p / pbc;
   }
   __syncthreads();
-  return np_pairwise_block(sh->dens, len, sh->nsum);
+  return np_pairwise_block<LEVELS>(sh->dens, len, sh->nsum);
 }
 
 // exact fp64 pdf of one KDE at the point staged by exact_setup, one block, all units in turn
@@ -949,10 +950,10 @@ __device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64
 // Exact re-score of the shortlist.  Small shortlists (<= EXACT_SPLIT_CAP): one work item per
 // (candidate, KDE, 8192-buffer, unit) so one candidate spreads over many CUs; the unit sums go to
 // `part` and kde_final combines them.  Larger: one item per (candidate, KDE), all units in turn.
-// threads per block of the acquisition's exact re-score: one unit (<= 1040 observations) per block, so
-// 1024 threads compute its terms in one pass (16 waves: 4 per SIMD hide the fp64 exp latency)
+// threads per block of the acquisition's exact re-score: one unit (<= 263 observations) per block, one
+// observation per thread (one wave per SIMD; the 32 units of a buffer run on 32 CUs)
 #ifndef EXACT_ACQ_THREADS
-#define EXACT_ACQ_THREADS 1024
+#define EXACT_ACQ_THREADS 256
 #endif
 __global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
     const double* __restrict__ cand, int32_t D,
@@ -963,7 +964,7 @@ __global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
   __shared__ ExactShared sh;
   const int cnt = *count;
   const bool split = cnt <= EXACT_SPLIT_CAP;
-  const int per = split ? nbuf * PW_UNITS : 1;  // items per (candidate, KDE)
+  const int per = split ? nbuf * PW_SPLIT_UNITS : 1;  // items per (candidate, KDE)
   const int64_t items = (int64_t)cnt * 2 * per;
   for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
     const int64_t pk = item / per;  // (candidate, KDE)
@@ -973,14 +974,14 @@ __global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
     const double* X = isl ? Xg : Xb;
     const int64_t* rows = isl ? rows_g : rows_b;
     if (split) {
-      const int r = (int)(item % per), b = r / PW_UNITS, u = r % PW_UNITS;
+      const int r = (int)(item % per), b = r / PW_SPLIT_UNITS, u = r % PW_SPLIT_UNITS;
       const int n = P->n, c = b * PW_BUF;
       if (c >= n) continue;
       const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
       int off, len;
-      if (!pw_unit(m, u, &off, &len)) continue;
+      if (!pw_unit<PW_SPLIT_CUT>(m, u, &off, &len)) continue;
       exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
-      const double v = exact_unit(X, D, rows, P, c + off, len, &sh);
+      const double v = exact_unit<PW_SPLIT_LEVELS>(X, D, rows, P, c + off, len, &sh);
       if (threadIdx.x == 0) part[pk * per + r] = v;
     } else {
       exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
@@ -1000,17 +1001,18 @@ __global__ __launch_bounds__(256) void kde_exact_combine_kernel(const KdeParams*
                                                                 double* __restrict__ exact_g) {
   const int cnt = *count;
   if (cnt > EXACT_SPLIT_CAP) return;
-  const int64_t pk = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (pk >= 2 * (int64_t)cnt) return;
+  // one wave per (candidate, KDE)
+  const int64_t pk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pk >= 2 * (int64_t)cnt) return;  // whole wave
   const bool isl = pk & 1;
   const int n = (isl ? Pg : Pb)->n;
-  const double* us = part + pk * nbuf * PW_UNITS;
+  const double* us = part + pk * nbuf * PW_SPLIT_UNITS;
   double acc = 0.0;
   for (int c = 0, b = 0; c < n; c += PW_BUF, ++b) {
     const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
-    acc = acc + pw_combine_units(m, us + b * PW_UNITS);
+    acc = acc + pw_combine_units_wave<PW_SPLIT_CUT>(m, us + b * PW_SPLIT_UNITS);
   }
-  (isl ? exact_l : exact_g)[pk >> 1] = acc / (double)n;
+  if ((threadIdx.x & 63) == 0) (isl ? exact_l : exact_g)[pk >> 1] = acc / (double)n;
 }
 
 // exact fp64 pdf of one KDE at every row of pts (grid-stride over points, one block per point)
@@ -1166,16 +1168,16 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
   __shared__ int32_t nnear;
   const int cnt = *count;
   if (part && cnt <= EXACT_SPLIT_CAP) {  // the split re-score's unit sums -> pdfs (kde_exact_combine's work)
-    for (int pk = threadIdx.x; pk < 2 * cnt; pk += 256) {
+    for (int pk = threadIdx.x >> 6; pk < 2 * cnt; pk += 4) {  // one wave per (candidate, KDE)
       const bool isl = pk & 1;
       const int n = (isl ? Pg : Pb)->n;
-      const double* us = part + (int64_t)pk * nbuf * PW_UNITS;
+      const double* us = part + (int64_t)pk * nbuf * PW_SPLIT_UNITS;
       double acc = 0.0;
       for (int c = 0, b = 0; c < n; c += PW_BUF, ++b) {
         const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
-        acc = acc + pw_combine_units(m, us + b * PW_UNITS);
+        acc = acc + pw_combine_units_wave<PW_SPLIT_CUT>(m, us + b * PW_SPLIT_UNITS);
       }
-      (isl ? exact_lw : exact_gw)[pk >> 1] = acc / (double)n;
+      if ((threadIdx.x & 63) == 0) (isl ? exact_lw : exact_gw)[pk >> 1] = acc / (double)n;
     }
     __threadfence_block();
     __syncthreads();
@@ -1516,7 +1518,7 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.near = take(4 * Nc);
   w.exact_l = take(8 * Nc);
   w.exact_g = take(8 * Nc);
-  w.part = take(8 * (size_t)2 * EXACT_SPLIT_CAP * PW_UNITS * ((nmax + PW_BUF - 1) / PW_BUF));
+  w.part = take(8 * (size_t)2 * EXACT_SPLIT_CAP * PW_SPLIT_UNITS * ((nmax + PW_BUF - 1) / PW_BUF));
   w.total = o;
   return w;
 }
@@ -1799,7 +1801,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     // single acquisition: the final kernel combines the unit sums itself (one launch less)
     fuse_combine = !batch_res && !(exact_only && (logl_out || logg_out));
     if (!fuse_combine) {
-      hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 255) / 256), dim3(256), 0, s,
+      hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 3) / 4), dim3(256), 0, s,
                          (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,
                          exact_g);
       HBX_LAUNCH_CHECK();
