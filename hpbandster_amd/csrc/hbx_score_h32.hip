@@ -402,7 +402,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
           const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
           if (fabsf(dl) < 60000.f) lo_err += fabsf(dl - (float)(_Float16)dl);
         }
-        if (o.err > 0.f) o.err += 2.f * lo_err * HBX_LN2f;
+        // every term is off by a factor in [2^-L, 2^L], L = lo_err: the sums' relative bound e becomes
+        // (1 + e) 2^L - 1 (rounded up)
+        if (o.err > 0.f) o.err = (1.f + o.err) * exp2f(lo_err) * (1.f + 0x1p-20f) - 1.f;
       }
       if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) o.err = -1.f;  // rescue marker
       out[ii] = o;
