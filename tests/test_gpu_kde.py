@@ -498,3 +498,31 @@ def test_h32_every_instance_matches_oracle(device, dc, du):
     fast = pair.acquire(C)  # no ln-pdf estimates requested: the FAST scoring instance
     assert fast.index == res.index
     assert (fast.score, fast.pdf_l, fast.pdf_g) == (res.score, res.pdf_l, res.pdf_g)
+
+
+def test_fast_instance_extreme_categorical_bandwidths(device):
+    """The acquisition's FAST instance (one-hot lo parts in the bound) where the categorical deltas are
+    large and far from f16 values: bandwidths from 1e-3 to 0.7 on 8 four-level dims (|delta| up to
+    ~11.5 log2 units, lo parts up to 2^-8 each).  The winner is the oracle's and the record equals the
+    precise instance's."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, n = 24, 8, 3000
+    X = S.make_observations(n, dc, du, 4, seed=51)
+    L = S.make_losses(n, seed=52)
+    vt = S.var_type_string(dc, du)
+    g_idx, b_idx = O.bohb_split(X, L, dc + du + 1)
+    bwg, bwb = O.normal_reference_bw(X[g_idx]), O.normal_reference_bw(X[b_idx])
+    cat = np.array([1e-3, 0.003, 0.01, 0.05, 0.2, 0.37, 0.5, 0.7])
+    bwg[dc:], bwb[dc:] = cat, cat[::-1]
+    pair = kde.fit_pair_from_rows(X, g_idx, b_idx, vt, bwg, bwb, O.num_levels(X[g_idx], vt),
+                                  O.num_levels(X[b_idx], vt))
+    assert (pair.bad.variant >> 6) & 1 == 1 and not pair.bad.has_neg and not pair.good.has_neg
+    C = S.make_candidates(700, dc, du, 4, seed=53)
+    C[::2, dc:] = X[g_idx[np.arange(350) % len(g_idx)], dc:]  # half the candidates match a good row's levels
+    fast = pair.acquire(C)
+    res, _, _ = pair.acquire(C, logs=True)
+    l = O.pdf_many(X[g_idx], bwg, vt, C, O.num_levels(X[g_idx], vt))
+    g = O.pdf_many(X[b_idx], bwb, vt, C, O.num_levels(X[b_idx], vt))
+    assert fast.index == res.index == O.select(l, g)[0]
+    assert (fast.score, fast.pdf_l, fast.pdf_g) == (res.score, res.pdf_l, res.pdf_g)
