@@ -762,95 +762,135 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 // Candidates whose l and g are both certainly below 1e-8 score exactly 1e-8/1e-8 = 1 (bohb.py:129):
 // they tie, so only the first of them per segment (first1[b]) can win and needs the exact re-score
 // (BOHB's own sampler puts most candidates there at D = 32: the truncnorm scale is 3 bw).
+#define COMBINE_SUB 4  // 256-candidate sub-blocks per block of kde_combine_kernel
 __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
                                                           const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo, float* __restrict__ hi,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                                           int32_t* __restrict__ first1) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  float h = INFINITY;
-  bool one = false;
-  const uint32_t sg = (uint32_t)(i < Nc ? i : Nc - 1) / seg;
-  if (i < Nc) {
-    const KdeEst a = el[i], b = eg[i];
-    const float C = (float)HBX_LN_CLAMP;
-    float slo, shi;
-    bool of = false;
-    float llo, lhi, lpt, glo, ghi, gpt;
-    if (a.lpos != a.lpos) {  // l NaN -> max(l, 1e-8) is NaN -> score NaN (never selected)
-      slo = shi = NAN;
-      lpt = NAN;
-      est_interval(b, &glo, &ghi, &gpt);
-      if (b.lpos != b.lpos) gpt = NAN;
-    } else {
-      est_interval(a, &llo, &lhi, &lpt);
-      float Glo, Ghi;
-      if (b.lpos != b.lpos) {  // g NaN -> max(1e-8, g) == 1e-8
-        Glo = Ghi = C;
-        gpt = NAN;
-      } else {
-        est_interval(b, &glo, &ghi, &gpt);
-        Glo = fmaxf(glo, C);
-        Ghi = fmaxf(ghi, C);
-        of = ghi > 700.f;
-      }
-      of = of || lhi > 700.f;
-      slo = Glo - fmaxf(lhi, C);
-      shi = Ghi - fmaxf(llo, C);
-      h = shi;
-      const float C1 = C - 1e-4f;  // margin for the rounding of ln(1e-8) to float
-      if (lhi < C1 && (b.lpos != b.lpos || ghi < C1)) {  // both clamped: score exactly 1 (ln 0)
-        one = true;
-        slo = NAN;  // excluded from the shortlist unless it is the segment's first exact tie
-        shi = h = 0.f;
-      }
+  // COMBINE_SUB consecutive 256-candidate sub-blocks per block: every sub-block's loads are issued first
+  // (the kernel is latency-bound with one candidate per thread), then each runs as its own block would
+  KdeEst ea[COMBINE_SUB], eb[COMBINE_SUB];
+#pragma unroll
+  for (int r = 0; r < COMBINE_SUB; ++r) {
+    const int64_t i = ((int64_t)blockIdx.x * COMBINE_SUB + r) * 256 + threadIdx.x;
+    if (i < Nc) {
+      ea[r] = el[i];
+      eb[r] = eg[i];
     }
-    if (logl) logl[i] = lpt;
-    if (logg) logg[i] = gpt;
-    lo[i] = slo;
-    hi[i] = shi;
-    if (of) atomicOr(flags + sg, 1);
   }
-  // min of hi and first exact tie per segment.  Same-address atomics serialise in L2 (~10 ns each),
-  // so: block reduction when the block lies in one segment (the common case), one wave-level atomic
-  // when the wave does, per lane otherwise; and an atomic only when it can still lower the value.
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t blk0 = (int64_t)blockIdx.x * 256;
-  const int64_t blk1 = (blk0 + 255 < Nc ? blk0 + 255 : Nc - 1);
-  auto lower_u = [&](uint32_t sgi, float hv) {
-    const uint32_t o = hbx_f2ord(hv);
-    if (hv < INFINITY && o < __hip_atomic_load(U + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(U + sgi, o);
-  };
-  auto lower_first = [&](uint32_t sgi, int32_t iv) {
-    if (iv < __hip_atomic_load(first1 + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(first1 + sgi, iv);
-  };
-  const uint32_t s0 = __shfl(sg, 0), s63 = __shfl(sg, 63);
-  if (s0 == s63) {
-    for (int o = 32; o > 0; o >>= 1) h = fminf(h, __shfl_xor(h, o));
-    const uint64_t ones = __ballot(one);
-    const int32_t f1 = ones ? (int32_t)(blk0 + 64 * wv + __ffsll((long long)ones) - 1) : INT32_MAX;
-    if ((uint32_t)(blk0 / seg) == (uint32_t)(blk1 / seg)) {
-      __shared__ float rh[4];
-      __shared__ int32_t rf[4];
-      if (lane == 0) {
-        rh[wv] = h;
-        rf[wv] = f1;
+  __shared__ float rh[COMBINE_SUB][4];
+  __shared__ int32_t rf[COMBINE_SUB][4];
+  // thread 0: the whole-block sub-blocks' minima of one segment, lowered into U / first1 once per segment
+  // (an atomic round trip per sub-block made thread 0 -- and the next sub-block's barrier -- wait 4x)
+  uint32_t acc_sg = ~0u;
+  float acc_h = INFINITY;
+  int32_t acc_f = INT32_MAX;
+#pragma unroll
+  for (int r = 0; r < COMBINE_SUB; ++r) {
+    const int64_t blkr = (int64_t)blockIdx.x * COMBINE_SUB + r;
+    if (blkr * 256 >= Nc) break;  // uniform
+    const int64_t i = blkr * 256 + threadIdx.x;
+    float h = INFINITY;
+    bool one = false;
+    const uint32_t sg = (uint32_t)(i < Nc ? i : Nc - 1) / seg;
+    if (i < Nc) {
+      const KdeEst a = ea[r], b = eb[r];
+      const float C = (float)HBX_LN_CLAMP;
+      float slo, shi;
+      bool of = false;
+      float llo, lhi, lpt, glo, ghi, gpt;
+      if (a.lpos != a.lpos) {  // l NaN -> max(l, 1e-8) is NaN -> score NaN (never selected)
+        slo = shi = NAN;
+        lpt = NAN;
+        est_interval(b, &glo, &ghi, &gpt);
+        if (b.lpos != b.lpos) gpt = NAN;
+      } else {
+        est_interval(a, &llo, &lhi, &lpt);
+        float Glo, Ghi;
+        if (b.lpos != b.lpos) {  // g NaN -> max(1e-8, g) == 1e-8
+          Glo = Ghi = C;
+          gpt = NAN;
+        } else {
+          est_interval(b, &glo, &ghi, &gpt);
+          Glo = fmaxf(glo, C);
+          Ghi = fmaxf(ghi, C);
+          of = ghi > 700.f;
+        }
+        of = of || lhi > 700.f;
+        slo = Glo - fmaxf(lhi, C);
+        shi = Ghi - fmaxf(llo, C);
+        h = shi;
+        const float C1 = C - 1e-4f;  // margin for the rounding of ln(1e-8) to float
+        if (lhi < C1 && (b.lpos != b.lpos || ghi < C1)) {  // both clamped: score exactly 1 (ln 0)
+          one = true;
+          slo = NAN;  // excluded from the shortlist unless it is the segment's first exact tie
+          shi = h = 0.f;
+        }
       }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const float hb = fminf(fminf(rh[0], rh[1]), fminf(rh[2], rh[3]));
-        const int32_t fb = min(min(rf[0], rf[1]), min(rf[2], rf[3]));
-        lower_u(sg, hb);
-        if (fb != INT32_MAX) lower_first(sg, fb);
-      }
-    } else if (lane == 0) {
-      lower_u(sg, h);
-      if (f1 != INT32_MAX) lower_first(sg, f1);
+      if (logl) logl[i] = lpt;
+      if (logg) logg[i] = gpt;
+      lo[i] = slo;
+      hi[i] = shi;
+      if (of) atomicOr(flags + sg, 1);
     }
-  } else {
-    lower_u(sg, h);
-    if (one) lower_first(sg, (int32_t)i);
+    // min of hi and first exact tie per segment.  Same-address atomics serialise in L2 (~10 ns each),
+    // so: block reduction when the block lies in one segment (the common case), one wave-level atomic
+    // when the wave does, per lane otherwise; and an atomic only when it can still lower the value.
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t blk0 = blkr * 256;
+    const int64_t blk1 = (blk0 + 255 < Nc ? blk0 + 255 : Nc - 1);
+    auto lower_u = [&](uint32_t sgi, float hv) {
+      const uint32_t o = hbx_f2ord(hv);
+      if (hv < INFINITY && o < __hip_atomic_load(U + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(U + sgi, o);
+    };
+    auto lower_first = [&](uint32_t sgi, int32_t iv) {
+      if (iv < __hip_atomic_load(first1 + sgi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(first1 + sgi, iv);
+    };
+    const uint32_t s0 = __shfl(sg, 0), s63 = __shfl(sg, 63);
+    if (s0 == s63) {
+      for (int o = 32; o > 0; o >>= 1) h = fminf(h, __shfl_xor(h, o));
+      const uint64_t ones = __ballot(one);
+      const int32_t f1 = ones ? (int32_t)(blk0 + 64 * wv + __ffsll((long long)ones) - 1) : INT32_MAX;
+      if ((uint32_t)(blk0 / seg) == (uint32_t)(blk1 / seg)) {
+        if (lane == 0) {
+          rh[r][wv] = h;
+          rf[r][wv] = f1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const float hb = fminf(fminf(rh[r][0], rh[r][1]), fminf(rh[r][2], rh[r][3]));
+          const int32_t fb = min(min(rf[r][0], rf[r][1]), min(rf[r][2], rf[r][3]));
+          if (sg != acc_sg) {
+            if (acc_sg != ~0u) {
+              lower_u(acc_sg, acc_h);
+              if (acc_f != INT32_MAX) lower_first(acc_sg, acc_f);
+            }
+            acc_sg = sg;
+            acc_h = hb;
+            acc_f = fb;
+          } else {
+            acc_h = fminf(acc_h, hb);
+            acc_f = min(acc_f, fb);
+          }
+        }
+      } else if (lane == 0) {
+        lower_u(sg, h);
+        if (f1 != INT32_MAX) lower_first(sg, f1);
+      }
+    } else {
+      lower_u(sg, h);
+      if (one) lower_first(sg, (int32_t)i);
+    }
+  }  // sub-block
+  if (threadIdx.x == 0 && acc_sg != ~0u) {
+    const uint32_t o = hbx_f2ord(acc_h);
+    if (acc_h < INFINITY && o < __hip_atomic_load(U + acc_sg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin(U + acc_sg, o);
+    if (acc_f != INT32_MAX &&
+        acc_f < __hip_atomic_load(first1 + acc_sg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin(first1 + acc_sg, acc_f);
   }
 }
 
@@ -1786,7 +1826,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
       hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
       HBX_LAUNCH_CHECK();
     } else {
-      hipLaunchKernelGGL(kde_combine_kernel, grid, dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
+      hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
+                         dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
                          flags, first1);
       HBX_LAUNCH_CHECK();
     }
