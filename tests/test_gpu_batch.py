@@ -158,3 +158,23 @@ def test_get_config_batch_equals_sequential_zero_bandwidth(device):
     np.testing.assert_array_equal(np.random.get_state()[1], state)
     assert seq == bat
     assert not any(i["model_based_pick"] for _, i in bat)
+
+
+@pytest.mark.parametrize("seg", [300, 1000, 1024, 2500])
+def test_batch_segments_across_combine_sub_blocks(device, seg):
+    """Segment lengths that end inside, at and across the combine kernel's 256-candidate sub-blocks and
+    its 1024-candidate blocks (segment minima accumulated per block, lowered per segment): every call's
+    record equals the separate acquisition of its segment."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(3000, 24, 8, 4, seed=61)
+    L = S.make_losses(3000, seed=62)
+    pair = kde.fit_pair(X, L, S.var_type_string(24, 8), 33, device=device)
+    C = S.make_candidates(9000, 24, 8, 4, seed=63)
+    res = pair.acquire_batch(C, seg)
+    assert len(res) == (len(C) + seg - 1) // seg
+    for b in range(len(res)):
+        one = pair.acquire(C[seg * b:seg * (b + 1)])
+        r = res[b]
+        assert (one.index, one.score, one.pdf_l, one.pdf_g, one.shortlist) == \
+            (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist), (seg, b)
