@@ -61,11 +61,10 @@ def kernel_model(kde_obj, dc, du):
     if h32:
         nd = (6 + 24 * nsc + 15) // 16  # h32_nd(nsc) dense steps
         kp = (kc + 1) // 2  # 32-position one-hot steps
-        fast = (not signed) and kp > 0  # the acquisition's instance
+        fast = kp > 0  # the acquisition's instance
         n_mat = nd + kp * (1 if fast else 2) + (kp if signed else 0)  # per 1024 pairs (+ signed parity)
         valu = 16 * 8 + 16 * 4 + (32 * 4 if signed else 0)  # exp2, add (+ fract, fma when signed)
-        name = ("kde_logpdf_h32s_kernel<%d,%d>" % (nsc, kp) if signed else
-                "kde_logpdf_h32_kernel<%d,%d,%s>" % (nsc, kp, "true" if fast else "false"))
+        name = "kde_logpdf_h32%s_kernel<%d,%d,%s>" % ("s" if signed else "", nsc, kp, "true" if fast else "false")
         return {"kernel": name,
                 "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
                           "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + valu) / 4,

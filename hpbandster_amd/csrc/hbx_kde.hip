@@ -1469,7 +1469,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
   if (hm && ((variant >> 6) & 1)) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
     const int kp = h32_kp(kc);
-    const bool fa = fast && !sg && kp > 0;
+    const bool fa = fast && kp > 0;
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa), r, 32 * H16_WAVES, 64 * H16_WAVES,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa),
             sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};

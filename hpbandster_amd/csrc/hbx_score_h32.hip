@@ -12,7 +12,8 @@
 // in the table, hbx_kde_impl.h h32 layout), B = candidates (32 columns per wave, resident in registers).
 // One-hot part: KP steps of 32 positions, the deltas' f16 hi parts then their lo parts against the same
 // candidate fragments and index words; the FAST instance (acquisition) multiplies the hi parts only and
-// adds the lo parts' bound: 6 matrix instructions per 1024 pairs at 24c + 8u instead of 7.
+// widens the bound by the lo parts (every term, of either sign, is off by a factor within 2^+-L): 6
+// matrix instructions per 1024 pairs at 24c + 8u instead of 7 (signed sums: + KP parity products).
 // The output column of a lane is ONE candidate, so a lane's 16 accumulator registers are 16
 // observations of the same candidate: the exp2 sum is an in-register tree and a lane carries one
 // running sum (the 16x16 kernel's A = candidates layout needs 16 per lane here).  The candidate's
@@ -79,7 +80,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   constexpr int CHF = h32_chunk_floats(NSC, KP, SG);
   constexpr int PAR = h32_par(NSC, KP);  // signed: the parity block (halves into the row)
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
-  static_assert(!FAST || (KP > 0 && !SG), "the fast instance drops one-hot lo parts of unsigned sums");
+  static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
   constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
   constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -431,36 +432,36 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
 // and a 256-register budget
-template <int NSC, int KP>
+template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KP, true, false>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, true, FAST>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
-template <int NSC, int KP>
+template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;
-  kde_logpdf_h32_body<NSC, KP, true, false>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, true, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                           second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
 }
 
-// instances: h32_ok (hbx_kde_impl.h); FAST for unsigned sums with a one-hot part
+// instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part
 template <int NSC, int KP, bool SG, bool PAIR, bool FAST>
 static constexpr auto h32_inst() {
   if constexpr (PAIR) {
-    if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KP>;
+    if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KP, FAST>;
     else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KP, FAST>;
   } else {
-    if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KP>;
+    if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KP, FAST>;
     else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KP, FAST>;
   }
 }
 
 template <int NSC, int KP, bool SG, bool PAIR>
 static auto pick32_fast(bool fast) {
-  if constexpr (!SG && KP > 0)
+  if constexpr (KP > 0)
     if (fast) return h32_inst<NSC, KP, SG, PAIR, true>();
   return h32_inst<NSC, KP, SG, PAIR, false>();
 }

@@ -464,6 +464,8 @@ def test_h32_kernel_choice_and_large_shift_rescue(device, monkeypatch):
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
         assert res.index == O.select(l, g)[0]
+        fast = pair.acquire(C)  # the FAST instances (the signed good KDE's too)
+        assert (fast.index, fast.score, fast.pdf_l, fast.pdf_g) == (res.index, res.score, res.pdf_l, res.pdf_g)
 
 
 @pytest.mark.parametrize("dc,du", [(8, 4), (6, 8), (8, 12), (16, 0), (12, 4), (16, 8), (24, 4), (32, 0), (16, 12),
