@@ -99,7 +99,8 @@ __host__ __device__ constexpr int h_chunk_floats(int dc_pad, int kc, int sgn) {
 //                          product, 2:4-compressed like the one-hot part and sharing its index words:
 //                          0.5 in the slot of the observation's level when its dim has a negative match
 //                          factor, so the accumulated value is 0.5 x (matched negative dims)
-// instances built: those whose registers fit 4 waves per SIMD without spills (unsigned), 2 (signed)
+// instances built: those whose registers fit 4 waves per SIMD (unsigned), 2 (signed) -- without spills,
+// except the precise unsigned <4,1> (16 bytes; it only serves reported ln-pdfs, its FAST twin has none)
 __host__ __device__ constexpr int h32_nd(int nsc) { return (6 + 24 * nsc + 15) / 16; }  // dense K-steps
 __host__ __device__ constexpr int h32_kp(int kc) { return (kc + 1) / 2; }  // 32-position steps of kc 16-position ones
 __host__ __device__ constexpr bool h32_ok(int nsc, int kp, int sgn = 0) {
