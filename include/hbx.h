@@ -116,8 +116,10 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
 /* One acquisition: l = good KDE, g = bad KDE; selects the first index of the minimum of
  * max(1e-8, g)/max(l, 1e-8) over the candidates, exactly (fp64 re-score of every candidate whose
  * fp32 score interval reaches the minimum).  index_base is added to the reported index (GPU
- * sharding).  logl_out/logg_out: nullable device f32[Nc] (ln pdf estimates; -inf for pdf <= 0,
- * NaN for NaN).  The result record lives in the workspace: hbx_kde_result_ptr(workspace).
+ * sharding).  logl_out/logg_out: nullable device f32[Nc] (ln pdf estimates within 1e-5 of the
+ * reference's; -inf for pdf <= 0, NaN for NaN).  With both NULL the scoring runs the fast instance (the
+ * one-hot deltas' f16 lo parts moved into the bound: looser estimates, the same exact selection).  The
+ * result record lives in the workspace: hbx_kde_result_ptr(workspace).
  * events: NULL or hipEvent_t[3] (see hbx_event_create). */
 int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
                     const void* params_good, const float* table_good, const double* X_good,
