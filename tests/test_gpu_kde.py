@@ -528,3 +528,38 @@ def test_fast_instance_extreme_categorical_bandwidths(device):
     g = O.pdf_many(X[b_idx], bwb, vt, C, O.num_levels(X[b_idx], vt))
     assert fast.index == res.index == O.select(l, g)[0]
     assert (fast.score, fast.pdf_l, fast.pdf_g) == (res.score, res.pdf_l, res.pdf_g)
+
+
+def test_fast_and_precise_records_agree_on_random_shapes(device):
+    """200 random (continuous, categorical, levels, observations, bandwidth scale) shapes -- small
+    observation counts give signed KDEs -- and 400 candidates each, a third of them on observed
+    categorical levels: the acquisition through the FAST scoring instance returns the precise instance's
+    record (index, score, pdfs); every tenth shape also against the oracle's winner."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    rs = np.random.RandomState(71)
+    for case in range(200):
+        dc, du = int(rs.randint(5, 33)), int(rs.randint(1, 13))
+        lev = int(rs.randint(2, 7))
+        n = int(rs.choice([60, 150, 400, 1200, 2500]))
+        vt = S.var_type_string(dc, du)
+        X = S.make_observations(n, dc, du, lev, seed=1000 + case)
+        L = S.make_losses(n, seed=2000 + case)
+        g_idx, b_idx = O.bohb_split(X, L, dc + du + 1) or (None, None)
+        if g_idx is None:
+            continue
+        scale = float(rs.choice([0.3, 1.0, 2.5]))
+        bwg, bwb = O.normal_reference_bw(X[g_idx]) * scale, O.normal_reference_bw(X[b_idx]) * scale
+        bwg, bwb = np.clip(bwg, 1e-3, None), np.clip(bwb, 1e-3, None)
+        nlg, nlb = O.num_levels(X[g_idx], vt), O.num_levels(X[b_idx], vt)
+        pair = kde.fit_pair_from_rows(X, g_idx, b_idx, vt, bwg, bwb, nlg, nlb)
+        C = S.make_candidates(400, dc, du, lev, seed=3000 + case)
+        C[::3, dc:] = X[g_idx[np.arange(len(C[::3])) % len(g_idx)], dc:]
+        fast = pair.acquire(C)
+        res, _, _ = pair.acquire(C, logs=True)
+        assert (fast.index, fast.score, fast.pdf_l, fast.pdf_g) == (res.index, res.score, res.pdf_l, res.pdf_g), \
+            (case, dc, du, lev, n, scale, pair.good.has_neg, pair.bad.has_neg)
+        if case % 10 == 0:
+            l = O.pdf_many(X[g_idx], bwg, vt, C, nlg)
+            g = O.pdf_many(X[b_idx], bwb, vt, C, nlb)
+            assert fast.index == O.select(l, g)[0], case
