@@ -140,13 +140,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
   double fz = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r) fz = fma(v[r], 0.0, fz);
-  // lanes past n become NaN (the partial row and the absent rows), then min / max
-  const int nfull = n >> 6;
-  const bool inpart = lane < (n & 63);
+  // lanes past n become NaN (the partial row and the absent rows), then min / max: one vector compare
+  // of lane - n against -64 r and a select of the high dword per row (a uniform row test would
+  // become per-row scalar mask arithmetic on the CU's shared scalar unit)
+  const int nl = lane - n;
   const double qnan = __builtin_nan("");
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (r >= nfull) v[r] = (r == nfull && inpart) ? v[r] : qnan;
+  for (int r = 0; r < R; ++r) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v[r]);
+    const uint32_t hi = nl < -64 * r ? (uint32_t)(u >> 32) : 0x7ff80000u;
+    v[r] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)u);
+  }
   double mn = __builtin_inf(), mx = -__builtin_inf();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
