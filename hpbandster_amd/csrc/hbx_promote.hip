@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
                                                         uint8_t* __restrict__ advance,
                                                         int64_t* __restrict__ n_advance) {
   constexpr int R = PW_PER_LANE;  // 16 registers x 64 lanes = 1024 elements
-  __shared__ double cbuf[4][64];  // per wave: the compacted bracket
+  __shared__ double cbuf[4][128];  // per wave: the compacted bracket, then one dummy slot per lane
   // the wave index made visibly uniform: the bracket's bounds, k and buffer resources live in SGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t b = (int64_t)blockIdx.x * 4 + wv;
@@ -130,25 +130,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
     return;
   }
   // the bracket as buffer resources: loads past n return 0 and stores past n are dropped by the
-  // hardware range check, so all 16 loads (and stores) are unconditional, one address VGPR each
+  // hardware range check, so all 16 loads (and stores) are unconditional; the row offset goes in the
+  // vector offset, whose constant part the compiler folds into the 12-bit immediate (no per-row SGPR)
   const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)(loss + s), (short)0, n * 8, kBufDword3);
   const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)(advance + s), (short)0, n, kBufDword3);
   double v[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane, 512 * r, 0));
+  for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane + 512 * r, 0, 0));
   // fz = sum of x * 0: NaN iff some loss is not finite (the loads past n returned 0.0)
   double fz = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r) fz = fma(v[r], 0.0, fz);
   // lanes past n become NaN (the partial row and the absent rows), then min / max: one vector compare
-  // of lane - n against -64 r and a select of the high dword per row (a uniform row test would
-  // become per-row scalar mask arithmetic on the CU's shared scalar unit)
-  const int nl = lane - n;
+  // of floor((lane - n) / 64) against -r (lane + 64 r < n) and a select of the high dword per row (a
+  // uniform row test would become per-row scalar mask arithmetic on the CU's shared scalar unit)
+  const int nl = (lane - n) >> 6;
   const double qnan = __builtin_nan("");
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v[r]);
-    const uint32_t hi = nl < -64 * r ? (uint32_t)(u >> 32) : 0x7ff80000u;
+    const uint32_t hi = nl < -r ? (uint32_t)(u >> 32) : 0x7ff80000u;
     v[r] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)u);
   }
   double mn = __builtin_inf(), mx = -__builtin_inf();
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
   const int kk = __builtin_amdgcn_readfirstlane(kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0);
   if (kk == nfin || kk == 0) {  // all the finite entries, or none
 #pragma unroll
-    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk && v[r] == v[r] ? 1u : 0u), ars, lane, 64 * r, 0);
+    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk && v[r] == v[r] ? 1u : 0u), ars, lane + 64 * r, 0, 0);
     if (lane == 0 && n_advance) n_advance[b] = kk;
     return;
   }
@@ -251,10 +252,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
     int base = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const bool a = !(v[r] < Ld) && v[r] < Hd;
+      // branchless: a lane outside the bracket writes its own dummy slot 64 + lane
       const uint64_t m = __builtin_amdgcn_ballot_w64(v[r] < Hd) & ~__builtin_amdgcn_ballot_w64(v[r] < Ld);
       const int at = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (a) cbuf[wv][at] = v[r];
+      cbuf[wv][__builtin_amdgcn_inverse_ballot_w64(m) ? at : 64 + lane] = v[r];
       base += (int)__popcll(m);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
   if (cL == kk || cH == kk) {  // exactly kk keys below T
     const double T = sel_val(cL == kk ? Lk : Hk);
 #pragma unroll
-    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[r] < T ? 1u : 0u), ars, lane, 64 * r, 0);
+    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[r] < T ? 1u : 0u), ars, lane + 64 * r, 0, 0);
   } else {  // Hk = Lk + 1: the bracket holds copies of one key, the first kk - cL of them by position advance
     const double P = sel_val(Lk);
     const int need = kk - cL;
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
       const int at = taken + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       const bool take = v[r] < P || (eq && at < need);
       taken += (int)__popcll(m);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1u : 0u), ars, lane, 64 * r, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1u : 0u), ars, lane + 64 * r, 0, 0);
     }
   }
   if (lane == 0 && n_advance) n_advance[b] = kk;
