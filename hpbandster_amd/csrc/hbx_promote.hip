@@ -263,9 +263,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int c0 = cL;
     const uint64_t key1 = lane < cH - cL ? sel_key(cbuf[wv][lane]) : ~0ull;
+    Lk = sel_uniform(Lk);
+    Hk = sel_uniform(Hk);
     while (HBX_SEL_OPEN) {
-      Lk = sel_uniform(Lk);
-      Hk = sel_uniform(Hk);
       const int bt = 63 - __clzll((long long)(Lk ^ (Hk - 1ull)));
       const uint64_t M = (Lk & ~((2ull << bt) - 1ull)) | (1ull << bt);
       const int cM = c0 + (int)__popcll(__builtin_amdgcn_ballot_w64(key1 < M));
