@@ -137,7 +137,9 @@ __device__ __forceinline__ double tn_invert_f32(double plo, double phi, double l
   return fmin(fmax(z, lo), hi);
 }
 
-// One draw of dim d of a candidate whose datum row is xr: w0 the uniform, w1 the categorical level draw
+// One draw of dim d of a candidate whose datum row is xr: w0 the uniform, w1 the categorical level draw.
+// TAB: the Phi table is given (one instance each way: the table instance carries no inlined normcdf)
+template <bool TAB>
 __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int d, int32_t idx, int32_t D,
                                              const double* __restrict__ bw, const double* __restrict__ rbw,
                                              const int32_t* __restrict__ levels,
@@ -155,7 +157,7 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
     return NAN;
   }
   double plo, phi;
-  if (tab) {
+  if constexpr (TAB) {
     const double2 p = tab[(int64_t)idx * D + d];
     plo = p.x;
     phi = p.y;
@@ -173,6 +175,7 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
 // dims, stream) and arithmetic as before: the draws do not depend on the launch shape.  Results go
 // through an LDS tile (row stride S doubles, even) and leave as contiguous 16-byte stores of the block's
 // 64 rows.  The datum draw of each candidate is made once (wave 0) and shared through LDS.
+template <bool TAB>
 __global__ __launch_bounds__(512) void kde_sample_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
     const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
@@ -203,9 +206,9 @@ __global__ __launch_bounds__(512) void kde_sample_kernel(
     for (int k = wave; k < D2; k += W) {
       const int d = 2 * k;
       const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
-      const double v0 = sample_dim(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
+      const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
       if (d + 1 < D) {
-        const double v1 = sample_dim(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
+        const double v1 = sample_dim<TAB>(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
         *(double2*)(tile + lane * S + d) = make_double2(v0, v1);
       } else {
         tile[lane * S + d] = v0;
@@ -279,9 +282,10 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   const size_t lds = (size_t)64 * ((D + 2) & ~1) * sizeof(double);
   const int64_t blocks = (Nc + 63) / 64;
   if (blocks > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
+  const void* kfn = tab ? (const void*)kde_sample_kernel<true> : (const void*)kde_sample_kernel<false>;
   if (lds > 65536)  // D > 126: the tile needs more than the default dynamic LDS limit (<= 132 KB at D = 256)
-    HBX_HIP(hipFuncSetAttribute((const void*)kde_sample_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kde_sample_kernel, dim3((unsigned)blocks), dim3(64 * W), lds, s, X, D, rows, n, bw, levels,
+    HBX_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(tab ? kde_sample_kernel<true> : kde_sample_kernel<false>, dim3((unsigned)blocks), dim3(64 * W), lds, s, X, D, rows, n, bw, levels,
                      (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
