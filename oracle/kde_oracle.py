@@ -20,6 +20,8 @@ import math
 
 import numpy as np
 
+from oracle import np_argsort
+
 CLAMP = 1e-8  # bohb.py:129
 
 
@@ -44,7 +46,7 @@ def bohb_split(X, losses, min_points, top_n_percent=15):
     if n <= min_points + 1:
         return None
     n_good, n_bad = bohb_split_sizes(n, min_points, top_n_percent)
-    idx = np.argsort(losses)
+    idx = np_argsort.argsort(losses)  # numpy 1.26.4's unstable order, ties included
     good, bad = idx[:n_good], idx[-n_bad:]
     if good.shape[0] <= D or bad.shape[0] <= D:
         return None
@@ -185,18 +187,19 @@ def select(pdf_l, pdf_g):
 # successive halving promotion (HB_iteration.py:179-182, 239-242)
 
 
-def sh_advance(losses, k):
+def sh_advance(losses, k, stable=False):
     """ranks = argsort(argsort(losses)); advance = ranks < k, over the REVIEW (finite) entries only.
 
     Non-finite losses are CRASHED in register_result (HB_iteration.py:102-106) and never ranked.
-    Returns a bool mask over all entries.  Ties are resolved stably (by position); the reference's
-    unstable argsort agrees on tie-free inputs (the only ones the fixtures use).
+    Returns a bool mask over all entries.  Tied losses are ordered as numpy 1.26.4's default argsort
+    orders them (np_argsort.py); ``stable=True`` ranks ties by position instead.
     """
     losses = np.asarray(losses, dtype=np.float64)
     ok = np.isfinite(losses)
     adv = np.zeros(losses.shape[0], dtype=bool)
     sub = losses[ok]
-    ranks = np.argsort(np.argsort(sub, kind="stable"), kind="stable")
+    inner = np.argsort(sub, kind="stable") if stable else np_argsort.argsort(sub)
+    ranks = np.argsort(inner, kind="stable")  # a permutation: no ties
     adv[np.nonzero(ok)[0]] = ranks < k
     return adv
 

@@ -609,7 +609,109 @@ def gen_npexp(ref):
     print("wrote np_exp.npz (%d values, numpy %s)" % (x.size, np.__version__))
 
 
-GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp", "kdeei"]
+# ----------------------------------------------------------------------------------------
+# tied losses: crashed runs (+inf, bohb.py:189-192) and quantised losses.  numpy's default argsort is
+# not stable (bohb.py:229, HB_iteration.py:180), so these pin the reference's own tie order end to end
+
+
+def tie_losses(n, decimals, crash_frac, seed):
+    rs = np.random.RandomState(seed)
+    L = np.round(rs.rand(n), decimals)
+    crashed = rs.rand(n) < crash_frac
+    return L, crashed
+
+
+def gen_tie_cases(ref):
+    S = ref.synth
+    # many crashed runs: the bad KDE's +inf rows, in numpy's order
+    X = S.make_observations(400, 5, 3, [2, 3, 5], seed=81)
+    L, cr = tie_losses(400, 3, 0.3, 82)
+    kde_case(ref, "tie_inf", X, L, S.make_candidates(500, 5, 3, [2, 3, 5], seed=83), 5, 3, [2, 3, 5], crashed=cr)
+    # losses rounded to 2 decimals: 100 distinct values over 1000 runs, ties across the good/bad boundary
+    X = S.make_observations(1000, 8, 0, 2, seed=84)
+    L, cr = tie_losses(1000, 2, 0.0, 85)
+    kde_case(ref, "tie_q2", X, L, S.make_candidates(600, 8, 0, 2, seed=86), 8, 0, 2, crashed=cr)
+    # > 256 rows per partition (numpy's unrolled partition), 1 decimal + 10 % crashed, mixed dims
+    X = S.make_observations(3000, 6, 2, [3, 4], seed=87)
+    L, cr = tie_losses(3000, 1, 0.1, 88)
+    kde_case(ref, "tie_q1m", X, L, S.make_candidates(400, 6, 2, [3, 4], seed=89), 6, 2, [3, 4], crashed=cr,
+             store_inputs=False)
+    # config #3's dims (24c + 8u, L=4), 3 decimals + 5 % crashed
+    X = S.make_observations(2000, 24, 8, 4, seed=90)
+    L, cr = tie_losses(2000, 3, 0.05, 91)
+    kde_case(ref, "tie_d32", X, L, S.make_candidates(256, 24, 8, 4, seed=92), 24, 8, 4, crashed=cr,
+             store_inputs=False)
+
+
+def gen_sh_ties(ref):
+    """promotion masks where tied losses straddle the k-th place (and crashed runs are filtered)"""
+    rs = np.random.RandomState(41)
+    sizes = [5, 9, 27, 64, 65, 81, 100, 257, 333, 1000, 1024, 2048, 3000]
+    out = {}
+    for i, n in enumerate(sizes):
+        q = 1 if n < 100 else 2
+        losses = np.round(rs.rand(n), q)
+        crashed = rs.rand(n) < 0.05
+        for tag, cls in (("sh", ref.HB_iteration.SuccessiveHalving),
+                         ("sr", ref.HB_iteration.SuccessiveResampling)):
+            k = max(n // 3, 1)
+            adv, count = run_sh(ref, cls, losses, k, crashed)
+            out["%s%02d_adv" % (tag, i)] = adv
+            out["%s%02d_count" % (tag, i)] = count
+        out["b%02d_losses" % i] = losses
+        out["b%02d_crashed" % i] = crashed
+        out["b%02d_k" % i] = max(n // 3, 1)
+    out["n_cases"] = len(sizes)
+    np.savez_compressed(os.path.join(HERE, "sh_ties.npz"), **out)
+    print("wrote sh_ties.npz (%d cases)" % len(sizes))
+
+
+def gen_np_argsort(ref):
+    """numpy's own argsort of float64 on tie-heavy inputs (the third-party order oracle/np_argsort.py
+    restates: numpy 1.26.4, AVX512_SKX dispatch)."""
+    rs = np.random.RandomState(43)
+    xs, outs, offs = [], [], [0]
+
+    def add(a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        xs.append(a)
+        outs.append(np.argsort(a).astype(np.int32))
+        offs.append(offs[-1] + a.size)
+
+    for n in list(range(1, 70)) + [255, 256, 257, 258, 300, 511, 512, 513, 1000, 4097, 10000]:
+        add(rs.randint(0, 3, size=n).astype(float))
+    for t in range(120):
+        n = int(np.exp(rs.uniform(np.log(2), np.log(4000))))
+        kind = t % 8
+        if kind == 0:
+            a = np.round(rs.rand(n), 2)
+        elif kind == 1:
+            a = rs.rand(n); a[rs.rand(n) < 0.3] = np.inf
+        elif kind == 2:
+            a = rs.randint(0, 50, size=n).astype(float); a[rs.rand(n) < 0.1] = np.inf
+        elif kind == 3:
+            a = rs.choice([-0.0, 0.0, 1.0, -1.0, np.inf, -np.inf], size=n)
+        elif kind == 4:
+            a = rs.rand(n); a[rs.rand(n) < 0.05] = np.nan; a[rs.rand(n) < 0.2] = 0.5
+        elif kind == 5:
+            a = np.sort(rs.randint(0, 20, size=n).astype(float))
+            if rs.rand() < 0.5:
+                a = a[::-1].copy()
+        elif kind == 6:
+            a = np.round(rs.randn(n) * 3, 0)
+        else:
+            a = (np.arange(n) % rs.randint(2, 9)).astype(float)
+        add(a)
+    for n in (300, 1000, 4000):  # depth budget spent -> std::sort on the sub-ranges
+        add(np.concatenate([np.arange(n // 2), np.arange(n // 2)[::-1]]).astype(float))
+        b = np.arange(n, dtype=float); b[8::max(1, (n - 1) // 8)] = 1e9; add(b)
+    np.savez_compressed(os.path.join(HERE, "np_argsort.npz"), x=np.concatenate(xs), order=np.concatenate(outs),
+                        off=np.array(offs, dtype=np.int64), numpy=np.array(np.__version__),
+                        avx512_skx=np.array(bool(np.core._multiarray_umath.__cpu_features__["AVX512_SKX"])))
+    print("wrote np_argsort.npz (%d arrays, %d values, numpy %s)" % (len(xs), offs[-1], np.__version__))
+
+
+GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp", "kdeei", "ties", "shties", "npargsort"]
 
 
 def main():
@@ -622,7 +724,7 @@ def main():
     todo = a.only or GENERATORS
     fns = {"kde": gen_kde_cases, "neartie": gen_neartie_cases, "getcfg": gen_get_config, "sh": gen_sh,
            "brackets": gen_brackets, "e2e": gen_e2e, "npexp": gen_npexp,
-           "kdeei": gen_kdeei}
+           "kdeei": gen_kdeei, "ties": gen_tie_cases, "shties": gen_sh_ties, "npargsort": gen_np_argsort}
     for name in todo:
         fns[name](ref)
     with open(os.path.join(HERE, "PROVENANCE.json"), "w") as fh:

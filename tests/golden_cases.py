@@ -18,7 +18,19 @@ _REGEN = {
     "d8c": lambda: (S.make_observations(1000, 8, 0, 2), S.make_losses(1000), S.make_candidates(1000, 8, 0, 2)),
     "d32m": lambda: (S.make_observations(10000, 24, 8, 4), S.make_losses(10000),
                      S.make_candidates(256, 24, 8, 4)),
+    "tie_q1m": lambda: (S.make_observations(3000, 6, 2, [3, 4], seed=87), tie_losses(3000, 1, 0.1, 88)[0],
+                        S.make_candidates(400, 6, 2, [3, 4], seed=89)),
+    "tie_d32": lambda: (S.make_observations(2000, 24, 8, 4, seed=90), tie_losses(2000, 3, 0.05, 91)[0],
+                        S.make_candidates(256, 24, 8, 4, seed=92)),
 }
+
+
+def tie_losses(n, decimals, crash_frac, seed):
+    """Quantised losses and crash flags of the tie fixtures (tests/golden/gen_golden.py:tie_losses)."""
+    rs = np.random.RandomState(seed)
+    L = np.round(rs.rand(n), decimals)
+    crashed = rs.rand(n) < crash_frac
+    return L, crashed
 
 
 def kde_case_names():
@@ -56,8 +68,8 @@ def getcfg_names():
     return sorted(os.path.basename(p)[7:-4] for p in glob.glob(os.path.join(GOLDEN, "getcfg_*.npz")))
 
 
-def load_sh():
-    z = np.load(os.path.join(GOLDEN, "sh_promotion.npz"))
+def load_sh(which="sh_promotion"):
+    z = np.load(os.path.join(GOLDEN, which + ".npz"))
     cases = []
     for i in range(int(z["n_cases"])):
         cases.append(dict(losses=z["b%02d_losses" % i], crashed=z["b%02d_crashed" % i], k=int(z["b%02d_k" % i]),

@@ -13,11 +13,9 @@ def test_fit_matches_reference(name):
     split = O.bohb_split(X, L, int(c["min_points"]))
     assert split is not None
     good, bad = split
-    if np.unique(L).size == L.size:
-        np.testing.assert_array_equal(good, c["good_idx"])
-        np.testing.assert_array_equal(bad, c["bad_idx"])
-    else:  # tied (+inf crashed) losses: np.argsort is unstable -> set equality (hard part 4)
-        assert set(good) == set(c["good_idx"]) and set(bad) == set(c["bad_idx"])
+    # the rows in the reference's own order, ties included (numpy 1.26.4's argsort, oracle/np_argsort.py)
+    np.testing.assert_array_equal(good, c["good_idx"])
+    np.testing.assert_array_equal(bad, c["bad_idx"])
     # bandwidths in the reference's own row order are bit-exact
     np.testing.assert_array_equal(O.normal_reference_bw(X[c["good_idx"]]), c["bw_good"])
     np.testing.assert_array_equal(O.normal_reference_bw(X[c["bad_idx"]]), c["bw_bad"])
@@ -35,8 +33,10 @@ def test_pdf_and_selection_match_reference(name):
     vt = c["var_type"]
     l = O.pdf_many(good, c["bw_good"], vt, C)
     g = O.pdf_many(bad, c["bw_bad"], vt, C)
-    np.testing.assert_allclose(l, c["pdf_l"][:len(C)], rtol=1e-13, atol=0, equal_nan=True)
-    np.testing.assert_allclose(g, c["pdf_g"][:len(C)], rtol=1e-13, atol=0, equal_nan=True)
+    # this process's numpy exp differs from numpy 1.26.4's in the last ulp: products of D of them
+    rtol = 1e-13 if X.shape[1] < 24 else 4e-13
+    np.testing.assert_allclose(l, c["pdf_l"][:len(C)], rtol=rtol, atol=0, equal_nan=True)
+    np.testing.assert_allclose(g, c["pdf_g"][:len(C)], rtol=rtol, atol=0, equal_nan=True)
     if len(C) == len(c["cands"]) and not name.startswith("neartie"):
         # (near ties are decided by the reference numpy's own exp rounding; this restatement uses the
         # process's numpy -- the C oracle's exact mode pins them, test_c_oracle_matches_reference)
@@ -60,8 +60,9 @@ def test_log_pdf_restatement(name):
         assert np.array_equal(np.isnan(lp), np.isnan(lref))
 
 
-def test_sh_promotion_matches_reference():
-    for c in G.load_sh():
+@pytest.mark.parametrize("which", ["sh_promotion", "sh_ties"])
+def test_sh_promotion_matches_reference(which):
+    for c in G.load_sh(which):
         losses = np.where(c["crashed"], np.nan, c["losses"])
         adv = O.sh_advance(losses, c["k"])
         np.testing.assert_array_equal(adv, c["sh_adv"])
@@ -69,6 +70,18 @@ def test_sh_promotion_matches_reference():
         k_sr = max(1, c["k"] * (1 - 0.5))
         adv = O.sh_advance(losses, k_sr)
         np.testing.assert_array_equal(adv, c["sr_adv"])
+
+
+def test_np_argsort_restatement_known_answers():
+    """numpy 1.26.4's own argsort of tie-heavy float64 arrays (+-inf, +-0, NaN, quantised, sorted,
+    periodic, sizes 1..10000: the bitonic networks, both partitions, the std::sort fallbacks)."""
+    from oracle import np_argsort as NA
+    z = np.load(G.GOLDEN + "/np_argsort.npz")
+    assert str(z["numpy"]) == "1.26.4" and bool(z["avx512_skx"])
+    x, order, off = z["x"], z["order"], z["off"]
+    for i in range(off.size - 1):
+        a = x[off[i]:off[i + 1]]
+        np.testing.assert_array_equal(NA.argsort(a), order[off[i]:off[i + 1]], err_msg="case %d n=%d" % (i, a.size))
 
 
 def test_hb_brackets_match_reference():
