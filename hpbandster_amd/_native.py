@@ -72,7 +72,27 @@ SIGNATURES = {
     "hbx_argmax_allreduce": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "hbx_argmax_records": (c_i32, [c_vp, c_i32, c_vp, c_vp]),
     "hbx_sh_promote": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hbx_seg_argsort_ex": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "hbx_sh_promote_scratch_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i32, c_i32]),
+    "hbx_sh_promote_ex": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
+                                  c_vp]),
+    "hbx_sh_promote_one": (c_i32, [c_vp, c_i64, ctypes.c_double, c_vp, c_vp, c_i32, c_vp]),
+    "hbx_host_alloc": (c_i32, [c_i64, c_vp]),
+    "hbx_host_free": (c_i32, [c_vp]),
 }
+
+# tie order of the sorts (include/hbx.h): numpy's unstable argsort (the reference's) or by position
+ORDER_NUMPY = 0
+ORDER_STABLE = 1
+
+
+def order_mode(name):
+    """'numpy' (the reference's tie order, default) or 'stable' -> the HBX_ORDER_* code."""
+    if name in ("numpy", ORDER_NUMPY):
+        return ORDER_NUMPY
+    if name in ("stable", ORDER_STABLE):
+        return ORDER_STABLE
+    raise ValueError("tie order must be 'numpy' or 'stable', got %r" % (name,))
 
 
 class HbxError(RuntimeError):

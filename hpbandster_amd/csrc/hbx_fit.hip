@@ -11,6 +11,7 @@
 // 8192-element buffers.  The factor n**(-1/(4+D)) is a host-side glibc pow() per segment, passed in,
 // because the device pow() is not guaranteed to round the same way.
 #include "hbx_common.h"
+#include "hbx_npsort.h"
 #include "hbx_sort.h"
 #include <stdlib.h>
 
@@ -167,6 +168,88 @@ __global__ __launch_bounds__(256) void seg_rank_scatter_kernel(const int64_t* __
   const int n = (int)(seg_off[b + 1] - s);
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) order[s + rank[s + i]] = i;
+}
+
+// ---- numpy's tie order (hbx_npsort.h) ------------------------------------------------------------
+// One wave per segment: does the stable order hold tied keys?  -> the segment joins `list`.
+//   promote = 0 (argsort): any two equal keys (hbx_d2ord: -0.0 == 0.0, every NaN one key);
+//   promote = 1 (promotion ranks over the finite losses, which the stable order puts first): with the
+//   order wanted, any two equal finite keys; for the mask alone, equal keys at ranks kk-1 and kk.
+__global__ __launch_bounds__(256) void seg_tie_flag_kernel(const double* __restrict__ loss,
+                                                           const int64_t* __restrict__ seg_off, int64_t B,
+                                                           const int64_t* __restrict__ order,
+                                                           const double* __restrict__ k, int promote,
+                                                           int want_order, int32_t* __restrict__ list,
+                                                           int32_t* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole wave
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  auto key = [&](int r) -> uint64_t {
+    const double v = loss[s + order[s + r]];
+    return promote ? key_promote(v) : key_argsort(v);
+  };
+  bool tie = false;
+  if (!promote || want_order) {
+    for (int i = lane; i + 1 < n; i += 64) {
+      const uint64_t a = key(i), c = key(i + 1);
+      tie |= a == c && (!promote || a != ~0ull);
+    }
+  } else {
+    int nf = 0;
+    for (int i = lane; i < n; i += 64) nf += key(i) != ~0ull;
+    for (int o = 32; o > 0; o >>= 1) nf += __shfl_xor(nf, o);
+    const double kb = k[b];
+    const int kk = kb > 0.0 ? (kb >= (double)nf ? nf : (int)ceil(kb)) : 0;
+    tie = lane == 0 && kk > 0 && kk < nf && key(kk - 1) == key(kk);
+  }
+  if (__ballot(tie) && lane == 0) list[atomicAdd(count, 1)] = (int32_t)b;
+}
+
+// The flagged segments, one workgroup each (grid-stride over the list): A[0, m) = the positions to
+// rank -- every position (argsort), or the finite losses' in position order (promotion) -- sorted in
+// numpy's order.  Scratch arrays A/T/W/Lst are indexed by the segment's offset (slot_stride == 0) or
+// by the block (slot_stride elements per block: a fixed pool).
+__global__ __launch_bounds__(NPS_THREADS) void seg_np_order_kernel(
+    const double* __restrict__ loss, const int64_t* __restrict__ seg_off, const double* __restrict__ k,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int32_t* A0, int32_t* T0, int32_t* W0,
+    int32_t* L0, int64_t slot_stride, int promote, int64_t* __restrict__ order, uint8_t* __restrict__ advance) {
+  const int c = *count;
+  for (int q = blockIdx.x; q < c; q += gridDim.x) {
+    const int64_t b = list[q];
+    const int64_t s = seg_off[b];
+    const int n = (int)(seg_off[b + 1] - s);
+    const int64_t o = slot_stride ? (int64_t)blockIdx.x * slot_stride : s;
+    nps_order_segment(loss + s, n, promote, promote ? k[b] : 0.0, A0 + o, T0 + o, W0 + o, L0 + o,
+                      order ? order + s : nullptr, advance ? advance + s : nullptr);
+  }
+}
+
+// host: flag the segments of a stable order that hold ties, then re-rank them in numpy's order.
+// arrays: int32 [A | T | W | Lst], `slots` entries each -- slot_stride 0: indexed by segment offset
+// (slots = N), else a pool of slots / slot_stride blocks; cnt_list: int32 [16] counter + the list (<= B)
+// (flagged: the list is filled already -- sh_select_kernel flags its tie-straddling brackets itself)
+int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, const int64_t* order_in, const double* k,
+                     int promote, int want_order, int64_t* order_out, uint8_t* advance, int32_t* arrays,
+                     int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged, hipStream_t s) {
+  int32_t* A = arrays;
+  int32_t* T = A + slots;
+  int32_t* W = T + slots;
+  int32_t* L = W + slots;
+  int32_t* cnt = cnt_list;
+  int32_t* list = cnt_list + 16;
+  if (!flagged) {
+    HBX_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
+    hipLaunchKernelGGL(seg_tie_flag_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, loss, seg_off, B, order_in,
+                       k, promote, want_order, list, cnt);
+    HBX_LAUNCH_CHECK();
+  }
+  const int64_t nblk = slot_stride ? slots / slot_stride : (B < 1024 ? B : 1024);
+  hipLaunchKernelGGL(seg_np_order_kernel, dim3((unsigned)(nblk > 0 ? nblk : 1)), dim3(NPS_THREADS), 0, s, loss,
+                     seg_off, k, list, cnt, A, T, W, L, slot_stride, promote, order_out, advance);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
 }
 
 // one thread per (segment, set in {good, bad}, dim): bandwidth and observed level count
@@ -355,6 +438,9 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
 
 extern "C" {
 
+int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                       int64_t* order, void* scratch, int64_t scratch_bytes, int32_t order_mode, void* stream);
+
 // Scratch bytes hbx_kde_fit / hbx_sh_promote need for N total rows.
 // sort scratch: two (key, position) ping-pong arrays, then room for the promotion's sorted positions
 // when its caller passes no `order` buffer (hbx_sh_promote, brackets > 1024)
@@ -370,8 +456,30 @@ static int sort_tile(int64_t max_seg) {
 
 // Stable argsort of each segment's losses (np.argsort order; ties by position).  seg_off: device
 // int64[B+1]; max_seg: host upper bound on segment length; order: device int64[N] (segment-local).
+static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream);
+
 int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                     int64_t* order, void* scratch, int64_t scratch_bytes, void* stream) {
+  return hbx_seg_argsort_ex(loss, seg_off, B, max_seg, N, order, scratch, scratch_bytes, HBX_ORDER_STABLE, stream);
+}
+
+// numpy mode: the stable sort, then the segments holding ties re-sorted in numpy's order; the scratch
+// (32 N + 64 bytes) is free again after the stable sort: A/T/W/Lst take 4 N int32 (indexed by segment
+// offset), the flagged list <= N / 2 + 16 more (only segments of >= 2 elements can tie)
+int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                       int64_t* order, void* scratch, int64_t scratch_bytes, int32_t order_mode, void* stream) {
+  if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
+    return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort_ex: order_mode %d", order_mode);
+  int rc = seg_argsort_stable(loss, seg_off, B, max_seg, N, order, scratch, scratch_bytes, stream);
+  if (rc || order_mode == HBX_ORDER_STABLE || B <= 0 || N < 2) return rc;
+  int32_t* arrays = (int32_t*)scratch;
+  return hbx_np_order_fix(loss, seg_off, B, order, nullptr, 0, 1, order, nullptr, arrays, N, 0, arrays + 4 * N, false,
+                          (hipStream_t)stream);
+}
+
+static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream) {
   if (!loss || !seg_off || !order || (!scratch && N > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort: null");
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");

@@ -1731,7 +1731,10 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
   const unsigned gmeta = (unsigned)(per > 0 ? ((per + 255) / 256 < 1024 ? (per + 255) / 256 : 1024) : 1);
   hipLaunchKernelGGL(kde_refit_meta_kernel, dim3(gmeta), dim3(256), 0, s, X, loss, staged, n_new, ma, m);
   HBX_LAUNCH_CHECK();
-  rc = hbx_seg_argsort(loss, m->seg, 1, n, n, order, sort_scratch, hbx_sort_scratch_bytes(n), stream);
+  // numpy's argsort order (bohb.py:229): tied losses -- crashed +inf runs, quantised losses -- give the
+  // reference's rows in the reference's order
+  rc = hbx_seg_argsort_ex(loss, m->seg, 1, n, n, order, sort_scratch, hbx_sort_scratch_bytes(n), HBX_ORDER_NUMPY,
+                          stream);
   if (rc) return rc;
   rc = hbx_kde_fit(X, D, m->seg, 1, order, &m->n_good, &m->n_bad, &m->fac_good, &m->fac_bad, m->vt, bw_g, bw_b, nl_g,
                    nl_b, stream);

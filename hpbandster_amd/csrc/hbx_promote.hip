@@ -7,11 +7,18 @@
 // HB_iteration.py:102-106) never advance.  Mask only (the drop-in's need): a selection of the k-th
 // (key, position) per bracket (sh_select_kernel: interpolation, then bisection of the key range).  With the sorted order requested: a stable sort of
 // the losses (hbx_sort.h; one wave per bracket <= 1024, else one workgroup), then
-// advance[position] = (rank < k).  Ties are ranked by position (stable);
-// numpy's argsort is unstable, so on tied losses the reference's choice is platform dependent.
+// advance[position] = (rank < k).  Ties are ranked by position (stable), or -- HBX_ORDER_NUMPY, what the
+// drop-in uses -- as numpy 1.26.4's unstable argsort ranks them (hbx_npsort.h): brackets whose tied
+// losses straddle the k-th place are re-ranked on the device in numpy's order.
 #include "hbx_common.h"
+#include "hbx_npsort.h"
 #include "hbx_sort.h"
 #include <stdlib.h>
+
+int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, const int64_t* order_in, const double* k,
+                     int promote, int want_order, int64_t* order_out, uint8_t* advance, int32_t* arrays,
+                     int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged, hipStream_t s);
+#define NPS_POOL 64  // workgroups (scratch slots) re-ranking flagged brackets after the selection
 
 __global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restrict__ loss,
                                                          const int64_t* __restrict__ seg_off,
@@ -112,28 +119,22 @@ __device__ __forceinline__ uint64_t sel_uniform(uint64_t x) {
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void sh_select_kernel(const double* __restrict__ loss,
-                                                        const int64_t* __restrict__ seg_off, int64_t B,
-                                                        const double* __restrict__ k,
-                                                        uint8_t* __restrict__ advance,
-                                                        int64_t* __restrict__ n_advance) {
+// One bracket (n <= 1024) by one wave: the mask written through `advp`, the count to *nadvp (nullable).
+// Returns true (uniform) when tied losses straddle the k-th place: the copies of that key were taken by
+// position, and numpy's order may take others (HBX_ORDER_NUMPY re-ranks the bracket afterwards).
+__device__ __forceinline__ bool sh_select_wave(const double* __restrict__ lossp, int n, double kb,
+                                               uint8_t* __restrict__ advp, int64_t* __restrict__ nadvp,
+                                               double* __restrict__ cb, int lane) {
   constexpr int R = PW_PER_LANE;  // 16 registers x 64 lanes = 1024 elements
-  __shared__ double cbuf[4][128];  // per wave: the compacted bracket, then one dummy slot per lane
-  // the wave index made visibly uniform: the bracket's bounds, k and buffer resources live in SGPRs
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = (int64_t)blockIdx.x * 4 + wv;
-  if (b >= B) return;  // whole wave
-  const int64_t s = seg_off[b];
-  const int n = (int)(seg_off[b + 1] - s);
   if (n <= 0) {
-    if (lane == 0 && n_advance) n_advance[b] = 0;
-    return;
+    if (lane == 0 && nadvp) *nadvp = 0;
+    return false;
   }
   // the bracket as buffer resources: loads past n return 0 and stores past n are dropped by the
   // hardware range check, so all 16 loads (and stores) are unconditional; the row offset goes in the
   // vector offset, whose constant part the compiler folds into the 12-bit immediate (no per-row SGPR)
-  const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)(loss + s), (short)0, n * 8, kBufDword3);
-  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)(advance + s), (short)0, n, kBufDword3);
+  const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)lossp, (short)0, n * 8, kBufDword3);
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)advp, (short)0, n, kBufDword3);
   double v[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) v[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, 8 * lane + 512 * r, 0, 0));
@@ -173,13 +174,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
     }
   }
   // rank < k advances: the first kk ranks, kk = min(nfin, ceil(k)) (k > 0; NaN or k <= 0: none)
-  const double kb = k[b];
   const int kk = __builtin_amdgcn_readfirstlane(kb > 0.0 ? (kb >= (double)nfin ? nfin : (int)ceil(kb)) : 0);
   if (kk == nfin || kk == 0) {  // all the finite entries, or none
 #pragma unroll
     for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kk && v[r] == v[r] ? 1u : 0u), ars, lane + 64 * r, 0, 0);
-    if (lane == 0 && n_advance) n_advance[b] = kk;
-    return;
+    if (lane == 0 && nadvp) *nadvp = kk;
+    return false;
   }
   // the bracket: the high key words of the minimum and the maximum (a lane without a finite loss
   // contributes key(+inf) / key(-inf)); exact bounds only when the two coincide
@@ -255,14 +255,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
       // branchless: a lane outside the bracket writes its own dummy slot 64 + lane
       const uint64_t m = __builtin_amdgcn_ballot_w64(v[r] < Hd) & ~__builtin_amdgcn_ballot_w64(v[r] < Ld);
       const int at = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      cbuf[wv][__builtin_amdgcn_inverse_ballot_w64(m) ? at : 64 + lane] = v[r];
+      cb[__builtin_amdgcn_inverse_ballot_w64(m) ? at : 64 + lane] = v[r];
       base += (int)__popcll(m);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int c0 = cL;
-    const uint64_t key1 = lane < cH - cL ? sel_key(cbuf[wv][lane]) : ~0ull;
+    const uint64_t key1 = lane < cH - cL ? sel_key(cb[lane]) : ~0ull;
     Lk = sel_uniform(Lk);
     Hk = sel_uniform(Hk);
     while (HBX_SEL_OPEN) {
@@ -279,6 +279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
     }
   }
 #undef HBX_SEL_OPEN
+  bool tie = false;
   if (cL == kk || cH == kk) {  // exactly kk keys below T
     const double T = sel_val(cL == kk ? Lk : Hk);
 #pragma unroll
@@ -296,8 +297,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
       taken += (int)__popcll(m);
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(take ? 1u : 0u), ars, lane + 64 * r, 0, 0);
     }
+    tie = true;  // tied losses straddle the k-th place: numpy's order decides which copies advance
   }
-  if (lane == 0 && n_advance) n_advance[b] = kk;
+  if (lane == 0 && nadvp) *nadvp = kk;
+  return tie;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void sh_select_kernel(const double* __restrict__ loss,
+                                                        const int64_t* __restrict__ seg_off, int64_t B,
+                                                        const double* __restrict__ k,
+                                                        uint8_t* __restrict__ advance,
+                                                        int64_t* __restrict__ n_advance,
+                                                        int32_t* __restrict__ tie_list,
+                                                        int32_t* __restrict__ tie_count) {
+  __shared__ double cbuf[4][128];  // per wave: the compacted bracket, then one dummy slot per lane
+  // the wave index made visibly uniform: the bracket's bounds, k and buffer resources live in SGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * 4 + wv;
+  if (b >= B) return;  // whole wave
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  const bool tie = sh_select_wave(loss + s, n, k[b], advance + s, n_advance ? n_advance + b : nullptr, cbuf[wv], lane);
+  if (tie && tie_list && lane == 0) tie_list[atomicAdd(tie_count, 1)] = (int32_t)b;  // re-ranked after
+}
+
+// One bracket of n <= 1024 in ONE launch (the drop-in's process_results: HpBandSter ranks one bracket per
+// call): wave 0 selects; when tied losses straddle the k-th place and numpy's order is asked for, the
+// workgroup re-ranks the bracket in numpy's order (scratch: 4 x n int32).  loss / advance may be mapped
+// host memory (no copies).
+__global__ __launch_bounds__(NPS_THREADS) void sh_promote_one_kernel(const double* __restrict__ loss, int n, double kb,
+                                                                     uint8_t* __restrict__ advance, int np_order,
+                                                                     int32_t* __restrict__ scr) {
+  __shared__ double cbuf[128];
+  __shared__ int tie_sh;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    const bool tie = sh_select_wave(loss, n, kb, advance, nullptr, cbuf, lane);
+    if (lane == 0) tie_sh = tie ? 1 : 0;
+  }
+  __syncthreads();
+  if (np_order && tie_sh) nps_order_segment(loss, n, 1, kb, scr, scr + n, scr + 2 * n, scr + 3 * n, nullptr, advance);
 }
 
 extern "C" {
@@ -307,36 +346,102 @@ int64_t hbx_sort_scratch_bytes(int64_t N);
 // loss: device fp64[N] (non-finite = not ranked); seg_off: device int64[B+1]; k: device fp64[B];
 // max_seg: host bound on the longest bracket; order: device int64[N] (sorted positions per bracket) or
 // NULL when only the mask is wanted; advance: device uint8[N]; n_advance: device int64[B] (nullable).
+int64_t hbx_sh_promote_scratch_bytes(int64_t B, int64_t max_seg, int64_t N, int32_t order_requested,
+                                     int32_t order_mode) {
+  const int64_t listb = 64 + 4 * (B + 1);
+  if (max_seg <= 64 * PW_PER_LANE && !order_requested)  // selection: a pool of NPS_POOL re-ranking slots
+    return order_mode == HBX_ORDER_NUMPY ? 16 * NPS_POOL * max_seg + listb : 0;
+  return hbx_sort_scratch_bytes(N) + (order_mode == HBX_ORDER_NUMPY ? listb : 0);
+}
+
 int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                    const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                    int64_t scratch_bytes, void* stream) {
+  return hbx_sh_promote_ex(loss, seg_off, B, max_seg, N, k, order, advance, n_advance, scratch, scratch_bytes,
+                           HBX_ORDER_STABLE, stream);
+}
+
+int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                      const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
+                      int64_t scratch_bytes, int32_t order_mode, void* stream) {
   if (!loss || !seg_off || !k || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
+  if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
+    return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_ex: order_mode %d", order_mode);
   if (B <= 0) return HBX_OK;
-  if (max_seg <= 64 * PW_PER_LANE && !order) {  // mask only: O(n) selection, no scratch
-    hipLaunchKernelGGL(sh_select_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, loss,
-                       seg_off, B, k, advance, n_advance);
+  const bool np = order_mode == HBX_ORDER_NUMPY;
+  const bool want_order = order != nullptr;
+  const int64_t need = hbx_sh_promote_scratch_bytes(B, max_seg, N, want_order, order_mode);
+  if (need > 0 && (!scratch || scratch_bytes < need))
+    return hbx_fail(HBX_ERR_ARG, "promotion scratch too small: %lld < %lld bytes", (long long)scratch_bytes,
+                    (long long)need);
+  hipStream_t st = (hipStream_t)stream;
+  if (max_seg <= 64 * PW_PER_LANE && !order) {  // mask only: O(n) selection
+    int32_t* pool = (int32_t*)scratch;
+    const int64_t slots = (int64_t)NPS_POOL * max_seg;
+    int32_t* cnt_list = np ? pool + 4 * slots : nullptr;
+    if (np) HBX_HIP(hipMemsetAsync(cnt_list, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(sh_select_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, loss, seg_off, B, k, advance,
+                       n_advance, np ? cnt_list + 16 : (int32_t*)nullptr, cnt_list);
     HBX_LAUNCH_CHECK();
-    return HBX_OK;
+    if (!np) return HBX_OK;
+    return hbx_np_order_fix(loss, seg_off, B, nullptr, k, 1, 0, nullptr, advance, pool, slots, max_seg, cnt_list, true,
+                            st);
   }
-  if (!scratch || scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
   char* sc = (char*)scratch;
   uint64_t* gk = (uint64_t*)sc;
   uint64_t* gk2 = gk + N;
   int32_t* gi = (int32_t*)(gk2 + N);
   int32_t* gi2 = gi + N;
-  if (!order) order = (int64_t*)(sc + ((2 * (sizeof(uint64_t) + sizeof(int32_t)) * N + 7) & ~(size_t)7));
+  int64_t* ord = order ? order : (int64_t*)(sc + ((2 * (sizeof(uint64_t) + sizeof(int32_t)) * N + 7) & ~(size_t)7));
   const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-bracket kernel for every size
   if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0)) {
-    hipLaunchKernelGGL(sh_promote_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, loss,
-                       seg_off, B, k, order, advance, n_advance);
-    HBX_LAUNCH_CHECK();
-    return HBX_OK;
+    hipLaunchKernelGGL(sh_promote_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, loss, seg_off, B, k,
+                       ord, advance, n_advance);
+  } else {
+    int tile = 64;
+    while (tile < max_seg && tile < 4096) tile <<= 1;
+    hipLaunchKernelGGL(sh_promote_kernel, dim3((unsigned)B), dim3(256), (sizeof(uint64_t) + sizeof(int32_t)) * tile,
+                       st, loss, seg_off, k, tile, gk, gi, gk2, gi2, ord, advance, n_advance);
   }
-  int tile = 64;
-  while (tile < max_seg && tile < 4096) tile <<= 1;
-  hipLaunchKernelGGL(sh_promote_kernel, dim3((unsigned)B), dim3(256), (sizeof(uint64_t) + sizeof(int32_t)) * tile,
-                     (hipStream_t)stream, loss, seg_off, k, tile, gk, gi, gk2, gi2, order, advance, n_advance);
   HBX_LAUNCH_CHECK();
+  if (!np || N < 2) return HBX_OK;
+  // the sort's key / position arrays are free again: [A | T | W | Lst] over the first 16 N bytes (indexed
+  // by bracket offset; the order stays at 24 N), the flagged list after the sort scratch
+  return hbx_np_order_fix(loss, seg_off, B, ord, k, 1, want_order ? 1 : 0, order, advance, (int32_t*)sc, N, 0,
+                          (int32_t*)(sc + hbx_sort_scratch_bytes(N)), false, st);
+}
+
+// One bracket, one launch (sh_promote_one_kernel): loss / advance device or mapped host pointers,
+// n <= 1024, k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY only, else NULL).
+int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
+                       void* stream) {
+  if (!loss || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: null pointer");
+  if (n < 0 || n > 64 * PW_PER_LANE) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: n=%lld", (long long)n);
+  if (order_mode == HBX_ORDER_NUMPY && !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: scratch");
+  if (n == 0) return HBX_OK;
+  hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(NPS_THREADS), 0, (hipStream_t)stream, loss, (int)n, k, advance,
+                     order_mode == HBX_ORDER_NUMPY ? 1 : 0, (int32_t*)scratch);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// pinned host memory the device reads and writes directly (coherent, mapped): the drop-in promotion's
+// losses and mask travel with the kernel's own loads and stores, no copies
+int hbx_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes <= 0) return hbx_fail(HBX_ERR_ARG, "hbx_host_alloc: %lld bytes", (long long)bytes);
+  HBX_HIP(hipHostMalloc(out, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  void* dp = nullptr;  // the engine passes the host address itself to kernels: it must be the device's too
+  HBX_HIP(hipHostGetDevicePointer(&dp, *out, 0));
+  if (dp != *out) {
+    (void)hipHostFree(*out);
+    *out = nullptr;
+    return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+  }
+  return HBX_OK;
+}
+
+int hbx_host_free(void* p) {
+  if (p) HBX_HIP(hipHostFree(p));
   return HBX_OK;
 }
 

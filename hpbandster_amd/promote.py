@@ -1,11 +1,15 @@
 """Batched successive-halving promotion on the GPU (HB_iteration.py:149-190, 203-250).
 
 ``advance = argsort(argsort(losses)) < k`` per bracket, over the REVIEW (finite-loss) entries;
-CRASHED entries (non-finite loss) never advance.  Many brackets are ranked in one launch
-(a radix select of the k-th loss per bracket, one wave each), which is what config #5 of the
-benchmark exercises.
+CRASHED entries (non-finite loss) never advance.  Many brackets are ranked in one launch (a selection
+of the k-th loss per bracket, one wave each), which is what config #5 of the benchmark exercises.
+
+Tied losses: ``ties='numpy'`` (default) ranks them as the reference's ``np.argsort`` does -- numpy
+1.26.4's unstable AVX-512 quicksort, restated on the device (``hbx_npsort.h``): brackets whose tied
+losses straddle the k-th place are re-ranked in that order.  ``ties='stable'`` ranks them by position.
 """
 
+import ctypes
 import threading
 
 import numpy as np
@@ -14,20 +18,19 @@ from . import _native as N
 from .kde import default_device
 
 
-def promote_segments(loss, seg_off, k, device=None, stream=None, return_order=False):
+def promote_segments(loss, seg_off, k, device=None, stream=None, return_order=False, ties="numpy"):
     """loss: fp64 [N] (numpy or device tensor); seg_off: int64 [B+1]; k: per-bracket threshold [B].
 
     Returns a bool numpy mask [N]; with ``return_order`` the device tensors (advance u8, sorted
     positions i64, advancing count per bracket i64).
     """
-    import torch
     L = N.lib()
     device = device or default_device()
     with N.on_device(device, stream):
-        return _promote_segments(L, loss, seg_off, k, device, stream, return_order)
+        return _promote_segments(L, loss, seg_off, k, device, stream, return_order, N.order_mode(ties))
 
 
-def _promote_segments(L, loss, seg_off, k, device, stream, return_order):
+def _promote_segments(L, loss, seg_off, k, device, stream, return_order, mode):
     import torch
 
     def dev(a, dt):
@@ -42,40 +45,56 @@ def _promote_segments(L, loss, seg_off, k, device, stream, return_order):
     B = seg_h.shape[0] - 1
     Ntot = int(loss_d.shape[0])
     max_seg = int(np.max(np.diff(seg_h))) if B > 0 else 0
-    # the sorted order only on request: brackets <= 1024 then take the O(n) select (no scratch)
+    # the sorted order only on request: brackets <= 1024 then take the O(n) select
     order = torch.empty(Ntot, dtype=torch.int64, device=device) if return_order else None
     adv = torch.empty(Ntot, dtype=torch.uint8, device=device)
     nadv = torch.empty(max(B, 1), dtype=torch.int64, device=device)
-    scratch, sb = None, 0
-    if return_order or max_seg > 1024:
-        sb = int(L.hbx_sort_scratch_bytes(Ntot))
-        scratch = torch.empty(sb, dtype=torch.uint8, device=device)
-    N.check(L.hbx_sh_promote(N.ptr(loss_d), N.ptr(seg_d), B, max_seg, Ntot, N.ptr(k_d), N.ptr(order), N.ptr(adv),
-                             N.ptr(nadv), N.ptr(scratch), sb, N.stream_handle(stream, device)))
+    sb = int(L.hbx_sh_promote_scratch_bytes(B, max_seg, Ntot, 1 if return_order else 0, mode))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=device) if sb > 0 else None
+    N.check(L.hbx_sh_promote_ex(N.ptr(loss_d), N.ptr(seg_d), B, max_seg, Ntot, N.ptr(k_d), N.ptr(order), N.ptr(adv),
+                                N.ptr(nadv), N.ptr(scratch), sb, mode, N.stream_handle(stream, device)))
     if return_order:
         return adv, order, nadv
     return adv.cpu().numpy().astype(bool)
 
 
 class _Staging(object):
-    """Per-thread, per-device buffers of advance_mask: pinned host in/out and their device twins,
-    grown on demand.  Every call synchronises its stream before returning, so a buffer is free again
-    when the next call of the same thread starts."""
+    """Per-thread, per-device buffers of advance_mask: device-mapped coherent host memory for the
+    losses (in) and the mask (out) -- the kernel reads and writes them directly, no copies -- and the
+    device scratch of the numpy-order re-rank, grown on demand.  Every call synchronises its stream
+    before returning, so the buffers are free again when the next call of the same thread starts."""
 
     def __init__(self, device):
         self.device = device
         self.cap = 0
+        self._ptrs = []
 
     def get(self, n):
         import torch
         if n > self.cap:
+            L = N.lib()
             cap = max(1024, 1 << (int(n) - 1).bit_length())
-            self.h_in = torch.empty(cap + 3, dtype=torch.float64, pin_memory=True)
-            self.h_out = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
-            self.d_in = torch.empty(cap + 3, dtype=torch.float64, device=self.device)
-            self.d_out = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            self._release()
+            pin, pout = ctypes.c_void_p(), ctypes.c_void_p()
+            N.check(L.hbx_host_alloc(8 * cap, ctypes.addressof(pin)))
+            N.check(L.hbx_host_alloc(cap, ctypes.addressof(pout)))
+            self._ptrs = [pin.value, pout.value]
+            self.h_in = np.ctypeslib.as_array((ctypes.c_double * cap).from_address(pin.value))
+            self.h_out = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(pout.value))
+            self.scratch = torch.empty(4 * cap, dtype=torch.int32, device=self.device)
             self.cap = cap
         return self
+
+    def _release(self):
+        for p in self._ptrs:
+            N.lib().hbx_host_free(p)
+        self._ptrs = []
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
 
 
 _tls = threading.local()
@@ -92,32 +111,29 @@ def _staging(device):
     return st[key]
 
 
-def advance_mask(losses, k, device=None, stream=None):
+def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
-    What SuccessiveHalving.process_results calls once per bracket: segment bounds, k and the losses
-    travel in one pinned host->device copy, the select kernel runs, the mask comes back in one pinned
-    copy, one stream synchronisation."""
+    What SuccessiveHalving.process_results calls once per bracket: the losses are written into
+    device-mapped host memory, ONE kernel (hbx_sh_promote_one: the selection, and the numpy-order
+    re-rank when tied losses straddle the k-th place) reads them and writes the mask back there, one
+    stream synchronisation."""
     import torch
     losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
     if n == 0:
         return np.zeros(0, dtype=bool)
     if n > 1024:
-        return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream)
+        return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream,
+                                ties=ties)
+    mode = N.order_mode(ties)
     device = device or default_device()
     L = N.lib()
     with N.on_device(device, stream):
         st = _staging(device).get(n)
-        hb = st.h_in.numpy()
-        hb[:2].view(np.int64)[:] = (0, n)
-        hb[2] = float(k)
-        hb[3:3 + n] = losses
+        st.h_in[:n] = losses
         cur = stream if stream is not None else torch.cuda.current_stream(device)
-        st.d_in[:n + 3].copy_(st.h_in[:n + 3], non_blocking=True)
-        base = st.d_in.data_ptr()
-        N.check(L.hbx_sh_promote(base + 24, base, 1, n, n, base + 16, None, N.ptr(st.d_out), None, None, 0,
-                                 cur.cuda_stream))
-        st.h_out[:n].copy_(st.d_out[:n], non_blocking=True)
+        N.check(L.hbx_sh_promote_one(st._ptrs[0], n, float(k), st._ptrs[1],
+                                     N.ptr(st.scratch) if mode == N.ORDER_NUMPY else None, mode, cur.cuda_stream))
         cur.synchronize()
-        return st.h_out[:n].numpy().astype(bool)
+        return st.h_out[:n].astype(bool)

@@ -12,7 +12,7 @@
  *     from hbx_last_error() (thread-local).  Calls are reentrant; nothing is cached globally.
  *
  * Reference interfaces replaced (paths relative to the HpBandSter snapshot):
- *   hbx_seg_argsort + hbx_kde_fit   <- bohb.py:220-246 (BOHB.new_result refit:
+ *   hbx_seg_argsort(_ex) + hbx_kde_fit <- bohb.py:220-246 (BOHB.new_result refit:
  *                                      np.argsort + sm.nonparametric.KDEMultivariate(..,'normal_reference'))
  *   hbx_kde_refit                   <- bohb.py:211-251 (the same refit plus both KDEs' preparation, one call)
  *   hbx_kde_prepare                 <- KDEMultivariate.__init__ model state (statsmodels 0.12.2
@@ -21,7 +21,7 @@
  *                                      candidate, minimize_me, strict-'<' argmin)
  *   hbx_kde_logpdf                  <- KDEMultivariate.pdf (kernel_density.py:162-196), fp32 log domain
  *   hbx_kde_pdf_exact               <- KDEMultivariate.pdf, fp64, reference operation order
- *   hbx_sh_promote                  <- HB_iteration.py:149-190 (SuccessiveHalving.process_results ranks)
+ *   hbx_sh_promote(_ex)             <- HB_iteration.py:149-190 (SuccessiveHalving.process_results ranks)
  *   hbx_argmax_allreduce            <- bohb.py:150-152 'if val < best' across candidate shards on many GPUs
  *                                      (the reference has no multi-GPU path)
  */
@@ -56,6 +56,21 @@ int64_t hbx_sort_scratch_bytes(int64_t N);
 int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                     int64_t* order, void* scratch, int64_t scratch_bytes, void* stream);
 
+/* Tie order of the sorts (argsort split and promotion ranks).
+ *   HBX_ORDER_NUMPY: numpy 1.26.4's default np.argsort on an AVX-512 host -- the order the reference's
+ *     np.argsort(losses) (bohb.py:229) and np.argsort(np.argsort(losses)) (HB_iteration.py:180,240) give
+ *     tied losses (crashed +inf runs, quantised losses): the vendored x86-simd-sort avx512_argsort
+ *     <double> restated on the device (hpbandster_amd/csrc/hbx_npsort.h; oracle/np_argsort.py pinned
+ *     by numpy's own outputs).  Segments without ties cost one check pass over the sorted order.
+ *   HBX_ORDER_STABLE: ties by position. */
+#define HBX_ORDER_NUMPY 0
+#define HBX_ORDER_STABLE 1
+
+/* hbx_seg_argsort with the tie order chosen (hbx_seg_argsort itself = HBX_ORDER_STABLE); scratch:
+ * hbx_sort_scratch_bytes(N). */
+int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                       int64_t* order, void* scratch, int64_t scratch_bytes, int32_t order_mode, void* stream);
+
 /* Normal-reference bandwidths and observed level counts of the good (head n_good of the argsort)
  * and bad (tail n_bad) rows of every segment, bit-exact with numpy's np.std.
  * X: device f64[N][D]; order: from hbx_seg_argsort; n_good/n_bad: device i64[B] (0 = skip);
@@ -80,6 +95,7 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
  *   out: device, hbx_kde_refit_out_bytes(n, D) bytes = order i64[n] | bw_good f64[D] | bw_bad f64[D] |
  *     nlev_good i32[D] | nlev_bad i32[D] | info_good i32[8] | info_bad i32[8] (info as hbx_kde_prepare);
  *     the KDEs' rows are order[0..n_good) and order[n-n_bad..n) -- keep `out` alive with the model.
+ *     The argsort is numpy's (HBX_ORDER_NUMPY): tied losses give the reference's rows, in its order.
  *   scratch: device, hbx_kde_refit_scratch_bytes(n, D) bytes. */
 int64_t hbx_kde_refit_out_bytes(int64_t n, int32_t D);
 int64_t hbx_kde_refit_scratch_bytes(int64_t n, int32_t D);
@@ -259,6 +275,27 @@ int hbx_argmax_records(const void* all, int32_t nranks, void* out, void* stream)
 int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                    const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                    int64_t scratch_bytes, void* stream);
+
+/* hbx_sh_promote with the tie order chosen (hbx_sh_promote itself = HBX_ORDER_STABLE).  HBX_ORDER_NUMPY:
+ * the finite losses of a bracket are ranked in numpy's argsort order (HB_iteration.py:179-180 sees only
+ * the REVIEW configurations); brackets whose tied losses straddle the k-th place (or, with `order`
+ * requested, hold any tie) are re-ranked on the device.  scratch: hbx_sh_promote_scratch_bytes(...)
+ * bytes (never NULL in HBX_ORDER_NUMPY). */
+int64_t hbx_sh_promote_scratch_bytes(int64_t B, int64_t max_seg, int64_t N, int32_t order_requested,
+                                     int32_t order_mode);
+int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
+                      const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
+                      int64_t scratch_bytes, int32_t order_mode, void* stream);
+
+/* One bracket of n <= 1024 configurations in one launch (what SuccessiveHalving.process_results ranks per
+ * call, HB_iteration.py:179-182): loss f64[n] and advance u8[n] may be device pointers or mapped host
+ * memory from hbx_host_alloc (no copies); k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY), or
+ * NULL (HBX_ORDER_STABLE). */
+int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
+                       void* stream);
+/* Pinned, device-mapped, coherent host memory (hipHostMalloc) and its release. */
+int hbx_host_alloc(int64_t bytes, void** out);
+int hbx_host_free(void* p);
 
 #ifdef __cplusplus
 }

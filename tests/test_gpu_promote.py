@@ -35,11 +35,14 @@ def test_batched_promotion_matches_oracle(device, B, n):
         np.testing.assert_array_equal(adv[s:e], O.sh_advance(loss[s:e], k[b]))
 
 
-def test_promotion_ties_are_stable(device):
+def test_promotion_ties_stable_and_numpy(device):
     from hpbandster_amd import promote
     loss = np.array([1.0] * 40 + [0.5] * 10)
-    adv = promote.advance_mask(loss, 15, device=device)
+    adv = promote.advance_mask(loss, 15, device=device, ties="stable")
     assert adv[40:].all() and adv[:5].all() and not adv[5:40].any()
+    # numpy 1.26.4's argsort of this array starts [40..45, 48, 49, 46, 47, 0, 1, 4, 5, 2, 3, ...]
+    adv = promote.advance_mask(loss, 15, device=device)
+    assert sorted(np.nonzero(adv)[0].tolist()) == [0, 1, 2, 4, 5] + list(range(40, 50))
 
 
 def test_config5_shape_with_fit(device):
@@ -225,7 +228,7 @@ def test_select_kernel_counts_and_extreme_keys(device):
             cnt = torch.empty(1, dtype=torch.int64, device=device)
             N.check(L.hbx_sh_promote(N.ptr(ld), N.ptr(seg), 1, n, n, N.ptr(kd), None, N.ptr(adv), N.ptr(cnt), None, 0,
                                      N.stream_handle()))
-            want = O.sh_advance(loss, kk)
+            want = O.sh_advance(loss, kk, stable=True)  # hbx_sh_promote: ties by position
             np.testing.assert_array_equal(adv.cpu().numpy().astype(bool), want, err_msg="k=%d" % kk)
             assert int(cnt.item()) == int(want.sum())
 

@@ -1,0 +1,167 @@
+"""GPU parity on TIED losses: numpy 1.26.4's argsort order restated on the device (hbx_npsort.h).
+
+The reference splits with np.argsort(losses) (bohb.py:229) and promotes with
+np.argsort(np.argsort(losses)) < k (HB_iteration.py:180-182); numpy's default sort is unstable, and
+crashed runs (+inf, bohb.py:189-192) and quantised losses tie.  Pinned by numpy's own outputs
+(np_argsort.npz) and by reference runs on tie-heavy losses (kde_tie_*.npz, sh_ties.npz), all through
+the C-ABI: raw losses in, the reference's rows / bandwidth bits / picks / masks out.
+"""
+import numpy as np
+import pytest
+
+from oracle import kde_oracle as O
+from oracle import np_argsort as NA
+from tests import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+TIE_CASES = [n for n in G.kde_case_names() if n.startswith("tie_") or n == "mixed8"]
+
+
+def _np_cases():
+    z = np.load(G.GOLDEN + "/np_argsort.npz")
+    x, order, off = z["x"], z["order"], z["off"]
+    return [(x[off[i]:off[i + 1]], order[off[i]:off[i + 1]]) for i in range(off.size - 1)]
+
+
+def _seg_argsort(device, loss, seg, mode):
+    import torch
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    n = int(seg[-1])
+    ld = torch.from_numpy(loss).to(device)
+    segd = torch.from_numpy(seg).to(device)
+    sb = int(L.hbx_sort_scratch_bytes(n))
+    scr = torch.empty(max(sb, 1), dtype=torch.uint8, device=device)
+    order = torch.full((max(n, 1),), -1, dtype=torch.int64, device=device)
+    N.call("hbx_seg_argsort_ex", N.ptr(ld), N.ptr(segd), len(seg) - 1, int(np.diff(seg).max()), n, N.ptr(order),
+           N.ptr(scr), sb, mode, N.stream_handle())
+    return order.cpu().numpy()[:n]
+
+
+@pytest.mark.parametrize("path", ["wave", "rank", "block"])
+def test_np_argsort_known_answers(device, path, monkeypatch):
+    """Every numpy 1.26.4 argsort of np_argsort.npz (sizes 1..10000: +-inf, +-0, NaN, quantised, sorted,
+    periodic) as segments of ONE hbx_seg_argsort_ex(HBX_ORDER_NUMPY) call, behind each stable kernel."""
+    from hpbandster_amd import _native as N
+    monkeypatch.setenv("HBX_PROMOTE_WAVE", "0" if path == "block" else "1")
+    monkeypatch.setenv("HBX_SORT_RANK", "0" if path == "block" else "1")
+    cases = _np_cases()
+    if path == "wave":  # many segments <= 1024: the wave kernel
+        cases = [c for c in cases if c[0].size <= 1024]
+    elif path == "rank":  # few segments: the counting rank
+        cases = [c for c in cases if c[0].size > 200][:40]
+    loss = np.concatenate([c[0] for c in cases])
+    seg = np.concatenate([[0], np.cumsum([c[0].size for c in cases])]).astype(np.int64)
+    got = _seg_argsort(device, loss, seg, N.ORDER_NUMPY)
+    for i, (x, want) in enumerate(cases):
+        np.testing.assert_array_equal(got[seg[i]:seg[i + 1]], want, err_msg="case %d n=%d" % (i, x.size))
+
+
+def test_np_argsort_random_against_oracle(device):
+    """Tie-heavy random segments against the restatement (oracle/np_argsort.py)."""
+    from hpbandster_amd import _native as N
+    rs = np.random.RandomState(17)
+    lens = np.concatenate([rs.randint(2, 70, 60), rs.randint(65, 300, 30), rs.randint(250, 3000, 10)])
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = np.round(rs.rand(seg[-1]), 1)
+    loss[rs.rand(seg[-1]) < 0.1] = np.inf
+    loss[rs.rand(seg[-1]) < 0.02] = -0.0
+    got = _seg_argsort(device, loss, seg, N.ORDER_NUMPY)
+    for b in range(lens.size):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(got[s:e], NA.argsort(loss[s:e]), err_msg="segment %d n=%d" % (b, e - s))
+
+
+@pytest.mark.parametrize("name", TIE_CASES)
+def test_refit_from_raw_tied_losses(device, name):
+    """The refit from the raw losses (ObservationStore.refit / hbx_kde_refit): the reference's rows in its
+    order, its bandwidths bit for bit, its level counts."""
+    from hpbandster_amd import kde
+    c = G.load_kde_case(name)
+    pair = kde.fit_pair(c["X"], c["eff_losses"], c["var_type"], int(c["min_points"]), device=device)
+    np.testing.assert_array_equal(pair.good.rows_dev.cpu().numpy(), c["good_idx"])
+    np.testing.assert_array_equal(pair.bad.rows_dev.cpu().numpy(), c["bad_idx"])
+    np.testing.assert_array_equal(pair.good.bw, c["bw_good"])
+    np.testing.assert_array_equal(pair.bad.bw, c["bw_bad"])
+    np.testing.assert_array_equal(pair.good.nlev, c["nlev_good"])
+    np.testing.assert_array_equal(pair.bad.nlev, c["nlev_bad"])
+
+
+@pytest.mark.parametrize("name", TIE_CASES)
+def test_acquire_end_to_end_on_tied_losses(device, name):
+    """Raw tied losses -> engine split -> acquisition: the reference's pick, its score and both pdfs bit
+    for bit (single call and incrementally grown store)."""
+    from hpbandster_amd import kde
+    c = G.load_kde_case(name)
+    pair = kde.fit_pair(c["X"], c["eff_losses"], c["var_type"], int(c["min_points"]), device=device)
+    r = pair.acquire(c["cands"])
+    assert r.index == c["chosen"]
+    assert (r.score, r.pdf_l, r.pdf_g) == (c["scores"][c["chosen"]], c["pdf_l"][c["chosen"]], c["pdf_g"][c["chosen"]])
+    # the same rows arriving one new_result at a time (bohb.py:211-251): the last refit equals the fixture
+    store = kde.ObservationStore(c["X"].shape[1], c["var_type"], device=device, capacity=16)
+    n = c["X"].shape[0]
+    cut = max(int(c["min_points"]) + 2, n - 5)
+    store.add(c["X"][:cut], c["eff_losses"][:cut])
+    store.refit(int(c["min_points"]))
+    for i in range(cut, n):
+        store.add(c["X"][i], c["eff_losses"][i])
+        p2 = store.refit(int(c["min_points"]))
+    np.testing.assert_array_equal(p2.good.rows_dev.cpu().numpy(), c["good_idx"])
+    np.testing.assert_array_equal(p2.bad.rows_dev.cpu().numpy(), c["bad_idx"])
+    assert p2.acquire(c["cands"]).index == c["chosen"]
+
+
+@pytest.mark.parametrize("which", ["sh_ties", "sh_promotion"])
+def test_promotion_masks_on_ties(device, which):
+    """sh_ties.npz: the reference's SuccessiveHalving / SuccessiveResampling masks where tied losses
+    straddle the k-th place -- per bracket (the drop-in's one-launch path) and batched (select and
+    sort paths)."""
+    from hpbandster_amd import promote
+    cases = G.load_sh(which)
+    for c in cases:
+        losses = np.where(c["crashed"], np.nan, c["losses"])
+        np.testing.assert_array_equal(promote.advance_mask(losses, c["k"], device=device), c["sh_adv"])
+        np.testing.assert_array_equal(promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device),
+                                      c["sr_adv"])
+    loss = np.concatenate([np.where(c["crashed"], np.nan, c["losses"]) for c in cases])
+    seg = np.concatenate([[0], np.cumsum([c["losses"].size for c in cases])]).astype(np.int64)
+    k = np.array([c["k"] for c in cases], dtype=np.float64)
+    want = np.concatenate([c["sh_adv"] for c in cases])
+    np.testing.assert_array_equal(promote.promote_segments(loss, seg, k, device=device), want)
+    adv, order, cnt = promote.promote_segments(loss, seg, k, device=device, return_order=True)
+    np.testing.assert_array_equal(adv.cpu().numpy().astype(bool), want)
+    o = order.cpu().numpy()
+    for b, c in enumerate(cases):  # the order: numpy's over the finite losses, then the crashed positions
+        x = loss[seg[b]:seg[b + 1]]
+        fin = np.nonzero(np.isfinite(x))[0]
+        np.testing.assert_array_equal(o[seg[b]:seg[b] + fin.size], fin[NA.argsort(x[fin])])
+
+
+def test_promotion_stable_mode_ranks_by_position(device):
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(3)
+    lens = rs.randint(1, 1025, 50)
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = np.round(rs.rand(seg[-1]), 1)
+    k = np.maximum(lens // 3, 1).astype(np.float64)
+    a_st = promote.promote_segments(loss, seg, k, device=device, ties="stable")
+    a_np = promote.promote_segments(loss, seg, k, device=device)
+    for b in range(lens.size):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(a_st[s:e], O.sh_advance(loss[s:e], k[b], stable=True))
+        np.testing.assert_array_equal(a_np[s:e], O.sh_advance(loss[s:e], k[b]))
+
+
+def test_config5_shape_with_quantised_losses(device):
+    """1e3 brackets x 1e3 configs with losses rounded to 3 decimals (ties straddle k in most brackets):
+    every mask equal to numpy's ranks."""
+    from hpbandster_amd import promote
+    B, n, k = 1000, 1000, 333
+    rs = np.random.RandomState(8)
+    losses = np.round(rs.rand(B, n), 3)
+    seg = np.arange(B + 1, dtype=np.int64) * n
+    adv = promote.promote_segments(losses.reshape(-1), seg, np.full(B, float(k)), device=device).reshape(B, n)
+    assert (adv.sum(1) == k).all()
+    for b in range(0, B, 37):
+        np.testing.assert_array_equal(adv[b], O.sh_advance(losses[b], k))
