@@ -100,6 +100,13 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="winner exchange: nccl (= RCCL over xGMI) or gloo (CPU, multi-process rehearsal)")
     ap.add_argument("--share-gpu", action="store_true", help="ranks share the visible GPUs (rehearsal only)")
+    ap.add_argument("--total-candidates", type=int, default=None,
+                    help="strong scaling: the main line scores this many candidates in total, sharded over the "
+                         "ranks (config #4: 10000000); default: --candidates per GPU (weak)")
+    ap.add_argument("--strong-total", type=int, default=10_000_000,
+                    help="N>1: the config #4 side line (this many candidates in total over the ranks); 0 = off")
+    ap.add_argument("--profile-tag", default=None,
+                    help="profiles/ directory holding the rocprofv3 summaries of this very run (recorded in the line)")
     return ap.parse_args()
 
 
@@ -290,6 +297,49 @@ def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
             "winner_8_shards": sharded, "winners_identical": r.index == sharded, "shortlist": r.shortlist}
 
 
+def strong_line(pair, device, a, rank, world, dist, xchg, reps=10):
+    """Side line at N > 1: BASELINE config #4 -- a fixed total of candidates (1e7) x config #3's
+    observations, sharded over the ranks (each scores shard_range(total, rank, N) with global indices,
+    drawn on its own device), one winner exchange per step; max-over-ranks time (strong scaling)."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd.distributed import shard_range
+    lo, hi = shard_range(a.strong_total, rank, world)
+    Nc = hi - lo
+    g = torch.Generator(device=device)
+    g.manual_seed(4400 + rank)
+    C = torch.empty((Nc, a.dc + a.du), dtype=torch.float64, device=device)
+    C[:, :a.dc] = torch.rand((Nc, a.dc), dtype=torch.float64, device=device, generator=g)
+    if a.du:
+        C[:, a.dc:] = torch.randint(0, a.levels, (Nc, a.du), device=device, generator=g).to(torch.float64)
+    ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
+
+    def step():
+        rv = pair.acquire(C, index_base=lo, workspace=ws, sync=False)
+        if xchg is not None:
+            rv = xchg.exchange(rv)
+        return kde.AcqResult.from_bytes(kde.fetch_bytes(rv))
+
+    step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    del C, ws
+    torch.cuda.empty_cache()
+    pairs = a.strong_total * (pair.good.nobs + pair.bad.nobs)
+    return {"workload": "kde_acquisition_d%d_obs%d_total%d_sharded" % (a.dc + a.du, a.obs, a.strong_total),
+            "scaling": "strong", "value": pairs * reps / el, "unit": "pairs/s", "ms_per_step": el / reps * 1e3,
+            "candidates_per_rank": Nc, "ranks": world, "winner": r.index}
+
+
 def promote_dropin(device, n=1000, reps=50):
     """Side line: the drop-in SuccessiveHalving.process_results at one bracket of n configurations
     (HB_iteration.py:149-190 as HpBandSter calls it: one bracket per call), wall clock per call, beside
@@ -423,10 +473,16 @@ def refit_line(X, losses, var_type, device, reps=20):
     store.add(X[:n0], losses[:n0])
     store.refit(D + 1)
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gpu_ms = []
     t0 = time.perf_counter()
     for r in range(reps):
         store.add(X[n0 + r], losses[n0 + r])
-        store.refit(D + 1)
+        e0.record()
+        store.refit(D + 1)  # ends with a stream synchronisation: e1 below is already complete when read
+        e1.record()
+        e1.synchronize()
+        gpu_ms.append(e0.elapsed_time(e1))
     inc_ms = (time.perf_counter() - t0) / reps * 1e3
     kde.fit_pair(X, losses, var_type, D + 1, device=device)
     torch.cuda.synchronize()
@@ -445,6 +501,9 @@ def refit_line(X, losses, var_type, device, reps=20):
     host_ms = (time.perf_counter() - t0) / reps * 1e3
     return {"workload": "bohb_refit_obs%d_d%d" % X.shape, "ms_per_refit": inc_ms, "host_numpy_ms": host_ms,
             "ms_per_refit_host_arrays": full_ms,
+            "stream_ms_median": float(np.median(gpu_ms)),
+            "stream_ms_note": "events bracketing store.refit on its stream: the kernels plus the host's enqueue gaps "
+                              "(wall clock ms_per_refit adds add(), allocation and the read-back)",
             "note": "wall clock per new_result refit: one row appended in HBM, one hbx_kde_refit, one read-back; "
                     "host_arrays = every row uploaded"}
 
@@ -500,12 +559,25 @@ def sampler_line(pair, device, dc, du, levels, Nc, ws, reps=10):
         r = pair.acquire(samp(k + 100), workspace=ws)
     torch.cuda.synchronize()
     ms_e2e = (time.perf_counter() - t0) / reps * 1e3
+    # the acquisition alone on BOHB-distributed candidates (around the good observations, bohb.py:133-147):
+    # its scoring launch and how many candidates the exact re-score takes (data dependent)
+    ev = kde.ScoreEvents()
+    C = samp(7)
+    pair.acquire(C, workspace=ws, events=ev)
+    launch, shortlists = [], []
+    for k in range(reps):
+        rr = pair.acquire(C, workspace=ws, events=ev)
+        ml, mg = ev.elapsed_ms(True)
+        launch.append(ml)
+        shortlists.append(rr.shortlist)
     gbs = Nc * D * 8 / (ms * 1e-3) / 1e9
     return {"workload": "gpu_sampler_cand%d_d%d" % (Nc, D), "ms_per_launch": ms,
             "candidates_per_s": Nc / (ms * 1e-3),
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
                          "bytes_per_element": 8},
-            "ms_sample_plus_acquire": ms_e2e, "last_winner": r.index}
+            "ms_sample_plus_acquire": ms_e2e, "last_winner": r.index,
+            "bohb_distributed_acquisition": {"pair_launch_ms_median": float(np.median(launch)),
+                                             "shortlist": int(np.max(shortlists)), "winner": rr.index}}
 
 
 def kde_result_bytes():
@@ -570,10 +642,14 @@ def main():
     losses = S.make_losses(a.obs)
     pair = kde.fit_pair(X, losses, var_type, D + 1, device=device)
     Ng, Nb = pair.good.nobs, pair.bad.nobs
-    Nc = a.candidates
+    from hpbandster_amd.distributed import shard_range
+    if a.total_candidates:  # strong scaling: this rank's contiguous shard of the total, global indices
+        lo, hi = shard_range(a.total_candidates, rank, world)
+        Nc, base = hi - lo, lo
+    else:
+        Nc, base = a.candidates, rank * a.candidates
     cands = S.make_candidates(Nc, a.dc, a.du, a.levels, seed=S.SEED_CAND + rank)
     c_dev = torch.from_numpy(cands).to(device)
-    base = rank * Nc
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     ev = kde.ScoreEvents()
     # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
@@ -603,6 +679,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_l = t_g = 0.0
+    launch_ms = []  # the scoring launch of every timed step (HIP events on its stream)
     t0 = time.perf_counter()
     winner = None
     for s in range(a.steps):
@@ -610,6 +687,7 @@ def main():
         ml, mg = ev.elapsed_ms(fused)  # step() synchronised on the result: events are complete
         t_l += ml
         t_g += mg
+        launch_ms.append(ml + mg)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -621,13 +699,15 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    pairs_step = world * Nc * (Ng + Nb)
+    pairs_step = (a.total_candidates if a.total_candidates else world * Nc) * (Ng + Nb)
     value = pairs_step * a.steps / el
     W = 3 * a.dc + 2 * a.du + 4
     avg_l, avg_g = t_l / a.steps, t_g / a.steps
     kernel_rate = Nc * (Ng + Nb) / ((avg_l + avg_g) * 1e-3)  # pairs/s inside the scoring launches
     achieved = W * kernel_rate / 1e12
     workload = "kde_acquisition_d%d_%dc%du_obs%d_cand%d" % (D, a.dc, a.du, a.obs, Nc)
+    if a.total_candidates:
+        workload = "kde_acquisition_d%d_%dc%du_obs%d_total%d_sharded" % (D, a.dc, a.du, a.obs, a.total_candidates)
     traffic = load_traffic(workload)
     km = kernel_model(pair.bad, a.dc, a.du)
     if fused:
@@ -649,9 +729,11 @@ def main():
             issue_bound["frac_at_measured_clock"] = kernel_rate / (N_SIMD * clk * 1e9 * 256 / m["bound_cycles"])
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if a.total_candidates else "weak",
         "vs_baseline": None, "dtype": "f16 hi/lo MFMA (3 products per dim), f32 accumulate, f64 re-score", "data": "synthetic",
-        "config": {"workload": workload, "candidates_per_gpu": Nc, "observations": a.obs, "n_good": Ng,
+        "config": {"workload": workload, "candidates_per_gpu": Nc,
+                   "total_candidates": a.total_candidates or world * Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,
                    "parallelism": "candidate-sharded x%d, %s" % (
                        world, "one collective: hbx_argmax_allreduce (RCCL all-gather of result records)"
@@ -671,9 +753,21 @@ def main():
                               "(valu_basis) frac > 1" % (km["model"] or {}).get("dense_equiv_flops_per_pair", "-"),
                      "ms_per_launch": ({"l+g": avg_l + avg_g, "pairs_per_launch": Nc * (Ng + Nb)} if fused else
                                        {"l": avg_l, "g": avg_g, "mean": (avg_l + avg_g) / 2}),
+                     # every timed step's launch: what rocprofv3's kernel trace of the same run must show
+                     "launch_ms_stats": {"mean": float(np.mean(launch_ms)), "median": float(np.median(launch_ms)),
+                                         "min": float(np.min(launch_ms)), "max": float(np.max(launch_ms)),
+                                         "samples": len(launch_ms),
+                                         "timing": "HIP events on the launch stream around the scoring launch(es) "
+                                                   "of each timed step"},
+                     "profiles": a.profile_tag,
                      "mfma_util": mfma_util, "issue_bound": issue_bound},
         "cpu_baseline": None,
     }
+    if world > 1 and a.strong_total and not a.total_candidates:
+        try:  # config #4 beside the weak line: the same total at every N (strong scaling)
+            out["strong_config4"] = strong_line(pair, device, a, rank, world, dist, xchg)
+        except Exception as e:
+            out["strong_config4"] = {"error": repr(e)}
     if not a.no_config5:  # every rank promotes its share of the brackets
         try:
             out["config5"] = config5(device, rank=rank, world=world, dist=dist if world > 1 else None)

@@ -697,12 +697,17 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
 }
 
 // both KDEs' rescue passes in one launch (blocks [0, nblk0) KDE 0, the rest KDE 1)
+// grid-stride over the 2 nblk0 logical blocks; with the scoring kernel's marker count available and 0
+// (the common case) every workgroup exits after one load
 template <int DCP, bool SIGNED>
 __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                               KdePairArgs a) {
-  const bool second = blockIdx.x >= a.nblk0;
-  kde_rescue_body<DCP, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                               second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+  if (a.rescue && __hip_atomic_load(a.rescue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  for (unsigned b = blockIdx.x; b < 2 * a.nblk0; b += gridDim.x) {
+    const bool second = b >= a.nblk0;
+    kde_rescue_body<DCP, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                 second ? a.out1 : a.out0, second ? b - a.nblk0 : b);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -768,7 +773,10 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo, float* __restrict__ hi,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
-                                                          int32_t* __restrict__ first1) {
+                                                          int32_t* __restrict__ first1,
+                                                          int32_t* __restrict__ rescue_cnt) {
+  // the rescue pass of this acquisition has run: its marker count starts the next one at 0
+  if (rescue_cnt && blockIdx.x == 0 && threadIdx.x == 0) *rescue_cnt = 0;
   // COMBINE_SUB consecutive 256-candidate sub-blocks per block: every sub-block's loads are issued first
   // (the kernel is latency-bound with one candidate per thread), then each runs as its own block would
   KdeEst ea[COMBINE_SUB], eb[COMBINE_SUB];
@@ -1501,17 +1509,19 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 // records [0] and [1] only ([1] after everything).
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
-                         int32_t D, hipEvent_t* ev, hipStream_t s) {
+                         int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s) {
   if (ev) HBX_HIP(hipEventRecord(ev[0], s));
   if (f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled()) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
-    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm};
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt};
     hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
-    hipLaunchKernelGGL(f0.rescue_pair, dim3(2 * gr), dim3(256), 0, s, cand, Nc, D, a);
+    // the rescue pass: grid-stride, exits at once unless the scoring kernel counted a marker
+    const unsigned grr = rescue_cnt ? (2 * gr < 1024u ? 2 * gr : 1024u) : 2 * gr;
+    hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     if (ev) HBX_HIP(hipEventRecord(ev[1], s));
     return HBX_OK;
@@ -1529,8 +1539,8 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
 // of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
 // comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t res, U, count, flags, segcnt, segnear, best, key, first1, est_l, est_g, lo, hi, list, near, exact_l, exact_g,
-      part, total;
+  size_t res, U, count, flags, segcnt, segnear, best, key, first1, rescue, est_l, est_g, lo, hi, list, near, exact_l,
+      exact_g, part, total;
 };
 
 static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
@@ -1550,6 +1560,7 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.best = take(8 * B);
   w.key = take(8 * B);
   w.first1 = take(4 * B);
+  w.rescue = take(4);
   w.est_l = take(sizeof(KdeEst) * Nc);
   w.est_g = take(sizeof(KdeEst) * Nc);
   w.lo = take(4 * Nc);
@@ -1813,7 +1824,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   const bool scored = Nc > 0 && !exact_only;
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
-    const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev, s);
+    const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
+                                 (int32_t*)(ws + w.rescue), s);
     if (rc) return rc;
   }
   if (batch_res)
@@ -1831,7 +1843,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     } else {
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
                          dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
-                         flags, first1);
+                         flags, first1, (int32_t*)(ws + w.rescue));
       HBX_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,

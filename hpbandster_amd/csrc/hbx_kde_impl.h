@@ -208,6 +208,9 @@ struct KdePairArgs {
   KdeEst* out0;
   KdeEst* out1;
   unsigned nblk0;
+  // acquisition workspace counter of rescue-marked candidates (nullable): the scoring kernel counts its
+  // markers, the rescue pass exits at once on 0, the combine kernel zeroes it for the next acquisition
+  int32_t* rescue;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
 

@@ -48,7 +48,7 @@ template <int NSC, int KC, bool SIGNED>
 __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                   const KdeParams* __restrict__ P,
                                                   const float* __restrict__ table, KdeEst* __restrict__ out,
-                                                  const unsigned blk) {
+                                                  const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr) {
   constexpr int RT = H_ROW_TILES;           // 16-candidate row tiles per wave
   constexpr int NSH = NSC + KC;             // f16 K-steps of 32
   // one-hot product on the sparse matrix cores (v_smfmac_f32_16x16x64_f16, 2:4 structured sparsity:
@@ -506,7 +506,10 @@ __device__ __forceinline__ void kde_logpdf_h_body(const double* __restrict__ can
         // f16 hi/lo representation error of both coordinates and the three lo.lo products given up
         // to the C_j pieces (each <= 2^-22 sum|x''X'|), plus the pieces' subnormal rounding
         if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-20f) * HBX_LN2f;
-        if (!nq && Sq == Sq && (Sq < 0x1p-64f || Sq > 0x1p100f)) o.err = -1.f;
+        if (!nq && Sq == Sq && (Sq < 0x1p-64f || Sq > 0x1p100f)) {
+          o.err = -1.f;  // rescue marker
+          if (rescue_cnt) atomicAdd(rescue_cnt, 1);
+        }
         out[ii] = o;
       }
     }
@@ -528,7 +531,7 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   kde_logpdf_h_body<NSC, KC, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                     second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+                                     second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x, a.rescue);
 }
 
 template <int NSC, bool SG>

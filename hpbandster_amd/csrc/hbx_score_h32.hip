@@ -71,7 +71,7 @@ template <int NSC, int KP, bool SG, bool FAST>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
-                                                    const unsigned blk) {
+                                                    const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr) {
   constexpr int ND = h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + 3 slots per continuous dim)
   constexpr int KS = KP;                     // sparse 32-wide K-steps (one-hot positions), hi parts
   constexpr int KL = FAST ? 0 : KP;          // ... and lo parts
@@ -407,7 +407,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
         // (1 + e) 2^L - 1 (rounded up)
         if (o.err > 0.f) o.err = (1.f + o.err) * exp2f(lo_err) * (1.f + 0x1p-20f) - 1.f;
       }
-      if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) o.err = -1.f;  // rescue marker
+      if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) {  // rescue marker
+        o.err = -1.f;
+        if (rescue_cnt) atomicAdd(rescue_cnt, 1);
+      }
       out[ii] = o;
     }
   }
@@ -427,7 +430,8 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   kde_logpdf_h32_body<NSC, KP, false, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
+                                            a.rescue);
 }
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
@@ -444,7 +448,8 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;
   kde_logpdf_h32_body<NSC, KP, true, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                           second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x);
+                                           second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
+                                           a.rescue);
 }
 
 // instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part

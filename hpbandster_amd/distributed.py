@@ -79,6 +79,19 @@ def reduce_winners(score, index, group=None, device=None, rel=0.0):
     return recs[best].index, float(recs[best].score)
 
 
+def broadcast_from_group_root(payload, group, world):
+    """``payload`` of the group's rank 0 on every rank of ``group``.  broadcast_object_list takes a
+    GLOBAL source rank: the group's rank 0 is global rank get_global_rank(group, 0), which is 0 only for
+    the default group."""
+    import torch.distributed as dist
+    if world <= 1:
+        return payload
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    box = [payload]
+    dist.broadcast_object_list(box, src=src, group=group)
+    return box[0]
+
+
 class WinnerExchange(object):
     """The per-acquisition collective of a candidate-sharded run.
 
@@ -107,15 +120,16 @@ class WinnerExchange(object):
                 buf = (np.frombuffer(uid, dtype=np.uint8)).copy()
                 N.check(L.hbx_rccl_get_unique_id(N.ptr(buf)))
                 uid = bytearray(buf.tobytes())
-            if self.world > 1:
-                box = [bytes(uid)]
-                dist.broadcast_object_list(box, src=0, group=group)
-                uid = bytearray(box[0])
+            uid = broadcast_from_group_root(bytes(uid), group, self.world)
             import ctypes
             idb = np.frombuffer(bytes(uid), dtype=np.uint8).copy()
             h = ctypes.c_void_p()
-            N.check(L.hbx_rccl_comm_init(ctypes.addressof(h), self.world, N.ptr(idb), self.rank,
-                                         int(torch.device(device).index or 0)))
+            dev = torch.device(device)
+            dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+            # hbx_rccl_comm_init selects the device itself: inside on_device, torch's current device is
+            # restored afterwards
+            with N.on_device(torch.device("cuda", dev_index)):
+                N.check(L.hbx_rccl_comm_init(ctypes.addressof(h), self.world, N.ptr(idb), self.rank, dev_index))
             self.comm = h.value
         elif transport != "records":
             raise ValueError("transport must be 'rccl' or 'records'")
@@ -181,10 +195,13 @@ def acquire_sharded(pair, cands_local, index_base, exchange, stream=None, worksp
         mine = _unpack(fetch_bytes(rv, stream))
         pick = None
         if exchange.rank in near:
-            if mine.flags & ACQ_NEAR_TIE:  # this rank's own near set (candidate indices local to the shard)
-                o = pair._ws_offsets(Nc, Nc)
-                idx = ws[o[2]:o[2] + 4 * mine.near].view(torch.int32).cpu().numpy().astype(np.int64)
-            else:
+            # every candidate of this rank's shortlist (indices local to the shard): its own near set is
+            # taken against its own winner's bound, and for signed KDEs (per-candidate rel) a candidate can
+            # lie within the GLOBAL winner's bound yet outside its rank winner's -- the shortlist holds both
+            o = pair._ws_offsets(Nc, Nc)
+            cnt = int(ws[o[0]:o[0] + 4].view(torch.int32).item())
+            idx = np.unique(ws[o[1]:o[1] + 4 * cnt].view(torch.int32).cpu().numpy().astype(np.int64))
+            if idx.size == 0:
                 idx = np.array([mine.index - index_base], dtype=np.int64)
             pick = exact_host.resolve(pair.good, pair.bad, _rows_of(cands_local, idx), idx)
         if pick is None:

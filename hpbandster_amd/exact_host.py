@@ -9,7 +9,9 @@ on the host, with the very numpy expressions the reference evaluates -- KDEMulti
 (_kernel_base.py:456-518) -> gaussian / aitchison_aitken (kernels.py:108-125, 23-65) -- and BOHB's
 ``max(1e-8, g) / max(l, 1e-8)`` with a strict ``<`` over the candidates in index order
 (bohb.py:129, 149-152).  This is part of the engine (a few candidates, a few numpy calls each), not
-a fallback: by default the GPU's pinned-reference pick is final.
+a fallback: by default the GPU's pinned-reference pick is final.  The KDEs' rows are in the
+reference's order even where losses tie (the refit's argsort is numpy's, hbx_npsort.h), so these
+expressions see the reference's very arrays.
 """
 
 import warnings

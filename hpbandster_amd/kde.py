@@ -593,6 +593,11 @@ class ObservationStore(object):
         losses = np.asarray(losses, dtype=np.float64).reshape(-1)
         if losses.shape[0] != rows.shape[0]:
             raise N.HbxError("observation store: %d rows, %d losses" % (rows.shape[0], losses.shape[0]))
+        cat = self.vt != 0
+        if cat.any():  # checked before the rows enter the store: a bad row would fail every later refit
+            codes = rows[:, cat]
+            if not (np.all((codes >= 0) & (codes < 1024)) and np.all(codes == np.floor(codes))):
+                raise N.HbxError("categorical codes must be integers in [0, 1024)")
         m = self.nh + rows.shape[0]
         if m > self._hcap:
             cap = max(self._init_cap, self._hcap)
@@ -659,7 +664,6 @@ class ObservationStore(object):
                                 n_good, n_bad, bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D),
                                 N.ptr(pg), N.ptr(tg), tg.numel(), N.ptr(pbad), N.ptr(tb), tb.numel(),
                                 N.ptr(out), N.ptr(scratch), sb, sh))
-        self.n = n
         oh = self._pinned("_out_h", ob)
         oh[:ob].copy_(out, non_blocking=True)
         cur.synchronize()
@@ -674,6 +678,7 @@ class ObservationStore(object):
         info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32).copy()
         if (nl_gh < 0).any() or (nl_bh < 0).any():
             raise N.HbxError("categorical codes must be integers in [0, 1024)")
+        self.n = n  # the rows count as resident only once the refit has completed and validated
         order = out[:8 * n].view(torch.int64)
         X_dev = self.X_dev
         good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, (X_host, order_h[:n_good]),

@@ -167,3 +167,37 @@ def test_winner_exchange_gloo_world2(case):
     for p in ps:
         p.join(60)
     assert out[0][0] == out[1][0] == want
+
+
+def _subgroup_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hpbandster_amd.distributed import broadcast_from_group_root
+    grp = dist.new_group([1, 2])  # every rank creates it; only 1 and 2 belong
+    if rank in (1, 2):
+        got = broadcast_from_group_root(b"uid-of-rank-%d" % rank, grp, 2)
+        q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_uid_broadcast_in_a_subgroup_without_global_rank0():
+    """WinnerExchange's RCCL unique id travels from the GROUP's rank 0 (global rank 1 here): world size
+    3, subgroup {1, 2} (broadcast_object_list takes a global source rank)."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert out == {1: b"uid-of-rank-1", 2: b"uid-of-rank-1"}

@@ -1,17 +1,23 @@
 #!/bin/bash
-# One round's measurement set on the GPU box (run via gpurun): the default bench line, a rocprofv3
-# kernel trace of the bench workload, and PMC passes (traffic, issue, clock) -- each pass its own run.
-#   bash tools/profile_round.sh r02      -> gpurun_out/r02/
+# One round's measurement set on ONE GPU box (run via gpurun), every file from the same session:
+#   1. the default bench line (what the driver runs),
+#   2. the same bench under rocprofv3 --kernel-trace --stats: its JSON line and the kernel trace come from
+#      ONE process, so the line's per-launch HIP-event times and rocprof's durations describe the same
+#      launches (tools/ksteady.py reads the trace; tools/trace_vs_line.py checks the two agree),
+#   3. PMC passes (traffic, issue, clock) of the scoring step, each pass its own run.
+#   bash tools/profile_round.sh r03      -> gpurun_out/r03/
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/$1
+TAG=$1
+OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
 timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+  python3 $R/bench.py --no-cpu --profile-tag profiles/$TAG > $OUT/bench_traced.json 2> $OUT/trace.log || { echo "trace failed"; tail -5 $OUT/trace.log; exit 2; }
 B="$R/bench.py --steps 5 --warmup 1 --no-cpu --no-config5"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace.log; exit 2; }
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE GRBM_GUI_ACTIVE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
@@ -23,8 +29,10 @@ cd $R
 W=kde_acquisition_d32_24c8u_obs10000_cand1000000
 T=$(ls $OUT/trace/*kernel_trace.csv | head -1)
 python3 tools/pmc_summary.py $OUT --kernel kde_logpdf_h --traffic-out $OUT/pmc_traffic.json --workload $W --trace $T > $OUT/pmc_summary.txt || exit 4
-python3 tools/ksteady.py $(ls $OUT/trace/*kernel_trace.csv | head -1) > $OUT/kernel_steady.txt || exit 5
+python3 tools/ksteady.py $T --skip 3 > $OUT/kernel_steady.txt || exit 5
+python3 tools/trace_vs_line.py $T $OUT/bench_traced.json > $OUT/trace_vs_line.txt || exit 6
 cp $(ls $OUT/trace/*kernel_stats.csv | head -1) $OUT/kernel_stats.csv
 rm -rf $OUT/pmc[0-9]/ $OUT/trace/*kernel_trace.csv
-head -5 $OUT/kernel_steady.txt
+head -8 $OUT/kernel_steady.txt
+cat $OUT/trace_vs_line.txt
 echo profile done
