@@ -173,7 +173,7 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
 def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     """Secondary line: BASELINE config #5, batched successive-halving promotion (eta=3 -> k=333) over
     B brackets x n configs (fp64 losses resident in HBM) plus one batched KDE refit of every bracket
-    (D=8 continuous).  Brackets are independent: with N ranks each promotes its own B/N brackets (no
+    (D = 32: 24 continuous + 8 categorical, bandwidths and level counts).  Brackets are independent: with N ranks each promotes its own B/N brackets (no
     collective; weak scaling of the bracket count per GPU is not applied -- the total stays B).
     Algorithmic HBM bytes per promoted config: 8 (loss read) + 1 (mask written)."""
     import torch
@@ -190,10 +190,15 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     adv = torch.empty(Bl * n, dtype=torch.uint8, device=device)
     nadv = torch.empty(Bl, dtype=torch.int64, device=device)
     sh = N.stream_handle(None, device)
+    # numpy's tie order (the drop-in's): the selection flags brackets whose ties straddle k, a re-rank
+    # kernel follows (a pool of 64 workgroups, exiting at once when none is flagged)
+    sb = int(L.hbx_sh_promote_scratch_bytes(Bl, n, Bl * n, 0, N.ORDER_NUMPY))
+    scr = torch.empty(sb, dtype=torch.uint8, device=device)
+    kev = kde.ScoreEvents()  # stamped at the selection kernel's start and end (hipExtLaunchKernel)
 
-    def promote():  # mask only (what process_results needs): the O(n) select kernel, no order, no scratch
-        N.check(L.hbx_sh_promote(N.ptr(losses), N.ptr(seg), Bl, n, Bl * n, N.ptr(k), None, N.ptr(adv),
-                                 N.ptr(nadv), None, 0, sh))
+    def promote(ev=None):  # mask only (what process_results needs): the O(n) select kernel
+        N.check(L.hbx_sh_promote_ex(N.ptr(losses), N.ptr(seg), Bl, n, Bl * n, N.ptr(k), None, N.ptr(adv),
+                                    N.ptr(nadv), N.ptr(scr), sb, N.ORDER_NUMPY, ev, sh))
     promote()
     torch.cuda.synchronize()
     if dist is not None:
@@ -206,15 +211,29 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     e1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1) / reps
+    ms_call = e0.elapsed_time(e1) / reps
+    kms = []
+    for _ in range(reps):  # the selection kernel alone, what rocprof's kernel trace shows
+        promote(kev.address)
+        torch.cuda.synchronize()
+        kms.append(kev.elapsed_ms(True)[0])
+    ms = float(np.median(kms))
     ok = bool((nadv == n // 3).all().item())
     if dist is not None:
         t = torch.tensor([wall, ms, 0.0 if ok else 1.0], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, ms, ok = float(t[0]), float(t[1]), float(t[2]) == 0.0
-    # batched refit of every bracket's KDE pair (argsort + normal-reference bandwidths), D = 8
-    D = 8
-    X = torch.from_numpy(np.random.RandomState(4).rand(Bl * n, D)).to(device)
+    # batched refit of every bracket's KDE pair at config #3's dims ("plus per-bracket fit on
+    # D=32"): numpy-order argsort of each bracket's losses, good = head / bad = tail, normal-reference
+    # bandwidths (np.std bit for bit) and observed level counts of 24 continuous + 8 categorical dims.
+    # Observations drawn on the device (1e7 x 32 f64 = 2.56 GB resident)
+    dc, du, lev = 24, 8, 4
+    D = dc + du
+    g = torch.Generator(device=device)
+    g.manual_seed(4 + rank)
+    X = torch.empty((Bl * n, D), dtype=torch.float64, device=device)
+    X[:, :dc] = torch.rand((Bl * n, dc), dtype=torch.float64, device=device, generator=g)
+    X[:, dc:] = torch.randint(0, lev, (Bl * n, du), device=device, generator=g).to(torch.float64)
     order = torch.empty(Bl * n, dtype=torch.int64, device=device)
     sb = int(L.hbx_sort_scratch_bytes(Bl * n))
     scr = torch.empty(sb, dtype=torch.uint8, device=device)
@@ -223,14 +242,15 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     nbd = torch.full((Bl,), nb, dtype=torch.int64, device=device)
     fg = torch.full((Bl,), kde.bandwidth_factor(ng, D), dtype=torch.float64, device=device)
     fb = torch.full((Bl,), kde.bandwidth_factor(nb, D), dtype=torch.float64, device=device)
-    vt = torch.zeros(D, dtype=torch.int32, device=device)
+    vt = torch.tensor([0] * dc + [1] * du, dtype=torch.int32, device=device)
     bwg = torch.empty((Bl, D), dtype=torch.float64, device=device)
     bwb = torch.empty((Bl, D), dtype=torch.float64, device=device)
     nlg = torch.empty((Bl, D), dtype=torch.int32, device=device)
     nlb = torch.empty((Bl, D), dtype=torch.int32, device=device)
 
     def refit():
-        N.check(L.hbx_seg_argsort(N.ptr(losses), N.ptr(seg), Bl, n, Bl * n, N.ptr(order), N.ptr(scr), sb, sh))
+        N.check(L.hbx_seg_argsort_ex(N.ptr(losses), N.ptr(seg), Bl, n, Bl * n, N.ptr(order), N.ptr(scr), sb,
+                                     N.ORDER_NUMPY, sh))
         N.check(L.hbx_kde_fit(N.ptr(X), D, N.ptr(seg), Bl, N.ptr(order), N.ptr(ngd), N.ptr(nbd), N.ptr(fg),
                               N.ptr(fb), N.ptr(vt), N.ptr(bwg), N.ptr(bwb), N.ptr(nlg), N.ptr(nlb), sh))
     refit()
@@ -241,6 +261,18 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     e1.record()
     torch.cuda.synchronize()
     ms_fit = e0.elapsed_time(e1) / reps
+    # spot check against the host restatement (oracle-free: numpy's order restated in this module's
+    # tests; here the tie-free losses make any argsort numpy's)
+    b = Bl // 2
+    rows = np.argsort(S.make_bracket_losses(B, n)[b0 + b], kind="stable")
+    Xb = X[b * n:(b + 1) * n].cpu().numpy()
+    bw_ok = bool(np.array_equal(bwg[b].cpu().numpy(), 1.06 * np.std(Xb[rows[:ng]], axis=0) * ng ** (-1. / (4 + D))))
+    # algorithmic HBM bytes: losses read (8) and the order written and read (16) per config, each KDE's rows
+    # read twice (mean pass, deviation pass) through the order: 2 (ng + nb) D 8 per bracket
+    fit_bytes = Bl * (24 * n + 2 * (ng + nb) * D * 8)
+    fit_gbs = fit_bytes / (ms_fit * 1e-3) / 1e9
+    del X
+    torch.cuda.empty_cache()
     gbs = Bl * n * 9 / (ms * 1e-3) / 1e9
     # the reference rule on the host (HB_iteration.py:180-182: argsort(argsort(losses)) < k per bracket),
     # a bracket subsample, x B
@@ -252,9 +284,16 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     cpu_s = (time.perf_counter() - t0) / nb_cpu * B
     out = {"workload": "sh_promotion_B%d_n%d_eta3" % (B, n), "brackets_per_rank": Bl, "ranks": world,
            "configs_per_s": B * n / (wall / reps), "ms_per_launch": ms, "masks_ok": ok,
+           "ms_per_call": ms_call, "tie_order": "numpy",
+           "timing": "ms_per_launch: median of the selection kernel's start/end stamps (hipExtLaunchKernel); "
+                     "ms_per_call: events around back-to-back calls (selection + numpy-order re-rank launch)",
            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
                         "bytes_per_config": 9, "kernel": "sh_select_kernel"},
-           "refit_all_brackets_ms": ms_fit, "refit_dims": D,
+           "refit_all_brackets_ms": ms_fit, "refit_dims": "%dc+%du (L=%d)" % (dc, du, lev),
+           "refit_bandwidths_spot_check": bw_ok,
+           "refit_roofline": {"bound": "hbm", "achieved": fit_gbs, "peak": 8000.0, "unit": "GB/s",
+                              "frac": fit_gbs / 8000.0, "bytes": fit_bytes,
+                              "basis": "losses 8 + order 16 per config, + 2 (n_good + n_bad) D 8 per bracket"},
            "cpu_reference_rule": {"s_for_all_brackets": cpu_s, "cores": 1,
                                   "sample": "%d brackets of numpy argsort(argsort) < k, x %d" % (nb_cpu, B)}}
     return out
@@ -434,6 +473,64 @@ def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
             "candidates_per_call": per_call, "records_identical": same,
             "ms_sequential": res["sequential"] * 1e3, "ms_batched": res["batched"] * 1e3,
             "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
+
+
+def sh_stage_line(device, n_obs=400, stage=81, reps=3):
+    """Side measurement (SURVEY 8f row 1 through the drop-in): the first stage of an eta=3 bracket -- 81
+    configurations requested through SuccessiveHalving.get_next_run, as HpBandSter.run requests them --
+    from BOHB (config #3's dims, 24c + 8u, GPU sampler, num_samples=64) with speculative batching (one
+    hbx_kde_acquire_batch pass) against one get_config per request; the proposals must be identical."""
+    import torch
+    from hpbandster_amd import configspace as CS
+    from hpbandster_amd.config_generators import BOHB
+    from hpbandster_amd.HB_iteration import SuccessiveHalving
+    from hpbandster_amd import synthetic as S
+
+    def make():
+        space = CS.ConfigurationSpace(seed=3)
+        for i in range(24):
+            space.add_hyperparameter(CS.UniformFloatHyperparameter("x%02d" % i, lower=0, upper=1))
+        for i in range(8):
+            space.add_hyperparameter(CS.CategoricalHyperparameter("y%02d" % i, ["a", "b", "c", "d"]))
+        cg = BOHB(space, device=device, sampler="gpu", sampler_seed=77)
+        X = S.make_observations(n_obs, 24, 8, 4, seed=51)
+        Lo = S.make_losses(n_obs, seed=52)
+
+        class Job(object):
+            pass
+        for i in range(n_obs):
+            j = Job()
+            j.id, j.exception, j.timestamps = (0, 0, i), None, {}
+            j.kwargs = {"config": CS.Configuration(space, vector=X[i]).get_dictionary(), "budget": 1.0}
+            j.result = {"loss": float(Lo[i]), "info": None}
+            cg.new_result(j)
+        return cg, space
+
+    def run(batch):
+        cg, space = make()
+        np.random.seed(5)
+        space.seed(6)
+        sh = SuccessiveHalving(0, [stage, stage // 3, stage // 9, 3, 1], [1.0, 3.0, 9.0, 27.0, 81.0], cg.get_config,
+                               device=device, batch_sampling=batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cfgs = [sh.get_next_run()[1] for _ in range(stage)]
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, cfgs
+
+    res = {}
+    for batch in (False, True):
+        ts, cfgs = [], None
+        for _ in range(reps):
+            t, c = run(batch)
+            ts.append(t)
+            cfgs = c
+        res[batch] = (min(ts), cfgs)
+    return {"workload": "sh_stage_%d_get_next_run_d32_obs%d" % (stage, n_obs),
+            "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
+            "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],
+            "note": "SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
+                    "batched = one speculative get_config_batch_spec" % stage}
 
 
 def config2_line(device, reps=50):
@@ -787,6 +884,10 @@ def main():
             out["batched_acquisition"] = batched(pair, device, a.dc, a.du, a.levels)
         except Exception as e:
             out["batched_acquisition"] = {"error": repr(e)}
+        try:
+            out["sh_stage"] = sh_stage_line(device)
+        except Exception as e:
+            out["sh_stage"] = {"error": repr(e)}
         try:
             out["gpu_sampler"] = sampler_line(pair, device, a.dc, a.du, a.levels, Nc, ws)
         except Exception as e:

@@ -14,7 +14,7 @@ from . import promote
 class SuccessiveHalving(object):
     """One Hyperband bracket (reference HB_iteration.py:7-198)."""
 
-    def __init__(self, iter_number, num_configs, budgets, config_sampler, device=None):
+    def __init__(self, iter_number, num_configs, budgets, config_sampler, device=None, batch_sampling=True):
         self.data = {}
         self.is_finished = False
         self.HB_iter = iter_number
@@ -25,10 +25,34 @@ class SuccessiveHalving(object):
         self.config_sampler = config_sampler
         self.num_running = 0
         self.device = device
+        # a stage's configurations requested back to back come from ONE batched acquisition
+        # when the sampler's generator offers get_config_batch_spec (BOHB); each is used only while it is
+        # exactly the sequential call's result (same model, same RNG states), else sampled afresh
+        self.batch_sampling = batch_sampling
+        self._spec = None
+        self._batch_cap = None  # after a batch was cut short at m results: batches of m
+
+    def _sample(self, budget):
+        gen = getattr(self.config_sampler, "__self__", None)
+        spec_fn = getattr(gen, "get_config_batch_spec", None) if self.batch_sampling else None
+        if spec_fn is None or getattr(self.config_sampler, "__name__", "") != "get_config":
+            return self.config_sampler(budget)
+        if self._spec is not None:
+            if self._spec.valid():
+                return self._spec.pop()
+            if self._spec.served < len(self._spec.out):  # cut short: results arrive between requests
+                self._batch_cap = max(1, self._spec.served)
+            self._spec = None
+        remaining = self.num_configs[self.SH_iter] - self.actual_num_configs[self.SH_iter]
+        size = remaining if self._batch_cap is None else min(remaining, self._batch_cap)
+        if size <= 1:
+            return self.config_sampler(budget)
+        self._spec = spec_fn(budget, size)
+        return self._spec.pop()
 
     def add_configuration(self, config=None, config_info={}):
         if config is None:
-            config, config_info = self.config_sampler(self.budgets[self.SH_iter])
+            config, config_info = self._sample(self.budgets[self.SH_iter])
         if self.is_finished:
             raise RuntimeError("This HB iteration is finished, you can't  add more results!")
         if self.actual_num_configs[self.SH_iter] == self.num_configs[self.SH_iter]:

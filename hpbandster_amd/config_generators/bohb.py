@@ -26,6 +26,48 @@ from .base import base_config_generator
 from ._cs import ConfigSpace
 
 
+def _rng_snapshot(gen):
+    return (np.random.get_state(), gen.configspace.random.get_state(), gen._sample_counter)
+
+
+def _rng_same(a, b):
+    """Two snapshots of (global RNG, configspace RNG, GPU sampler counter) equal."""
+    for x, y in ((a[0], b[0]), (a[1], b[1])):
+        if x[0] != y[0] or x[2:] != y[2:] or not np.array_equal(x[1], y[1]):
+            return False
+    return a[2] == b[2]
+
+
+def _rng_set(gen, snap):
+    np.random.set_state(snap[0])
+    gen.configspace.random.set_state(snap[1])
+    gen._sample_counter = snap[2]
+
+
+class SpeculativeBatch(object):
+    """get_config results computed ahead in one batched acquisition (BOHB.get_config_batch_spec)."""
+
+    def __init__(self, gen, out, before, after, version):
+        self.gen, self.out, self.after, self.version = gen, out, after, version
+        self.served = 0
+        _rng_set(gen, before)  # nothing consumed yet: pop() moves the RNGs call by call
+
+    def valid(self):
+        """The next result is exactly the sequential call's: same model, RNGs where the last call left them."""
+        g = self.gen
+        if self.served >= len(self.out) or g._model_version != self.version:
+            return False
+        if self.served == 0:
+            return True
+        return _rng_same(_rng_snapshot(g), self.after[self.served - 1])
+
+    def pop(self):
+        r = self.out[self.served]
+        _rng_set(self.gen, self.after[self.served])
+        self.served += 1
+        return r
+
+
 class BOHB(base_config_generator):
     def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
                  random_fraction=1 / 3, bandwidth_factor=3, device=None, sampler="host", sampler_seed=None,
@@ -77,6 +119,7 @@ class BOHB(base_config_generator):
         self.good_config_rankings = dict()
         self.kde_models = dict()
         self._stores = dict()  # budget -> ObservationStore: the budget's rows resident in HBM
+        self._model_version = 0  # bumped whenever kde_models changes (speculative batches check it)
 
     # -- candidates ---------------------------------------------------------------------------
     def sample_candidates(self, kde_good, num_samples):
@@ -144,7 +187,20 @@ class BOHB(base_config_generator):
                 info_dict['model_based_pick'] = False
         return sample, info_dict
 
-    def get_config_batch(self, budget, k):
+    def get_config_batch_spec(self, budget, k):
+        """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass), handed out one at a
+        time by the returned SpeculativeBatch -- each only while it is exactly what the sequential call
+        would return at that moment: the model unchanged (no refit since, ``_model_version``) and every
+        RNG the calls consume (numpy's global one, the configspace's, the GPU sampler's counter) in the
+        state the previous call left.  The RNGs are rewound to the state after call 1 at once, so
+        anything else drawing in between (a worker, another generator) sees the sequential stream."""
+        before = _rng_snapshot(self)
+        after = []
+        out = self.get_config_batch(budget, k, _snapshots=after)
+        spec = SpeculativeBatch(self, out, before, after, self._model_version)
+        return spec
+
+    def get_config_batch(self, budget, k, _snapshots=None):
         """``[self.get_config(budget) for _ in range(k)]`` with one GPU pass for all model-based calls.
 
         Valid while no result arrives in between (the model is fixed): an SH stage's first
@@ -156,7 +212,11 @@ class BOHB(base_config_generator):
         plan = []  # per call: None (random pick) or the row offset of its candidates
         blocks = []
         pair = None
+        g_after = []  # numpy's global RNG state after each call's draws (speculative batches)
+        counter0 = self._sample_counter
         for _ in range(int(k)):
+            if _snapshots is not None and plan:
+                g_after.append(np.random.get_state())
             if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
                 plan.append(None)
                 continue
@@ -176,6 +236,8 @@ class BOHB(base_config_generator):
                 continue
             plan.append(len(blocks) * self.num_samples)
             blocks.append(block)
+        if _snapshots is not None and plan:
+            g_after.append(np.random.get_state())
         results, bad = [], None
         if blocks:
             if self.sampler == "gpu":  # one draw for all calls: same Philox counters as call by call
@@ -185,7 +247,13 @@ class BOHB(base_config_generator):
                 cands = np.concatenate(blocks, axis=0)
             results = pair.acquire_batch(cands, self.num_samples)
         out = []
-        for off in plan:
+        nmodel = 0
+        for i, off in enumerate(plan):
+            if _snapshots is not None and i > 0:  # call i-1 is complete: every RNG's state after it
+                _snapshots.append((g_after[i - 1], self.configspace.random.get_state(),
+                                   counter0 + nmodel * self.num_samples))
+            if off is not None:
+                nmodel += 1
             if off is None:
                 out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
                 continue
@@ -204,6 +272,9 @@ class BOHB(base_config_generator):
                     vec = vec.cpu().numpy()
                 out.append((ConfigSpace.Configuration(self.configspace, vector=vec).get_dictionary(),
                             {'model_based_pick': True}))
+        if _snapshots is not None and plan:
+            _snapshots.append((g_after[-1], self.configspace.random.get_state(),
+                               counter0 + nmodel * self.num_samples))
         return out
 
     # -- observations ---------------------------------------------------------------------------
@@ -235,6 +306,7 @@ class BOHB(base_config_generator):
         if pair is None:  # bohb.py:234-237: too few rows for a KDE
             return
         self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
+        self._model_version += 1
         self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
                           'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,
                                                        np.min(store.losses_host)))

@@ -207,6 +207,29 @@ __global__ __launch_bounds__(256) void seg_tie_flag_kernel(const double* __restr
   if (__ballot(tie) && lane == 0) list[atomicAdd(count, 1)] = (int32_t)b;
 }
 
+// Few segments (a single refit's split): one thread per adjacent pair of the sorted order over a 2-D
+// grid (pair chunks x segments) -- one wave per segment would walk 1e4 dependent gathers in a row; the
+// first block to see a tie in segment b claims flags[b] and appends b (flags: B <= 15 ints, zeroed)
+__global__ __launch_bounds__(256) void seg_tie_flag_wide_kernel(const double* __restrict__ loss,
+                                                                const int64_t* __restrict__ seg_off,
+                                                                const int64_t* __restrict__ order,
+                                                                int32_t* __restrict__ flags,
+                                                                int32_t* __restrict__ list,
+                                                                int32_t* __restrict__ count) {
+  const int64_t b = blockIdx.y;
+  const int64_t s = seg_off[b];
+  const int n = (int)(seg_off[b + 1] - s);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool tie = false;
+  if (i + 1 < n) tie = key_argsort(loss[s + order[s + i]]) == key_argsort(loss[s + order[s + i + 1]]);
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  if (__ballot(tie) && (threadIdx.x & 63) == 0) any = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && any && atomicCAS(flags + b, 0, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)b;
+}
+
 // The flagged segments, one workgroup each (grid-stride over the list): A[0, m) = the positions to
 // rank -- every position (argsort), or the finite losses' in position order (promotion) -- sorted in
 // numpy's order.  Scratch arrays A/T/W/Lst are indexed by the segment's offset (slot_stride == 0) or
@@ -230,9 +253,10 @@ __global__ __launch_bounds__(NPS_THREADS) void seg_np_order_kernel(
 // arrays: int32 [A | T | W | Lst], `slots` entries each -- slot_stride 0: indexed by segment offset
 // (slots = N), else a pool of slots / slot_stride blocks; cnt_list: int32 [16] counter + the list (<= B)
 // (flagged: the list is filled already -- sh_select_kernel flags its tie-straddling brackets itself)
-int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, const int64_t* order_in, const double* k,
-                     int promote, int want_order, int64_t* order_out, uint8_t* advance, int32_t* arrays,
-                     int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged, hipStream_t s) {
+int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, const int64_t* order_in,
+                     const double* k, int promote, int want_order, int64_t* order_out, uint8_t* advance,
+                     int32_t* arrays, int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged,
+                     hipStream_t s) {
   int32_t* A = arrays;
   int32_t* T = A + slots;
   int32_t* W = T + slots;
@@ -240,9 +264,16 @@ int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, cons
   int32_t* cnt = cnt_list;
   int32_t* list = cnt_list + 16;
   if (!flagged) {
-    HBX_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
-    hipLaunchKernelGGL(seg_tie_flag_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, loss, seg_off, B, order_in,
-                       k, promote, want_order, list, cnt);
+    // argsort mode, a few segments: the wide kernel (its per-segment claim flags sit in cnt_list[1..])
+    const bool wide = !promote && B <= 15 && max_seg > 256;
+    HBX_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (wide ? 16 : 1), s));
+    if (wide) {
+      hipLaunchKernelGGL(seg_tie_flag_wide_kernel, dim3((unsigned)((max_seg + 255) / 256), (unsigned)B), dim3(256), 0,
+                         s, loss, seg_off, order_in, cnt + 1, list, cnt);
+    } else {
+      hipLaunchKernelGGL(seg_tie_flag_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, loss, seg_off, B,
+                         order_in, k, promote, want_order, list, cnt);
+    }
     HBX_LAUNCH_CHECK();
   }
   const int64_t nblk = slot_stride ? slots / slot_stride : (B < 1024 ? B : 1024);
@@ -474,8 +505,8 @@ int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, in
   int rc = seg_argsort_stable(loss, seg_off, B, max_seg, N, order, scratch, scratch_bytes, stream);
   if (rc || order_mode == HBX_ORDER_STABLE || B <= 0 || N < 2) return rc;
   int32_t* arrays = (int32_t*)scratch;
-  return hbx_np_order_fix(loss, seg_off, B, order, nullptr, 0, 1, order, nullptr, arrays, N, 0, arrays + 4 * N, false,
-                          (hipStream_t)stream);
+  return hbx_np_order_fix(loss, seg_off, B, max_seg, order, nullptr, 0, 1, order, nullptr, arrays, N, 0, arrays + 4 * N,
+                          false, (hipStream_t)stream);
 }
 
 static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,

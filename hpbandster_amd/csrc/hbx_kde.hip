@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "hbx_common.h"
+#include <hip/hip_ext.h>
 #include "hbx_kde_impl.h"
 
 // ------------------------------------------------------------------------------------------
@@ -1064,16 +1065,24 @@ __global__ __launch_bounds__(256) void kde_exact_combine_kernel(const KdeParams*
 }
 
 // exact fp64 pdf of one KDE at every row of pts (grid-stride over points, one block per point)
+// list (nullable): only the points list[0 .. *count), written at their own index; take_log: ln of the
+// pdf, and only for KDEs the fp64 log-space kernel does not cover (negative factors, structural NaN)
 __global__ __launch_bounds__(EXACT_THREADS) void kde_pdf_exact_kernel(const double* __restrict__ pts, int64_t Np,
                                                                       int32_t D, const KdeParams* __restrict__ P,
                                                                       const double* __restrict__ X,
                                                                       const int64_t* __restrict__ rows,
-                                                                      double* __restrict__ out) {
+                                                                      double* __restrict__ out,
+                                                                      const int32_t* __restrict__ list,
+                                                                      const int32_t* __restrict__ count,
+                                                                      int take_log) {
   __shared__ ExactShared sh;
-  for (int64_t p = blockIdx.x; p < Np; p += gridDim.x) {
-    exact_setup(P, D, pts + p * D, &sh);
+  if (take_log && !(P->has_neg || P->nan_all || P->nconst)) return;
+  const int64_t np = list ? (int64_t)*count : Np;
+  for (int64_t p = blockIdx.x; p < np; p += gridDim.x) {
+    const int64_t q = list ? (int64_t)list[p] : p;
+    exact_setup(P, D, pts + q * D, &sh);
     const double v = exact_pdf(X, D, rows, P, &sh);
-    if (threadIdx.x == 0) out[p] = v;
+    if (threadIdx.x == 0) out[q] = take_log ? log(v) : v;
     __syncthreads();
   }
 }
@@ -1089,13 +1098,17 @@ __global__ __launch_bounds__(256) void kde_logpdf_exact_kernel(const double* __r
                                                               const KdeParams* __restrict__ P,
                                                               const double* __restrict__ X,
                                                               const int64_t* __restrict__ rows,
-                                                              double* __restrict__ out) {
+                                                              double* __restrict__ out,
+                                                              const int32_t* __restrict__ list,
+                                                              const int32_t* __restrict__ count) {
   __shared__ double c0[HBX_MAX_D], c1[HBX_MAX_D], xd[HBX_MAX_D];
   __shared__ int32_t cont[HBX_MAX_D];
   __shared__ double rm[4], rs[4];
   __shared__ double lconst;
   const int n = P->n;
-  for (int64_t p = blockIdx.x; p < Np; p += gridDim.x) {
+  const int64_t np = list ? (int64_t)*count : Np;  // list: only those points, written at their own index
+  for (int64_t pi = blockIdx.x; pi < np; pi += gridDim.x) {
+    const int64_t p = list ? (int64_t)list[pi] : pi;
     const double* x = pts + p * D;
     for (int d = threadIdx.x; d < D; d += blockDim.x) {
       const double h = P->bw[d];
@@ -1510,20 +1523,23 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
                          int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s) {
-  if (ev) HBX_HIP(hipEventRecord(ev[0], s));
-  if (f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled()) {
+  const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
+  if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
+  if (pair) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
     KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt};
-    hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
+    if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
+      hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
+    else
+      hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
     // the rescue pass: grid-stride, exits at once unless the scoring kernel counted a marker
     const unsigned grr = rescue_cnt ? (2 * gr < 1024u ? 2 * gr : 1024u) : 2 * gr;
     hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
-    if (ev) HBX_HIP(hipEventRecord(ev[1], s));
     return HBX_OK;
   }
   int rc = launch_score(f0, cand, Nc, D, params0, table0, est0, s);
@@ -1944,7 +1960,7 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
   hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(EXACT_THREADS), 0, (hipStream_t)stream, pts, Np, D,
-                     (const KdeParams*)params, X, rows, out);
+                     (const KdeParams*)params, X, rows, out, (const int32_t*)nullptr, (const int32_t*)nullptr, 0);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
@@ -1958,7 +1974,74 @@ int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* p
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
   hipLaunchKernelGGL(kde_logpdf_exact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, pts, Np, D,
-                     (const KdeParams*)params, X, rows, out);
+                     (const KdeParams*)params, X, rows, out, (const int32_t*)nullptr, (const int32_t*)nullptr);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+}  // extern "C"
+
+// ln pdf within rtol * max(1, |ln p|) of the reference's (the north-star contract), per candidate: the
+// fp32 estimate where its rigorous bound guarantees it, else queued for an fp64 evaluation
+__global__ __launch_bounds__(256) void kde_logpdf_classify_kernel(const KdeEst* __restrict__ est, int64_t Nc,
+                                                                 double rtol, int exact_all, double* __restrict__ out,
+                                                                 int32_t* __restrict__ list,
+                                                                 int32_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= Nc) return;
+  bool ok = false;
+  if (!exact_all) {
+    const KdeEst e = est[i];
+    const double lp = e.lpos, ln = e.lneg, er = e.err;
+    const double m = fmax(lp, ln);
+    const double a = exp(lp - m), b = exp(ln - m), S = a - b;
+    const double pt = S > 0.0 ? m + log(S) : -INFINITY;
+    const double rel = er * (a + b) / S;  // relative bound of the sum: |ln S_est - ln S| <= -ln(1 - rel)
+    const double bound = -log1p(-fmin(rel, 0.5)) + 4e-7 * fmax(1.0, fabs(m));  // + fp32 rounding of the logs
+    ok = pt - pt == 0.0 && er >= 0.0 && rel < 0.5 && bound <= 0.5 * rtol * fmax(1.0, fabs(pt));
+    if (ok) out[i] = pt;
+  }
+  if (!ok) list[atomicAdd(count, 1)] = (int32_t)i;
+}
+
+extern "C" {
+
+int64_t hbx_kde_logpdf_rtol_scratch_bytes(int64_t Nc) { return 16 * Nc + 4 * Nc + 256; }
+
+int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
+                        const double* X, const int64_t* rows, int32_t dc_pad, int32_t du_pad, int32_t variant,
+                        double rtol, double* out, void* scratch, int64_t scratch_bytes, void* stream) {
+  if ((!cand || !out) && Nc > 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: null pointer");
+  if (!params || !X || !rows || !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: null pointer");
+  if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: D=%d", D);
+  if (!(rtol > 0.0)) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: rtol %g", rtol);
+  if (scratch_bytes < hbx_kde_logpdf_rtol_scratch_bytes(Nc)) return hbx_fail(HBX_ERR_ARG, "logpdf scratch too small");
+  if (Nc <= 0) return HBX_OK;
+  hipStream_t s = (hipStream_t)stream;
+  char* sc = (char*)scratch;
+  int32_t* count = (int32_t*)sc;
+  KdeEst* est = (KdeEst*)(sc + 256);
+  int32_t* list = (int32_t*)(sc + 256 + 16 * Nc);
+  const bool exact_only = (variant >> 5) & 1;
+  if (!exact_only) {  // the estimate (the precise instance: hbx_kde_logpdf's)
+    if (!table) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: null table");
+    ScoreFns f = pick_logpdf(dc_pad, du_pad, variant);
+    if (!f.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
+    const int rc = launch_score(f, cand, Nc, D, params, table, est, s);
+    if (rc) return rc;
+  }
+  HBX_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), s));
+  hipLaunchKernelGGL(kde_logpdf_classify_kernel, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, est, Nc, rtol,
+                     exact_only ? 1 : 0, out, list, count);
+  HBX_LAUNCH_CHECK();
+  const unsigned grid = (unsigned)(Nc < EXACT_GRID ? Nc : EXACT_GRID);
+  // the rest in fp64: log space (positive factors) ...
+  hipLaunchKernelGGL(kde_logpdf_exact_kernel, dim3(grid), dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params, X,
+                     rows, out, list, count);
+  HBX_LAUNCH_CHECK();
+  // ... or ln of the exact pdf (negative categorical factors, structural NaN: every block exits otherwise)
+  hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(EXACT_THREADS), 0, s, cand, Nc, D,
+                     (const KdeParams*)params, X, rows, out, list, count, 1);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }

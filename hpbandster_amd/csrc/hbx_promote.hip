@@ -11,13 +11,15 @@
 // drop-in uses -- as numpy 1.26.4's unstable argsort ranks them (hbx_npsort.h): brackets whose tied
 // losses straddle the k-th place are re-ranked on the device in numpy's order.
 #include "hbx_common.h"
+#include <hip/hip_ext.h>
 #include "hbx_npsort.h"
 #include "hbx_sort.h"
 #include <stdlib.h>
 
-int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, const int64_t* order_in, const double* k,
-                     int promote, int want_order, int64_t* order_out, uint8_t* advance, int32_t* arrays,
-                     int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged, hipStream_t s);
+int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, const int64_t* order_in,
+                     const double* k, int promote, int want_order, int64_t* order_out, uint8_t* advance,
+                     int32_t* arrays, int64_t slots, int64_t slot_stride, int32_t* cnt_list, bool flagged,
+                     hipStream_t s);
 #define NPS_POOL 64  // workgroups (scratch slots) re-ranking flagged brackets after the selection
 
 __global__ __launch_bounds__(256) void sh_promote_kernel(const double* __restrict__ loss,
@@ -327,7 +329,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
 // host memory (no copies).
 __global__ __launch_bounds__(NPS_THREADS) void sh_promote_one_kernel(const double* __restrict__ loss, int n, double kb,
                                                                      uint8_t* __restrict__ advance, int np_order,
-                                                                     int32_t* __restrict__ scr) {
+                                                                     int32_t* __restrict__ scr, int32_t* done,
+                                                                     int32_t seq) {
   __shared__ double cbuf[128];
   __shared__ int tie_sh;
   const int lane = threadIdx.x & 63;
@@ -337,6 +340,11 @@ __global__ __launch_bounds__(NPS_THREADS) void sh_promote_one_kernel(const doubl
   }
   __syncthreads();
   if (np_order && tie_sh) nps_order_segment(loss, n, 1, kb, scr, scr + n, scr + 2 * n, scr + 3 * n, nullptr, advance);
+  if (done) {  // every mask byte is out (system scope) before the sequence number the host polls for
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 extern "C" {
@@ -358,12 +366,12 @@ int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_
                    const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                    int64_t scratch_bytes, void* stream) {
   return hbx_sh_promote_ex(loss, seg_off, B, max_seg, N, k, order, advance, n_advance, scratch, scratch_bytes,
-                           HBX_ORDER_STABLE, stream);
+                           HBX_ORDER_STABLE, nullptr, stream);
 }
 
 int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                       const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
-                      int64_t scratch_bytes, int32_t order_mode, void* stream) {
+                      int64_t scratch_bytes, int32_t order_mode, void* events, void* stream) {
   if (!loss || !seg_off || !k || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
   if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
     return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_ex: order_mode %d", order_mode);
@@ -380,12 +388,17 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
     const int64_t slots = (int64_t)NPS_POOL * max_seg;
     int32_t* cnt_list = np ? pool + 4 * slots : nullptr;
     if (np) HBX_HIP(hipMemsetAsync(cnt_list, 0, sizeof(int32_t), st));
-    hipLaunchKernelGGL(sh_select_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, loss, seg_off, B, k, advance,
-                       n_advance, np ? cnt_list + 16 : (int32_t*)nullptr, cnt_list);
+    hipEvent_t* ev = (hipEvent_t*)events;  // optional: stamped at the selection kernel's start and end
+    if (ev)
+      hipExtLaunchKernelGGL(sh_select_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, ev[0], ev[1], 0, loss,
+                            seg_off, B, k, advance, n_advance, np ? cnt_list + 16 : (int32_t*)nullptr, cnt_list);
+    else
+      hipLaunchKernelGGL(sh_select_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, loss, seg_off, B, k,
+                         advance, n_advance, np ? cnt_list + 16 : (int32_t*)nullptr, cnt_list);
     HBX_LAUNCH_CHECK();
     if (!np) return HBX_OK;
-    return hbx_np_order_fix(loss, seg_off, B, nullptr, k, 1, 0, nullptr, advance, pool, slots, max_seg, cnt_list, true,
-                            st);
+    return hbx_np_order_fix(loss, seg_off, B, max_seg, nullptr, k, 1, 0, nullptr, advance, pool, slots, max_seg,
+                            cnt_list, true, st);
   }
   char* sc = (char*)scratch;
   uint64_t* gk = (uint64_t*)sc;
@@ -407,20 +420,19 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
   if (!np || N < 2) return HBX_OK;
   // the sort's key / position arrays are free again: [A | T | W | Lst] over the first 16 N bytes (indexed
   // by bracket offset; the order stays at 24 N), the flagged list after the sort scratch
-  return hbx_np_order_fix(loss, seg_off, B, ord, k, 1, want_order ? 1 : 0, order, advance, (int32_t*)sc, N, 0,
+  return hbx_np_order_fix(loss, seg_off, B, max_seg, ord, k, 1, want_order ? 1 : 0, order, advance, (int32_t*)sc, N, 0,
                           (int32_t*)(sc + hbx_sort_scratch_bytes(N)), false, st);
 }
 
 // One bracket, one launch (sh_promote_one_kernel): loss / advance device or mapped host pointers,
 // n <= 1024, k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY only, else NULL).
 int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
-                       void* stream) {
+                       int32_t* done, int32_t seq, void* stream) {
   if (!loss || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: null pointer");
   if (n < 0 || n > 64 * PW_PER_LANE) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: n=%lld", (long long)n);
   if (order_mode == HBX_ORDER_NUMPY && !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: scratch");
-  if (n == 0) return HBX_OK;
   hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(NPS_THREADS), 0, (hipStream_t)stream, loss, (int)n, k, advance,
-                     order_mode == HBX_ORDER_NUMPY ? 1 : 0, (int32_t*)scratch);
+                     order_mode == HBX_ORDER_NUMPY ? 1 : 0, (int32_t*)scratch, done, seq);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }

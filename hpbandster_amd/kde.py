@@ -238,37 +238,27 @@ class DeviceKDE(object):
         return cands, datum, err
 
     def logpdf(self, cands, rtol=1e-5, stream=None):
-        """ln pdf per candidate within ``rtol * max(1, |ln p|)`` (the north-star contract): the fp32
-        matrix-core estimate wherever its rigorous per-candidate bound guarantees that, an fp64 log-space
-        evaluation for the rest -- candidates whose fp32 expansion cancels large terms (next to outlying
-        observations, beyond D = 32) and exact-only KDEs -- or, for KDEs with negative categorical
-        factors, ln of the exact fp64 pdf.  Returns float64 [Nc]."""
+        """ln pdf per candidate within ``rtol * max(1, |ln p|)`` (the north-star contract), through
+        ``hbx_kde_logpdf_rtol``: the fp32 matrix-core estimate wherever its rigorous per-candidate bound
+        guarantees that, fp64 log space on the device for the rest (candidates whose fp32 expansion
+        cancels large terms -- next to outlying observations, beyond D = 32 -- and exact-only KDEs), ln of
+        the exact fp64 pdf for KDEs with negative categorical factors.  Returns float64 [Nc]."""
         torch = _torch()
+        L = N.lib()
         C = np.ascontiguousarray(np.asarray(cands, dtype=np.float64).reshape(-1, self.k_vars))
         Nc = C.shape[0]
         if Nc == 0:
             return np.zeros(0)
-        if self.exact_only:
-            return self._logpdf_exact(C, stream)
         with N.on_device(self.device, stream):
             c_dev = torch.from_numpy(C).to(self.device)
-        lpos, lneg, err = self.logpdf_est(c_dev, stream)
-        lpos, lneg, err = (np.asarray(v, dtype=np.float64) for v in (lpos, lneg, err))
-        out = np.full(Nc, np.nan)
-        with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
-            m = np.maximum(lpos, lneg)
-            a, b = np.exp(lpos - m), np.exp(lneg - m)
-            S = a - b
-            pt = np.where(S > 0, m + np.log(S), -np.inf)
-            # |ln S_est - ln S| <= -ln(1 - e), e = err (a + b) / S plus the fp32 rounding of the logs
-            e = err * (a + b) / S
-            bound = -np.log1p(-np.minimum(e, 0.5)) + 4e-7 * np.maximum(1.0, np.abs(m))
-        ok = np.isfinite(pt) & (err >= 0) & (e < 0.5) & (bound <= 0.5 * rtol * np.maximum(1.0, np.abs(pt)))
-        out[ok] = pt[ok]
-        redo = np.nonzero(~ok)[0]
-        if redo.size:
-            out[redo] = self._logpdf_exact(C[redo], stream)
-        return out
+            out = torch.empty(Nc, dtype=torch.float64, device=self.device)
+            sb = int(L.hbx_kde_logpdf_rtol_scratch_bytes(Nc))
+            scr = torch.empty(sb, dtype=torch.uint8, device=self.device)
+            N.check(L.hbx_kde_logpdf_rtol(N.ptr(c_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
+                                          N.ptr(self.X_dev), N.ptr(self.rows_dev), self.dc_pad, self.du_pad,
+                                          self.variant, float(rtol), N.ptr(out), N.ptr(scr), sb,
+                                          N.stream_handle(stream, self.device)))
+            return out.cpu().numpy()
 
     def _logpdf_exact(self, C, stream):
         """ln pdf at the rows of C: fp64 log space (hbx_kde_logpdf_exact: no underflow, ~1e-15) where

@@ -52,7 +52,7 @@ def _promote_segments(L, loss, seg_off, k, device, stream, return_order, mode):
     sb = int(L.hbx_sh_promote_scratch_bytes(B, max_seg, Ntot, 1 if return_order else 0, mode))
     scratch = torch.empty(sb, dtype=torch.uint8, device=device) if sb > 0 else None
     N.check(L.hbx_sh_promote_ex(N.ptr(loss_d), N.ptr(seg_d), B, max_seg, Ntot, N.ptr(k_d), N.ptr(order), N.ptr(adv),
-                                N.ptr(nadv), N.ptr(scratch), sb, mode, N.stream_handle(stream, device)))
+                                N.ptr(nadv), N.ptr(scratch), sb, mode, None, N.stream_handle(stream, device)))
     if return_order:
         return adv, order, nadv
     return adv.cpu().numpy().astype(bool)
@@ -61,8 +61,9 @@ def _promote_segments(L, loss, seg_off, k, device, stream, return_order, mode):
 class _Staging(object):
     """Per-thread, per-device buffers of advance_mask: device-mapped coherent host memory for the
     losses (in) and the mask (out) -- the kernel reads and writes them directly, no copies -- and the
-    device scratch of the numpy-order re-rank, grown on demand.  Every call synchronises its stream
-    before returning, so the buffers are free again when the next call of the same thread starts."""
+    device scratch of the numpy-order re-rank, grown on demand.  Every call waits for its kernel's
+    completion word before returning, so the buffers are free again when the next call of the same
+    thread starts."""
 
     def __init__(self, device):
         self.device = device
@@ -77,10 +78,15 @@ class _Staging(object):
             self._release()
             pin, pout = ctypes.c_void_p(), ctypes.c_void_p()
             N.check(L.hbx_host_alloc(8 * cap, ctypes.addressof(pin)))
-            N.check(L.hbx_host_alloc(cap, ctypes.addressof(pout)))
+            N.check(L.hbx_host_alloc(cap + 64, ctypes.addressof(pout)))
             self._ptrs = [pin.value, pout.value]
             self.h_in = np.ctypeslib.as_array((ctypes.c_double * cap).from_address(pin.value))
             self.h_out = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(pout.value))
+            # the completion word the kernel stores last (after the mask, system scope)
+            self.done_addr = pout.value + cap
+            self.done = ctypes.c_int32.from_address(self.done_addr)
+            self.done.value = 0
+            self.seq = 0
             self.scratch = torch.empty(4 * cap, dtype=torch.int32, device=self.device)
             self.cap = cap
         return self
@@ -116,8 +122,8 @@ def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
 
     What SuccessiveHalving.process_results calls once per bracket: the losses are written into
     device-mapped host memory, ONE kernel (hbx_sh_promote_one: the selection, and the numpy-order
-    re-rank when tied losses straddle the k-th place) reads them and writes the mask back there, one
-    stream synchronisation."""
+    re-rank when tied losses straddle the k-th place) reads them and writes the mask back there, and
+    the host polls the kernel's completion word (stored last) instead of synchronising the stream."""
     import torch
     losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
@@ -133,7 +139,15 @@ def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
         st = _staging(device).get(n)
         st.h_in[:n] = losses
         cur = stream if stream is not None else torch.cuda.current_stream(device)
+        st.seq = (st.seq % 0x7ffffffe) + 1
         N.check(L.hbx_sh_promote_one(st._ptrs[0], n, float(k), st._ptrs[1],
-                                     N.ptr(st.scratch) if mode == N.ORDER_NUMPY else None, mode, cur.cuda_stream))
-        cur.synchronize()
+                                     N.ptr(st.scratch) if mode == N.ORDER_NUMPY else None, mode, st.done_addr, st.seq,
+                                     cur.cuda_stream))
+        # the kernel's last store is the sequence number: poll it (a stream synchronisation would wait on
+        # the runtime's completion signal); after a bounded spin, fall back to the synchronisation
+        for _ in range(20000):
+            if st.done.value == st.seq:
+                break
+        else:
+            cur.synchronize()
         return st.h_out[:n].astype(bool)

@@ -132,8 +132,12 @@ int64_t hbx_kde_workspace_bytes(int64_t Nc, int64_t nmax);
 /* One acquisition: l = good KDE, g = bad KDE; selects the first index of the minimum of
  * max(1e-8, g)/max(l, 1e-8) over the candidates, exactly (fp64 re-score of every candidate whose
  * fp32 score interval reaches the minimum).  index_base is added to the reported index (GPU
- * sharding).  logl_out/logg_out: nullable device f32[Nc] (ln pdf estimates within 1e-5 of the
- * reference's; -inf for pdf <= 0, NaN for NaN).  With both NULL the scoring runs the fast instance (the
+ * sharding).  logl_out/logg_out: nullable device f32[Nc]: the fp32 ln pdf point estimates the
+ * selection used (-inf for pdf <= 0, NaN for NaN).  Each lies within its own rigorous bound (what keeps
+ * the selection exact), which is 1e-5 relative at D <= 32 away from outlying observations but NOT in
+ * general (the fp32 expansion -|x'|^2 - |X'|^2 + 2 x'.X' cancels large terms next to outliers and beyond
+ * D = 32); ln pdfs within the north-star 1e-5 everywhere come from hbx_kde_logpdf_rtol.  With both NULL
+ * the scoring runs the fast instance (the
  * one-hot deltas' f16 lo parts moved into the bound: looser estimates, the same exact selection).  The
  * result record lives in the workspace: hbx_kde_result_ptr(workspace).
  * events: NULL or hipEvent_t[3] (see hbx_event_create). */
@@ -199,6 +203,19 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
  * negative categorical factors or structural NaNs -- use hbx_kde_pdf_exact there.  out: device f64[Np]. */
 int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                          const int64_t* rows, double* out, void* stream);
+
+/* ln pdf of one prepared KDE at Nc candidates within rtol * max(1, |ln pdf|) of the reference's
+ * KDEMultivariate.pdf (kernel_density.py:162-196) -- the north-star contract at every D: the fp32
+ * estimate (hbx_kde_logpdf) wherever its rigorous per-candidate bound guarantees rtol, the fp64 log-space
+ * evaluation (hbx_kde_logpdf_exact) for the rest -- candidates next to outlying observations, beyond
+ * D = 32, exact-only KDEs -- and ln of the exact fp64 pdf for KDEs with negative categorical factors.
+ * All on the device.  cand: device f64[Nc][D]; X / rows: the KDE's observations (as hbx_kde_pdf_exact);
+ * out: device f64[Nc] (-inf: pdf 0; NaN where the reference's pdf is NaN or negative);
+ * scratch: hbx_kde_logpdf_rtol_scratch_bytes(Nc) device bytes. */
+int64_t hbx_kde_logpdf_rtol_scratch_bytes(int64_t Nc);
+int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
+                        const double* X, const int64_t* rows, int32_t dc_pad, int32_t du_pad, int32_t variant,
+                        double rtol, double* out, void* scratch, int64_t scratch_bytes, void* stream);
 
 /* numpy 1.26.4's float64 exp (what the reference's np.exp computes on AVX512_SKX hosts), element-wise
  * on the device: the known-answer check of the exact re-score's exp.  x, y: device f64[n]. */
@@ -285,14 +302,16 @@ int64_t hbx_sh_promote_scratch_bytes(int64_t B, int64_t max_seg, int64_t N, int3
                                      int32_t order_mode);
 int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                       const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
-                      int64_t scratch_bytes, int32_t order_mode, void* stream);
+                      int64_t scratch_bytes, int32_t order_mode, void* events, void* stream);
+/*   events: NULL, or hipEvent_t[2] stamped at the start and end of the selection kernel (mask-only path). */
 
 /* One bracket of n <= 1024 configurations in one launch (what SuccessiveHalving.process_results ranks per
  * call, HB_iteration.py:179-182): loss f64[n] and advance u8[n] may be device pointers or mapped host
  * memory from hbx_host_alloc (no copies); k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY), or
- * NULL (HBX_ORDER_STABLE). */
+ * NULL (HBX_ORDER_STABLE).  done (nullable, mapped host memory): set to `seq` once every mask byte is
+ * visible to the host, so a caller may poll it instead of synchronising the stream. */
 int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
-                       void* stream);
+                       int32_t* done, int32_t seq, void* stream);
 /* Pinned, device-mapped, coherent host memory (hipHostMalloc) and its release. */
 int hbx_host_alloc(int64_t bytes, void** out);
 int hbx_host_free(void* p);

@@ -178,3 +178,68 @@ def test_batch_segments_across_combine_sub_blocks(device, seg):
         r = res[b]
         assert (one.index, one.score, one.pdf_l, one.pdf_g, one.shortlist) == \
             (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist), (seg, b)
+
+
+class _Counter(object):
+    def __init__(self, monkeypatch):
+        from hpbandster_amd import kde
+        self.n = {"acquire": 0, "acquire_batch": 0}
+        for name in self.n:
+            orig = getattr(kde.KDEPair, name)
+
+            def wrap(selfp, *a, _orig=orig, _name=name, **k):
+                self.n[_name] += 1
+                return _orig(selfp, *a, **k)
+            monkeypatch.setattr(kde.KDEPair, name, wrap)
+
+
+def _job(cid, cfg, budget, loss):
+    class Job(object):
+        pass
+    j = Job()
+    j.id, j.kwargs, j.exception, j.timestamps = cid, {"config": cfg, "budget": budget}, None, {}
+    j.result = {"loss": float(loss), "info": None}
+    return j
+
+
+def _stage(device, seed, batch, results_between, monkeypatch=None):
+    """An SH bracket's first stage (27 configurations) requested through get_next_run, as HpBandSter.run
+    requests them; with results_between every run's result (and the model refit it triggers) and a worker
+    draw from the global RNG land before the next request."""
+    from hpbandster_amd.HB_iteration import SuccessiveHalving
+    cg, space = _fitted_bohb(device, seed)
+    np.random.seed(31)
+    space.seed(41)
+    cnt = _Counter(monkeypatch) if monkeypatch is not None else None
+    sh = SuccessiveHalving(0, [27, 9, 3, 1], [1.0, 3.0, 9.0, 27.0], cg.get_config, device=device,
+                           batch_sampling=batch)
+    runs = []
+    for i in range(27):
+        cid, cfg, b = sh.get_next_run()
+        runs.append((cid, cfg, sh.data[cid]["config_info"]))
+        if results_between:
+            np.random.rand()  # the worker's own draw (toy function noise)
+            cg.new_result(_job(cid, cfg, 1.0, np.random.RandomState(i).rand()))
+    return runs, np.random.get_state(), cnt
+
+
+def test_sh_stage_served_by_one_batched_acquisition(device, monkeypatch):
+    """SURVEY 8f row 1 wired into the drop-in: the 27 back-to-back get_config requests of an SH stage
+    come from ONE hbx_kde_acquire_batch pass -- and are exactly the sequential calls' proposals, with the
+    global RNG left where 27 sequential calls leave it."""
+    seq, st_seq, _ = _stage(device, 11, False, False)
+    bat, st_bat, cnt = _stage(device, 11, True, False, monkeypatch)
+    assert cnt.n == {"acquire": 0, "acquire_batch": 1}
+    assert sum(i["model_based_pick"] for _, _, i in seq) >= 10
+    assert [(c, i) for _, c, i in seq] == [(c, i) for _, c, i in bat]
+    np.testing.assert_array_equal(st_seq[1], st_bat[1])
+    assert st_seq[2] == st_bat[2]
+
+
+def test_sh_stage_with_results_between_requests_stays_sequential(device):
+    """Results (model refits) and a worker's RNG draws between requests: every speculative proposal
+    that is no longer the sequential call's result is dropped, so the run equals the sequential one."""
+    seq, st_seq, _ = _stage(device, 12, False, True)
+    bat, st_bat, _ = _stage(device, 12, True, True)
+    assert [(c, i) for _, c, i in seq] == [(c, i) for _, c, i in bat]
+    np.testing.assert_array_equal(st_seq[1], st_bat[1])

@@ -559,3 +559,62 @@ def test_fast_and_precise_records_agree_on_random_shapes(device):
             l = O.pdf_many(X[g_idx], bwg, vt, C, nlg)
             g = O.pdf_many(X[b_idx], bwb, vt, C, nlb)
             assert fast.index == O.select(l, g)[0], case
+
+
+def _capi_logpdf_rtol(k, C, rtol=1e-5):
+    """hbx_kde_logpdf_rtol called straight through the C-ABI (what a reference-side integrator binds)."""
+    import torch
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    C = np.ascontiguousarray(C, dtype=np.float64)
+    c_dev = torch.from_numpy(C).to(k.device)
+    out = torch.full((C.shape[0],), 123.0, dtype=torch.float64, device=k.device)
+    sb = int(L.hbx_kde_logpdf_rtol_scratch_bytes(C.shape[0]))
+    scr = torch.empty(sb, dtype=torch.uint8, device=k.device)
+    N.call("hbx_kde_logpdf_rtol", N.ptr(c_dev), C.shape[0], C.shape[1], N.ptr(k.params), N.ptr(k.table),
+           N.ptr(k.X_dev), N.ptr(k.rows_dev), k.dc_pad, k.du_pad, k.variant, rtol, N.ptr(out), N.ptr(scr), sb,
+           N.stream_handle(None, k.device))
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", ["outlier", "d46", "signed", "d32m"])
+def test_capi_logpdf_rtol_contract(device, case):
+    """The north-star ln-pdf contract at the C-ABI (not through DeviceKDE): within 1e-5 * max(1, |ln p|)
+    of the reference's ln pdf for every candidate where that is finite, NaN where it is NaN -- next to an
+    outlying observation (the fp32 estimates there are off by up to 5e-2), at D = 46 (3e-5), on a KDE with
+    negative categorical factors, and at config #3's shape."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    rs = np.random.RandomState(11)
+    if case == "outlier":
+        n, D = 8500, 16
+        X = 0.5 + 1e-3 * rs.rand(n, D)
+        X[17] = 0.0
+        Lo = rs.rand(n)
+        Lo[17] = np.sort(Lo)[n // 2]
+        vt = "c" * D
+        C = np.vstack([0.5 + 1e-3 * rs.rand(200, D), 0.02 * rs.rand(56, D)])
+    elif case == "d46":
+        dc, lv = 30, [4] * 16
+        X = S.make_observations(2000, dc, 16, lv, seed=21)
+        Lo = S.make_losses(2000, seed=22)
+        vt = S.var_type_string(dc, 16)
+        C = S.make_candidates(256, dc, 16, lv, seed=23)
+    elif case == "signed":
+        c = G.load_kde_case("hgt1")
+        X, Lo, vt, C = c["X"], c["eff_losses"], c["var_type"], c["cands"]
+    else:
+        c = G.load_kde_case("d32m")
+        X, Lo, vt, C = c["X"], c["eff_losses"], c["var_type"], c["cands"][:96]
+    pair = kde.fit_pair(X, Lo, vt, len(vt) + 1, device=device)
+    for k in (pair.good, pair.bad):
+        lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        if k.has_neg:  # negative factors: ln of the reference's own (possibly negative) pdf
+            with np.errstate(divide="ignore", invalid="ignore"):
+                lref = np.log(O.pdf_many(k.data, k.bw, vt, C, k.nlev))
+        got = _capi_logpdf_rtol(k, C)
+        fin = np.isfinite(lref)
+        assert fin.sum() > 0
+        assert np.array_equal(np.isnan(got), np.isnan(lref)), case
+        err = np.abs(got[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        assert err.max() <= 1e-5, (case, err.max())

@@ -165,3 +165,47 @@ def test_config5_shape_with_quantised_losses(device):
     assert (adv.sum(1) == k).all()
     for b in range(0, B, 37):
         np.testing.assert_array_equal(adv[b], O.sh_advance(losses[b], k))
+
+
+def test_batched_refit_d32_mixed_numpy_order(device):
+    """Config #5's per-bracket refit at config #3's dims (24c + 8u, L=4): hbx_seg_argsort_ex in numpy's
+    order over quantised (tied) losses, then hbx_kde_fit -- every bracket's bandwidths bit-exact and level
+    counts equal to the oracle's (numpy 1.26.4's split restated, np.std, np.unique)."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    B, n, dc, du = 120, 1000, 24, 8
+    D = dc + du
+    rs = np.random.RandomState(12)
+    losses = np.round(rs.rand(B, n), 2)
+    losses[rs.rand(B, n) < 0.05] = np.inf
+    X = np.hstack([rs.rand(B * n, dc), rs.randint(0, 4, (B * n, du)).astype(np.float64)])
+    L = N.lib()
+    seg = np.arange(B + 1, dtype=np.int64) * n
+    ld, segd, Xd = (torch.from_numpy(a).to(device) for a in (losses.reshape(-1), seg, X))
+    order = torch.empty(B * n, dtype=torch.int64, device=device)
+    sb = int(L.hbx_sort_scratch_bytes(B * n))
+    scr = torch.empty(sb, dtype=torch.uint8, device=device)
+    N.call("hbx_seg_argsort_ex", N.ptr(ld), N.ptr(segd), B, n, B * n, N.ptr(order), N.ptr(scr), sb, N.ORDER_NUMPY,
+           N.stream_handle())
+    ng, nb = kde.bohb_split_sizes(n, D + 1)
+    t = lambda v, dt: torch.full((B,), v, dtype=dt, device=device)  # noqa: E731
+    vt = torch.tensor([0] * dc + [1] * du, dtype=torch.int32, device=device)
+    outs = [torch.empty((B, D), dtype=torch.float64, device=device) for _ in range(2)] + \
+           [torch.empty((B, D), dtype=torch.int32, device=device) for _ in range(2)]
+    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(order), N.ptr(t(ng, torch.int64)),
+           N.ptr(t(nb, torch.int64)), N.ptr(t(kde.bandwidth_factor(ng, D), torch.float64)),
+           N.ptr(t(kde.bandwidth_factor(nb, D), torch.float64)), N.ptr(vt), *[N.ptr(o) for o in outs],
+           N.stream_handle())
+    bwg, bwb, nlg, nlb = (o.cpu().numpy() for o in outs)
+    o = order.cpu().numpy().reshape(B, n)
+    vts = "c" * dc + "u" * du
+    for b in range(B):
+        rows = NA.argsort(losses[b])
+        np.testing.assert_array_equal(o[b], rows, err_msg="bracket %d" % b)
+        Xb = X[b * n:(b + 1) * n]
+        good, bad = Xb[rows[:ng]], Xb[rows[-nb:]]
+        np.testing.assert_array_equal(bwg[b], 1.06 * np.std(good, axis=0) * ng ** (-1. / (4 + D)))
+        np.testing.assert_array_equal(bwb[b], 1.06 * np.std(bad, axis=0) * nb ** (-1. / (4 + D)))
+        np.testing.assert_array_equal(nlg[b], O.num_levels(good, vts))
+        np.testing.assert_array_equal(nlb[b], O.num_levels(bad, vts))
