@@ -59,12 +59,17 @@ def kernel_model(kde_obj, dc, du):
         return {"kernel": "kde_logpdf_%s_kernel (f32 MFMA fallback)" % ("oh" if kc else ""), "model": None}
     nsc = (4 * kde_obj.dc_pad + 31) // 32
     if h32:
-        nd = (6 + 24 * nsc + 15) // 16  # h32_nd(nsc) dense steps
+        coarse = bool((v >> 7) & 1) and not signed  # the acquisition's coarse pre-screen instance
+        nd = (6 + (8 if coarse else 24) * nsc + 15) // 16  # h32c_nd / h32_nd dense steps
         kp = (kc + 1) // 2  # 32-position one-hot steps
-        fast = kp > 0  # the acquisition's instance
-        n_mat = nd + kp * (1 if fast else 2) + (kp if signed else 0)  # per 1024 pairs (+ signed parity)
+        fast = kp > 0 and not coarse  # the acquisition's instance
+        n_mat = nd + kp * (1 if (fast or coarse) else 2) + (kp if signed else 0)  # per 1024 pairs (+ parity)
         valu = 16 * 8 + 16 * 4 + (32 * 4 if signed else 0)  # exp2, add (+ fract, fma when signed)
-        name = "kde_logpdf_h32%s_kernel<%d,%d,%s>" % ("s" if signed else "", nsc, kp, "true" if fast else "false")
+        if signed:
+            name = "kde_logpdf_h32s_kernel<%d,%d,%s>" % (nsc, kp, "true" if fast else "false")
+        else:
+            name = "kde_logpdf_h32_kernel<%d,%d,%s,%s>" % (nsc, kp, "true" if fast else "false",
+                                                           "true" if coarse else "false")
         return {"kernel": name,
                 "model": {"matrix_instr_per_1024_pairs": n_mat, "sparse_onehot": kc > 0,
                           "pipe_cycles": 32 * n_mat / 4, "issue_cycles": (8 * n_mat + valu) / 4,
@@ -828,7 +833,10 @@ def main():
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True,
         "scaling": "strong" if a.total_candidates else "weak",
-        "vs_baseline": None, "dtype": "f16 hi/lo MFMA (3 products per dim), f32 accumulate, f64 re-score", "data": "synthetic",
+        "vs_baseline": None,
+        "dtype": ("f16 MFMA coarse pre-screen (1 product per dim, rigorous bound), f32 accumulate, f64 re-score"
+                  if (pair.bad.variant >> 7) & 1 else "f16 hi/lo MFMA (3 products per dim), f32 accumulate, f64 re-score"),
+        "data": "synthetic",
         "config": {"workload": workload, "candidates_per_gpu": Nc,
                    "total_candidates": a.total_candidates or world * Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,

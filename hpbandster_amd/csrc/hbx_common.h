@@ -63,6 +63,8 @@ struct KdeParams {
   int32_t nsc;        // hmode: f16 K-steps (of 32) of the continuous product = ceil(4 dc_pad / 32)
   int32_t chunk_floats; // floats per 64-observation chunk of this KDE's table (layout depends on kc)
   int32_t oh_total;   // one-hot width: sum over active categorical dims of (max observed code + 1)
+  int32_t coarse_off; // floats into the table where the coarse h32 layout starts (0: none)
+  int32_t coarse_chunk_floats; // floats per 64-observation chunk of the coarse table
   const double* X;    // the KDE's data (device): X[rows[j]] is observation j (rescue / exact paths)
   const int64_t* rows;
   int32_t oh_dim[64];   // one-hot slot -> active categorical dim u

@@ -39,6 +39,7 @@ __host__ __device__ static void bucket_dims(int dc, int du, int* dc_pad, int* du
 
 __host__ __device__ static int table_stride(int dc_pad, int du_pad) { return chunk_floats(dc_pad, du_pad); }
 static int64_t n_chunks(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
+__device__ __forceinline__ int64_t n_chunks_dev(int64_t n) { return (n + OBS_CHUNK - 1) / OBS_CHUNK; }
 // capacity of a table: the largest layout hbx_kde_prepare may choose for this bucket (exact-only KDEs,
 // outside every bucket, keep no table: one float)
 static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
@@ -47,7 +48,9 @@ static int64_t table_floats(int64_t n, int dc_pad, int du_pad) {
   const int c = h_chunk_floats(dc_pad, OH_MAX_KC, 1), d = h32_chunk_floats(nsc_of(dc_pad), OH_MAX_KC, 1);
   a = a > b ? a : b;
   a = a > d ? a : d;
-  return n_chunks(n) * (int64_t)(a > c ? a : c);
+  // + the coarse h32 table (hbx_kde_impl.h), after the main one
+  const int e = h32c_chunk_floats(nsc_of(dc_pad), 2);
+  return n_chunks(n) * (int64_t)((a > c ? a : c) + e);
 }
 
 // Model preparation runs on the device from (data rows, bandwidths, level counts), so a refit needs
@@ -63,6 +66,7 @@ struct PrepArgs {
   int32_t n, D;
   int32_t hm_allowed;   // HBX_HMODE not 0
   int32_t h32_allowed;  // HBX_H32 not 0
+  int32_t co_allowed;   // HBX_COARSE not 0: the coarse h32 table beside the precise one
   int32_t nblk_table;   // blocks of this KDE in the table launches
   uint32_t vt[HBX_MAX_D / 32];  // bit d: dim d categorical ('u')
 };
@@ -279,6 +283,10 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   P->nsc = nsc_of(dcp);
   P->chunk_floats = hmode == 2 ? h32_chunk_floats(nsc_of(dcp), h32_kp(kc), has_neg)
                                : (hmode ? h_chunk_floats(dcp, kc, has_neg) : chunk_floats(dcp, dup, kc, kc ? has_neg : 0));
+  // the coarse pre-screen table (unsigned h32 KDEs): after the main table in the same buffer
+  const bool co = hmode == 2 && !has_neg && A.co_allowed;
+  P->coarse_chunk_floats = co ? h32c_chunk_floats(nsc_of(dcp), h32_kp(kc)) : 0;
+  P->coarse_off = co ? (int32_t)(n_chunks_dev(n) * P->chunk_floats) : 0;
 }
 
 // Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
@@ -302,6 +310,11 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   // hm: 0 = f32 layout, 1 = hmode (16x16 kernel), 2 = h32 (32x32 kernel, no chunk header)
   const int KTP = hm == 2 ? h32_ktp(P->nsc, h32_kp(P->kc), P->has_neg) : h_ktp(dcp, P->kc);
   _Float16* hrow = (_Float16*)(hm == 2 ? ch : ch + OBS_CHUNK) + jj * KTP;
+  // the coarse pre-screen row (h32 KDEs with a coarse table; hbx_kde_impl.h): dense C pieces, ones, Xh
+  _Float16* crow = (hm == 2 && P->coarse_off > 0 && slot)
+                       ? (_Float16*)(table + P->coarse_off + (int64_t)(j / OBS_CHUNK) * P->coarse_chunk_floats) +
+                             jj * h32c_ktp(P->nsc, h32_kp(P->kc))
+                       : nullptr;
   double C = 0.0;
   // hmode rows are written 16 bytes (8 halves) at a time: two dims' h, l, h, l per store
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -391,17 +404,23 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
       *(h8*)(cz + 16 * s + 8) = vh[1];
       *(h8*)(cz + 16 * kp + 16 * s) = vl[0];
       *(h8*)(cz + 16 * kp + 16 * s + 8) = vl[1];
+      if (crow) {  // the coarse row: the hi parts only
+        *(h8*)(crow + 16 * h32c_nd(P->nsc) + 16 * s) = vh[0];
+        *(h8*)(crow + 16 * h32c_nd(P->nsc) + 16 * s + 8) = vh[1];
+      }
       if (P->has_neg) {
         *(h8*)(cp + 16 * s) = pv[0];
         *(h8*)(cp + 16 * s + 8) = pv[1];
       }
     }
-    uint32_t* ix = (uint32_t*)(hrow + 16 * nd32 + 32 * kp);
-    if (kp == 1) {  // dwords 2b + h, b = bit 4 of the row (bank spread of the kernel's b64 reads)
-      const int b = (jj >> 4) & 1;
-      for (int q = 0; q < 4; ++q) ix[q] = (q >> 1) == b ? iw[q & 1] : 0u;
-    } else {
-      for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
+    for (int w = 0; w < (crow ? 2 : 1); ++w) {  // index words of the precise row, then of the coarse row
+      uint32_t* ix = w == 0 ? (uint32_t*)(hrow + 16 * nd32 + 32 * kp) : (uint32_t*)(crow + 16 * h32c_nd(P->nsc) + 16 * kp);
+      if (kp == 1) {  // dwords 2b + h, b = bit 4 of the row (bank spread of the kernel's b64 reads)
+        const int b = (jj >> 4) & 1;
+        for (int q = 0; q < 4; ++q) ix[q] = (q >> 1) == b ? iw[q & 1] : 0u;
+      } else {
+        for (int q = 0; q < 2 * ksp; ++q) ix[q] = iw[q];
+      }
     }
   } else if (slot) {
     const int W = P->kc * 32;  // one-hot halves per observation
@@ -457,6 +476,19 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
         hst[2] = c2;
         hst[3] = hst[4] = hst[5] = (_Float16)1.f;
         for (int q = 0; q < 2 * nd32; ++q) *(h8*)(hrow + 8 * q) = *(const h8*)(hst + 8 * q);
+        if (crow) {  // coarse dense slots: the same six, then Xh of continuous dim c at 6 + c; row padding
+          const int ndc = h32c_nd(P->nsc), kpc = h32_kp(P->kc), ktpc = h32c_ktp(P->nsc, kpc);
+          for (int q = 0; q < 2 * ndc; ++q) {
+            h8 g;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int k = 8 * q + e;
+              g[e] = k < 6 ? hst[k] : (k - 6 < dcp ? hst[6 + 3 * (k - 6)] : (_Float16)0.f);
+            }
+            *(h8*)(crow + 8 * q) = g;
+          }
+          for (int k = (16 * ndc + 16 * kpc + 2 * h32_ixw(kpc) + 7) & ~7; k < ktpc; k += 8) *(h8*)(crow + k) = z8;
+        }
       } else {
         hrow[3] = c0;
         hrow[7] = c1;
@@ -539,8 +571,8 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
 }
 
 // Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
-// du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6
-// selects the scoring kernel.
+// du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6 |
+// (coarse table) << 7 selects the scoring kernel.
 __global__ void kde_prep_finish_kernel(PrepSet ps) {
   const int k = threadIdx.x;
   if (k >= ps.nk) return;
@@ -550,9 +582,11 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
     P->hmode = 0;
     P->chunk_floats = chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0);
     P->cmax = P->cmax2;
+    P->coarse_off = 0;
   }
   int32_t* info = A.info;
-  info[0] = P->has_neg | (P->kc << 1) | ((P->hmode != 0) << 4) | (P->exact_only << 5) | ((P->hmode == 2) << 6);
+  info[0] = P->has_neg | (P->kc << 1) | ((P->hmode != 0) << 4) | (P->exact_only << 5) | ((P->hmode == 2) << 6) |
+            ((P->hmode == 2 && P->coarse_off > 0) << 7);
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
@@ -596,6 +630,8 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
   A->hm_allowed = !(hm_env && hm_env[0] == '0');
   const char* h32_env = getenv("HBX_H32");  // 0: the 16x16-tile hmode kernel instead of the 32x32 one
   A->h32_allowed = !(h32_env && h32_env[0] == '0');
+  const char* co_env = getenv("HBX_COARSE");  // 0: no coarse pre-screen table (the FAST instance scores)
+  A->co_allowed = !(co_env && co_env[0] == '0');
   A->nblk_table = (dcp < 0 || dup < 0) ? 0 : (int32_t)prep_table_blocks(n);
   return HBX_OK;
 }
@@ -1490,9 +1526,10 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
   if (hm && ((variant >> 6) & 1)) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
     const int kp = h32_kp(kc);
+    const bool co = fast && !sg && ((variant >> 7) & 1);  // the acquisition's coarse pre-screen instance
     const bool fa = fast && kp > 0;
-    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa), r, 32 * H16_WAVES, 64 * H16_WAVES,
-            hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa),
+    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * H16_WAVES, 64 * H16_WAVES,
+            hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
             sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }
   if (hm) {

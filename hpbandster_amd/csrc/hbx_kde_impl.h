@@ -118,6 +118,19 @@ __host__ __device__ constexpr int h32_chunk_floats(int nsc, int kp, int sgn = 0)
   return (OBS_CHUNK * h32_ktp(nsc, kp, sgn) / 2 + 255) & ~255;
 }
 #define H32_ROW_MAX 112  // dense halves of the largest h32 row (nsc = 4: 7 steps)
+// Coarse h32 layout (hbx_score_h32.hip <CO = true>: the acquisition's pre-screen instance, unsigned KDEs):
+// ONE f16 product per continuous dim.  Row = [16 ndc dense: slots 0-2 the C_j pieces, 3-5 = 1, 6 + c = Xh
+// of continuous dim c] [16 kp one-hot hi part, 2:4-compressed as above] [index words as above]; no lo
+// parts.  xh.Xh stands for x''.X': the dropped xh.Xl + xl.X' (<= |xh| (2^-11 xmax + 2^-25) + |xl| xmax per
+// dim, log2 units) goes into the candidate's bound, and the exact re-score resolves what it leaves near
+// the minimum.  2 dense + 1 sparse matrix instructions per 1024 pairs at 24c + 8u instead of 6.  The
+// table is a second region of the same buffer (KdeParams::coarse_off floats in).
+__host__ __device__ constexpr int h32c_nd(int nsc) { return (6 + 8 * nsc + 15) / 16; }
+__host__ __device__ constexpr int h32c_par(int nsc, int kp) { return (16 * h32c_nd(nsc) + 16 * kp + 2 * h32_ixw(kp) + 7) & ~7; }
+__host__ __device__ constexpr int h32c_ktp(int nsc, int kp) { return 8 * (((h32c_par(nsc, kp) + 7) / 8) | 1); }
+__host__ __device__ constexpr int h32c_chunk_floats(int nsc, int kp) {
+  return (OBS_CHUNK * h32c_ktp(nsc, kp) / 2 + 255) & ~255;
+}
 // ------------------------------------------------------------------------------------------
 // fp32 log-domain scoring
 //
@@ -178,6 +191,25 @@ __device__ __forceinline__ KdeEst finish_est(const KdeParams* __restrict__ P, fl
 // row: ~16 serialized HBM round trips per wave at D = 32, the largest piece of a block's prologue).
 __device__ __forceinline__ void stage_rows(const double* __restrict__ src, int64_t nv, int D, int DS, double* xs,
                                            int lane) {
+  if (D <= 64) {  // rows of D <= 64: lane = (row in pass, column), one division per lane instead of one per element
+    const int rpp = 64 / D;  // rows per pass (uniform)
+    const int lr = lane / D, lc = lane - lr * D;
+    const bool act = lr < rpp;
+    for (int r0 = 0; r0 < (int)nv; r0 += 16 * rpp) {
+      double t[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = r0 + q * rpp + lr;
+        t[q] = (act && row < nv) ? src[row * D + lc] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = r0 + q * rpp + lr;
+        if (act && row < nv) xs[row * DS + lc] = t[q];
+      }
+    }
+    return;
+  }
   const int tot = (int)nv * D;
   for (int e0 = 0; e0 < tot; e0 += 16 * 64) {
     double t[16];
@@ -219,5 +251,5 @@ logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
 logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
 logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
-logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast);  // hbx_score_h32.hip
-logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast);
+logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse = false);  // hbx_score_h32.hip
+logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse = false);

@@ -38,6 +38,9 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define H32_CMAX 30000.f    // |shifted c_i| limit of the three-piece split (else: rescue pass)
+#ifndef HBX_PK_SUM
+#define HBX_PK_SUM 0        // 1: a tile's exp2 terms summed with packed f32 adds (A/B: tools/build_variant.sh)
+#endif
 
 // sparse index words of one tile: KS dwords (one ds_read).  KS = 1: both lane halves read the row's two
 // dwords and take theirs (ds_read_b64 banks over 64 dwords, b32 over 32: 4-way on these rows)
@@ -67,20 +70,22 @@ struct SgbH32<NM, NM, NV, NRL> {
   static __device__ __forceinline__ void run() {}
 };
 
-template <int NSC, int KP, bool SG, bool FAST>
+template <int NSC, int KP, bool SG, bool FAST, bool CO = false>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
                                                     const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr) {
-  constexpr int ND = h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + 3 slots per continuous dim)
+  // CO: the coarse pre-screen (hbx_kde_impl.h coarse layout): one product per continuous dim, no lo parts
+  constexpr int ND = CO ? h32c_nd(NSC) : h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + per dim)
   constexpr int KS = KP;                     // sparse 32-wide K-steps (one-hot positions), hi parts
-  constexpr int KL = FAST ? 0 : KP;          // ... and lo parts
+  constexpr int KL = (FAST || CO) ? 0 : KP;  // ... and lo parts
   constexpr int NMT = ND + KS + KL;          // matrix instructions per 32x32 tile
-  constexpr int KTP = h32_ktp(NSC, KP, SG);
-  constexpr int CHF = h32_chunk_floats(NSC, KP, SG);
+  constexpr int KTP = CO ? h32c_ktp(NSC, KP) : h32_ktp(NSC, KP, SG);
+  constexpr int CHF = CO ? h32c_chunk_floats(NSC, KP) : h32_chunk_floats(NSC, KP, SG);
   constexpr int PAR = h32_par(NSC, KP);  // signed: the parity block (halves into the row)
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
   static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
+  static_assert(!CO || !SG, "the coarse instance is built for unsigned sums");
   constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
   constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -91,6 +96,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   static_assert(GP * 1024 == CHF * 4, "chunk must be a multiple of 1 KB");
   __shared__ __align__(16) float lds[NBUF * CHF + AUXF];  // the kernel's only LDS object
   float* aux = lds + NBUF * CHF;
+  if constexpr (CO) table += P->coarse_off;  // the coarse layout follows the precise table
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, h = lane >> 5;
@@ -127,7 +133,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // one-hot positions 32s + 8h + j (half j) and 32s + 16 + 8h + j (half 8 + j), 1 on a match.
   f16x8 bd[ND];
   f16x16 bsp[KS > 0 ? KS : 1];
-  float ci = 0.f, bnd = 0.f;
+  float ci = 0.f, bnd = 0.f, cer = 0.f;  // cer: the coarse instance's dropped products (log2 units)
   auto build = [&](const double* x) {
     auto coord = [&](int d) {  // 2 x'_d (0 past the continuous dims), clamped to the f16 range
       const ContPrm q = cprm[d];
@@ -137,19 +143,45 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
     for (int s = 0; s < ND; ++s) bd[s] = f16x8{};
     if (h == 0) bd[0][0] = bd[0][1] = bd[0][2] = (_Float16)1.f;
-    // every lane walks all dims (compile-time slot positions; each lane keeps its half's slots)
+    if constexpr (CO) {
+      // coarse: slot k = 6 + d, so element j of a lane half's B fragments is slot 16 (j / 8) + 8 h + j % 8 --
+      // the two halves walk DIFFERENT dims with the same register index: each dim is built once per
+      // candidate, the sums (c_i, bound terms) are half sums added across the halves below
 #pragma unroll
-    for (int d = 0; d < 8 * NSC; ++d) {
-      const float v = coord(d);
-      ci = fmaf(-v, v, ci);
-      bnd = fmaf(2.f * fabsf(v), cprm[d].xmax, bnd);
-      const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
-      const _Float16 hi = (_Float16)xc;
-      const _Float16 lo = (_Float16)(xc - (float)hi);
+      for (int j = 0; j < 8 * ND; ++j) {
+        const int d = 16 * (j >> 3) + 8 * h + (j & 7) - 6;  // per lane half
+        if (d < 0) continue;  // slots 0-5 (set above / after the probe)
+        const bool act = d < 8 * NSC;
+        const ContPrm q = cprm[act ? d : 0];
+        const float v0 = (float)(q.scale * (x[q.col] - q.center));
+        const float v = (act && d < dc) ? v0 : 0.f;
+        ci = fmaf(-v, v, ci);
+        const float xm = act ? q.xmax : 0.f;
+        bnd = fmaf(2.f * fabsf(v), xm, bnd);
+        const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
+        const _Float16 hi = (_Float16)xc;
+        bd[j >> 3][j & 7] = hi;  // |x''.X' - xh.Xh| <= |xh| |Xl| + |xl| |X'|
+        cer = fmaf(fabsf((float)hi), fmaf(0x1p-11f, xm, 0x1p-25f), cer);
+        cer = fmaf(fabsf(xc - (float)hi), xm, cer);
+      }
+      ci += __shfl_xor(ci, 32);
+      bnd += __shfl_xor(bnd, 32);
+      cer += __shfl_xor(cer, 32);
+    } else {
+      // every lane walks all dims (compile-time slot positions; each lane keeps its half's slots)
 #pragma unroll
-      for (int comp = 0; comp < 3; ++comp) {
-        const int k = 6 + 3 * d + comp;
-        if (h == ((k >> 3) & 1)) bd[k >> 4][k & 7] = comp < 2 ? hi : lo;
+      for (int d = 0; d < 8 * NSC; ++d) {
+        const float v = coord(d);
+        ci = fmaf(-v, v, ci);
+        bnd = fmaf(2.f * fabsf(v), cprm[d].xmax, bnd);
+        const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
+        const _Float16 hi = (_Float16)xc;
+        const _Float16 lo = (_Float16)(xc - (float)hi);
+#pragma unroll
+        for (int comp = 0; comp < 3; ++comp) {
+          const int k = 6 + 3 * d + comp;
+          if (h == ((k >> 3) & 1)) bd[k >> 4][k & 7] = comp < 2 ? hi : lo;
+        }
       }
     }
 #pragma unroll
@@ -208,7 +240,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   f16x8 apar[SG ? KS : 1];  // signed: parity fragments (the one-hot part's positions, 0.5 per negative dim)
   typename H32Idx<KS>::T aix;
   // index words relative to arow (KP = 1: dwords 2b, 2b + 1, b = bit 4 of the row -- hbx_kde_impl.h)
-  const int ixo = 16 * ND + 32 * KP + (KP == 1 ? 4 * ((c >> 4) & 1) : 2 * h32_ksp(KP) * h) - 8 * h;
+  const int ixo = 16 * ND + (CO ? 16 : 32) * KP + (KP == 1 ? 4 * ((c >> 4) & 1) : 2 * h32_ksp(KP) * h) - 8 * h;
   auto arow = [&](const float* buf, int jt) { return (const _Float16*)buf + (32 * jt + c) * KTP + 8 * h; };
   auto readA = [&](const float* buf, int jt) {
     const _Float16* a = arow(buf, jt);
@@ -301,7 +333,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       ax[0] = ci;
       ax[1] = bnd;
       ax[2] = dl;
-      ax[3] = big ? 1.f : 0.f;
+      ax[3] = big ? -1.f : cer * (1.f + 0x1p-18f);  // rescue flag, else the coarse bound (rounded up)
     }
   }
 
@@ -316,11 +348,25 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
       for (int r = 1; r < 16; ++r) sn = fmaf(__builtin_amdgcn_fractf(ap[r]), e[r], sn);
     }
+#if HBX_PK_SUM
+    // packed pairwise tree (v_pk_add_f32: two adds per lane per instruction): lanes of the pair (r, r + 8),
+    // then (r, r + 4), (r, r + 2), (r, r + 1) -- depth 4 like the scalar tree, 7 packed adds + 1 add
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2 p[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) p[r] = f32x2{e[r], e[r + 8]};
+#pragma unroll
+    for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+      for (int r = 0; r < w; ++r) p[r] = p[r] + p[r + w];
+    return p[0][0] + p[0][1];
+#else
 #pragma unroll
     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
       for (int r = 0; r < w; ++r) e[r] = e[2 * r] + e[2 * r + 1];
     return e[0];
+#endif
   };
   auto schedule = [&]() {
     SgbH32<0, NMT, 32, (KS > 0 ? 2 : 1)>::run();
@@ -385,7 +431,8 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     if (ii < Nc) {
       const float* ax = aux + (wave * 32 + c) * 4;
       const float ci_q = ax[0], bnd_q = ax[1], dq = ax[2];
-      const bool big = ax[3] != 0.f;
+      const bool big = ax[3] < 0.f;
+      const float cer_q = big ? 0.f : ax[3];
       const double* x = cand + ii * (int64_t)D;
       bool nq = P->nan_all != 0;
       for (int k = 0; k < P->nconst; ++k)
@@ -397,15 +444,15 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       // f16 hi/lo representation error of both coordinates (2 x 2^-22 sum|x''X'|) and the lo.lo products
       // given up (together <= 2^-22 sum|x''X'|), plus the C_j / c_i pieces' subnormal rounding
       if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-19f) * HBX_LN2f;
-      if constexpr (FAST) {  // the one-hot lo parts left out: |sum_u lo_u m_u| <= sum_u |lo_u| (log2 units)
-        float lo_err = 0.f;
+      if constexpr (FAST || CO) {  // the one-hot lo parts left out: |sum_u lo_u m_u| <= sum_u |lo_u| (log2)
+        float lo_err = CO ? cer_q : 0.f;  // coarse: the dropped continuous products as well
         for (int u = 0; u < P->du; ++u) {
           const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
           if (fabsf(dl) < 60000.f) lo_err += fabsf(dl - (float)(_Float16)dl);
         }
         // every term is off by a factor in [2^-L, 2^L], L = lo_err: the sums' relative bound e becomes
         // (1 + e) 2^L - 1 (rounded up)
-        if (o.err > 0.f) o.err = (1.f + o.err) * exp2f(lo_err) * (1.f + 0x1p-20f) - 1.f;
+        if (o.err > 0.f) o.err = (1.f + o.err) * exp2f(lo_err * (1.f + 0x1p-20f)) * (1.f + 0x1p-20f) - 1.f;
       }
       if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) {  // rescue marker
         o.err = -1.f;
@@ -417,21 +464,21 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 }
 
 // unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU)
-template <int NSC, int KP, bool FAST>
+template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KP, false, FAST>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
 // both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
-template <int NSC, int KP, bool FAST>
+template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
-  kde_logpdf_h32_body<NSC, KP, false, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
-                                            a.rescue);
+  kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                                second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
+                                                a.rescue);
 }
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
@@ -452,50 +499,52 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
                                            a.rescue);
 }
 
-// instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part
-template <int NSC, int KP, bool SG, bool PAIR, bool FAST>
+// instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part; CO (coarse) for unsigned sums
+template <int NSC, int KP, bool SG, bool PAIR, bool FAST, bool CO>
 static constexpr auto h32_inst() {
   if constexpr (PAIR) {
     if constexpr (SG) return (logpdf_pair_fn)kde_logpdf_h32s_pair_kernel<NSC, KP, FAST>;
-    else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KP, FAST>;
+    else return (logpdf_pair_fn)kde_logpdf_h32_pair_kernel<NSC, KP, FAST, CO>;
   } else {
     if constexpr (SG) return (logpdf_fn)kde_logpdf_h32s_kernel<NSC, KP, FAST>;
-    else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KP, FAST>;
+    else return (logpdf_fn)kde_logpdf_h32_kernel<NSC, KP, FAST, CO>;
   }
 }
 
 template <int NSC, int KP, bool SG, bool PAIR>
-static auto pick32_fast(bool fast) {
+static auto pick32_fast(bool fast, bool coarse) {
+  if constexpr (!SG)
+    if (coarse) return h32_inst<NSC, KP, SG, PAIR, false, true>();
   if constexpr (KP > 0)
-    if (fast) return h32_inst<NSC, KP, SG, PAIR, true>();
-  return h32_inst<NSC, KP, SG, PAIR, false>();
+    if (fast) return h32_inst<NSC, KP, SG, PAIR, true, false>();
+  return h32_inst<NSC, KP, SG, PAIR, false, false>();
 }
 
 template <int NSC, bool SG, bool PAIR>
-static auto pick32_kp(int kp, bool fast) {
+static auto pick32_kp(int kp, bool fast, bool coarse) {
   switch (kp) {
-    case 0: if constexpr (h32_ok(NSC, 0, SG)) return pick32_fast<NSC, 0, SG, PAIR>(fast); break;
-    case 1: if constexpr (h32_ok(NSC, 1, SG)) return pick32_fast<NSC, 1, SG, PAIR>(fast); break;
-    case 2: if constexpr (h32_ok(NSC, 2, SG)) return pick32_fast<NSC, 2, SG, PAIR>(fast); break;
+    case 0: if constexpr (h32_ok(NSC, 0, SG)) return pick32_fast<NSC, 0, SG, PAIR>(fast, coarse); break;
+    case 1: if constexpr (h32_ok(NSC, 1, SG)) return pick32_fast<NSC, 1, SG, PAIR>(fast, coarse); break;
+    case 2: if constexpr (h32_ok(NSC, 2, SG)) return pick32_fast<NSC, 2, SG, PAIR>(fast, coarse); break;
   }
-  return decltype(h32_inst<NSC, 1, SG, PAIR, false>())(nullptr);
+  return decltype(h32_inst<NSC, 1, SG, PAIR, false, false>())(nullptr);
 }
 
 template <bool SG, bool PAIR>
-static auto pick32(int nsc, int kp, bool fast) {
+static auto pick32(int nsc, int kp, bool fast, bool coarse) {
   switch (nsc) {  // nsc_of(dc_pad) for dc_pad in {8, 16, 24, 32}
-    case 1: return pick32_kp<1, SG, PAIR>(kp, fast);
-    case 2: return pick32_kp<2, SG, PAIR>(kp, fast);
-    case 3: return pick32_kp<3, SG, PAIR>(kp, fast);
-    case 4: return pick32_kp<4, SG, PAIR>(kp, fast);
+    case 1: return pick32_kp<1, SG, PAIR>(kp, fast, coarse);
+    case 2: return pick32_kp<2, SG, PAIR>(kp, fast, coarse);
+    case 3: return pick32_kp<3, SG, PAIR>(kp, fast, coarse);
+    case 4: return pick32_kp<4, SG, PAIR>(kp, fast, coarse);
   }
-  return decltype(pick32_kp<1, SG, PAIR>(0, false))(nullptr);
+  return decltype(pick32_kp<1, SG, PAIR>(0, false, false))(nullptr);
 }
 
-logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast) {
-  return sg ? pick32<true, false>(nsc, kp, fast) : pick32<false, false>(nsc, kp, fast);
+logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse) {
+  return sg ? pick32<true, false>(nsc, kp, fast, false) : pick32<false, false>(nsc, kp, fast, coarse);
 }
 
-logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast) {
-  return sg ? pick32<true, true>(nsc, kp, fast) : pick32<false, true>(nsc, kp, fast);
+logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse) {
+  return sg ? pick32<true, true>(nsc, kp, fast, false) : pick32<false, true>(nsc, kp, fast, coarse);
 }

@@ -618,3 +618,33 @@ def test_capi_logpdf_rtol_contract(device, case):
         assert np.array_equal(np.isnan(got), np.isnan(lref)), case
         err = np.abs(got[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
         assert err.max() <= 1e-5, (case, err.max())
+
+
+@pytest.mark.parametrize("dc,du,lev", [(24, 8, 4), (8, 0, 2), (16, 4, 3), (32, 4, 2)])
+def test_coarse_prescreen_matches_fast_and_oracle(device, dc, du, lev, monkeypatch):
+    """The acquisition's coarse pre-screen (one f16 product per continuous dim, the dropped products in
+    each candidate's bound; variant bit 7) against the FAST instance (HBX_COARSE=0: three products per
+    dim) and the oracle: the same record (index, score, pdfs) at config #3's dims and others; the exact
+    re-score takes a few more candidates."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    n = 3000
+    X = S.make_observations(n, dc, du, lev, seed=81)
+    L = S.make_losses(n, seed=82)
+    vt = S.var_type_string(dc, du)
+    C = S.make_candidates(5000, dc, du, lev, seed=83)
+    monkeypatch.setenv("HBX_COARSE", "1")
+    pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    for k in (pair.good, pair.bad):  # every unsigned h32 KDE carries the coarse table
+        assert (k.variant >> 7) & 1 == (0 if k.has_neg else 1)
+    assert not pair.bad.has_neg
+    co = pair.acquire(C)
+    monkeypatch.setenv("HBX_COARSE", "0")
+    pair0 = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    assert (pair0.bad.variant >> 7) & 1 == 0
+    fa = pair0.acquire(C)
+    assert (co.index, co.score, co.pdf_l, co.pdf_g) == (fa.index, fa.score, fa.pdf_l, fa.pdf_g)
+    assert co.shortlist >= fa.shortlist >= 1
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C[:800], pair.good.nlev)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C[:800], pair.bad.nlev)
+    assert pair.acquire(C[:800]).index == O.select(l, g)[0]

@@ -47,8 +47,11 @@ if a.traffic_out:
                    % ("l and g in one launch" if any("pair" in k for k in ks) else "mean over the l and g launches")}
     if a.trace:
         import statistics
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in csv.DictReader(open(a.trace))
-                if a.kernel in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
+        grid = lambda r: int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)  # noqa: E731
+        gmax = max(grid(r) for r in rows) if rows else 0
+        # the main step's launches only (the largest grid; side lines launch the kernel on fewer candidates)
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rows if grid(r) == gmax]
         grbm = sum(out[k].get("GRBM_GUI_ACTIVE", 0) * out[k]["dispatches"] for k in ks) / \
             sum(out[k]["dispatches"] for k in ks)
         if durs and grbm:

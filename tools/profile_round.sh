@@ -30,7 +30,7 @@ W=kde_acquisition_d32_24c8u_obs10000_cand1000000
 T=$(ls $OUT/trace/*kernel_trace.csv | head -1)
 python3 tools/pmc_summary.py $OUT --kernel kde_logpdf_h --traffic-out $OUT/pmc_traffic.json --workload $W --trace $T > $OUT/pmc_summary.txt || exit 4
 python3 tools/ksteady.py $T --skip 3 > $OUT/kernel_steady.txt || exit 5
-python3 tools/trace_vs_line.py $T $OUT/bench_traced.json > $OUT/trace_vs_line.txt || exit 6
+python3 tools/trace_vs_line.py $T $OUT/bench_traced.json $OUT/bench.json > $OUT/trace_vs_line.txt || exit 6
 cp $(ls $OUT/trace/*kernel_stats.csv | head -1) $OUT/kernel_stats.csv
 rm -rf $OUT/pmc[0-9]/ $OUT/trace/*kernel_trace.csv
 head -8 $OUT/kernel_steady.txt

@@ -5,7 +5,10 @@ the next `steps` taken -- the launches the line timed with HIP events.  Reports 
 of those, the line's event mean, and roofline.frac recomputed from rocprof (within 3 % of the line's is
 the bar).  Likewise config #5's select kernel and the refit kernels.
 
-    python tools/trace_vs_line.py <run_kernel_trace.csv> <bench_traced.json>
+    python tools/trace_vs_line.py <run_kernel_trace.csv> <bench_traced.json> [<bench.json>]
+
+(bench.json: the same session's untraced line -- a 20 us kernel's HIP-event stamps move by ~10 us under
+the tracer, so the short kernels are compared with the untraced line too.)
 """
 import csv
 import json
@@ -22,14 +25,20 @@ def rows(path):
     return sorted(out)
 
 
-def main():
-    trace, line_path = sys.argv[1], sys.argv[2]
+def load_line(path):
     line = None
-    for ln in open(line_path):
+    for ln in open(path):
         ln = ln.strip()
         if ln.startswith("{"):
             line = json.loads(ln)
-    assert line is not None, "no JSON line in %s" % line_path
+    assert line is not None, "no JSON line in %s" % path
+    return line
+
+
+def main():
+    trace, line_path = sys.argv[1], sys.argv[2]
+    line = load_line(line_path)
+    plain = load_line(sys.argv[3]) if len(sys.argv) > 3 else None
     R = rows(trace)
     rf = line["roofline"]
     kname = rf["kernel"].split("<")[0].split(" ")[0]
@@ -57,9 +66,13 @@ def main():
         big = [r[1] for r in R if "sh_select_kernel" in r[2] and r[3] == max(x[3] for x in R if "sh_select" in x[2])]
         m = statistics.mean(big[1:]) if len(big) > 1 else big[0]
         gbs = c5["roofline"]["bytes_per_config"] * 1e7 / (m * 1e-6) / 1e9
-        print("config5 sh_select_kernel: rocprof mean %.1f us over %d launches, line %.1f us; HBM frac from "
-              "rocprof %.3f, line %.3f" % (m, len(big) - 1, c5["ms_per_launch"] * 1e3, gbs / 8000.0,
-                                           c5["roofline"]["frac"]))
+        print("config5 sh_select_kernel: rocprof mean %.1f us over %d launches, traced line %.1f us; HBM frac "
+              "from rocprof %.3f, traced line %.3f" % (m, len(big) - 1, c5["ms_per_launch"] * 1e3, gbs / 8000.0,
+                                                      c5["roofline"]["frac"]))
+        if plain and "ms_per_launch" in (plain.get("config5") or {}):
+            p5 = plain["config5"]
+            print("  untraced line of the session: %.1f us, HBM frac %.3f (%.2f %% from rocprof's)" % (
+                p5["ms_per_launch"] * 1e3, p5["roofline"]["frac"], 100 * (p5["roofline"]["frac"] / (gbs / 8000.0) - 1)))
     rf_line = line.get("refit") or {}
     names = ("kde_refit_meta", "seg_rank", "seg_argsort", "seg_tie_flag", "seg_np_order", "kde_fit_col", "kde_colstats",
              "kde_params", "kde_table", "kde_prep_finish")
