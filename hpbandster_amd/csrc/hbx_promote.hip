@@ -10,6 +10,8 @@
 // advance[position] = (rank < k).  Ties are ranked by position (stable), or -- HBX_ORDER_NUMPY, what the
 // drop-in uses -- as numpy 1.26.4's unstable argsort ranks them (hbx_npsort.h): brackets whose tied
 // losses straddle the k-th place are re-ranked on the device in numpy's order.
+#include <cstring>
+
 #include "hbx_common.h"
 #include <hip/hip_ext.h>
 #include "hbx_npsort.h"
@@ -434,6 +436,28 @@ int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance
   hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(NPS_THREADS), 0, (hipStream_t)stream, loss, (int)n, k, advance,
                      order_mode == HBX_ORDER_NUMPY ? 1 : 0, (int32_t*)scratch, done, seq);
   HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+// The drop-in's whole ranking step in ONE host call: the losses copied into the mapped buffer `pin`, the
+// one-launch promotion above, a spin on the completion word the kernel stores last (bounded: then the
+// stream is synchronised), the mask copied out of `pout` into `mask` (host uint8[n]).
+int hbx_sh_advance_mapped(const double* losses, int64_t n, double k, uint8_t* mask, double* pin, uint8_t* pout,
+                          int32_t* done, int32_t seq, void* scratch, int32_t order_mode, void* stream) {
+  if (!losses || !mask || !pin || !pout || !done) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_mapped: null pointer");
+  if (n <= 0) return HBX_OK;
+  memcpy(pin, losses, sizeof(double) * (size_t)n);
+  const int rc = hbx_sh_promote_one(pin, n, k, pout, scratch, order_mode, done, seq, stream);
+  if (rc) return rc;
+  // ~0.1 ms of polling covers the launch and the kernel; past it, block on the stream instead
+  bool seen = false;
+  for (int i = 0; i < 200000 && !seen; ++i) seen = __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq;
+  if (!seen) {
+    HBX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
+      return hbx_fail(HBX_ERR_HIP, "hbx_sh_advance_mapped: the kernel did not store its completion word");
+  }
+  memcpy(mask, pout, (size_t)n);
   return HBX_OK;
 }
 

@@ -67,8 +67,12 @@ class _Staging(object):
 
     def __init__(self, device):
         self.device = device
+        self.index = device.index
         self.cap = 0
         self._ptrs = []
+        self.seq = 0
+        self.fn = N.lib().hbx_sh_advance_mapped
+        self.stream_of = _current_stream_fn()
 
     def get(self, n):
         import torch
@@ -80,14 +84,13 @@ class _Staging(object):
             N.check(L.hbx_host_alloc(8 * cap, ctypes.addressof(pin)))
             N.check(L.hbx_host_alloc(cap + 64, ctypes.addressof(pout)))
             self._ptrs = [pin.value, pout.value]
-            self.h_in = np.ctypeslib.as_array((ctypes.c_double * cap).from_address(pin.value))
-            self.h_out = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(pout.value))
+            self.pin, self.pout = pin.value, pout.value
             # the completion word the kernel stores last (after the mask, system scope)
             self.done_addr = pout.value + cap
-            self.done = ctypes.c_int32.from_address(self.done_addr)
-            self.done.value = 0
-            self.seq = 0
-            self.scratch = torch.empty(4 * cap, dtype=torch.int32, device=self.device)
+            ctypes.c_int32.from_address(self.done_addr).value = 0
+            with torch.cuda.device(self.device):
+                self.scratch = torch.empty(4 * cap, dtype=torch.int32, device=self.device)
+            self.scr_ptr = self.scratch.data_ptr()
             self.cap = cap
         return self
 
@@ -107,47 +110,66 @@ _tls = threading.local()
 
 
 def _staging(device):
-    import torch
-    key = str(torch.device(device))
+    """The calling thread's staging of `device` (None: torch's current device)."""
     st = getattr(_tls, "staging", None)
     if st is None:
         st = _tls.staging = {}
-    if key not in st:
-        st[key] = _Staging(device)
-    return st[key]
+    if device is None:
+        import torch
+        device = torch.cuda.current_device()
+    s = st.get(device)
+    if s is None:
+        import torch
+        if not torch.cuda.is_available():
+            raise N.HbxError("hpbandster_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                             "the engine has no CPU path")
+        dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        key = str(dev)
+        s = st.get(key)
+        if s is None:
+            s = st[key] = _Staging(dev)
+        st[device] = s
+    return s
+
+
+def _current_stream_fn():
+    import torch
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)  # the handle without a Stream object
+    if raw is not None:
+        return raw
+    return lambda idx: torch.cuda.current_stream(idx).cuda_stream
+
+
+_MODES = {"numpy": N.ORDER_NUMPY, "stable": N.ORDER_STABLE, N.ORDER_NUMPY: N.ORDER_NUMPY,
+          N.ORDER_STABLE: N.ORDER_STABLE}
 
 
 def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
-    What SuccessiveHalving.process_results calls once per bracket: the losses are written into
-    device-mapped host memory, ONE kernel (hbx_sh_promote_one: the selection, and the numpy-order
-    re-rank when tied losses straddle the k-th place) reads them and writes the mask back there, and
-    the host polls the kernel's completion word (stored last) instead of synchronising the stream."""
-    import torch
-    losses = np.asarray(losses, dtype=np.float64).reshape(-1)
+    What SuccessiveHalving.process_results calls once per bracket: ONE host call into libhbx
+    (hbx_sh_advance_mapped) copies the losses into device-mapped host memory, launches the one-kernel
+    promotion (the selection, and the numpy-order re-rank when tied losses straddle the k-th place), spins
+    on the kernel's completion word (stored last) instead of synchronising the stream, and copies the
+    mask out."""
+    losses = np.ascontiguousarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
     if n == 0:
         return np.zeros(0, dtype=bool)
     if n > 1024:
         return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream,
                                 ties=ties)
-    mode = N.order_mode(ties)
-    device = device or default_device()
-    L = N.lib()
-    with N.on_device(device, stream):
-        st = _staging(device).get(n)
-        st.h_in[:n] = losses
-        cur = stream if stream is not None else torch.cuda.current_stream(device)
-        st.seq = (st.seq % 0x7ffffffe) + 1
-        N.check(L.hbx_sh_promote_one(st._ptrs[0], n, float(k), st._ptrs[1],
-                                     N.ptr(st.scratch) if mode == N.ORDER_NUMPY else None, mode, st.done_addr, st.seq,
-                                     cur.cuda_stream))
-        # the kernel's last store is the sequence number: poll it (a stream synchronisation would wait on
-        # the runtime's completion signal); after a bounded spin, fall back to the synchronisation
-        for _ in range(20000):
-            if st.done.value == st.seq:
-                break
-        else:
-            cur.synchronize()
-        return st.h_out[:n].astype(bool)
+    mode = _MODES.get(ties)
+    if mode is None:
+        mode = N.order_mode(ties)
+    st = _staging(device).get(n)
+    h = stream.cuda_stream if stream is not None else st.stream_of(st.index)
+    mask = np.empty(n, dtype=np.bool_)
+    st.seq = (st.seq % 0x7ffffffe) + 1
+    rc = st.fn(losses.ctypes.data, n, float(k), mask.ctypes.data, st.pin, st.pout, st.done_addr, st.seq,
+               st.scr_ptr if mode == N.ORDER_NUMPY else None, mode, h)
+    if rc:
+        N.check(rc)
+    return mask

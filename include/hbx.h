@@ -312,6 +312,13 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
  * visible to the host, so a caller may poll it instead of synchronising the stream. */
 int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
                        int32_t* done, int32_t seq, void* stream);
+/* The same ranking step as ONE host call (what the drop-in's advance_mask makes): losses (host f64[n]) are
+ * copied into `pin` (hbx_host_alloc, >= n doubles), hbx_sh_promote_one runs with advance = `pout`
+ * (hbx_host_alloc, >= n bytes), the host spins on `done` (mapped, after pout) until the kernel stores
+ * `seq` (bounded: then the stream is synchronised), and the mask is copied into `mask` (host u8[n]).
+ * Replaces np.argsort(np.argsort(losses)) < k of HB_iteration.py:179-182 for one bracket. */
+int hbx_sh_advance_mapped(const double* losses, int64_t n, double k, uint8_t* mask, double* pin, uint8_t* pout,
+                          int32_t* done, int32_t seq, void* scratch, int32_t order_mode, void* stream);
 /* Pinned, device-mapped, coherent host memory (hipHostMalloc) and its release. */
 int hbx_host_alloc(int64_t bytes, void** out);
 int hbx_host_free(void* p);

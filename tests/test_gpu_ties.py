@@ -193,10 +193,11 @@ def test_batched_refit_d32_mixed_numpy_order(device):
     vt = torch.tensor([0] * dc + [1] * du, dtype=torch.int32, device=device)
     outs = [torch.empty((B, D), dtype=torch.float64, device=device) for _ in range(2)] + \
            [torch.empty((B, D), dtype=torch.int32, device=device) for _ in range(2)]
-    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(order), N.ptr(t(ng, torch.int64)),
-           N.ptr(t(nb, torch.int64)), N.ptr(t(kde.bandwidth_factor(ng, D), torch.float64)),
-           N.ptr(t(kde.bandwidth_factor(nb, D), torch.float64)), N.ptr(vt), *[N.ptr(o) for o in outs],
-           N.stream_handle())
+    # held by name: a temporary freed at N.ptr would hand its block to the next array
+    ngd, nbd = t(ng, torch.int64), t(nb, torch.int64)
+    fgd, fbd = t(kde.bandwidth_factor(ng, D), torch.float64), t(kde.bandwidth_factor(nb, D), torch.float64)
+    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(order), N.ptr(ngd), N.ptr(nbd), N.ptr(fgd),
+           N.ptr(fbd), N.ptr(vt), *[N.ptr(o) for o in outs], N.stream_handle())
     bwg, bwb, nlg, nlb = (o.cpu().numpy() for o in outs)
     o = order.cpu().numpy().reshape(B, n)
     vts = "c" * dc + "u" * du

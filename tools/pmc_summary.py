@@ -18,12 +18,15 @@ ap.add_argument("--trace", help="kernel_trace.csv of the same command: the kerne
                                 "effective clock GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md)")
 a = ap.parse_args()
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
+grids = collections.defaultdict(collections.Counter)  # kernel -> grid sizes of its profiled dispatches
 for p in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
     per = collections.defaultdict(float)
     names = {}
     for row in csv.DictReader(open(p)):
         key = (row["Dispatch_Id"], row["Counter_Name"])
         per[key] += float(row["Counter_Value"])  # sum over dimensions (XCD/SE instances)
+        if row["Dispatch_Id"] not in names:
+            grids[row["Kernel_Name"]][int(row.get("Grid_Size") or row.get("Grid_Size_X") or 0)] += 1
         names[row["Dispatch_Id"]] = row["Kernel_Name"]
     for (d, c), v in per.items():
         vals[names[d]][c].append(v)
@@ -49,9 +52,14 @@ if a.traffic_out:
         import statistics
         rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
         grid = lambda r: int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)  # noqa: E731
-        gmax = max(grid(r) for r in rows) if rows else 0
-        # the main step's launches only (the largest grid; side lines launch the kernel on fewer candidates)
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rows if grid(r) == gmax]
+        # the traced launches with the grid the counter passes profiled (the main step's; the traced bench
+        # also runs side lines whose grids differ)
+        gc = collections.Counter()
+        for k in ks:
+            gc.update(grids[k])
+        gpmc = gc.most_common(1)[0][0] if gc else 0
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rows if grid(r) == gpmc]
+        rec["grid"] = gpmc
         grbm = sum(out[k].get("GRBM_GUI_ACTIVE", 0) * out[k]["dispatches"] for k in ks) / \
             sum(out[k]["dispatches"] for k in ks)
         if durs and grbm:
