@@ -304,6 +304,24 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     return out
 
 
+def device_candidates(total, lo, hi, dc, du, levels, device, seed=44):
+    """Rows [lo, hi) of a seeded set of `total` candidates drawn on the device (U[0,1) continuous,
+    U{0..L-1} categorical): the whole set is drawn on every rank and sliced, so a sharded run scores the
+    same candidates at every rank count (its winner cannot depend on N)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    C = torch.empty((total, dc + du), dtype=torch.float64, device=device)
+    C[:, :dc] = torch.rand((total, dc), dtype=torch.float64, device=device, generator=g)
+    if du:
+        C[:, dc:] = torch.randint(0, levels, (total, du), device=device, generator=g).to(torch.float64)
+    if lo == 0 and hi == total:
+        return C
+    out = C[lo:hi].clone()
+    del C
+    return out
+
+
 def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
     """Side line: BASELINE config #4's whole workload on ONE MI355X -- 1e7 candidates x config #3's 1e4
     observations (D = 32) -- as one acquisition, and as the 8 per-rank shards of the 8-GPU run
@@ -313,12 +331,7 @@ def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
     import torch
     from hpbandster_amd import kde
     from hpbandster_amd.distributed import reduce_records_host, shard_range
-    g = torch.Generator(device=device)
-    g.manual_seed(44)
-    C = torch.empty((Nc, dc + du), dtype=torch.float64, device=device)
-    C[:, :dc] = torch.rand((Nc, dc), dtype=torch.float64, device=device, generator=g)
-    if du:
-        C[:, dc:] = torch.randint(0, levels, (Nc, du), device=device, generator=g).to(torch.float64)
+    C = device_candidates(Nc, 0, Nc, dc, du, levels, device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     r = pair.acquire(C, workspace=ws)
     torch.cuda.synchronize()
@@ -344,18 +357,14 @@ def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
 def strong_line(pair, device, a, rank, world, dist, xchg, reps=10):
     """Side line at N > 1: BASELINE config #4 -- a fixed total of candidates (1e7) x config #3's
     observations, sharded over the ranks (each scores shard_range(total, rank, N) with global indices,
-    drawn on its own device), one winner exchange per step; max-over-ranks time (strong scaling)."""
+    drawn on its own device: config4_line's set, so the winner is config4_line's at every N), one winner
+    exchange per step; max-over-ranks time (strong scaling)."""
     import torch
     from hpbandster_amd import kde
     from hpbandster_amd.distributed import shard_range
     lo, hi = shard_range(a.strong_total, rank, world)
     Nc = hi - lo
-    g = torch.Generator(device=device)
-    g.manual_seed(4400 + rank)
-    C = torch.empty((Nc, a.dc + a.du), dtype=torch.float64, device=device)
-    C[:, :a.dc] = torch.rand((Nc, a.dc), dtype=torch.float64, device=device, generator=g)
-    if a.du:
-        C[:, a.dc:] = torch.randint(0, a.levels, (Nc, a.du), device=device, generator=g).to(torch.float64)
+    C = device_candidates(a.strong_total, lo, hi, a.dc, a.du, a.levels, device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
 
     def step():
@@ -745,13 +754,15 @@ def main():
     pair = kde.fit_pair(X, losses, var_type, D + 1, device=device)
     Ng, Nb = pair.good.nobs, pair.bad.nobs
     from hpbandster_amd.distributed import shard_range
-    if a.total_candidates:  # strong scaling: this rank's contiguous shard of the total, global indices
+    if a.total_candidates:  # strong scaling: this rank's contiguous shard of ONE seeded set, global indices
         lo, hi = shard_range(a.total_candidates, rank, world)
         Nc, base = hi - lo, lo
+        c_dev = device_candidates(a.total_candidates, lo, hi, a.dc, a.du, a.levels, device)
+        cands = None
     else:
         Nc, base = a.candidates, rank * a.candidates
-    cands = S.make_candidates(Nc, a.dc, a.du, a.levels, seed=S.SEED_CAND + rank)
-    c_dev = torch.from_numpy(cands).to(device)
+        cands = S.make_candidates(Nc, a.dc, a.du, a.levels, seed=S.SEED_CAND + rank)
+        c_dev = torch.from_numpy(cands).to(device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     ev = kde.ScoreEvents()
     # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
@@ -915,7 +926,9 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),
-                                               pair, var_type, cands, a.cpu_seconds)
+                                               pair, var_type,
+                                               cands if cands is not None else c_dev[:400_000].cpu().numpy(),
+                                               a.cpu_seconds)
         except Exception as e:  # the baseline is a side measurement; report why it is missing
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
