@@ -32,6 +32,13 @@
 // half the LDS-DMA instructions per pair -- ended in a GPU memory fault on its first launch; cause not
 // found, so it is not offered.)
 #define H16_WAVES 8
+// the coarse pre-screen instance of the 32x32 kernel: waves per block and minimum waves per SIMD
+#ifndef H32C_WAVES
+#define H32C_WAVES 8
+#endif
+#ifndef H32C_EU
+#define H32C_EU 4
+#endif
 
 // Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
 //   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0

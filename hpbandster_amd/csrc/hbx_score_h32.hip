@@ -86,7 +86,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
   static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
   static_assert(!CO || !SG, "the coarse instance is built for unsigned sums");
-  constexpr int HW = H16_WAVES;  // waves per block, 32 candidates each
+  constexpr int HW = CO ? H32C_WAVES : H16_WAVES;  // waves per block, 32 candidates each
   constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
   constexpr int NBUF = 2 * (4 * CHF + AUXF) * 4 <= 160 * 1024 ? 4 : 3;
@@ -342,7 +342,11 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   auto tile_sum = [&](const f32x16& a, const f32x16& ap, float& sn) -> float {
     float e[16];
 #pragma unroll
+#ifdef HBX_ABL_NOEXP
+    for (int r = 0; r < 16; ++r) e[r] = fabsf(a[r]);  // ablation: no exp2 (positive sums, no rescue)
+#else
     for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(a[r]);
+#endif
     if constexpr (SG) {
       sn = __builtin_amdgcn_fractf(ap[0]) * e[0];
 #pragma unroll
@@ -389,7 +393,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     const float* buf = lds + b * CHF;
     const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
     // chunk cc+PD's buffer was last read before the previous iteration's barrier
+#ifndef HBX_ABL_NODMA
     issue(cc + PD, (b + PD) % NBUF, 0);
+#endif
     mma_rd(accA, accpA, buf, 1);  // T0(cc); fragments of T1(cc)
     float tn;
     Sb += tile_sum(accB, accpB, tn);  // T1(cc-1): chunk cc-1 complete
@@ -399,11 +405,15 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       Sn += Snb;
     }
     schedule();
+#ifndef HBX_ABL_NODMA
     issue(cc + PD, (b + PD) % NBUF, 1);
+#endif
     // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
     // the barrier makes chunk cc+1 visible to every wave
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+#ifndef HBX_ABL_NOBAR
     __builtin_amdgcn_s_barrier();
+#endif
     mma_rd(accB, accpB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
     Sb = tile_sum(accA, accpA, tn);  // T0(cc)
     if constexpr (SG) Snb = tn;
@@ -463,9 +473,10 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   }
 }
 
-// unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU)
+// unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU); the coarse instance: H32C_WAVES-wave
+// blocks at >= H32C_EU waves per SIMD
 template <int NSC, int KP, bool FAST, bool CO>
-__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_kernel(
+__global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
   kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, P, table, out, blockIdx.x);
@@ -473,7 +484,7 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
 
 // both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
 template <int NSC, int KP, bool FAST, bool CO>
-__global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void kde_logpdf_h32_pair_kernel(
+__global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
