@@ -271,7 +271,11 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     b = Bl // 2
     rows = np.argsort(S.make_bracket_losses(B, n)[b0 + b], kind="stable")
     Xb = X[b * n:(b + 1) * n].cpu().numpy()
-    bw_ok = bool(np.array_equal(bwg[b].cpu().numpy(), 1.06 * np.std(Xb[rows[:ng]], axis=0) * ng ** (-1. / (4 + D))))
+    good_b, bad_b = Xb[rows[:ng]], Xb[rows[-nb:]]
+    lev_ok = all(int(nlg[b, d]) == len(np.unique(good_b[:, d])) and int(nlb[b, d]) == len(np.unique(bad_b[:, d]))
+                 for d in range(dc, D))
+    bw_ok = bool(np.array_equal(bwg[b].cpu().numpy(), 1.06 * np.std(good_b, axis=0) * ng ** (-1. / (4 + D))) and
+                 np.array_equal(bwb[b].cpu().numpy(), 1.06 * np.std(bad_b, axis=0) * nb ** (-1. / (4 + D))) and lev_ok)
     # algorithmic HBM bytes: losses read (8) and the order written and read (16) per config, each KDE's rows
     # read twice (mean pass, deviation pass) through the order: 2 (ng + nb) D 8 per bracket
     fit_bytes = Bl * (24 * n + 2 * (ng + nb) * D * 8)
