@@ -700,6 +700,9 @@ def kde_result_bytes():
     return kde.RESULT_BYTES
 
 
+PROFILE_SET = "profiles/r03"
+
+
 def load_traffic(workload):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -879,7 +882,10 @@ def main():
                                          "samples": len(launch_ms),
                                          "timing": "HIP events on the launch stream around the scoring launch(es) "
                                                    "of each timed step"},
-                     "profiles": a.profile_tag,
+                     # the committed same-session set for this workload (bench line + the same bench under
+                     # rocprofv3 + PMC passes: tools/profile_round.sh); traffic and measured clock come
+                     # from its pmc_traffic.json (copied to profiles/pmc_traffic.json)
+                     "profiles": a.profile_tag or PROFILE_SET,
                      "mfma_util": mfma_util, "issue_bound": issue_bound},
         "cpu_baseline": None,
     }
