@@ -1529,7 +1529,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     const bool co = fast && !sg && ((variant >> 7) & 1);  // the acquisition's coarse pre-screen instance
     const bool fa = fast && kp > 0;
     const int hw = co ? H32C_WAVES : H16_WAVES;
-    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw, 64 * hw,
+    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
             sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }

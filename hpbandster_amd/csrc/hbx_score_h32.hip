@@ -54,23 +54,23 @@ template <int KS, typename T> __device__ __forceinline__ int h32_idx(const T& v,
 
 // sched_group_barrier pattern of one phase: NM times {1 MFMA, its fragment re-read(s), a share of the
 // NV VALU ops} (the last matrix instruction re-reads its fragment and the index words)
-template <int I, int NM, int NV, int NRL>
+template <int I, int NM, int NV, int NRL, bool RD = true>
 struct SgbH32 {
   static __device__ __forceinline__ void run() {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    constexpr int nr = I == NM - 1 ? NRL : 1;
+    constexpr int nr = !RD ? 0 : I == NM - 1 ? NRL : 1;
     if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
     constexpr int n = NV / NM + (I < NV % NM ? 1 : 0);
     if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x002, n, 0);
-    SgbH32<I + 1, NM, NV, NRL>::run();
+    SgbH32<I + 1, NM, NV, NRL, RD>::run();
   }
 };
-template <int NM, int NV, int NRL>
-struct SgbH32<NM, NM, NV, NRL> {
+template <int NM, int NV, int NRL, bool RD>
+struct SgbH32<NM, NM, NV, NRL, RD> {
   static __device__ __forceinline__ void run() {}
 };
 
-template <int NSC, int KP, bool SG, bool FAST, bool CO = false>
+template <int NSC, int KP, bool SG, bool FAST, bool CO = false, int CT = 1>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
@@ -86,8 +86,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
   static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
   static_assert(!CO || !SG, "the coarse instance is built for unsigned sums");
-  constexpr int HW = CO ? H32C_WAVES : H16_WAVES;  // waves per block, 32 candidates each
-  constexpr int AUXF = HW * 32 * 4;  // per candidate: c_i, bound term, shift, rescue flag
+  static_assert(CT == 1 || (CT == 2 && CO), "two candidate column tiles per wave: the coarse instance");
+  constexpr int HW = CO ? H32C_WAVES : H16_WAVES;  // waves per block, 32 CT candidates each
+  constexpr int AUXF = HW * 32 * CT * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
   constexpr int NBUF = 2 * (4 * CHF + AUXF) * 4 <= 160 * 1024 ? 4 : 3;
   static_assert(2 * (NBUF * CHF + AUXF) * 4 <= 160 * 1024, "two blocks per CU");
@@ -100,7 +101,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, h = lane >> 5;
-  const int64_t cbase = ((int64_t)blk * HW + wave) * 32;
+  const int64_t cbase = ((int64_t)blk * HW + wave) * 32 * CT;
   const bool xpiece = wave < NX;
   const int n = P->n, dc = P->dc;
 
@@ -110,7 +111,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   constexpr int PRM_BYTES = 8 * NSC * (int)sizeof(ContPrm) + 32 * (KP > 0 ? KP : 1) * (int)sizeof(OhPrm);
   static_assert(PRM_BYTES <= NBUF * CHF * 4, "parameters must fit in the ring");
   const int DS = D | 1;  // odd row stride in doubles: conflict-free
-  const int64_t rows_bytes = (int64_t)HW * 32 * DS * 8;
+  const int64_t rows_bytes = (int64_t)HW * 32 * CT * DS * 8;
   const bool rows_fit = rows_bytes + PRM_BYTES <= (int64_t)NBUF * CHF * 4;
   ContPrm* cprm = (ContPrm*)((char*)lds + (rows_fit ? rows_bytes : 0));
   OhPrm* oprm = (OhPrm*)(cprm + 8 * NSC);
@@ -122,8 +123,8 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   }
   if (tid < 32 * KP) oprm[tid] = OhPrm{P->oh_val[tid], P->oh_col[tid], 0};  // padding: NaN, never equal
   const bool staged = rows_fit && cbase < Nc;
-  const int64_t nv = (Nc - cbase) < 32 ? (Nc - cbase) : 32;  // valid rows of this wave
-  double* xs = (double*)lds + (int64_t)wave * 32 * DS;
+  const int64_t nv = (Nc - cbase) < 32 * CT ? (Nc - cbase) : 32 * CT;  // valid rows of this wave
+  double* xs = (double*)lds + (int64_t)wave * 32 * CT * DS;
   if (staged) stage_rows(cand + cbase * (int64_t)D, nv, D, DS, xs, lane);
   __syncthreads();
 
@@ -131,18 +132,19 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   // 0-2: 1 (against the C_j pieces), 3-5: the pieces of the shifted c_i (against 1; 0 in the probe),
   // 6 + 3d + {0,1,2}: (hi, hi, lo) of x''_d against the observation's (Xh, Xl, Xh).  Sparse step s:
   // one-hot positions 32s + 8h + j (half j) and 32s + 16 + 8h + j (half 8 + j), 1 on a match.
-  f16x8 bd[ND];
-  f16x16 bsp[KS > 0 ? KS : 1];
-  float ci = 0.f, bnd = 0.f, cer = 0.f;  // cer: the coarse instance's dropped products (log2 units)
-  auto build = [&](const double* x) {
+  f16x8 bd[CT][ND];
+  f16x16 bsp[CT][KS > 0 ? KS : 1];
+  float ci[CT], bnd[CT], cer[CT];  // cer: the coarse instance's dropped products (log2 units)
+  auto build = [&](const double* x, const int t) {
+    ci[t] = bnd[t] = cer[t] = 0.f;
     auto coord = [&](int d) {  // 2 x'_d (0 past the continuous dims), clamped to the f16 range
       const ContPrm q = cprm[d];
       const float v0 = (float)(q.scale * (x[q.col] - q.center));
       return d < dc ? v0 : 0.f;
     };
 #pragma unroll
-    for (int s = 0; s < ND; ++s) bd[s] = f16x8{};
-    if (h == 0) bd[0][0] = bd[0][1] = bd[0][2] = (_Float16)1.f;
+    for (int s = 0; s < ND; ++s) bd[t][s] = f16x8{};
+    if (h == 0) bd[t][0][0] = bd[t][0][1] = bd[t][0][2] = (_Float16)1.f;
     if constexpr (CO) {
       // coarse: slot k = 6 + d, so element j of a lane half's B fragments is slot 16 (j / 8) + 8 h + j % 8 --
       // the two halves walk DIFFERENT dims with the same register index: each dim is built once per
@@ -155,32 +157,32 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
         const ContPrm q = cprm[act ? d : 0];
         const float v0 = (float)(q.scale * (x[q.col] - q.center));
         const float v = (act && d < dc) ? v0 : 0.f;
-        ci = fmaf(-v, v, ci);
+        ci[t] = fmaf(-v, v, ci[t]);
         const float xm = act ? q.xmax : 0.f;
-        bnd = fmaf(2.f * fabsf(v), xm, bnd);
+        bnd[t] = fmaf(2.f * fabsf(v), xm, bnd[t]);
         const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
         const _Float16 hi = (_Float16)xc;
-        bd[j >> 3][j & 7] = hi;  // |x''.X' - xh.Xh| <= |xh| |Xl| + |xl| |X'|
-        cer = fmaf(fabsf((float)hi), fmaf(0x1p-11f, xm, 0x1p-25f), cer);
-        cer = fmaf(fabsf(xc - (float)hi), xm, cer);
+        bd[t][j >> 3][j & 7] = hi;  // |x''.X' - xh.Xh| <= |xh| |Xl| + |xl| |X'|
+        cer[t] = fmaf(fabsf((float)hi), fmaf(0x1p-11f, xm, 0x1p-25f), cer[t]);
+        cer[t] = fmaf(fabsf(xc - (float)hi), xm, cer[t]);
       }
-      ci += __shfl_xor(ci, 32);
-      bnd += __shfl_xor(bnd, 32);
-      cer += __shfl_xor(cer, 32);
+      ci[t] += __shfl_xor(ci[t], 32);
+      bnd[t] += __shfl_xor(bnd[t], 32);
+      cer[t] += __shfl_xor(cer[t], 32);
     } else {
       // every lane walks all dims (compile-time slot positions; each lane keeps its half's slots)
 #pragma unroll
       for (int d = 0; d < 8 * NSC; ++d) {
         const float v = coord(d);
-        ci = fmaf(-v, v, ci);
-        bnd = fmaf(2.f * fabsf(v), cprm[d].xmax, bnd);
+        ci[t] = fmaf(-v, v, ci[t]);
+        bnd[t] = fmaf(2.f * fabsf(v), cprm[d].xmax, bnd[t]);
         const float xc = fminf(fmaxf(2.f * v, -60000.f), 60000.f);
         const _Float16 hi = (_Float16)xc;
         const _Float16 lo = (_Float16)(xc - (float)hi);
 #pragma unroll
         for (int comp = 0; comp < 3; ++comp) {
           const int k = 6 + 3 * d + comp;
-          if (h == ((k >> 3) & 1)) bd[k >> 4][k & 7] = comp < 2 ? hi : lo;
+          if (h == ((k >> 3) & 1)) bd[t][k >> 4][k & 7] = comp < 2 ? hi : lo;
         }
       }
     }
@@ -189,20 +191,23 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const OhPrm o0 = oprm[32 * s + 8 * h + j], o1 = oprm[32 * s + 16 + 8 * h + j];
-        bsp[s][j] = (x[o0.col] == o0.val) ? (_Float16)1.f : (_Float16)0.f;
-        bsp[s][8 + j] = (x[o1.col] == o1.val) ? (_Float16)1.f : (_Float16)0.f;
+        bsp[t][s][j] = (x[o0.col] == o0.val) ? (_Float16)1.f : (_Float16)0.f;
+        bsp[t][s][8 + j] = (x[o1.col] == o1.val) ? (_Float16)1.f : (_Float16)0.f;
       }
     }
   };
-  {
-    const int loc = c < nv ? c : (int)nv - 1;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int loc = 32 * t + c < nv ? 32 * t + c : (int)nv - 1;
     if (staged) {
-      build(xs + loc * DS);
+      build(xs + loc * DS, t);
     } else {
-      int64_t ii = cbase + c;
+      int64_t ii = cbase + 32 * t + c;
       if (ii >= Nc) ii = Nc - 1;
-      build(cand + ii * (int64_t)D);
+      build(cand + ii * (int64_t)D, t);
     }
+    // the next tile's build re-reads the parameters (no values kept live across the builds: no spills)
+    asm volatile("" ::: "memory");
   }
 
   const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
@@ -257,44 +262,44 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   };
   const f32x16 zero16 = {};
   // the tile's matrix instructions
-  auto mma = [&](f32x16& acc) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[0], zero16, 0, 0, 0);
+  auto mma = [&](f32x16& acc, const int t) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[t][0], zero16, 0, 0, 0);
 #pragma unroll
-    for (int s = 1; s < ND; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[s], acc, 0, 0, 0);
+    for (int s = 1; s < ND; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[t][s], acc, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[t][s], acc, h32_idx<KS>(aix, s, h), 0, 0);
 #pragma unroll
     for (int s = 0; s < KL; ++s)
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[t][s], acc, h32_idx<KS>(aix, s, h), 0, 0);
   };
   // the same, every fragment re-read (tile jt of nb) right behind the instruction that consumed it; a
   // signed KDE's parity product (the same index words) follows into accp
-  auto mma_rd = [&](f32x16& acc, f32x16& accp, const float* nb, int jt) {
+  auto mma_rd = [&](f32x16& acc, f32x16& accp, const float* nb, int jt, const int t = CT - 1) {
     const _Float16* a = arow(nb, jt);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[0], zero16, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[0], bd[t][0], zero16, 0, 0, 0);
     ad[0] = *(const f16x8*)a;
 #pragma unroll
     for (int s = 1; s < ND; ++s) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[s], bd[t][s], acc, 0, 0, 0);
       ad[s] = *(const f16x8*)(a + 16 * s);
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asp[s], bsp[t][s], acc, h32_idx<KS>(aix, s, h), 0, 0);
       asp[s] = *(const f16x8*)(a + 16 * ND + 16 * s);
       if (!SG && KL == 0 && s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
     }
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
-      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[s], acc, h32_idx<KS>(aix, s, h), 0, 0);
+      acc = __builtin_amdgcn_smfmac_f32_32x32x32_f16(asl[s], bsp[t][s], acc, h32_idx<KS>(aix, s, h), 0, 0);
       asl[s] = *(const f16x8*)(a + 16 * ND + 16 * KP + 16 * s);
       if (!SG && s == KL - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
     }
     if constexpr (SG) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        accp = __builtin_amdgcn_smfmac_f32_32x32x32_f16(apar[s], bsp[s], s == 0 ? zero16 : accp, h32_idx<KS>(aix, s, h),
+        accp = __builtin_amdgcn_smfmac_f32_32x32x32_f16(apar[s], bsp[t][s], s == 0 ? zero16 : accp, h32_idx<KS>(aix, s, h),
                                                         0, 0);
         apar[s] = *(const f16x8*)(a + PAR + 16 * s);
         if (s == KS - 1) aix = *(const typename H32Idx<KS>::T*)(a + ixo);
@@ -303,19 +308,20 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   };
   // Per-candidate shift (see hbx_score_h.hip): the exponent's maximum over chunk 0 is moved to 0.  The
   // probe runs without c_i (its B slots are 0); the maximum with it is c_i + the probe's maximum.
-  {
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
     f32x16 a0, a1;
     readA(lds, 0);
-    mma(a0);
+    mma(a0, t);
     readA(lds, 1);
-    mma(a1);
+    mma(a1, t);
     float mx = fmaxf(a0[0], a1[0]);
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(a0[r], a1[r]));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float d = rintf(-(ci + mx));
+    const float d = rintf(-(ci[t] + mx));
     const float dl = (d > 0.f && d < 1e30f) ? d : 0.f;  // NaN rows: no shift
-    const float cs = ci + dl;                           // the shifted c_i (its rounding is in the bound)
+    const float cs = ci[t] + dl;                        // the shifted c_i (its rounding is in the bound)
     const bool big = fabsf(cs) > H32_CMAX;              // beyond the split: the rescue pass
     const float cv = big ? 0.f : cs;
     const _Float16 p0 = (_Float16)cv;
@@ -324,16 +330,16 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     const _Float16 p2 = (_Float16)(r1 - (float)p1);
     // slots 3-5 = step 0, lane half 0, halves 3-5
     if (h == 0) {
-      bd[0][3] = p0;
-      bd[0][4] = p1;
-      bd[0][5] = p2;
+      bd[t][0][3] = p0;
+      bd[t][0][4] = p1;
+      bd[t][0][5] = p2;
     }
     if (h == 0) {
-      float* ax = aux + (wave * 32 + c) * 4;
-      ax[0] = ci;
-      ax[1] = bnd;
+      float* ax = aux + ((wave * CT + t) * 32 + c) * 4;
+      ax[0] = ci[t];
+      ax[1] = bnd[t];
       ax[2] = dl;
-      ax[3] = big ? -1.f : cer * (1.f + 0x1p-18f);  // rescue flag, else the coarse bound (rounded up)
+      ax[3] = big ? -1.f : cer[t] * (1.f + 0x1p-18f);  // rescue flag, else the coarse bound (rounded up)
     }
   }
 
@@ -376,10 +382,16 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     SgbH32<0, NMT, 32, (KS > 0 ? 2 : 1)>::run();
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto schedule_nr = [&]() {  // a phase without fragment re-reads (two column tiles: the first tile's)
+    SgbH32<0, NMT, 32, (KS > 0 ? 2 : 1), false>::run();
+    __builtin_amdgcn_sched_barrier(0);
+  };
 
   // Main loop.  Sums: a tile's 16 terms pairwise (depth 4), the chunk's two tiles (1), the chunks in
   // order (nchunks), the two lane halves (1).
-  float S = 0.f, Sb = 0.f, Sn = 0.f, Snb = 0.f;
+  float S[CT], Sb[CT], Sn = 0.f, Snb = 0.f;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) S[t] = Sb[t] = 0.f;
   f32x16 accA, accB, accpA, accpB;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -389,35 +401,87 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   readA(lds, 0);
   // one chunk; b = cc % NBUF.  The main loop is unrolled over the ring so that b is a constant there: the
   // fragment addresses are then one lane base plus ds_read immediates (no address arithmetic per tile)
-  auto chunk = [&](int cc, int b) {
+  auto chunk1 = [&](int cc, int b) {
     const float* buf = lds + b * CHF;
     const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
     // chunk cc+PD's buffer was last read before the previous iteration's barrier
-#ifndef HBX_ABL_NODMA
     issue(cc + PD, (b + PD) % NBUF, 0);
-#endif
     mma_rd(accA, accpA, buf, 1);  // T0(cc); fragments of T1(cc)
     float tn;
-    Sb += tile_sum(accB, accpB, tn);  // T1(cc-1): chunk cc-1 complete
-    S += Sb;
+    Sb[0] += tile_sum(accB, accpB, tn);  // T1(cc-1): chunk cc-1 complete
+    S[0] += Sb[0];
     if constexpr (SG) {
       Snb += tn;
       Sn += Snb;
     }
     schedule();
-#ifndef HBX_ABL_NODMA
     issue(cc + PD, (b + PD) % NBUF, 1);
-#endif
     // chunk cc+1 complete for this wave (PD-1 chunks stay in flight), every read of the ring retired;
     // the barrier makes chunk cc+1 visible to every wave
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
-#ifndef HBX_ABL_NOBAR
     __builtin_amdgcn_s_barrier();
-#endif
     mma_rd(accB, accpB, nbuf, 0);  // T1(cc); fragments of T0(cc+1)
-    Sb = tile_sum(accA, accpA, tn);  // T0(cc)
+    Sb[0] = tile_sum(accA, accpA, tn);  // T0(cc)
     if constexpr (SG) Snb = tn;
     schedule();
+  };
+  // two column tiles (unsigned sums): four phases per chunk, each one tile x one column tile; the
+  // fragments of a tile feed column tile 0 and then column tile 1, whose instructions re-read them for
+  // the next tile.  accA holds column tile 0's products, accB column tile 1's; each phase sums the
+  // accumulator the previous phase filled.  Per column tile the sums keep chunk1's association.
+  auto chunk2 = [&](int cc, int b) {
+    const float* buf = lds + b * CHF;
+    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
+    float tn;
+    issue(cc + PD, (b + PD) % NBUF, 0);
+    mma(accA, 0);                           // (T0(cc), 0)
+    Sb[CT - 1] += tile_sum(accB, accpB, tn);  // (T1(cc-1), 1): chunk cc-1 complete for column tile 1
+    S[CT - 1] += Sb[CT - 1];
+    schedule_nr();
+    mma_rd(accB, accpB, buf, 1);  // (T0(cc), 1); fragments of T1(cc)
+    Sb[0] = tile_sum(accA, accpA, tn);  // (T0(cc), 0)
+    schedule();
+    issue(cc + PD, (b + PD) % NBUF, 1);
+    mma(accA, 0);                           // (T1(cc), 0)
+    Sb[CT - 1] = tile_sum(accB, accpB, tn);  // (T0(cc), 1)
+    schedule_nr();
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    mma_rd(accB, accpB, nbuf, 0);  // (T1(cc), 1); fragments of T0(cc+1)
+    Sb[0] += tile_sum(accA, accpA, tn);  // (T1(cc), 0): chunk cc complete for column tile 0
+    S[0] += Sb[0];
+    schedule();
+  };
+  // the same in "snake" order: (T0, 0), (T0, 1), (T1, 1), (T1, 0), so every matrix instruction group shares
+  // one operand with the group before it (the A fragments, or column tile's B operands).  accA: the odd
+  // phases, accB: the even ones; column tile 0's T1 is summed in the next chunk's first phase
+  auto chunk2s = [&](int cc, int b) {
+    const float* buf = lds + b * CHF;
+    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
+    float tn;
+    issue(cc + PD, (b + PD) % NBUF, 0);
+    mma(accA, 0);                       // (T0(cc), 0)
+    Sb[0] += tile_sum(accB, accpB, tn);  // (T1(cc-1), 0): chunk cc-1 complete for column tile 0
+    S[0] += Sb[0];
+    schedule_nr();
+    mma_rd(accB, accpB, buf, 1, 1);     // (T0(cc), 1); fragments of T1(cc)
+    Sb[0] = tile_sum(accA, accpA, tn);  // (T0(cc), 0)
+    schedule();
+    issue(cc + PD, (b + PD) % NBUF, 1);
+    mma(accA, 1);                           // (T1(cc), 1)
+    Sb[CT - 1] = tile_sum(accB, accpB, tn);  // (T0(cc), 1)
+    schedule_nr();
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    mma_rd(accB, accpB, nbuf, 0, 0);          // (T1(cc), 0); fragments of T0(cc+1)
+    Sb[CT - 1] += tile_sum(accA, accpA, tn);  // (T1(cc), 1): chunk cc complete for column tile 1
+    S[CT - 1] += Sb[CT - 1];
+    schedule();
+  };
+  auto chunk = [&](int cc, int b) {
+    if constexpr (CT == 1) chunk1(cc, b);
+    else if constexpr (H32C_SNAKE) chunk2s(cc, b);
+    else chunk2(cc, b);
   };
   int cc = 0;
   for (; cc + NBUF <= nchunks; cc += NBUF) {
@@ -429,17 +493,21 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   for (; cc < nchunks; ++cc) chunk(cc, cc % NBUF);
   {
     float tn;
-    Sb += tile_sum(accB, accpB, tn);  // T1(last)
-    S += Sb;
+    constexpr int tl = (CT == 2 && H32C_SNAKE) ? 0 : CT - 1;  // the column tile of the last phase
+    Sb[tl] += tile_sum(accB, accpB, tn);  // T1(last)
+    S[tl] += Sb[tl];
     if constexpr (SG) Sn += Snb + tn;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-  S += __shfl_xor(S, 32);
+#pragma unroll
+  for (int t = 0; t < CT; ++t) S[t] += __shfl_xor(S[t], 32);
   if constexpr (SG) Sn = 2.f * (Sn + __shfl_xor(Sn, 32));  // the odd-parity terms' sum (exact doubling)
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
   if (h == 0) {
-    const int64_t ii = cbase + c;
+    const int64_t ii = cbase + 32 * t + c;
     if (ii < Nc) {
-      const float* ax = aux + (wave * 32 + c) * 4;
+      const float* ax = aux + ((wave * CT + t) * 32 + c) * 4;
       const float ci_q = ax[0], bnd_q = ax[1], dq = ax[2];
       const bool big = ax[3] < 0.f;
       const float cer_q = big ? 0.f : ax[3];
@@ -450,7 +518,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
       // S carries the factor 2^dq; |c_i| + dq bounds the rounding of the shifted c_i
       // sums: a tile's terms pairwise (depth 4; signed: its odd-parity terms in order, 16), the chunk's
       // two tiles, the chunks in order, the two lane halves
-      KdeEst o = finish_est_terms(P, S, Sn, -dq, nq, ci_q - dq, bnd_q, SG, (float)(nchunks + (SG ? 18 : 6) + 24));
+      KdeEst o = finish_est_terms(P, S[t], Sn, -dq, nq, ci_q - dq, bnd_q, SG, (float)(nchunks + (SG ? 18 : 6) + 24));
       // f16 hi/lo representation error of both coordinates (2 x 2^-22 sum|x''X'|) and the lo.lo products
       // given up (together <= 2^-22 sum|x''X'|), plus the C_j / c_i pieces' subnormal rounding
       if (o.err > 0.f) o.err += (6.f * 0x1p-22f * bnd_q + 0x1p-19f) * HBX_LN2f;
@@ -464,12 +532,13 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
         // (1 + e) 2^L - 1 (rounded up)
         if (o.err > 0.f) o.err = (1.f + o.err) * exp2f(lo_err * (1.f + 0x1p-20f)) * (1.f + 0x1p-20f) - 1.f;
       }
-      if (!nq && S == S && (big || S < 0x1p-64f || S > 0x1p100f)) {  // rescue marker
+      if (!nq && S[t] == S[t] && (big || S[t] < 0x1p-64f || S[t] > 0x1p100f)) {  // rescue marker
         o.err = -1.f;
         if (rescue_cnt) atomicAdd(rescue_cnt, 1);
       }
       out[ii] = o;
     }
+  }
   }
 }
 
@@ -479,7 +548,7 @@ template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, const KdeParams* __restrict__ P,
     const float* __restrict__ table, KdeEst* __restrict__ out) {
-  kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, P, table, out, blockIdx.x);
+  kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
 // both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
@@ -487,7 +556,7 @@ template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
-  kde_logpdf_h32_body<NSC, KP, false, FAST, CO>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+  kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
                                                 second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
                                                 a.rescue);
 }
