@@ -467,6 +467,170 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
   }
 }
 
+// Batched refit of many short segments (config #5: 1e4 brackets x 1e3 configurations at D = 32): one
+// workgroup per (segment, group of FIT_DQ dims).  The segment's rows are read ONCE, in storage order (a
+// group's slice of a row is one 64-byte piece; the segment is one contiguous block), and each slice is
+// written into LDS at its row's rank (the inverse of the argsort).  np.std's two sequential passes --
+// the sum, then the squared deviations, strictly in rank order (axis-0 order, D > 1) -- then read LDS
+// instead of gathering 256-byte rows from HBM twice (random row gathers ran at ~2 TB/s: kde_fit_stats).
+// One wave runs the 2 x FIT_DQ chains ({good, bad} x dims); the CU's other workgroup loads meanwhile.
+// Level counts: one bitmap per (set, dim), filled as the slices land (order-independent).  Segments
+// longer than FIT_LDS_ROWS take the per-column gather path inside the same kernel.
+#define FIT_LDS_ROWS 1024
+#ifndef FIT_DQ
+#define FIT_DQ 8  // dims per workgroup (LDS: FIT_LDS_ROWS x FIT_DQ doubles)
+#endif
+template <bool SQ>
+__device__ __forceinline__ double fit_chain8(const double* v, int m, double mean) {
+  auto val = [&](double x) {
+    if (SQ) {
+      const double q = x - mean;
+      return q * q;
+    }
+    return x;
+  };
+  double acc = 0.0;
+  const int m16 = m & ~15;
+  if (m16 > 0) {  // the next 16 LDS reads in flight during the current 16 dependent adds
+    double r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = v[FIT_DQ * k];
+    for (int i = 16; i < m16; i += 16) {
+      double nx[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) nx[k] = v[FIT_DQ * (i + k)];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc = acc + val(r[k]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) r[k] = nx[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc = acc + val(r[k]);
+  }
+  for (int i = m16; i < m; ++i) acc = acc + val(v[FIT_DQ * i]);
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void kde_fit_lds_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
+    const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
+    const double* __restrict__ fac_good, const double* __restrict__ fac_bad, const int32_t* __restrict__ vartype,
+    double* __restrict__ bw_good, double* __restrict__ bw_bad, int32_t* __restrict__ nlev_good,
+    int32_t* __restrict__ nlev_bad, int32_t ngroups, int64_t per_xcd) {
+  __shared__ double vals[FIT_LDS_ROWS * FIT_DQ];  // slot = rank, FIT_DQ dims per slot
+  __shared__ int16_t inv[FIT_LDS_ROWS];            // rank of each row of the segment
+  __shared__ uint32_t bits[2][FIT_DQ][32];         // observed levels per (set, dim)
+  __shared__ int32_t bad_code[2][FIT_DQ];
+  // XCD-aware: workgroup k of XCD x (blockIdx = 8 k + x) takes logical item x per_xcd + k, so the groups
+  // of one segment (neighbouring items, halves of the same 128-byte lines) run on one XCD's L2 together
+  const int64_t item = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (item >= B * ngroups) return;
+  const int64_t b = item / ngroups;
+  const int32_t d0 = (int32_t)(item % ngroups) * FIT_DQ;
+  const int nd = D - d0 < FIT_DQ ? D - d0 : FIT_DQ;
+  const int64_t s0 = seg_off[b], len = seg_off[b + 1] - s0;
+  const int64_t ng = n_good[b], nb = n_bad[b];
+  const bool okg = ng > 0 && ng <= len, okb = nb > 0 && nb <= len;
+  const int tid = threadIdx.x;
+  const int64_t* ord = order + s0;  // segment-local positions, rank order
+  const double* Xs = X + s0 * (int64_t)D;
+  auto outputs = [&](int set, int j, double bw, int32_t nl) {
+    ((set ? bw_bad : bw_good) + b * D + d0)[j] = bw;
+    ((set ? nlev_bad : nlev_good) + b * D + d0)[j] = nl;
+  };
+  if (len > FIT_LDS_ROWS) {  // long segment: one lane per (set, dim) gathers its column (kde_fit_stats' way)
+    if (tid < 2 * nd) {
+      const int set = tid / nd, j = tid % nd, d = d0 + j;
+      const int64_t ns = set ? nb : ng;
+      if (!(set ? okb : okg)) {
+        outputs(set, j, NAN, 0);
+      } else {
+        const int64_t* o = ord + (set ? len - ns : 0);
+        const double mean = np_sum_column(Xs, D, d, o, ns, 0.0, false) / (double)ns;
+        const double var = np_sum_column(Xs, D, d, o, ns, mean, true) / (double)ns;
+        int32_t cnt = 0;
+        if (vartype[d] != 0) {
+          uint32_t* bm = (uint32_t*)vals + tid * 33;
+          for (int w = 0; w < 32; ++w) bm[w] = 0u;
+          for (int64_t i = 0; i < ns && cnt >= 0; ++i) {
+            const double x = Xs[o[i] * (int64_t)D + d];
+            const int v = (int)x;
+            if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
+              cnt = -1;
+              break;
+            }
+            const uint32_t m = 1u << (v & 31);
+            if (!(bm[v >> 5] & m)) {
+              bm[v >> 5] |= m;
+              ++cnt;
+            }
+          }
+        }
+        outputs(set, j, (1.06 * sqrt(var)) * (set ? fac_bad[b] : fac_good[b]), cnt);
+      }
+    }
+    return;
+  }
+  for (int i = tid; i < 2 * FIT_DQ * 32; i += 256) (&bits[0][0][0])[i] = 0u;
+  if (tid < 2 * FIT_DQ) (&bad_code[0][0])[tid] = 0;
+  for (int64_t r = tid; r < len; r += 256) inv[ord[r]] = (int16_t)r;
+  __syncthreads();
+  // the slices: element e = (row e / FIT_DQ, dim e % FIT_DQ), U loads per thread in flight
+  const int64_t total = len * FIT_DQ;
+  const int j = tid % FIT_DQ;  // uniform per thread across e (256 is a multiple of FIT_DQ)
+  const bool catd = j < nd && vartype[d0 + j] != 0;
+  constexpr int U = 16;
+  for (int64_t e0 = 0; e0 < total; e0 += 256 * U) {
+    double v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t e = e0 + k * 256 + tid;
+      v[k] = (e < total && j < nd) ? Xs[(e / FIT_DQ) * D + d0 + j] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t e = e0 + k * 256 + tid;
+      if (e < total && j < nd) {
+        const int slot = inv[e / FIT_DQ];
+        vals[slot * FIT_DQ + j] = v[k];
+        if (catd) {
+          const double x = v[k];
+          const int iv = (int)x;
+          const bool in_g = okg && slot < ng, in_b = okb && slot >= len - nb;
+          if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) {
+            if (in_g) bad_code[0][j] = 1;
+            if (in_b) bad_code[1][j] = 1;
+          } else {
+            const uint32_t m = 1u << (iv & 31);
+            if (in_g) atomicOr(&bits[0][j][iv >> 5], m);
+            if (in_b) atomicOr(&bits[1][j][iv >> 5], m);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * FIT_DQ) {  // wave 0: the chains
+    const int set = tid / FIT_DQ, jj = tid % FIT_DQ;
+    if (jj < nd) {
+      const int64_t ns = set ? nb : ng;
+      if (!(set ? okb : okg)) {
+        outputs(set, jj, NAN, 0);
+      } else {
+        const double* col = vals + (set ? len - ns : 0) * FIT_DQ + jj;
+        const double mean = fit_chain8<false>(col, (int)ns, 0.0) / (double)ns;
+        const double var = fit_chain8<true>(col, (int)ns, mean) / (double)ns;
+        int32_t cnt = 0;
+        if (vartype[d0 + jj] != 0) {
+          for (int w = 0; w < 32; ++w) cnt += __popc(bits[set][jj][w]);
+          if (bad_code[set][jj]) cnt = -1;
+        }
+        outputs(set, jj, (1.06 * sqrt(var)) * (set ? fac_bad[b] : fac_good[b]), cnt);
+      }
+    }
+  }
+}
+
 extern "C" {
 
 int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
@@ -563,7 +727,15 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
   if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
   if (B <= 0) return HBX_OK;
   const int64_t total = B * 2 * D;
-  if (D > 1 && total < 16384) {  // few columns: one workgroup each (LDS-staged gathers)
+  const char* lenv = getenv("HBX_FIT_LDS");  // 0: the thread-per-column gather kernel for many segments
+  if (D > 1 && total >= 16384 && !(lenv && atoi(lenv) == 0)) {  // many segments: rows read once into LDS
+    const int32_t ngroups = (D + FIT_DQ - 1) / FIT_DQ;
+    const int64_t per_xcd = (B * ngroups + 7) / 8;
+    if (8 * per_xcd > 0x7fffffffLL) return hbx_fail(HBX_ERR_ARG, "hbx_kde_fit: too many segments");
+    hipLaunchKernelGGL(kde_fit_lds_kernel, dim3((unsigned)(8 * per_xcd)), dim3(256), 0, (hipStream_t)stream, X, D,
+                       seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good,
+                       nlev_bad, ngroups, per_xcd);
+  } else if (D > 1 && total < 16384) {  // few columns: one workgroup each (LDS-staged gathers)
     hipLaunchKernelGGL(kde_fit_col_kernel, dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, X, D, seg_off,
                        order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad);
   } else {

@@ -733,12 +733,32 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
   kde_rescue_body<DCP, SIGNED>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
+// a single acquisition's state before its combine / shortlist / exact / final steps
+__device__ __forceinline__ void acq_init_state(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1,
+                                               AcqResult* res) {
+  *U = hbx_f2ord(INFINITY);
+  *first1 = INT32_MAX;
+  *count = 0;
+  *flags = 0;
+  res->index = -1;
+  res->score = NAN;
+  res->pdf_l = NAN;
+  res->pdf_g = NAN;
+  res->shortlist = 0;
+  res->flags = 0;
+  res->near = 0;
+  res->rel = 0.f;
+}
+
 // both KDEs' rescue passes in one launch (blocks [0, nblk0) KDE 0, the rest KDE 1)
 // grid-stride over the 2 nblk0 logical blocks; with the scoring kernel's marker count available and 0
-// (the common case) every workgroup exits after one load
+// (the common case) every workgroup exits after one load; its first
+// workgroup also initialises a single acquisition's state (acq_init's work)
 template <int DCP, bool SIGNED>
 __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                               KdePairArgs a) {
+  if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)  // a single acquisition's state (acq_init's work)
+    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
   if (a.rescue && __hip_atomic_load(a.rescue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   for (unsigned b = blockIdx.x; b < 2 * a.nblk0; b += gridDim.x) {
     const bool second = b >= a.nblk0;
@@ -751,20 +771,7 @@ __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __re
 // score intervals, shortlist, exact re-score, final argmin
 
 __global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1, AcqResult* res) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    *U = hbx_f2ord(INFINITY);
-    *first1 = INT32_MAX;
-    *count = 0;
-    *flags = 0;
-    res->index = -1;
-    res->score = NAN;
-    res->pdf_l = NAN;
-    res->pdf_g = NAN;
-    res->shortlist = 0;
-    res->flags = 0;
-    res->near = 0;
-    res->rel = 0.f;
-  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) acq_init_state(U, count, flags, first1, res);
 }
 
 // batched acquisition: per-segment bound, flags, shortlist count, best score and (index, position) key
@@ -1248,17 +1255,15 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
   return s < INFINITY && s <= best * (1.0 + 1.0001 * (rp + rb));
 }
 
-__global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restrict__ list,
-                                                        const int32_t* __restrict__ count,
-                                                        const double* exact_l,  // (written in this kernel
-                                                        const double* exact_g,  //  through exact_lw / _gw)
-                                                        const int32_t* __restrict__ flags, int64_t index_base,
-                                                        const KdeParams* __restrict__ Pg,
-                                                        const KdeParams* __restrict__ Pb,
-                                                        const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
-                                                        int32_t* __restrict__ near_list, AcqResult* __restrict__ res,
-                                                        int32_t nbuf, const double* __restrict__ part,
-                                                        double* exact_lw, double* exact_gw) {
+// the final argmin of one acquisition (256 threads): the split re-score's unit sums -> pdfs, strict '<'
+// first-index argmin over the shortlist, the near set, the result record
+__device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                               const double* exact_l,  // (written here through exact_lw / _gw)
+                               const double* exact_g, const int32_t* __restrict__ flags, int64_t index_base,
+                               const KdeParams* __restrict__ Pg, const KdeParams* __restrict__ Pb,
+                               const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
+                               int32_t* __restrict__ near_list, AcqResult* __restrict__ res, int32_t nbuf,
+                               const double* part, double* exact_lw, double* exact_gw) {
   __shared__ double bs[256];
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
@@ -1337,6 +1342,19 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
       res->pdf_g = exact_g[wp];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ count, const double* exact_l,
+                                                        const double* exact_g, const int32_t* __restrict__ flags,
+                                                        int64_t index_base, const KdeParams* __restrict__ Pg,
+                                                        const KdeParams* __restrict__ Pb,
+                                                        const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
+                                                        int32_t* __restrict__ near_list, AcqResult* __restrict__ res,
+                                                        int32_t nbuf, const double* __restrict__ part,
+                                                        double* exact_lw, double* exact_gw) {
+  kde_final_body(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
+                 exact_lw, exact_gw);
 }
 
 // Batched argmin, three passes over the shortlist: (1) per-segment minimum of the exact score,
@@ -1560,20 +1578,23 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 // records [0] and [1] only ([1] after everything).
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
-                         int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s) {
+                         int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s,
+                         KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr) {
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
-    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt};
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt, {}};
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
       hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
       hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
+    a.init = init;  // the acquisition state, set by the rescue pass's first workgroup
+    if (inited) *inited = init.U != nullptr;
     // the rescue pass: grid-stride, exits at once unless the scoring kernel counted a marker
     const unsigned grr = rescue_cnt ? (2 * gr < 1024u ? 2 * gr : 1024u) : 2 * gr;
     hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
@@ -1876,18 +1897,23 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   // the scoring launch goes first (it touches none of the per-acquisition state), so the GPU starts on
   // it while the host is still enqueueing the rest
   const bool scored = Nc > 0 && !exact_only;
+  bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
+    KdePairArgs::AcqInitPtrs ip{};
+    if (!batch_res) ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res};
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
-                                 (int32_t*)(ws + w.rescue), s);
+                                 (int32_t*)(ws + w.rescue), s, ip, &inited);
     if (rc) return rc;
   }
-  if (batch_res)
+  if (batch_res) {
     hipLaunchKernelGGL(acq_init_batch_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, U, flags,
                        segcnt, best, key, first1, count, segnear);
-  else
+    HBX_LAUNCH_CHECK();
+  } else if (!inited) {
     hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res);
-  HBX_LAUNCH_CHECK();
+    HBX_LAUNCH_CHECK();
+  }
   const dim3 grid((unsigned)((Nc + 255) / 256));
   bool fuse_combine = false;
   if (Nc > 0) {
@@ -2099,6 +2125,65 @@ int hbx_event_elapsed_ms(void* start, void* stop, float* ms) {
 }
 
 void* hbx_kde_result_ptr(void* workspace) { return (char*)workspace + ws_layout(0, 0).res; }
+
+// A small device buffer (an acquisition's result record) to the host with no copy engine and no blocking
+// synchronisation: one wave copies it into this thread's device-mapped coherent host buffer, then stores a
+// completion word last (system scope, after a system fence); the host spins on that word (bounded: then
+// the stream is synchronised) and copies the bytes out.  A DMA copy + stream synchronisation of the
+// 48-byte record cost ~28 us per acquisition (tools/step_breakdown.py)
+__global__ void fetch_publish_kernel(const uint32_t* __restrict__ src, int32_t words, uint32_t* dst, int32_t* done,
+                                     int32_t seq) {
+  for (int i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+#define FETCH_MAPPED_BYTES 4096
+int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) {
+  if (bytes < 0 || (bytes > 0 && (!host_dst || !dev_src))) return hbx_fail(HBX_ERR_ARG, "hbx_fetch: bad arguments");
+  const hipStream_t s = (hipStream_t)stream;
+  // this thread's mapped buffer: FETCH_MAPPED_BYTES of data, then the completion word (kept for the thread)
+  thread_local char* mapped = nullptr;
+  thread_local int32_t seq = 0;
+  const bool small = bytes <= FETCH_MAPPED_BYTES && (bytes & 3) == 0 && ((uintptr_t)dev_src & 3) == 0;
+  if (small && !mapped) {
+    void* p = nullptr;
+    HBX_HIP(hipHostMalloc(&p, FETCH_MAPPED_BYTES + 64,
+                          hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    void* dp = nullptr;
+    HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
+    if (dp != p) {
+      (void)hipHostFree(p);
+      return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+    }
+    mapped = (char*)p;
+    *(volatile int32_t*)(mapped + FETCH_MAPPED_BYTES) = 0;
+  }
+  if (!small) {  // larger or unaligned: a copy, then the stream polled to completion
+    if (bytes > 0) HBX_HIP(hipMemcpyAsync(host_dst, dev_src, (size_t)bytes, hipMemcpyDeviceToHost, s));
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) return hbx_fail(HBX_ERR_HIP, "hbx_fetch: %s", hipGetErrorString(e));
+    return HBX_OK;
+  }
+  int32_t* done = (int32_t*)(mapped + FETCH_MAPPED_BYTES);
+  seq = seq == INT32_MAX ? 1 : seq + 1;
+  hipLaunchKernelGGL(fetch_publish_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)dev_src, (int32_t)(bytes / 4),
+                     (uint32_t*)mapped, done, seq);
+  HBX_LAUNCH_CHECK();
+  // ~0.1 s of polling covers any acquisition queued ahead on the stream; past it, block on the stream
+  bool seen = false;
+  for (int64_t i = 0; i < 20000000 && !seen; ++i) seen = __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq;
+  if (!seen) {
+    HBX_HIP(hipStreamSynchronize(s));
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
+      return hbx_fail(HBX_ERR_HIP, "hbx_fetch: the copy kernel did not store its completion word");
+  }
+  memcpy(host_dst, mapped, (size_t)bytes);
+  return HBX_OK;
+}
 
 // numpy's float64 exp (hbx_npexp.h) element-wise: the known-answer check of the exact re-score's exp
 __global__ void np_exp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {

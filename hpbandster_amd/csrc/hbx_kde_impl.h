@@ -258,6 +258,15 @@ struct KdePairArgs {
   // acquisition workspace counter of rescue-marked candidates (nullable): the scoring kernel counts its
   // markers, the rescue pass exits at once on 0, the combine kernel zeroes it for the next acquisition
   int32_t* rescue;
+  // single acquisition (nullable): the per-acquisition state the rescue pass initialises in its first
+  // block (acq_init's work, one launch less): U, count, flags, first1, the result record
+  struct AcqInitPtrs {
+    uint32_t* U;
+    int32_t* count;
+    int32_t* flags;
+    int32_t* first1;
+    struct AcqResult* res;
+  } init;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
 

@@ -69,9 +69,10 @@ _pinned_tls = threading.local()
 
 
 def fetch_bytes(dev_bytes, stream=None):
-    """Bytes of a small device uint8 tensor (a result record) on the host: one copy into a per-thread,
-    per-device pinned buffer on ``stream`` (default: the tensor's device's current stream), one
-    stream synchronisation -- instead of a pageable copy."""
+    """Bytes of a small device uint8 tensor (a result record) on the host: one native call (hbx_fetch)
+    copies them into a per-thread, per-device pinned buffer on ``stream`` (default: the tensor's
+    device's current stream) and polls that stream to completion -- instead of a pageable copy, or a
+    torch copy plus a blocking stream synchronisation (~25 us more per acquisition)."""
     torch = _torch()
     n = int(dev_bytes.numel())
     dev = dev_bytes.device
@@ -83,10 +84,10 @@ def fetch_bytes(dev_bytes, stream=None):
     if buf is None or buf.numel() < n:
         buf = torch.empty(max(n, 4096), dtype=torch.uint8, pin_memory=True)
         cache[key] = buf
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
-    with torch.cuda.stream(s):
-        buf[:n].copy_(dev_bytes, non_blocking=True)
-    s.synchronize()
+    if not dev_bytes.is_contiguous():
+        raise N.HbxError("fetch_bytes: contiguous device bytes expected")
+    # one native call: the copy into the pinned buffer, then the stream polled to completion
+    N.check(N.lib().hbx_fetch(buf.data_ptr(), dev_bytes.data_ptr(), n, N.stream_handle(stream, dev)))
     return buf[:n].numpy().tobytes()
 
 

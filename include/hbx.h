@@ -172,6 +172,11 @@ int hbx_event_create(void** ev);
 int hbx_event_destroy(void* ev);
 int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
+/* Copy `bytes` of device memory (e.g. the result record) to pinned host memory on `stream` and wait for
+ * that stream by polling it (no blocking synchronisation).  Replaces the caller's copy + synchronise
+ * after hbx_kde_acquire (the reference's get_config returns the pick to its caller: bohb.py:166). */
+int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
+
 /* Device address of the result record inside an acquisition workspace (48 bytes):
  *   {i64 index, f64 score, f32 rel, i32 flags, i32 shortlist, i32 near, f64 pdf_l, f64 pdf_g}
  * index: first index of the minimal exact score (-1: no finite score); rel: bound of
