@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
 // longer than FIT_LDS_ROWS take the per-column gather path inside the same kernel.
 #define FIT_LDS_ROWS 1024
 #ifndef FIT_DQ
-#define FIT_DQ 8  // dims per workgroup (LDS: FIT_LDS_ROWS x FIT_DQ doubles)
+#define FIT_DQ 4  // dims per workgroup (LDS: FIT_LDS_ROWS x FIT_DQ doubles; 4: four workgroups per CU)
 #endif
 template <bool SQ>
 __device__ __forceinline__ double fit_chain8(const double* v, int m, double mean) {
