@@ -511,6 +511,43 @@ __device__ __forceinline__ double fit_chain8(const double* v, int m, double mean
   return acc;
 }
 
+// One (set, dim) column of a segment by gathering its rows through the order (kde_fit_stats' way): the
+// long-segment path of the LDS kernels.  bm: 33 words of this lane's scratch (level bitmap).
+__device__ void fit_column_gather(const double* Xs, int32_t D, const int64_t* ord, int64_t len, int set, int d,
+                                  int64_t ng, int64_t nb, double fg, double fb, const int32_t* vartype, uint32_t* bm,
+                                  double* bwg, double* bwb, int32_t* nlg, int32_t* nlb) {
+  const int64_t ns = set ? nb : ng;
+  double* bwo = (set ? bwb : bwg) + d;
+  int32_t* nlo = (set ? nlb : nlg) + d;
+  if (ns <= 0 || ns > len) {
+    *bwo = NAN;
+    *nlo = 0;
+    return;
+  }
+  const int64_t* o = ord + (set ? len - ns : 0);
+  const double mean = np_sum_column(Xs, D, d, o, ns, 0.0, false) / (double)ns;
+  const double var = np_sum_column(Xs, D, d, o, ns, mean, true) / (double)ns;
+  int32_t cnt = 0;
+  if (vartype[d] != 0) {
+    for (int w = 0; w < 32; ++w) bm[w] = 0u;
+    for (int64_t i = 0; i < ns && cnt >= 0; ++i) {
+      const double x = Xs[o[i] * (int64_t)D + d];
+      const int v = (int)x;
+      if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
+        cnt = -1;
+        break;
+      }
+      const uint32_t m = 1u << (v & 31);
+      if (!(bm[v >> 5] & m)) {
+        bm[v >> 5] |= m;
+        ++cnt;
+      }
+    }
+  }
+  *bwo = (1.06 * sqrt(var)) * (set ? fb : fg);
+  *nlo = cnt;
+}
+
 __global__ __launch_bounds__(256) void kde_fit_lds_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
     const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
@@ -539,36 +576,10 @@ __global__ __launch_bounds__(256) void kde_fit_lds_kernel(
     ((set ? nlev_bad : nlev_good) + b * D + d0)[j] = nl;
   };
   if (len > FIT_LDS_ROWS) {  // long segment: one lane per (set, dim) gathers its column (kde_fit_stats' way)
-    if (tid < 2 * nd) {
-      const int set = tid / nd, j = tid % nd, d = d0 + j;
-      const int64_t ns = set ? nb : ng;
-      if (!(set ? okb : okg)) {
-        outputs(set, j, NAN, 0);
-      } else {
-        const int64_t* o = ord + (set ? len - ns : 0);
-        const double mean = np_sum_column(Xs, D, d, o, ns, 0.0, false) / (double)ns;
-        const double var = np_sum_column(Xs, D, d, o, ns, mean, true) / (double)ns;
-        int32_t cnt = 0;
-        if (vartype[d] != 0) {
-          uint32_t* bm = (uint32_t*)vals + tid * 33;
-          for (int w = 0; w < 32; ++w) bm[w] = 0u;
-          for (int64_t i = 0; i < ns && cnt >= 0; ++i) {
-            const double x = Xs[o[i] * (int64_t)D + d];
-            const int v = (int)x;
-            if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
-              cnt = -1;
-              break;
-            }
-            const uint32_t m = 1u << (v & 31);
-            if (!(bm[v >> 5] & m)) {
-              bm[v >> 5] |= m;
-              ++cnt;
-            }
-          }
-        }
-        outputs(set, j, (1.06 * sqrt(var)) * (set ? fac_bad[b] : fac_good[b]), cnt);
-      }
-    }
+    if (tid < 2 * nd)
+      fit_column_gather(Xs, D, ord, len, tid / nd, d0 + tid % nd, ng, nb, fac_good[b], fac_bad[b], vartype,
+                        (uint32_t*)vals + tid * 33, bw_good + b * D, bw_bad + b * D, nlev_good + b * D,
+                        nlev_bad + b * D);
     return;
   }
   for (int i = tid; i < 2 * FIT_DQ * 32; i += 256) (&bits[0][0][0])[i] = 0u;
@@ -630,6 +641,7 @@ __global__ __launch_bounds__(256) void kde_fit_lds_kernel(
     }
   }
 }
+
 
 extern "C" {
 
