@@ -648,3 +648,31 @@ def test_coarse_prescreen_matches_fast_and_oracle(device, dc, du, lev, monkeypat
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C[:800], pair.good.nlev)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C[:800], pair.bad.nlev)
     assert pair.acquire(C[:800]).index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("nc", [1, 31, 32, 33, 63, 64, 65, 100, 511, 512, 513, 577])
+def test_coarse_two_column_tiles_ragged(device, nc, monkeypatch):
+    """The coarse instance's waves hold 64 candidates (two 32-column tiles): candidate counts that end inside
+    the first or the second column tile of a wave, or of a 512-candidate block, give the FAST instance's
+    record; and with the oracle's best candidate moved to the LAST position (column tile 1 of the last wave
+    when nc mod 64 > 32) the pick follows it."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lev, n = 24, 8, 4, 2000
+    X = S.make_observations(n, dc, du, lev, seed=91)
+    L = S.make_losses(n, seed=92)
+    vt = S.var_type_string(dc, du)
+    C = S.make_candidates(max(nc, 2), dc, du, lev, seed=93)[:nc].copy()
+    monkeypatch.setenv("HBX_COARSE", "1")
+    pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    assert (pair.bad.variant >> 7) & 1 == 1
+    monkeypatch.setenv("HBX_COARSE", "0")
+    pair0 = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
+    l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+    g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+    best = O.select(l, g)[0]
+    order = [i for i in range(nc) if i != best] + [best]
+    for cands, want in ((C, best), (C[order], nc - 1)):
+        co, fa = pair.acquire(cands), pair0.acquire(cands)
+        assert (co.index, co.score, co.pdf_l, co.pdf_g) == (fa.index, fa.score, fa.pdf_l, fa.pdf_g)
+        assert co.index == want
