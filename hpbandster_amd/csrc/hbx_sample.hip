@@ -22,6 +22,8 @@
 
 #include "hbx_common.h"
 #include "hbx_philox.h"
+#include <string.h>
+#include <stdlib.h>
 
 #define SAMPLE_BLOCK 256
 #define DATUM_WORD 0xFFFFFFFFu  // counter word of the per-candidate datum draw (dims use 0..D-1)
@@ -236,6 +238,59 @@ __global__ __launch_bounds__(512) void kde_sample_kernel(
   }
 }
 
+// The same draws with one (candidate, pair of dims) per lane: 8 lanes per candidate, lane g of the group
+// takes the pairs g, g + 8, ...  A candidate's datum row and Phi-table row are then read by its 8 lanes
+// as contiguous 16-byte pieces (a wave touches ~6 cache lines per candidate instead of 64: the lane-per-
+// candidate kernel above waits on the 64 distinct lines every one of its gathers touches) and its output
+// row is written as contiguous 16-byte stores, no LDS tile.  Dim types and bandwidths vary across the
+// lanes (loaded per lane; the categorical branch is the cheap one).  Counter (candidate, pair, stream),
+// datum draw and arithmetic are the lane-per-candidate kernel's: the draws are identical.
+template <bool TAB>
+__global__ __launch_bounds__(256) void kde_sample_pair_kernel(
+    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
+    const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
+    double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
+    double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
+  __shared__ int32_t sdat[32];
+  __shared__ double srh[HBX_MAX_D];  // 1 / bw per dim
+  const int64_t c0 = (int64_t)blockIdx.x * 32;  // 32 candidates per block: 8 lanes each
+  const int nc = (int)(Nc - c0 < 32 ? Nc - c0 : 32);
+  for (int t = threadIdx.x; t < D; t += 256) srh[t] = 1.0 / bw[t];
+  if (threadIdx.x < nc) {
+    const int64_t i = c0 + threadIdx.x;
+    const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)i, DATUM_WORD, stream_id), 0);
+    const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
+    sdat[threadIdx.x] = idx;
+    if (datum) datum[i] = idx;
+  }
+  __syncthreads();
+  const int cl = threadIdx.x >> 3, g = threadIdx.x & 7;
+  if (cl >= nc) return;
+  const int64_t i = c0 + cl;
+  const int32_t idx = sdat[cl];
+  const double* xr = X + rows[idx] * (int64_t)D;
+  double* out = cands + i * (int64_t)D;
+  const int D2 = (D + 1) >> 1;
+  bool derr = false;
+  for (int k = g; k < D2; k += 8) {
+    const int d = 2 * k;
+    const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
+    const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
+    if (d + 1 < D) {
+      const double v1 = sample_dim<TAB>(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
+      if ((D & 1) == 0) {
+        *(double2*)(out + d) = make_double2(v0, v1);
+      } else {
+        out[d] = v0;
+        out[d + 1] = v1;
+      }
+    } else {
+      out[d] = v0;
+    }
+  }
+  if (derr && domain_err) domain_err[i] = 1;  // any of the candidate's lanes (same byte, same value)
+}
+
 extern "C" {
 
 int hbx_philox4x32_10(const uint32_t* counter, const uint32_t* key, uint32_t* out) {
@@ -282,6 +337,16 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   const size_t lds = (size_t)64 * ((D + 2) & ~1) * sizeof(double);
   const int64_t blocks = (Nc + 63) / 64;
   if (blocks > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
+  const char* kenv = getenv("HBX_SAMPLE_LANES");  // "candidate": the lane-per-candidate kernel
+  if (!(kenv && !strcmp(kenv, "candidate")) && D <= HBX_MAX_D) {  // one (candidate, pair of dims) per lane
+    const int64_t pb = (Nc + 31) / 32;
+    if (pb > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
+    hipLaunchKernelGGL(tab ? kde_sample_pair_kernel<true> : kde_sample_pair_kernel<false>, dim3((unsigned)pb), dim3(256),
+                       0, s, X, D, rows, n, bw, levels, (const double2*)tab, bw_factor, seed, counter_base, stream_id,
+                       Nc, cands, datum, domain_err);
+    HBX_LAUNCH_CHECK();
+    return HBX_OK;
+  }
   const void* kfn = tab ? (const void*)kde_sample_kernel<true> : (const void*)kde_sample_kernel<false>;
   if (lds > 65536)  // D > 126: the tile needs more than the default dynamic LDS limit (<= 132 KB at D = 256)
     HBX_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
