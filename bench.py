@@ -783,7 +783,7 @@ def main():
         from hpbandster_amd.distributed import WinnerExchange
         xchg = WinnerExchange(device, transport="rccl" if a.backend == "nccl" else "records")
 
-    def step():
+    def step(ev):
         rv = pair.acquire(c_dev, index_base=base, workspace=ws, sync=False, events=ev)
         if xchg is not None:
             rv = xchg.exchange(rv)
@@ -793,26 +793,30 @@ def main():
         return r.index, r.score
 
     for _ in range(a.warmup):
-        step()
+        step(ev)
+    # every timed step stamps its scoring launch with its own events, read after the timed region (the
+    # reads are measurement, not part of a step)
+    evs = [kde.ScoreEvents() for _ in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t_l = t_g = 0.0
-    launch_ms = []  # the scoring launch of every timed step (HIP events on its stream)
     t0 = time.perf_counter()
     winner = None
     for s in range(a.steps):
-        winner = step()
-        ml, mg = ev.elapsed_ms(fused)  # step() synchronised on the result: events are complete
-        t_l += ml
-        t_g += mg
-        launch_ms.append(ml + mg)
+        winner = step(evs[s])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    t_l = t_g = 0.0
+    launch_ms = []  # the scoring launch of every timed step (HIP events on its stream)
+    for e in evs:
+        ml, mg = e.elapsed_ms(fused)
+        t_l += ml
+        t_g += mg
+        launch_ms.append(ml + mg)
     last = kde.AcqResult.from_bytes(ws[int(pair.result_offset()):int(pair.result_offset()) + kde.RESULT_BYTES]
                                     .cpu().numpy().tobytes())
     if world > 1:

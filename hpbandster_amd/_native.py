@@ -151,8 +151,13 @@ def stream_handle(stream=None, device=None):
     """hipStream_t of ``stream``, else torch's current stream of ``device`` (not of the calling thread's
     current device: a dispatcher thread's current device is 0 whatever device the model lives on)."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream(device)
-    return s.cuda_stream
+    if stream is not None:
+        return stream.cuda_stream
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:  # the raw handle, without building a Stream object per engine call
+        idx = None if device is None else device if isinstance(device, int) else torch.device(device).index
+        return raw(torch.cuda.current_device() if idx is None else int(idx))
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 class on_device(object):
