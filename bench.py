@@ -784,9 +784,11 @@ def main():
         xchg = WinnerExchange(device, transport="rccl" if a.backend == "nccl" else "records")
 
     def step(ev):
+        if xchg is None:  # one rank: the acquisition's record reaches the host in the same native call
+            r = pair.acquire(c_dev, index_base=base, workspace=ws, events=ev)
+            return r.index, r.score
         rv = pair.acquire(c_dev, index_base=base, workspace=ws, sync=False, events=ev)
-        if xchg is not None:
-            rv = xchg.exchange(rv)
+        rv = xchg.exchange(rv)
         # the winner reaches the host (what BOHB needs); the exact scores are the pinned reference's
         # float64 values bit for bit, so the (score, index) reduction is the reference's pick
         r = kde.AcqResult.from_bytes(kde.fetch_bytes(rv))

@@ -42,6 +42,10 @@ SIGNATURES = {
                                 c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
                                 c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_acquire_host": (c_i32, [c_vp, c_i64, c_i32, c_i64,
+                                     c_vp, c_vp, c_vp, c_vp, c_i32,
+                                     c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
+                                     c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "hbx_kde_batch_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "hbx_kde_acquire_batch": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i64,
                                       c_vp, c_vp, c_vp, c_vp, c_i32,

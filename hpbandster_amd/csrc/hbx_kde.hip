@@ -1263,7 +1263,8 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
                                const KdeParams* __restrict__ Pg, const KdeParams* __restrict__ Pb,
                                const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
                                int32_t* __restrict__ near_list, AcqResult* __restrict__ res, int32_t nbuf,
-                               const double* part, double* exact_lw, double* exact_gw) {
+                               const double* part, double* exact_lw, double* exact_gw, AcqResult* host_res,
+                               int32_t* done, int32_t seq) {
   __shared__ double bs[256];
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
@@ -1341,6 +1342,11 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
       res->pdf_l = exact_l[wp];
       res->pdf_g = exact_g[wp];
     }
+    if (host_res) {  // hbx_kde_acquire_host: the record to mapped host memory, then the completion word
+      *host_res = *res;
+      __threadfence_system();
+      __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -1352,9 +1358,10 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
                                                         const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
                                                         int32_t* __restrict__ near_list, AcqResult* __restrict__ res,
                                                         int32_t nbuf, const double* __restrict__ part,
-                                                        double* exact_lw, double* exact_gw) {
+                                                        double* exact_lw, double* exact_gw, AcqResult* host_res,
+                                                        int32_t* done, int32_t seq) {
   kde_final_body(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
-                 exact_lw, exact_gw);
+                 exact_lw, exact_gw, host_res, done, seq);
 }
 
 // Batched argmin, three passes over the shortlist: (1) per-segment minimum of the exact score,
@@ -1853,7 +1860,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                         const int64_t* rows_good, int32_t variant_good, const void* params_bad,
                         const float* table_bad, const double* X_bad, const int64_t* rows_bad, int32_t variant_bad,
                         int32_t dc_pad, int32_t du_pad, int64_t nmax, float* logl_out, float* logg_out,
-                        AcqResult* batch_res, void* workspace, int64_t ws_bytes, void* events, void* stream) {
+                        AcqResult* batch_res, void* workspace, int64_t ws_bytes, void* events, void* stream,
+                        AcqResult* host_res = nullptr, int32_t* done = nullptr, int32_t seq = 0) {
   if ((!cand && Nc > 0) || !params_good || !table_good || !X_good || !rows_good || !params_bad || !table_bad ||
       !X_bad || !rows_bad || !workspace)
     return hbx_fail(HBX_ERR_ARG, "%s: null pointer", who);
@@ -1952,7 +1960,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
                        index_base, (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, res,
                        (int32_t)((nmax + PW_BUF - 1) / PW_BUF), fuse_combine ? part : (const double*)nullptr,
-                       exact_l, exact_g);
+                       exact_l, exact_g, host_res, done, seq);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }
@@ -2140,14 +2148,12 @@ __global__ void fetch_publish_kernel(const uint32_t* __restrict__ src, int32_t w
 }
 
 #define FETCH_MAPPED_BYTES 4096
-int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) {
-  if (bytes < 0 || (bytes > 0 && (!host_dst || !dev_src))) return hbx_fail(HBX_ERR_ARG, "hbx_fetch: bad arguments");
-  const hipStream_t s = (hipStream_t)stream;
-  // this thread's mapped buffer: FETCH_MAPPED_BYTES of data, then the completion word (kept for the thread)
-  thread_local char* mapped = nullptr;
-  thread_local int32_t seq = 0;
-  const bool small = bytes <= FETCH_MAPPED_BYTES && (bytes & 3) == 0 && ((uintptr_t)dev_src & 3) == 0;
-  if (small && !mapped) {
+// this thread's device-mapped coherent host buffer: FETCH_MAPPED_BYTES of data, then the completion word
+// (allocated on first use and kept for the thread's lifetime)
+thread_local char* t_mapped = nullptr;
+thread_local int32_t t_seq = 0;
+static int mapped_buffer(char** out) {
+  if (!t_mapped) {
     void* p = nullptr;
     HBX_HIP(hipHostMalloc(&p, FETCH_MAPPED_BYTES + 64,
                           hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
@@ -2157,8 +2163,33 @@ int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) 
       (void)hipHostFree(p);
       return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
     }
-    mapped = (char*)p;
-    *(volatile int32_t*)(mapped + FETCH_MAPPED_BYTES) = 0;
+    t_mapped = (char*)p;
+    *(volatile int32_t*)(t_mapped + FETCH_MAPPED_BYTES) = 0;
+  }
+  *out = t_mapped;
+  return HBX_OK;
+}
+
+// spin on the completion word (bounded: ~0.1 s, then the stream is synchronised)
+static int wait_done(int32_t* done, int32_t seq, hipStream_t s, const char* who) {
+  bool seen = false;
+  for (int64_t i = 0; i < 20000000 && !seen; ++i) seen = __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq;
+  if (!seen) {
+    HBX_HIP(hipStreamSynchronize(s));
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
+      return hbx_fail(HBX_ERR_HIP, "%s: the device did not store its completion word", who);
+  }
+  return HBX_OK;
+}
+
+int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) {
+  if (bytes < 0 || (bytes > 0 && (!host_dst || !dev_src))) return hbx_fail(HBX_ERR_ARG, "hbx_fetch: bad arguments");
+  const hipStream_t s = (hipStream_t)stream;
+  const bool small = bytes <= FETCH_MAPPED_BYTES && (bytes & 3) == 0 && ((uintptr_t)dev_src & 3) == 0;
+  char* mapped = nullptr;
+  if (small) {
+    const int rc = mapped_buffer(&mapped);
+    if (rc) return rc;
   }
   if (!small) {  // larger or unaligned: a copy, then the stream polled to completion
     if (bytes > 0) HBX_HIP(hipMemcpyAsync(host_dst, dev_src, (size_t)bytes, hipMemcpyDeviceToHost, s));
@@ -2169,21 +2200,43 @@ int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) 
     return HBX_OK;
   }
   int32_t* done = (int32_t*)(mapped + FETCH_MAPPED_BYTES);
-  seq = seq == INT32_MAX ? 1 : seq + 1;
+  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
   hipLaunchKernelGGL(fetch_publish_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)dev_src, (int32_t)(bytes / 4),
                      (uint32_t*)mapped, done, seq);
   HBX_LAUNCH_CHECK();
-  // ~0.1 s of polling covers any acquisition queued ahead on the stream; past it, block on the stream
-  bool seen = false;
-  for (int64_t i = 0; i < 20000000 && !seen; ++i) seen = __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq;
-  if (!seen) {
-    HBX_HIP(hipStreamSynchronize(s));
-    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
-      return hbx_fail(HBX_ERR_HIP, "hbx_fetch: the copy kernel did not store its completion word");
-  }
+  const int rc = wait_done(done, seq, s, "hbx_fetch");
+  if (rc) return rc;
   memcpy(host_dst, mapped, (size_t)bytes);
   return HBX_OK;
 }
+
+// hbx_kde_acquire whose final kernel also stores the record (48 bytes) into this thread's mapped host buffer
+// and a completion word last; the call spins on that word and copies the record to rec_out (host memory):
+// the acquisition and the record on the host in one call, no copy kernel, no blocking synchronisation.
+int hbx_kde_acquire_host(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
+                         const void* params_good, const float* table_good, const double* X_good,
+                         const int64_t* rows_good, int32_t variant_good,
+                         const void* params_bad, const float* table_bad, const double* X_bad,
+                         const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
+                         int64_t nmax, void* workspace, int64_t ws_bytes, void* events, void* stream,
+                         void* rec_out) {
+  if (!rec_out) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_host: null record");
+  char* mapped = nullptr;
+  int rc = mapped_buffer(&mapped);
+  if (rc) return rc;
+  int32_t* done = (int32_t*)(mapped + FETCH_MAPPED_BYTES);
+  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
+  rc = acquire_impl("hbx_kde_acquire_host", cand, Nc, Nc > 0 ? Nc : 1, D, index_base, params_good, table_good,
+                    X_good, rows_good, variant_good, params_bad, table_bad, X_bad, rows_bad, variant_bad, dc_pad,
+                    du_pad, nmax, nullptr, nullptr, nullptr, workspace, ws_bytes, events, stream, (AcqResult*)mapped,
+                    done, seq);
+  if (rc) return rc;
+  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_acquire_host");
+  if (rc) return rc;
+  memcpy(rec_out, mapped, sizeof(AcqResult));
+  return HBX_OK;
+}
+
 
 // numpy's float64 exp (hbx_npexp.h) element-wise: the known-answer check of the exact re-score's exp
 __global__ void np_exp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {

@@ -68,6 +68,15 @@ def scoring_bucket(vt):
 _pinned_tls = threading.local()
 
 
+def _record_buffer():
+    """This thread's host buffer for one result record (hbx_kde_acquire_host writes it)."""
+    import ctypes
+    b = getattr(_pinned_tls, "rec", None)
+    if b is None:
+        b = _pinned_tls.rec = ctypes.create_string_buffer(64)
+    return b
+
+
 def fetch_bytes(dev_bytes, stream=None):
     """Bytes of a small device uint8 tensor (a result record) on the host: one native call (hbx_fetch)
     copies them into a per-thread, per-device pinned buffer on ``stream`` (default: the tensor's
@@ -374,6 +383,15 @@ class KDEPair(object):
         logl = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         logg = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         wsp = ws.data_ptr()
+        if sync and not logs:  # one native call: the acquisition and its record on the host
+            rec = _record_buffer()
+            N.check(L.hbx_kde_acquire_host(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args, wsp,
+                                           ws.numel(), events.address if events is not None else None,
+                                           N.stream_handle(stream, dev), rec))
+            res = AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
+            if ties == "process" and res.flags & ACQ_NEAR_TIE:
+                self._resolve(res, ws, Nc, Nc, cands if isinstance(cands, np.ndarray) else c_dev, int(index_base))
+            return res
         N.check(L.hbx_kde_acquire(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args,
                                   N.ptr(logl), N.ptr(logg), wsp, ws.numel(),
                                   events.address if events is not None else None, N.stream_handle(stream, dev)))

@@ -149,6 +149,19 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
                     void* events, void* stream);
 
+/* hbx_kde_acquire with the record delivered to the host in the same call (bohb.py:124-169 returns the pick
+ * to get_config's caller): the final kernel also stores the 48-byte record into this thread's
+ * device-mapped host buffer and a completion word last; the call spins on that word (bounded, then it
+ * synchronises `stream`) and copies the record to rec_out (host memory, 48 bytes).  No ln-pdf outputs (the
+ * fast scoring instances).  The record also stays in the workspace (hbx_kde_result_ptr). */
+int hbx_kde_acquire_host(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
+                         const void* params_good, const float* table_good, const double* X_good,
+                         const int64_t* rows_good, int32_t variant_good,
+                         const void* params_bad, const float* table_bad, const double* X_bad,
+                         const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
+                         int64_t nmax, void* workspace, int64_t ws_bytes, void* events, void* stream,
+                         void* rec_out);
+
 /* Batched acquisition: B = ceil(Nc / seg) independent get_config calls against the same model in one
  * pass (replaces B sequential runs of the bohb.py:124-169 loop, as an SH stage issues
  * them back to back, HB_iteration.py:136-138).  Candidates [b*seg, min((b+1)*seg, Nc)) belong to call b;

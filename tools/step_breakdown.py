@@ -41,11 +41,21 @@ def main():
         t2 = time.perf_counter()
         if s >= 3:
             rows.append((t1 - t0, t2 - t1, t2 - t0, ev.elapsed_ms(True)[0] * 1e-3, e0.elapsed_time(e1) * 1e-3))
+    sync = []  # the drop-in's synchronous call: hbx_kde_acquire_host (the record on the host in one call)
+    for s in range(a.steps + 3):
+        t0 = time.perf_counter()
+        r2 = pair.acquire(C, workspace=ws, events=ev)
+        if s >= 3:
+            sync.append((time.perf_counter() - t0, ev.elapsed_ms(True)[0] * 1e-3))
+    assert r2.index == r.index
     m = np.median(np.array(rows), axis=0) * 1e6
+    ms = np.median(np.array(sync), axis=0) * 1e6
     out = {"steps": a.steps, "median_us": {"acquire_call_host": m[0], "fetch_host": m[1], "step_host": m[2],
                                            "scoring_launch": m[3], "gpu_span_call": m[4]},
            "winner": r.index}
     out["median_us"]["step_minus_scoring"] = m[2] - m[3]
+    out["median_us"]["sync_call_host"] = ms[0]
+    out["median_us"]["sync_call_minus_scoring"] = ms[0] - ms[1]
     print(json.dumps(out))
 
 
