@@ -811,7 +811,9 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 // Candidates whose l and g are both certainly below 1e-8 score exactly 1e-8/1e-8 = 1 (bohb.py:129):
 // they tie, so only the first of them per segment (first1[b]) can win and needs the exact re-score
 // (BOHB's own sampler puts most candidates there at D = 32: the truncnorm scale is 3 bw).
-#define COMBINE_SUB 4  // 256-candidate sub-blocks per block of kde_combine_kernel
+#ifndef COMBINE_SUB
+#define COMBINE_SUB 2  // 256-candidate sub-blocks per block of kde_combine_kernel (2: 13-15 us at 1e6, 4: 15-17, 8: 19)
+#endif
 __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
                                                           const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
