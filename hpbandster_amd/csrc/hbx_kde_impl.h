@@ -12,7 +12,9 @@
 #define HBX_LN2f 0.69314718055994531f
 #define HBX_LN_CLAMP (-18.420680743952367)   // ln(1e-8), bohb.py:129
 #define HBX_INV_SQRT_2PI 0.3989422804014327  // 1. / np.sqrt(2 * np.pi), SM:kernels.py:125
+#ifndef EXACT_GRID
 #define EXACT_GRID 2048  // blocks of the exact re-score (grid-stride over its work items)
+#endif
 #define SUM_BLOCK 32
 #define OBS_CHUNK 64   // observations per table chunk (= per LDS stage of the scoring kernel)
 #define KROW 80        // floats per k-row of a chunk: 64 observations + 16 pad (LDS bank spread)
