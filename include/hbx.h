@@ -185,8 +185,10 @@ int hbx_event_create(void** ev);
 int hbx_event_destroy(void* ev);
 int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
-/* Copy `bytes` of device memory (e.g. the result record) to pinned host memory on `stream` and wait for
- * that stream by polling it (no blocking synchronisation).  Replaces the caller's copy + synchronise
+/* Copy `bytes` of device memory (e.g. the result record) to host memory on `stream` and wait for it without
+ * a blocking synchronisation: up to 4096 bytes go through the calling thread's device-mapped host buffer
+ * (allocated on the thread's first call and kept for its lifetime, 4160 bytes) with a completion word the
+ * call spins on; larger or unaligned copies poll the stream.  Replaces the caller's copy + synchronise
  * after hbx_kde_acquire (the reference's get_config returns the pick to its caller: bohb.py:166). */
 int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
 
