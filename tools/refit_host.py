@@ -1,0 +1,57 @@
+"""Host-side pieces of one BOHB refit (ObservationStore.refit at config #3's 1e4 x 32), GPU box:
+    python tools/refit_host.py
+Wall time per refit, the native hbx_kde_refit call's own host time, and the stream time (events)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dev = torch.device("cuda", 0)
+    X = S.make_observations(10000, 24, 8, 4)
+    losses = S.make_losses(10000)
+    D = 32
+    reps = 30
+    n0 = X.shape[0] - reps - 1
+    store = kde.ObservationStore(D, S.var_type_string(24, 8), device=dev, capacity=2 * X.shape[0])
+    store.add(X[:n0], losses[:n0])
+    store.refit(D + 1)
+    torch.cuda.synchronize()
+    L = N.lib()
+    native = []
+    orig = L.hbx_kde_refit
+
+    def timed(*a):
+        t0 = time.perf_counter()
+        rc = orig(*a)
+        native.append(time.perf_counter() - t0)
+        return rc
+
+    L.hbx_kde_refit = timed
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    wall, stream = [], []
+    for r in range(reps):
+        store.add(X[n0 + r], losses[n0 + r])
+        t0 = time.perf_counter()
+        e0.record()
+        store.refit(D + 1)
+        e1.record()
+        e1.synchronize()
+        wall.append(time.perf_counter() - t0)
+        stream.append(e0.elapsed_time(e1) * 1e-3)
+    L.hbx_kde_refit = orig
+    print(json.dumps({"wall_us": float(np.median(wall)) * 1e6, "native_call_us": float(np.median(native)) * 1e6,
+                      "stream_us": float(np.median(stream)) * 1e6}))
+
+
+if __name__ == "__main__":
+    main()
