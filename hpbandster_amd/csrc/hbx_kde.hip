@@ -1270,8 +1270,16 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
   __shared__ double bs[256];
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
+  __shared__ double exl[256], exg[256];  // the exact pdfs of a shortlist of <= 256 (no global re-read)
+  __shared__ double rb_sh;
   __shared__ int32_t nnear;
   const int cnt = *count;
+  // shortlists of <= 256 (the common case): thread p owns candidate p -- its index and bound are loaded
+  // first, beside the unit sums' combination, and its pdfs come back through LDS
+  const bool small = cnt <= 256;
+  const int tp = threadIdx.x;
+  const int64_t my_idx = (small && tp < cnt) ? list[tp] : 0;
+  const double my_rel = (small && tp < cnt) ? score_rel(Pg, Pb, el, eg, my_idx) : 0.0;
   if (part && cnt <= EXACT_SPLIT_CAP) {  // the split re-score's unit sums -> pdfs (kde_exact_combine's work)
     for (int pk = threadIdx.x >> 6; pk < 2 * cnt; pk += 4) {  // one wave per (candidate, KDE)
       const bool isl = pk & 1;
@@ -1282,9 +1290,19 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
         const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
         acc = acc + pw_combine_units_wave<PW_SPLIT_CUT>(m, us + b * PW_SPLIT_UNITS);
       }
-      if ((threadIdx.x & 63) == 0) (isl ? exact_lw : exact_gw)[pk >> 1] = acc / (double)n;
+      if ((threadIdx.x & 63) == 0) {
+        const double pdf = acc / (double)n;
+        (isl ? exact_lw : exact_gw)[pk >> 1] = pdf;
+        if (small) (isl ? exl : exg)[pk >> 1] = pdf;
+      }
     }
     __threadfence_block();
+    __syncthreads();
+  } else if (small) {  // pdfs written by another kernel: one global read each
+    if (tp < cnt) {
+      exl[tp] = exact_l[tp];
+      exg[tp] = exact_g[tp];
+    }
     __syncthreads();
   }
   double best = INFINITY;
@@ -1294,9 +1312,9 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
   for (int p = threadIdx.x; p < cnt; p += 256) {
     // bohb.py:129 with Python max(): max(1e-8, g) keeps 1e-8 unless g > 1e-8 (NaN -> 1e-8);
     // max(l, 1e-8) keeps l unless 1e-8 > l (NaN -> NaN)
-    const double g = exact_g[p], l = exact_l[p];
+    const double g = small ? exg[p] : exact_g[p], l = small ? exl[p] : exact_l[p];
     const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
-    const int64_t idx = list[p];
+    const int64_t idx = small ? my_idx : list[p];
     // valid iff s < +inf (bohb.py:150 'val < best' with best = inf); strict '<', first index wins
     if (s < INFINITY && (s < best || (s == best && idx < bidx))) {
       best = s;
@@ -1323,13 +1341,20 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
   // the near set: every re-scored candidate the winner cannot be told apart from by these bounds
   const int32_t wp = bp[0];
   double rb = 0.0;
+  if (small) {  // the winner's thread holds its bound
+    if (tp == wp) rb_sh = my_rel;
+    __syncthreads();
+    if (wp >= 0) rb = rb_sh;
+  }
   if (wp >= 0) {
     const double sb = bs[0];
-    rb = score_rel(Pg, Pb, el, eg, list[wp]);
+    if (!small) rb = score_rel(Pg, Pb, el, eg, list[wp]);
     for (int p = threadIdx.x; p < cnt; p += 256) {
-      const double g = exact_g[p], l = exact_l[p];
+      const double g = small ? exg[p] : exact_g[p], l = small ? exl[p] : exact_l[p];
       const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
-      if (p == wp || near_best(s, score_rel(Pg, Pb, el, eg, list[p]), sb, rb)) near_list[atomicAdd(&nnear, 1)] = list[p];
+      const int64_t ip = small ? my_idx : list[p];
+      if (p == wp || near_best(s, small ? my_rel : score_rel(Pg, Pb, el, eg, ip), sb, rb))
+        near_list[atomicAdd(&nnear, 1)] = (int32_t)ip;
     }
   }
   __syncthreads();
@@ -1341,8 +1366,8 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     if (wp >= 0) {
       res->index = bi[0] + index_base;
       res->score = bs[0];
-      res->pdf_l = exact_l[wp];
-      res->pdf_g = exact_g[wp];
+      res->pdf_l = small ? exl[wp] : exact_l[wp];
+      res->pdf_g = small ? exg[wp] : exact_g[wp];
     }
     if (host_res) {  // hbx_kde_acquire_host: the record to mapped host memory, then the completion word
       *host_res = *res;
