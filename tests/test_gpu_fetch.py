@@ -1,0 +1,66 @@
+"""hbx_fetch (include/hbx.h) and hbx_kde_acquire_host: device bytes to the host without a blocking
+synchronisation -- through the thread's mapped buffer (<= 4096 aligned bytes, a completion word) or a
+copy plus stream polling (larger / unaligned) -- and the acquisition whose final kernel stores its record
+into mapped memory: the same bytes as the workspace's record."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nbytes,offset", [(0, 0), (4, 0), (48, 0), (4096, 0), (4100, 0), (100000, 0), (48, 1), (47, 4)])
+def test_fetch_sizes_and_alignment(device, nbytes, offset):
+    import torch
+    from hpbandster_amd import _native as N
+    src = torch.randint(0, 256, (nbytes + offset + 8,), dtype=torch.uint8, device=device)
+    want = src[offset:offset + nbytes].cpu().numpy()
+    dst = ctypes.create_string_buffer(max(nbytes, 1))
+    N.check(N.lib().hbx_fetch(dst, src.data_ptr() + offset, nbytes, N.stream_handle(None, device)))
+    assert np.frombuffer(dst.raw[:nbytes], dtype=np.uint8).tobytes() == want.tobytes()
+
+
+def test_fetch_waits_for_queued_work_and_threads(device):
+    """The record fetched after a long queue of work is the final value; two threads each with their own
+    mapped buffer."""
+    import torch
+    from hpbandster_amd import _native as N
+    out = {}
+
+    def run(tag):
+        x = torch.zeros(1 << 22, dtype=torch.float32, device=device)
+        for _ in range(20):
+            x += 1.0
+        s = x[-4:].view(torch.uint8)
+        dst = ctypes.create_string_buffer(16)
+        N.check(N.lib().hbx_fetch(dst, s.data_ptr(), 16, N.stream_handle(None, device)))
+        out[tag] = np.frombuffer(dst.raw, dtype=np.float32)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for i in range(2):
+        assert (out[i] == 20.0).all()
+
+
+def test_acquire_host_record_equals_workspace_record(device):
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(800, 6, 2, 3, seed=5)
+    pair = kde.fit_pair(X, S.make_losses(800, seed=6), S.var_type_string(6, 2), 9, device=device)
+    C = torch.from_numpy(S.make_candidates(3000, 6, 2, 3, seed=7)).to(device)
+    ws = torch.empty(pair.workspace_bytes(3000), dtype=torch.uint8, device=device)
+    r_host = pair.acquire(C, workspace=ws, index_base=11)  # hbx_kde_acquire_host
+    off = pair.result_offset()
+    r_ws = kde.AcqResult.from_bytes(ws[off:off + kde.RESULT_BYTES].cpu().numpy().tobytes())
+    r_async = kde.AcqResult.from_bytes(kde.fetch_bytes(pair.acquire(C, workspace=ws, index_base=11, sync=False)))
+    for r in (r_ws, r_async):
+        assert (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist, r.flags) == \
+               (r_host.index, r_host.score, r_host.pdf_l, r_host.pdf_g, r_host.shortlist, r_host.flags)
+    empty = pair.acquire(C[:0], workspace=ws)
+    assert empty.index == -1
