@@ -86,7 +86,8 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
   static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
   static_assert(!CO || !SG, "the coarse instance is built for unsigned sums");
-  static_assert(CT == 1 || (CT == 2 && CO), "two candidate column tiles per wave: the coarse instance");
+  static_assert(CT == 1 || ((CT == 2 || (CT >= 3 && H32C_SNAKE)) && CO),
+                "several candidate column tiles per wave: the coarse instance (three: snake order)");
   constexpr int HW = CO ? H32C_WAVES : H16_WAVES;  // waves per block, 32 CT candidates each
   constexpr int AUXF = HW * 32 * CT * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -478,8 +479,44 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     S[CT - 1] += Sb[CT - 1];
     schedule();
   };
+  // any CT >= 2, snake order (the build uses it for CT >= 3: an ablation): phase p < CT is (T0, p), phase p >= CT is (T1, 2 CT - 1 - p); even phases fill
+  // accA, odd ones accB, each phase sums the one before (a T0 term opens the column tile's chunk sum, a T1
+  // term closes it).  The loop is fully unrolled: every index below is a constant
+  auto chunkNs = [&](int cc, int b) {
+    const float* buf = lds + b * CHF;
+    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
+    float tn;
+#pragma unroll
+    for (int p = 0; p < 2 * CT; ++p) {
+      const int t = p < CT ? p : 2 * CT - 1 - p;                 // this phase's column tile
+      const int q = p > 0 ? p - 1 : 2 * CT - 1;                  // the phase summed beside it
+      const int tq = q < CT ? q : 2 * CT - 1 - q;
+      if (p == 0 || p == CT) issue(cc + PD, (b + PD) % NBUF, p == 0 ? 0 : 1);
+      if (p == 2 * CT - 1) {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      f32x16& acc = (p & 1) ? accB : accA;
+      f32x16& accp = (p & 1) ? accpB : accpA;
+      f32x16& prv = (p & 1) ? accA : accB;
+      f32x16& prvp = (p & 1) ? accpA : accpB;
+      if (p == CT - 1) mma_rd(acc, accp, buf, 1, t);           // last use of T0(cc): fragments of T1(cc)
+      else if (p == 2 * CT - 1) mma_rd(acc, accp, nbuf, 0, t);  // last use of T1(cc): fragments of T0(cc+1)
+      else mma(acc, t);
+      const float v = tile_sum(prv, prvp, tn);
+      if (q < CT) {
+        Sb[tq] = v;  // a T0 term: opens the column tile's chunk sum
+      } else {
+        Sb[tq] += v;  // a T1 term: the column tile's chunk complete
+        S[tq] += Sb[tq];
+      }
+      if (p == CT - 1 || p == 2 * CT - 1) schedule();
+      else schedule_nr();
+    }
+  };
   auto chunk = [&](int cc, int b) {
     if constexpr (CT == 1) chunk1(cc, b);
+    else if constexpr (CT >= 3) chunkNs(cc, b);
     else if constexpr (H32C_SNAKE) chunk2s(cc, b);
     else chunk2(cc, b);
   };
@@ -493,7 +530,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   for (; cc < nchunks; ++cc) chunk(cc, cc % NBUF);
   {
     float tn;
-    constexpr int tl = (CT == 2 && H32C_SNAKE) ? 0 : CT - 1;  // the column tile of the last phase
+    constexpr int tl = (CT > 1 && H32C_SNAKE) ? 0 : CT - 1;  // the column tile of the last phase
     Sb[tl] += tile_sum(accB, accpB, tn);  // T1(last)
     S[tl] += Sb[tl];
     if constexpr (SG) Sn += Snb + tn;
