@@ -84,6 +84,7 @@ SIGNATURES = {
     "hbx_sh_promote_one": (c_i32, [c_vp, c_i64, ctypes.c_double, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp]),
     "hbx_sh_advance_mapped": (c_i32, [c_vp, c_i64, ctypes.c_double, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32,
                                       c_vp]),
+    "hbx_sh_advance_state": (c_i32, [c_vp, c_i64, ctypes.c_double, c_vp]),
     "hbx_host_alloc": (c_i32, [c_i64, c_vp]),
     "hbx_kde_logpdf_rtol_scratch_bytes": (c_i64, [c_i64]),
     "hbx_kde_logpdf_rtol": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, ctypes.c_double,

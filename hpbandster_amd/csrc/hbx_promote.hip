@@ -325,24 +325,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(10))) void 
   if (tie && tie_list && lane == 0) tie_list[atomicAdd(tie_count, 1)] = (int32_t)b;  // re-ranked after
 }
 
-// One bracket of n <= 1024 in ONE launch (the drop-in's process_results: HpBandSter ranks one bracket per
-// call): wave 0 selects; when tied losses straddle the k-th place and numpy's order is asked for, the
-// workgroup re-ranks the bracket in numpy's order (scratch: 4 x n int32).  loss / advance may be mapped
+// One bracket of n <= 1024 (the drop-in's process_results: HpBandSter ranks one bracket per call), ONE
+// wave: the selection, no private segment (a kernel with scratch costs more to dispatch).  flag (device,
+// nullable): 1 when tied losses straddle the k-th place (numpy's order must then re-rank the bracket,
+// sh_rerank_one_kernel), else 0.  done (mapped, nullable): after every mask byte, `seq` -- or -seq when
+// neg_on_tie and the bracket needs the re-rank (the host then launches it).  loss / advance may be mapped
 // host memory (no copies).
-__global__ __launch_bounds__(NPS_THREADS) void sh_promote_one_kernel(const double* __restrict__ loss, int n, double kb,
-                                                                     uint8_t* __restrict__ advance, int np_order,
-                                                                     int32_t* __restrict__ scr, int32_t* done,
-                                                                     int32_t seq) {
+__global__ __launch_bounds__(64) void sh_promote_one_kernel(const double* __restrict__ loss, int n, double kb,
+                                                            uint8_t* __restrict__ advance, int32_t* flag,
+                                                            int32_t* done, int32_t seq, int neg_on_tie) {
   __shared__ double cbuf[128];
-  __shared__ int tie_sh;
-  const int lane = threadIdx.x & 63;
-  if (threadIdx.x < 64) {
-    const bool tie = sh_select_wave(loss, n, kb, advance, nullptr, cbuf, lane);
-    if (lane == 0) tie_sh = tie ? 1 : 0;
+  const int lane = threadIdx.x;
+  const bool tie = sh_select_wave(loss, n, kb, advance, nullptr, cbuf, lane);
+  if (flag && lane == 0) *flag = tie ? 1 : 0;
+  if (done) {  // every mask byte is out (system scope) before the word the host polls for
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(done, tie && neg_on_tie ? -seq : seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __syncthreads();
-  if (np_order && tie_sh) nps_order_segment(loss, n, 1, kb, scr, scr + n, scr + 2 * n, scr + 3 * n, nullptr, advance);
-  if (done) {  // every mask byte is out (system scope) before the sequence number the host polls for
+}
+
+// The numpy-order re-rank of that bracket (scratch: 4 x n int32, the flag in its first word): a no-op when
+// the selection found no straddling tie (force: the host already knows it did).  done as above (seq).
+__global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double* __restrict__ loss, int n, double kb,
+                                                                     uint8_t* __restrict__ advance, int32_t* __restrict__ scr,
+                                                                     int force, int32_t* done, int32_t seq) {
+  __shared__ int go;
+  if (threadIdx.x == 0) go = force || scr[0];
+  __syncthreads();  // every thread has the flag before the re-rank overwrites the scratch
+  if (go) nps_order_segment(loss, n, 1, kb, scr, scr + n, scr + 2 * n, scr + 3 * n, nullptr, advance);
+  if (done) {
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -426,39 +437,84 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
                           (int32_t*)(sc + hbx_sort_scratch_bytes(N)), false, st);
 }
 
-// One bracket, one launch (sh_promote_one_kernel): loss / advance device or mapped host pointers,
-// n <= 1024, k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY only, else NULL).
+// One bracket (sh_promote_one_kernel, then -- numpy's order only -- sh_rerank_one_kernel, which re-ranks when
+// the first one flagged a straddling tie): loss / advance device or mapped host pointers, n <= 1024, k by
+// value; scratch: device int32[4 n] (HBX_ORDER_NUMPY only, else NULL).  Stream-ordered; done = seq last.
 int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
                        int32_t* done, int32_t seq, void* stream) {
   if (!loss || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: null pointer");
   if (n < 0 || n > 64 * PW_PER_LANE) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: n=%lld", (long long)n);
-  if (order_mode == HBX_ORDER_NUMPY && !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: scratch");
-  hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(NPS_THREADS), 0, (hipStream_t)stream, loss, (int)n, k, advance,
-                     order_mode == HBX_ORDER_NUMPY ? 1 : 0, (int32_t*)scratch, done, seq);
+  const bool np = order_mode == HBX_ORDER_NUMPY;
+  if (np && !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_one: scratch");
+  int32_t* scr = (int32_t*)scratch;
+  hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, loss, (int)n, k, advance,
+                     np ? scr : (int32_t*)nullptr, np ? (int32_t*)nullptr : done, seq, 0);
   HBX_LAUNCH_CHECK();
+  if (np) {
+    hipLaunchKernelGGL(sh_rerank_one_kernel, dim3(1), dim3(NPS_THREADS), 0, (hipStream_t)stream, loss, (int)n, k,
+                       advance, scr, 0, done, seq);
+    HBX_LAUNCH_CHECK();
+  }
   return HBX_OK;
 }
 
 // The drop-in's whole ranking step in ONE host call: the losses copied into the mapped buffer `pin`, the
-// one-launch promotion above, a spin on the completion word the kernel stores last (bounded: then the
-// stream is synchronised), the mask copied out of `pout` into `mask` (host uint8[n]).
+// selection kernel, a spin on the word it stores last (bounded: then the stream is synchronised); only when
+// it reports a tie that straddles the k-th place (numpy's order) does a second launch re-rank the bracket,
+// then the mask is copied out of `pout` into `mask` (host uint8[n]).
+static int spin_done(int32_t* done, int32_t a, int32_t b, hipStream_t stream, int32_t* seen_out) {
+  // ~0.1 ms of polling covers the launch and the kernel; past it, block on the stream instead
+  int32_t v = 0;
+  bool seen = false;
+  for (int i = 0; i < 200000 && !seen; ++i) {
+    v = __atomic_load_n(done, __ATOMIC_ACQUIRE);
+    seen = v == a || v == b;
+  }
+  if (!seen) {
+    HBX_HIP(hipStreamSynchronize(stream));
+    v = __atomic_load_n(done, __ATOMIC_ACQUIRE);
+    if (v != a && v != b)
+      return hbx_fail(HBX_ERR_HIP, "hbx_sh_advance_mapped: the kernel did not store its completion word");
+  }
+  *seen_out = v;
+  return HBX_OK;
+}
+
 int hbx_sh_advance_mapped(const double* losses, int64_t n, double k, uint8_t* mask, double* pin, uint8_t* pout,
                           int32_t* done, int32_t seq, void* scratch, int32_t order_mode, void* stream) {
   if (!losses || !mask || !pin || !pout || !done) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_mapped: null pointer");
   if (n <= 0) return HBX_OK;
-  memcpy(pin, losses, sizeof(double) * (size_t)n);
-  const int rc = hbx_sh_promote_one(pin, n, k, pout, scratch, order_mode, done, seq, stream);
+  if (n > 64 * PW_PER_LANE) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_mapped: n=%lld", (long long)n);
+  if (seq <= 0) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_mapped: seq must be positive");
+  const bool np = order_mode == HBX_ORDER_NUMPY;
+  if (np && !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_mapped: scratch");
+  if (losses != pin) memcpy(pin, losses, sizeof(double) * (size_t)n);  // (the caller may have filled pin itself)
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sh_promote_one_kernel, dim3(1), dim3(64), 0, st, (const double*)pin, (int)n, k, pout,
+                     (int32_t*)nullptr, done, seq, np ? 1 : 0);
+  HBX_LAUNCH_CHECK();
+  int32_t v = 0;
+  int rc = spin_done(done, seq, -seq, st, &v);
   if (rc) return rc;
-  // ~0.1 ms of polling covers the launch and the kernel; past it, block on the stream instead
-  bool seen = false;
-  for (int i = 0; i < 200000 && !seen; ++i) seen = __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq;
-  if (!seen) {
-    HBX_HIP(hipStreamSynchronize((hipStream_t)stream));
-    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
-      return hbx_fail(HBX_ERR_HIP, "hbx_sh_advance_mapped: the kernel did not store its completion word");
+  if (v == -seq) {  // tied losses straddle the k-th place: numpy's order decides which copies advance
+    hipLaunchKernelGGL(sh_rerank_one_kernel, dim3(1), dim3(NPS_THREADS), 0, st, (const double*)pin, (int)n, k, pout,
+                       (int32_t*)scratch, 1, done, seq);
+    HBX_LAUNCH_CHECK();
+    rc = spin_done(done, seq, seq, st, &v);
+    if (rc) return rc;
   }
-  memcpy(mask, pout, (size_t)n);
+  if (mask != pout) memcpy(mask, pout, (size_t)n);
   return HBX_OK;
+}
+
+int hbx_sh_advance_state(int64_t* state, int64_t n, double k, void* stream) {
+  if (!state) return hbx_fail(HBX_ERR_ARG, "hbx_sh_advance_state: null state");
+  const int32_t seq = (int32_t)(state[5] % 0x7ffffffe) + 1;
+  state[5] = seq;
+  double* pin = (double*)(intptr_t)state[0];
+  uint8_t* pout = (uint8_t*)(intptr_t)state[1];
+  return hbx_sh_advance_mapped(pin, n, k, pout, pin, pout, (int32_t*)(intptr_t)state[2], seq,
+                               (void*)(intptr_t)state[3], (int32_t)state[4], stream);
 }
 
 // pinned host memory the device reads and writes directly (coherent, mapped): the drop-in promotion's

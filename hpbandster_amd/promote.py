@@ -70,8 +70,11 @@ class _Staging(object):
         self.index = device.index
         self.cap = 0
         self._ptrs = []
-        self.seq = 0
-        self.fn = N.lib().hbx_sh_advance_mapped
+        self.fn = N.lib().hbx_sh_advance_state
+        # hbx_sh_advance_state's block: {pin, pout, done, scratch, order_mode, seq}
+        self.state = (ctypes.c_int64 * 6)()
+        self.state_addr = ctypes.addressof(self.state)
+        self.mode = None
         self.stream_of = _current_stream_fn()
 
     def get(self, n):
@@ -85,6 +88,10 @@ class _Staging(object):
             N.check(L.hbx_host_alloc(cap + 64, ctypes.addressof(pout)))
             self._ptrs = [pin.value, pout.value]
             self.pin, self.pout = pin.value, pout.value
+            # numpy views of the mapped buffers: the call fills / reads them in place (an ndarray's
+            # .ctypes.data costs ~1 us per array, as much as the copies it would feed)
+            self.pin_v = np.frombuffer((ctypes.c_double * cap).from_address(self.pin), dtype=np.float64)
+            self.pout_v = np.frombuffer((ctypes.c_uint8 * cap).from_address(self.pout), dtype=np.bool_)
             # the completion word the kernel stores last (after the mask, system scope)
             self.done_addr = pout.value + cap
             ctypes.c_int32.from_address(self.done_addr).value = 0
@@ -92,6 +99,8 @@ class _Staging(object):
                 self.scratch = torch.empty(4 * cap, dtype=torch.int32, device=self.device)
             self.scr_ptr = self.scratch.data_ptr()
             self.cap = cap
+            self.state[0], self.state[1], self.state[2], self.state[3] = self.pin, self.pout, self.done_addr, \
+                self.scr_ptr
         return self
 
     def _release(self):
@@ -149,12 +158,13 @@ _MODES = {"numpy": N.ORDER_NUMPY, "stable": N.ORDER_STABLE, N.ORDER_NUMPY: N.ORD
 def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
-    What SuccessiveHalving.process_results calls once per bracket: ONE host call into libhbx
-    (hbx_sh_advance_mapped) copies the losses into device-mapped host memory, launches the one-kernel
+    What SuccessiveHalving.process_results calls once per bracket: the losses are copied into
+    device-mapped host memory, ONE host call into libhbx (hbx_sh_advance_mapped) launches the one-kernel
     promotion (the selection, and the numpy-order re-rank when tied losses straddle the k-th place), spins
     on the kernel's completion word (stored last) instead of synchronising the stream, and copies the
     mask out."""
-    losses = np.ascontiguousarray(losses, dtype=np.float64).reshape(-1)
+    if type(losses) is not np.ndarray or losses.ndim != 1:
+        losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
     if n == 0:
         return np.zeros(0, dtype=bool)
@@ -166,10 +176,10 @@ def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
         mode = N.order_mode(ties)
     st = _staging(device).get(n)
     h = stream.cuda_stream if stream is not None else st.stream_of(st.index)
-    mask = np.empty(n, dtype=np.bool_)
-    st.seq = (st.seq % 0x7ffffffe) + 1
-    rc = st.fn(losses.ctypes.data, n, float(k), mask.ctypes.data, st.pin, st.pout, st.done_addr, st.seq,
-               st.scr_ptr if mode == N.ORDER_NUMPY else None, mode, h)
+    st.pin_v[:n] = losses  # straight into the mapped buffer the kernel reads
+    if mode != st.mode:
+        st.state[4] = st.mode = mode
+    rc = st.fn(st.state_addr, n, float(k), h)  # the sequence number advances in the state block
     if rc:
         N.check(rc)
-    return mask
+    return st.pout_v[:n].copy()  # the mask, out of the mapped buffer the kernel wrote

@@ -325,20 +325,28 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
                       int64_t scratch_bytes, int32_t order_mode, void* events, void* stream);
 /*   events: NULL, or hipEvent_t[2] stamped at the start and end of the selection kernel (mask-only path). */
 
-/* One bracket of n <= 1024 configurations in one launch (what SuccessiveHalving.process_results ranks per
- * call, HB_iteration.py:179-182): loss f64[n] and advance u8[n] may be device pointers or mapped host
- * memory from hbx_host_alloc (no copies); k by value; scratch: device int32[4 n] (HBX_ORDER_NUMPY), or
- * NULL (HBX_ORDER_STABLE).  done (nullable, mapped host memory): set to `seq` once every mask byte is
- * visible to the host, so a caller may poll it instead of synchronising the stream. */
+/* One bracket of n <= 1024 configurations (what SuccessiveHalving.process_results ranks per call,
+ * HB_iteration.py:179-182): a one-wave selection launch, then (HBX_ORDER_NUMPY) a re-rank launch that works
+ * only when tied losses straddle the k-th place.  loss f64[n] and advance u8[n] may be device pointers or
+ * mapped host memory from hbx_host_alloc (no copies); k by value; scratch: device int32[4 n]
+ * (HBX_ORDER_NUMPY), or NULL (HBX_ORDER_STABLE).  done (nullable, mapped host memory): set to `seq` once
+ * every mask byte is visible to the host, so a caller may poll it instead of synchronising the stream. */
 int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance, void* scratch, int32_t order_mode,
                        int32_t* done, int32_t seq, void* stream);
 /* The same ranking step as ONE host call (what the drop-in's advance_mask makes): losses (host f64[n]) are
- * copied into `pin` (hbx_host_alloc, >= n doubles), hbx_sh_promote_one runs with advance = `pout`
+ * copied into `pin` (hbx_host_alloc, >= n doubles), the selection runs with advance = `pout`
  * (hbx_host_alloc, >= n bytes), the host spins on `done` (mapped, after pout) until the kernel stores
- * `seq` (bounded: then the stream is synchronised), and the mask is copied into `mask` (host u8[n]).
+ * `seq` (> 0; bounded: then the stream is synchronised) -- or -seq: a straddling tie, the re-rank is
+ * launched and waited for the same way -- and the mask is copied into `mask` (host u8[n]).
+ * losses == pin (filled by the caller) and mask == pout (read by the caller) skip those copies.
  * Replaces np.argsort(np.argsort(losses)) < k of HB_iteration.py:179-182 for one bracket. */
 int hbx_sh_advance_mapped(const double* losses, int64_t n, double k, uint8_t* mask, double* pin, uint8_t* pout,
                           int32_t* done, int32_t seq, void* scratch, int32_t order_mode, void* stream);
+/* hbx_sh_advance_mapped with its buffers in a state block (4 arguments: what a per-call FFI hop costs, the
+ * drop-in's advance_mask pays on every bracket): state = int64[6] {pin, pout, done, scratch, order_mode,
+ * seq}.  The caller has written the losses into pin; the mask is left in pout; seq is advanced by the call
+ * (1 ... 2^31 - 2, wrapping). */
+int hbx_sh_advance_state(int64_t* state, int64_t n, double k, void* stream);
 /* Pinned, device-mapped, coherent host memory (hipHostMalloc) and its release. */
 int hbx_host_alloc(int64_t bytes, void** out);
 int hbx_host_free(void* p);

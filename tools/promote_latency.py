@@ -4,6 +4,7 @@ hbx_sh_advance_mapped call with every argument prepared (the native floor the Py
 
     python tools/promote_latency.py [n] [reps]
 """
+import ctypes
 import os
 import sys
 import time
@@ -39,13 +40,22 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     mask = np.empty(n, dtype=np.bool_)
     fn = N.lib().hbx_sh_advance_mapped
+
+    def nxt():  # the staging's sequence number (one completion word for every call here)
+        st.state[5] = st.state[5] % 0x7ffffffe + 1
+        return st.state[5]
     lp, mp = losses.ctypes.data, mask.ctypes.data
 
     def bare():
-        st.seq += 1
-        fn(lp, n, float(k), mp, st._ptrs[0], st._ptrs[1], st.done_addr, st.seq, st.scr_ptr, N.ORDER_NUMPY, stream)
+        fn(lp, n, float(k), mp, st._ptrs[0], st._ptrs[1], st.done_addr, nxt(), st.scr_ptr, N.ORDER_NUMPY, stream)
 
     native = per_call(bare, reps)
+    # the state-block entry advance_mask uses (4 arguments; losses already in the mapped buffer)
+    st.pin_v[:n] = losses
+    st.state[4] = st.mode = N.ORDER_NUMPY
+    sfn, sa = N.lib().hbx_sh_advance_state, st.state_addr
+    state_us = per_call(lambda: sfn(sa, n, float(k), stream), reps)
+    assert (st.pout_v[:n] == want).all()
     assert (mask == want).all()
     # the host side of the launch alone (no wait; the stream is drained once at the end)
     one = N.lib().hbx_sh_promote_one
@@ -57,9 +67,46 @@ def main():
     torch.cuda.synchronize()
     # launch + stream synchronisation (no completion-word polling)
     sync_us = per_call(lambda: (launch(), torch.cuda.current_stream(dev).synchronize()), reps)
-    print({"n": n, "reps": reps, "host_numpy_us": round(host, 2), "advance_mask_us": round(drop, 2),
-           "native_call_us": round(native, 2), "launch_only_us": round(launch_us, 2),
-           "launch_sync_us": round(sync_us, 2)})
+    # the same on a side stream (torch's pool streams are non-blocking) instead of the null stream
+    side = torch.cuda.Stream(dev)
+    hs = side.cuda_stream
+
+    def bare_side():
+        fn(lp, n, float(k), mp, st._ptrs[0], st._ptrs[1], st.done_addr, nxt(), st.scr_ptr, N.ORDER_NUMPY, hs)
+
+    native_side = per_call(bare_side, reps)
+    assert (mask == want).all()
+    launch_side = per_call(lambda: one(st._ptrs[0], n, float(k), st._ptrs[1], st.scr_ptr, N.ORDER_NUMPY, None, 0, hs),
+                           200)
+    side.synchronize()
+    drop_side = per_call(lambda: promote.advance_mask(losses, k, device=dev, stream=side), reps)
+    # the floor of any one-launch round trip: hbx_fetch of 8 bytes (launch, a one-wave kernel storing them and
+    # its completion word into mapped memory, the host spin) -- no losses read, no selection
+    src = torch.zeros(1, dtype=torch.float64, device=dev)
+    dst = np.zeros(1)
+    fetch = N.lib().hbx_fetch
+    dp, sp = dst.ctypes.data, src.data_ptr()
+    floor_us = per_call(lambda: fetch(dp, sp, 8, stream), reps)
+    # the same kernel on device-resident losses and mask (the completion word still mapped, spun on from
+    # Python): what reading / writing host memory over PCIe costs inside the kernel
+    ld = torch.from_numpy(losses).to(dev)
+    ad = torch.empty(n, dtype=torch.uint8, device=dev)
+    dv = ctypes.c_int32.from_address(st.done_addr)
+
+    def dev_call():
+        q = nxt()
+        one(ld.data_ptr(), n, float(k), ad.data_ptr(), st.scr_ptr, N.ORDER_NUMPY, st.done_addr, q, stream)
+        while dv.value != q:
+            pass
+
+    devres_us = per_call(dev_call, reps)
+    torch.cuda.synchronize()
+    assert (ad.cpu().numpy().astype(bool) == want).all()
+    print({"n": n, "reps": reps, "fetch8_floor_us": round(floor_us, 2), "device_resident_us": round(devres_us, 2), "host_numpy_us": round(host, 2), "advance_mask_us": round(drop, 2),
+           "native_call_us": round(native, 2), "state_call_us": round(state_us, 2), "launch_only_us": round(launch_us, 2),
+           "launch_sync_us": round(sync_us, 2), "stream": stream,
+           "side_stream": {"advance_mask_us": round(drop_side, 2), "native_call_us": round(native_side, 2),
+                           "launch_only_us": round(launch_side, 2)}})
 
 
 if __name__ == "__main__":
