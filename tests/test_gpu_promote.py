@@ -45,6 +45,33 @@ def test_promotion_ties_stable_and_numpy(device):
     assert sorted(np.nonzero(adv)[0].tolist()) == [0, 1, 2, 4, 5] + list(range(40, 50))
 
 
+def test_one_bracket_entries_agree(device):
+    """hbx_sh_promote_one (stream-ordered: the selection launch, then the re-rank launch that works only on
+    a straddling tie) on device buffers, and advance_mask (the mapped one-call path: a second launch only
+    when the selection reports the tie), on tie-free, straddling-tie and non-straddling-tie brackets."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(21)
+    cases = [(rs.rand(1000), 333), (np.array([1.0] * 40 + [0.5] * 10), 15), (np.round(rs.rand(1024), 1), 500),
+             (np.array([0.25] * 7 + [0.75] * 9), 7), (np.array([3.0]), 1), (np.round(rs.rand(81), 2), 27)]
+    for losses, k in cases:
+        n = len(losses)
+        for ties, mode in (("numpy", N.ORDER_NUMPY), ("stable", N.ORDER_STABLE)):
+            want = promote.advance_mask(losses, k, device=device, ties=ties)
+            assert want.sum() == min(k, n)
+            ld = torch.from_numpy(losses).to(device)
+            ad = torch.full((n,), 7, dtype=torch.uint8, device=device)
+            scr = torch.full((4 * n,), -1, dtype=torch.int32, device=device)
+            N.check(N.lib().hbx_sh_promote_one(ld.data_ptr(), n, float(k), ad.data_ptr(),
+                                               scr.data_ptr() if mode == N.ORDER_NUMPY else None, mode, None, 0,
+                                               N.stream_handle()))
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(ad.cpu().numpy().astype(bool), want, err_msg="%s n=%d" % (ties, n))
+            if ties == "numpy" and len(np.unique(losses)) == n:
+                np.testing.assert_array_equal(want, np.argsort(np.argsort(losses)) < k)
+
+
 def test_config5_shape_with_fit(device):
     """B=1e3 brackets x 1e3 configs (config #5 at 1/10 the brackets): promotion + per-bracket refit."""
     import torch
