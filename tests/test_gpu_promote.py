@@ -72,6 +72,26 @@ def test_one_bracket_entries_agree(device):
                 np.testing.assert_array_equal(want, np.argsort(np.argsort(losses)) < k)
 
 
+def test_advance_state_sequence_wraps(device):
+    """hbx_sh_advance_state's sequence number wraps from 2^31 - 2 to 1 (the completion word is never 0 or
+    negative for a finished call) and a straddling tie (completion word -seq, then the re-rank launch)
+    on either side of the wrap still yields numpy's masks."""
+    from hpbandster_amd import promote
+    tie = np.array([1.0] * 40 + [0.5] * 10)
+    want_tie = promote.advance_mask(tie, 15, device=device)
+    assert sorted(np.nonzero(want_tie)[0].tolist()) == [0, 1, 2, 4, 5] + list(range(40, 50))
+    rnd = np.random.RandomState(5).rand(700)
+    want_rnd = np.argsort(np.argsort(rnd)) < 233
+    st = promote._staging(device).get(700)
+    st.state[5] = 0x7ffffffe - 2
+    seqs = []
+    for i in range(6):
+        losses, k, want = (tie, 15, want_tie) if i % 2 else (rnd, 233, want_rnd)
+        np.testing.assert_array_equal(promote.advance_mask(losses, k, device=device), want, err_msg="call %d" % i)
+        seqs.append(int(st.state[5]))
+    assert seqs == [0x7ffffffe - 1, 0x7ffffffe, 1, 2, 3, 4], seqs
+
+
 def test_config5_shape_with_fit(device):
     """B=1e3 brackets x 1e3 configs (config #5 at 1/10 the brackets): promotion + per-bracket refit."""
     import torch
