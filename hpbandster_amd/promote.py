@@ -71,6 +71,7 @@ class _Staging(object):
         self.cap = 0
         self._ptrs = []
         self.fn = N.lib().hbx_sh_advance_state
+        self.fast = _fast_module()
         # hbx_sh_advance_state's block: {pin, pout, done, scratch, order_mode, seq}
         self.state = (ctypes.c_int64 * 6)()
         self.state_addr = ctypes.addressof(self.state)
@@ -116,6 +117,26 @@ class _Staging(object):
 
 
 _tls = threading.local()
+_fast = None
+
+
+def _fast_module():
+    """_hbxfast (hbx_pyfast.c): advance_mask's call into hbx_sh_advance_state through the buffer protocol
+    instead of ctypes; None when it was not built (the ctypes call then makes the same GPU call)."""
+    global _fast
+    if _fast is None:
+        import importlib.util
+        import os
+        from . import build as B
+        path = B.pyfast_path()
+        mod = False
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location("hpbandster_amd._hbxfast", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            mod.set_entry(ctypes.cast(N.lib().hbx_sh_advance_state, ctypes.c_void_p).value)
+        _fast = mod
+    return _fast or None
 
 
 def _staging(device):
@@ -176,9 +197,16 @@ def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
         mode = N.order_mode(ties)
     st = _staging(device).get(n)
     h = stream.cuda_stream if stream is not None else st.stream_of(st.index)
-    st.pin_v[:n] = losses  # straight into the mapped buffer the kernel reads
     if mode != st.mode:
         st.state[4] = st.mode = mode
+    if st.fast is not None:  # the same call without ctypes (losses in / mask out through the buffer protocol)
+        mask = np.empty(n, dtype=np.bool_)
+        rc = st.fast.advance(st.state_addr, st.cap, losses, mask, float(k), h)
+        if rc <= 0:
+            if rc:
+                N.check(rc)
+            return mask
+    st.pin_v[:n] = losses  # straight into the mapped buffer the kernel reads
     rc = st.fn(st.state_addr, n, float(k), h)  # the sequence number advances in the state block
     if rc:
         N.check(rc)
