@@ -122,7 +122,8 @@ _fast = None
 
 def _fast_module():
     """_hbxfast (hbx_pyfast.c): advance_mask's call into hbx_sh_advance_state through the buffer protocol
-    instead of ctypes; None when it was not built (the ctypes call then makes the same GPU call)."""
+    instead of ctypes, with HBX_PYFAST=1 (not yet measured on the GPU: off by default); None otherwise or
+    when it was not built (the ctypes call then makes the same GPU call)."""
     global _fast
     if _fast is None:
         import importlib.util
@@ -130,7 +131,7 @@ def _fast_module():
         from . import build as B
         path = B.pyfast_path()
         mod = False
-        if os.path.exists(path):
+        if os.path.exists(path) and os.environ.get("HBX_PYFAST", "0") != "0":
             spec = importlib.util.spec_from_file_location("hpbandster_amd._hbxfast", path)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
