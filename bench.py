@@ -89,7 +89,7 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -112,7 +112,34 @@ def parse():
                     help="N>1: the config #4 side line (this many candidates in total over the ranks); 0 = off")
     ap.add_argument("--profile-tag", default=None,
                     help="profiles/ directory holding the rocprofv3 summaries of this very run (recorded in the line)")
-    return ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="ranks report (rank, world size) as JSON and exit before any GPU call (tests the launcher)")
+    return ap.parse_args(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def plan_launch(gpus, env, argv, script):
+    """How this process runs ``--gpus N`` (decided before any GPU call):
+    ("run", world) -- this process is one rank of `world` (WORLD_SIZE set by a launcher, or N = 1 alone);
+    ("spawn", cmd) -- N > 1 without a launcher: run N ranks as children of torch.distributed.run (one process
+    per GPU, rendezvous on 127.0.0.1) and exit with their status;
+    ("error", msg) -- WORLD_SIZE disagrees with --gpus: measuring another rank count than asked is refused."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return "run", 1
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script] + list(argv)
+        return "spawn", cmd
+    if int(ws) != gpus:
+        return "error", "--gpus %d but WORLD_SIZE %s: launch %d ranks, or pass --gpus %s" % (gpus, ws, gpus, ws)
+    return "run", int(ws)
 
 
 def host_info():
@@ -126,15 +153,22 @@ def host_info():
                     break
     except OSError:
         pass
+    quota = None
+    try:  # the job's cgroup CPU quota ("max" or "<quota_us> <period_us>")
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q = fh.read().split()
+        quota = q[0] if q[0] == "max" else "%.1f cpus" % (int(q[0]) / int(q[1]))
+    except (OSError, ValueError, IndexError):
+        pass
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_max": quota}
 
 
 def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     """CPU baselines on the host cores, bounded samples of the same workload:
     * value: the C oracle (oracle/kde_oracle.c, fp64, the reference's arithmetic, OpenMP over
-      candidates) on every core this process may use -- OMP_NUM_THREADS when set (the GPU box caps a
-      job's CPU share there), else the affinity mask;
+      candidates) with one thread per host core this process may run on (the affinity mask; the box's
+      OMP_NUM_THREADS and cgroup quota are recorded beside it);
     * reference_as_called: the reference's own path, KDEMultivariate.pdf for l and g per candidate
       (bohb.py:149), single core -- statsmodels is not installed on the box, so its numpy restatement
       oracle.kde_oracle.pdf stands in (bit-identical to statsmodels on every golden fixture), level
@@ -142,7 +176,7 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     from oracle import c_oracle
     from oracle import kde_oracle as O
     hi = host_info()
-    threads = int(hi["omp_num_threads"] or 0) or hi["affinity"] or 1
+    threads = hi["affinity"] or 1
     Xg, Xb = X[good_rows], X[bad_rows]
     args_g = (Xg, pair.good.bw, var_type, pair.good.nlev)
     args_b = (Xb, pair.bad.bw, var_type, pair.bad.nlev)
@@ -158,9 +192,8 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     nobs = Xg.shape[0] + Xb.shape[0]
     out = {"value": n * nobs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
            "sample": "%d of the %d candidates x %d observations (D=%d), fp64 C oracle (reference arithmetic), "
-                     "%d threads (%s), %.1f s" % (n, cands.shape[0], nobs, X.shape[1], threads,
-                                                  "OMP_NUM_THREADS: this job's CPU share of the host"
-                                                  if hi["omp_num_threads"] else "affinity mask", dt)}
+                     "%d OpenMP threads = the affinity mask (cgroup quota %s), %.1f s"
+                     % (n, cands.shape[0], nobs, X.shape[1], threads, hi["cgroup_cpu_max"], dt)}
     out.update(hi)
     m, t_ref = 0, 0.0
     t0 = time.perf_counter()
@@ -170,6 +203,7 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
         m += 1
         t_ref = time.perf_counter() - t0
     out["reference_as_called"] = {"value": m * nobs / t_ref, "unit": "pairs/s", "cores": 1,
+                                  "kind": "numpy restatement of KDEMultivariate.pdf (statsmodels absent on the box)",
                                   "sample": "%d candidates, KDEMultivariate.pdf arithmetic per candidate "
                                             "(numpy restatement, single core), %.1f s" % (m, t_ref)}
     return out
@@ -439,22 +473,27 @@ def promote_dropin(device, n=1000, reps=50):
         for sh in shs:
             fn(sh)
         res[name] = (time.perf_counter() - t0) / reps * 1e3
-    # the ranking step alone: advance_mask (pinned copies + select kernel + one sync) vs numpy's
+    # the ranking step alone: advance_mask under the size policy (host for tie-free brackets <= HOST_MAX),
+    # forced onto the GPU (mapped losses + one-wave select kernel + completion word), and numpy's rule
     from hpbandster_amd import promote
     losses = rs.rand(n)
     k = n // 3
-    promote.advance_mask(losses, k, device=device)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        promote.advance_mask(losses, k, device=device)
-    rank_gpu = (time.perf_counter() - t0) / reps * 1e3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        np.argsort(np.argsort(losses)) < k
-    rank_host = (time.perf_counter() - t0) / reps * 1e3
+
+    def per_call(fn, r=reps * 20):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(r):
+            fn()
+        return (time.perf_counter() - t0) / r * 1e3
+    rank_auto = per_call(lambda: promote.advance_mask(losses, k, device=device))
+    rank_gpu = per_call(lambda: promote.advance_mask(losses, k, device=device, policy="gpu"))
+    rank_host = per_call(lambda: np.argsort(np.argsort(losses)) < k)
+    tie = np.round(losses, 1)  # tied losses straddle the k-th place: numpy 1.26.4's order, on the GPU
+    rank_tie = per_call(lambda: promote.advance_mask(tie, k, device=device))
     return {"workload": "process_results_one_bracket_n%d" % n, "ms_per_call": res["gpu"],
-            "host_numpy_ms_per_call": res["host_numpy"], "rank_step_ms": rank_gpu,
-            "host_rank_step_ms": rank_host}
+            "host_numpy_ms_per_call": res["host_numpy"], "rank_step_ms": rank_auto,
+            "rank_step_gpu_ms": rank_gpu, "rank_step_tied_ms": rank_tie, "host_rank_step_ms": rank_host,
+            "policy": "host when tie-free and n <= %d (promote.HOST_MAX), else GPU" % promote.HOST_MAX}
 
 
 def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
@@ -493,16 +532,28 @@ def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
             "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
 
 
-def sh_stage_line(device, n_obs=400, stage=81, reps=3):
+def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
     """Side measurement (SURVEY 8f row 1 through the drop-in): the first stage of an eta=3 bracket -- 81
     configurations requested through SuccessiveHalving.get_next_run, as HpBandSter.run requests them --
-    from BOHB (config #3's dims, 24c + 8u, GPU sampler, num_samples=64) with speculative batching (one
-    hbx_kde_acquire_batch pass) against one get_config per request; the proposals must be identical."""
+    from BOHB (config #3's dims, 24c + 8u, GPU sampler, num_samples=64) with speculative batching (batches
+    of 1, 2, 4, ... while fully served) against one get_config per request; the proposals must be identical.
+    interleaved: every request is followed by its run's result (new_result, which refits the model) -- one
+    worker, the case where nothing can be computed ahead; the timed loop includes the refits."""
     import torch
     from hpbandster_amd import configspace as CS
     from hpbandster_amd.config_generators import BOHB
     from hpbandster_amd.HB_iteration import SuccessiveHalving
     from hpbandster_amd import synthetic as S
+
+    class Job(object):
+        pass
+
+    def job(cid, cfg, loss):
+        j = Job()
+        j.id, j.exception, j.timestamps = cid, None, {}
+        j.kwargs = {"config": cfg, "budget": 1.0}
+        j.result = {"loss": float(loss), "info": None}
+        return j
 
     def make():
         space = CS.ConfigurationSpace(seed=3)
@@ -513,15 +564,8 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=3):
         cg = BOHB(space, device=device, sampler="gpu", sampler_seed=77)
         X = S.make_observations(n_obs, 24, 8, 4, seed=51)
         Lo = S.make_losses(n_obs, seed=52)
-
-        class Job(object):
-            pass
         for i in range(n_obs):
-            j = Job()
-            j.id, j.exception, j.timestamps = (0, 0, i), None, {}
-            j.kwargs = {"config": CS.Configuration(space, vector=X[i]).get_dictionary(), "budget": 1.0}
-            j.result = {"loss": float(Lo[i]), "info": None}
-            cg.new_result(j)
+            cg.new_result(job((0, 0, i), CS.Configuration(space, vector=X[i]).get_dictionary(), Lo[i]))
         return cg, space
 
     def run(batch):
@@ -530,25 +574,77 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=3):
         space.seed(6)
         sh = SuccessiveHalving(0, [stage, stage // 3, stage // 9, 3, 1], [1.0, 3.0, 9.0, 27.0, 81.0], cg.get_config,
                                device=device, batch_sampling=batch)
+        lr = np.random.RandomState(9)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        cfgs = [sh.get_next_run()[1] for _ in range(stage)]
+        cfgs = []
+        for _ in range(stage):
+            cid, cfg, _ = sh.get_next_run()
+            cfgs.append(cfg)
+            if interleaved:
+                cg.new_result(job((1,) + tuple(cid[1:]), cfg, lr.rand()))
         torch.cuda.synchronize()
         return time.perf_counter() - t0, cfgs
 
     res = {}
-    for batch in (False, True):
-        ts, cfgs = [], None
-        for _ in range(reps):
-            t, c = run(batch)
-            ts.append(t)
-            cfgs = c
-        res[batch] = (min(ts), cfgs)
-    return {"workload": "sh_stage_%d_get_next_run_d32_obs%d" % (stage, n_obs),
+    for batch in (False, True) * reps:  # alternated, best of reps each
+        t, c = run(batch)
+        if batch not in res or t < res[batch][0]:
+            res[batch] = (t, c)
+    return {"workload": "sh_stage_%d_get_next_run_d32_obs%d%s" % (stage, n_obs, "_interleaved" if interleaved else ""),
             "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
             "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],
-            "note": "SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
-                    "batched = one speculative get_config_batch_spec" % stage}
+            "note": ("SuccessiveHalving.get_next_run x %d, each followed by its result (new_result + refit); "
+                     "batched = speculative batching on" % stage) if interleaved else
+                    ("SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
+                     "batched = speculative batches of 1, 2, 4, ... (hbx_kde_acquire_batch)" % stage)}
+
+
+def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
+    """Side line: the ln-pdf contract at config #3 -- hbx_kde_logpdf_rtol (the precise
+    instance: 3 f16 products per continuous dim, the one-hot hi and lo parts, then every candidate whose
+    rigorous bound does not guarantee rtol re-evaluated in fp64 log space on the device) for l(x) and g(x)
+    over the same 1e6 candidates (bohb.py:126-129: what a caller who wants the densities gets).  Time per
+    KDE call from HIP events on its stream; the fraction of candidates re-evaluated in fp64 read from the
+    call's scratch counter."""
+    import torch
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    Nc = int(c_dev.shape[0])
+    sh = N.stream_handle(None, device)
+    sb = int(L.hbx_kde_logpdf_rtol_scratch_bytes(Nc))
+    scr = torch.empty(sb, dtype=torch.uint8, device=device)
+    out = torch.empty(Nc, dtype=torch.float64, device=device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {}
+    for name, k in (("l", pair.good), ("g", pair.bad)):
+        def call():
+            N.check(L.hbx_kde_logpdf_rtol(N.ptr(c_dev), Nc, k.k_vars, N.ptr(k.params), N.ptr(k.table), N.ptr(k.X_dev),
+                                          N.ptr(k.rows_dev), k.dc_pad, k.du_pad, k.variant, float(rtol), N.ptr(out),
+                                          N.ptr(scr), sb, sh))
+        call()
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(reps):
+            e0.record()
+            call()
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        refined = int(scr[:4].view(torch.int32).item())
+        res[name] = {"ms_per_call": float(np.median(ms)), "observations": k.nobs, "fp64_reevaluated": refined,
+                     "fp64_fraction": refined / Nc, "finite": bool(torch.isfinite(out).all().item())}
+    t = res["l"]["ms_per_call"] + res["g"]["ms_per_call"]
+    pairs = Nc * (pair.good.nobs + pair.bad.nobs)
+    km = kernel_model(pair.bad, 0, 0)
+    name = km["kernel"].replace("true,true>", "false,false>").replace("false,true>", "false,false>")
+    rate = pairs / (t * 1e-3)
+    W = 92  # SURVEY 8d algorithmic flops per pair at 24c + 8u
+    return {"workload": "kde_logpdf_rtol%g_d32_obs%d_cand%d" % (rtol, pair.good.nobs + pair.bad.nobs, Nc),
+            "value": rate, "unit": "pairs/s", "ms_l_plus_g": t, "rtol": rtol, "kernel": name, "per_kde": res,
+            "roofline": {"bound": "mfma", "achieved": W * rate / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": W * rate / 1e12 / PEAK_F16_MFMA_TFLOPS,
+                         "basis": "whole hbx_kde_logpdf_rtol call (scoring launch + classify + fp64 re-evaluation)"}}
 
 
 def config2_line(device, reps=50):
@@ -731,19 +827,37 @@ def load_clock(workload):
 
 def main():
     a = parse()
+    # before anything touches the GPU: N ranks however bench.py was started
+    how, what = plan_launch(a.gpus, os.environ, sys.argv[1:], os.path.abspath(__file__))
+    if how == "error":
+        log("error: " + what)
+        sys.exit(2)
+    if how == "spawn":
+        import subprocess
+        log("launching %d ranks: %s" % (a.gpus, " ".join(what)))
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["HBX_BENCH_SPAWNED"] = "1"
+        sys.exit(subprocess.call(what, env=env))
+    world = what
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.launch_check:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local,
+                          "spawned": os.environ.get("HBX_BENCH_SPAWNED") == "1"}), flush=True)
+        return
     import torch
     import torch.distributed as dist
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world))
     # one process per GPU; --share-gpu maps every rank onto the visible devices round-robin (rehearsal
     # of the multi-process path on a 1-GPU box, with --backend gloo: RCCL refuses two ranks per GPU)
     ndev = torch.cuda.device_count()
+    if not a.share_gpu and local >= ndev:
+        log("error: rank %d needs GPU %d but %d are visible (--share-gpu rehearses several ranks on one)"
+            % (rank, local, ndev))
+        sys.exit(2)
     dev_idx = local % ndev if a.share_gpu else local
     torch.cuda.set_device(dev_idx)
     device = torch.device("cuda", dev_idx)
@@ -867,7 +981,10 @@ def main():
                    "parallelism": "candidate-sharded x%d, %s" % (
                        world, "one collective: hbx_argmax_allreduce (RCCL all-gather of result records)"
                        if a.backend == "nccl" else "gloo all_gather of result records (rehearsal)"),
-                   "winner": winner[0], "shortlist": last.shortlist},
+                   "winner": winner[0], "shortlist": last.shortlist,
+                   "world_size_rccl": xchg.rccl_world_size() if xchg is not None else None,
+                   "launcher": ("bench.py -> torch.distributed.run" if os.environ.get("HBX_BENCH_SPAWNED") == "1"
+                                else "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")},
         # the kernel runs on the f16 matrix cores: priced against their dense peak (no sparsity
         # credit), with SURVEY 8d's algorithmic W flops per pair; the formulation's own matrix work and
         # the VALU-basis figure SURVEY 8d first proposed are reported beside it
@@ -908,6 +1025,7 @@ def main():
     if rank == 0 and not a.no_config5:
         try:
             out["promote_dropin"] = promote_dropin(device)
+            out["promote_dropin_n81"] = promote_dropin(device, n=81)
         except Exception as e:
             out["promote_dropin"] = {"error": repr(e)}
         if world == 1:
@@ -924,9 +1042,17 @@ def main():
         except Exception as e:
             out["sh_stage"] = {"error": repr(e)}
         try:
+            out["sh_stage_interleaved"] = sh_stage_line(device, interleaved=True, reps=3)
+        except Exception as e:
+            out["sh_stage_interleaved"] = {"error": repr(e)}
+        try:
             out["gpu_sampler"] = sampler_line(pair, device, a.dc, a.du, a.levels, Nc, ws)
         except Exception as e:
             out["gpu_sampler"] = {"error": repr(e)}
+        try:
+            out["precise_logpdf"] = precise_line(pair, c_dev, device)
+        except Exception as e:
+            out["precise_logpdf"] = {"error": repr(e)}
         try:
             out["config2"] = config2_line(device)
         except Exception as e:

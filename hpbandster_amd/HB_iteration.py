@@ -25,30 +25,47 @@ class SuccessiveHalving(object):
         self.config_sampler = config_sampler
         self.num_running = 0
         self.device = device
-        # a stage's configurations requested back to back come from ONE batched acquisition
-        # when the sampler's generator offers get_config_batch_spec (BOHB); each is used only while it is
-        # exactly the sequential call's result (same model, same RNG states), else sampled afresh
+        # back-to-back requests are served from speculative batches when the sampler's
+        # generator offers them (BOHB.get_config_batch_spec); each result is used only while it is exactly
+        # the sequential call's (same model, same RNG states), else sampled afresh.  Batch sizes grow
+        # geometrically (1, 2, 4, ...) while every result of the last batch was served and nothing changed
+        # since; a batch cut short by a result (a model refit) or a draw in between falls back to single
+        # calls -- so with one worker, where every request follows a refit, nothing is computed ahead
         self.batch_sampling = batch_sampling
         self._spec = None
-        self._batch_cap = None  # after a batch was cut short at m results: batches of m
+        self._fp = None   # after a single call: the generator's state fingerprint (BOHB.spec_fingerprint)
+        self._next = 1    # size of the next speculative batch
+
+    MAX_BATCH = 128
 
     def _sample(self, budget):
         gen = getattr(self.config_sampler, "__self__", None)
         spec_fn = getattr(gen, "get_config_batch_spec", None) if self.batch_sampling else None
-        if spec_fn is None or getattr(self.config_sampler, "__name__", "") != "get_config":
+        if (spec_fn is None or getattr(self.config_sampler, "__name__", "") != "get_config"
+                or not gen.speculation_enabled()):
             return self.config_sampler(budget)
         if self._spec is not None:
-            if self._spec.valid():
-                return self._spec.pop()
-            if self._spec.served < len(self._spec.out):  # cut short: results arrive between requests
-                self._batch_cap = max(1, self._spec.served)
+            r = self._spec.take()
+            if r is not None:
+                return r
+            cont = self._spec.continues()
+            self._next = min(2 * len(self._spec), self.MAX_BATCH) if cont else 1
             self._spec = None
+        elif self._fp is not None:
+            self._next = 2 if gen.spec_fingerprint() == self._fp else 1
+        self._fp = None
         remaining = self.num_configs[self.SH_iter] - self.actual_num_configs[self.SH_iter]
-        size = remaining if self._batch_cap is None else min(remaining, self._batch_cap)
-        if size <= 1:
-            return self.config_sampler(budget)
-        self._spec = spec_fn(budget, size)
-        return self._spec.pop()
+        size = min(remaining, self._next)
+        if size > 1:
+            spec = spec_fn(budget, size)
+            r = spec.take() if spec is not None else None
+            if r is not None:
+                self._spec = spec
+                return r
+            self._next = 1
+        r = self.config_sampler(budget)
+        self._fp = gen.spec_fingerprint()
+        return r
 
     def add_configuration(self, config=None, config_info={}):
         if config is None:

@@ -72,6 +72,7 @@ SIGNATURES = {
     "hbx_rccl_unique_id_bytes": (c_i64, []),
     "hbx_rccl_get_unique_id": (c_i32, [c_vp]),
     "hbx_rccl_comm_init": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32]),
+    "hbx_rccl_comm_count": (c_i32, [c_vp, c_vp]),
     "hbx_rccl_comm_destroy": (c_i32, [c_vp]),
     "hbx_argmax_gather_bytes": (c_i64, [c_i32]),
     "hbx_argmax_allreduce": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),

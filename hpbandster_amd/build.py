@@ -66,32 +66,6 @@ def _compile(src, force):
     return obj, True
 
 
-PYFAST_SRC = os.path.join(CSRC, "hbx_pyfast.c")
-
-
-def pyfast_path():
-    import sysconfig
-    return os.path.join(LIBDIR, "_hbxfast" + sysconfig.get_config_var("EXT_SUFFIX"))
-
-
-def build_pyfast(force=False, verbose=True):
-    """The CPython module of the one-bracket promotion call (host marshalling only, hbx_pyfast.c)."""
-    import sysconfig
-    out = pyfast_path()
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(PYFAST_SRC):
-        return out
-    cc = os.environ.get("CC") or shutil.which("gcc") or "gcc"
-    tmp = out + ".tmp"
-    cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", "-I", sysconfig.get_paths()["include"], PYFAST_SRC, "-o", tmp]
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    if r.returncode != 0:
-        raise RuntimeError("gcc failed for %s:\n%s" % (PYFAST_SRC, r.stdout))
-    os.replace(tmp, out)
-    if verbose:
-        print("built %s" % out)
-    return out
-
-
 def build(force=False, jobs=None, verbose=True):
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = sources()
@@ -114,7 +88,6 @@ def build(force=False, jobs=None, verbose=True):
             print("built %s (%d objects)" % (LIB, len(objs)))
     elif verbose:
         print("%s is up to date" % LIB)
-    build_pyfast(force, verbose)
     return LIB
 
 

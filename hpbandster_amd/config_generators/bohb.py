@@ -15,6 +15,7 @@ reference's order), so a seeded run proposes the same configurations.  What move
 ``.bw`` and ``.pdf`` like the statsmodels objects of the reference.
 """
 
+import ctypes
 import traceback
 
 import numpy as np
@@ -26,53 +27,96 @@ from .base import base_config_generator
 from ._cs import ConfigSpace
 
 
-def _rng_snapshot(gen):
-    return (np.random.get_state(), gen.configspace.random.get_state(), gen._sample_counter)
+class _MT(object):
+    """The raw MT19937 state (key[624] words + position: 2500 bytes) of a legacy ``RandomState`` -- a
+    snapshot, compare or restore in ~1 us, where ``get_state`` / ``set_state`` cost ~60 us each (they
+    build and parse the state tuple).  The Gaussian cache of the legacy generator is not part of it:
+    BOHB's draws (``rand``, ``randint``, scipy's truncnorm by inversion of a uniform) never touch it."""
+    NB = 624 * 4 + 4
+
+    def __init__(self, rs):
+        bg = rs._bit_generator
+        if type(bg).__name__ != "MT19937":
+            raise TypeError("not an MT19937 RandomState")
+        self.rs, self.addr, self.lock = rs, bg.ctypes.state_address, bg.lock
+
+    def snap(self):
+        return ctypes.string_at(self.addr, self.NB)
+
+    def load(self, raw):
+        ctypes.memmove(self.addr, raw, self.NB)
 
 
-def _rng_same(a, b):
-    """Two snapshots of (global RNG, configspace RNG, GPU sampler counter) equal."""
-    for x, y in ((a[0], b[0]), (a[1], b[1])):
-        if x[0] != y[0] or x[2:] != y[2:] or not np.array_equal(x[1], y[1]):
-            return False
-    return a[2] == b[2]
+_GLOBAL = [None]
 
 
-def _rng_set(gen, snap):
-    np.random.set_state(snap[0])
-    gen.configspace.random.set_state(snap[1])
-    gen._sample_counter = snap[2]
+def _global_mt():
+    """_MT of numpy's global RandomState (the one np.random.rand / randint / scipy's rvs draw from)."""
+    R = np.random.mtrand._rand
+    g = _GLOBAL[0]
+    if g is None or g.rs is not R:
+        try:
+            g = _GLOBAL[0] = _MT(R)
+        except (TypeError, AttributeError):
+            return None
+    return g
 
 
 class SpeculativeBatch(object):
-    """get_config results computed ahead in one batched acquisition (BOHB.get_config_batch_spec)."""
+    """get_config results computed ahead in one batched acquisition (BOHB.get_config_batch_spec).
 
-    def __init__(self, gen, out, before, after, version):
-        self.gen, self.out, self.after, self.version = gen, out, after, version
+    The draws were made from a PRIVATE copy of the global RNG: nothing outside changes until a result is
+    served.  ``take()`` serves result j only when it is exactly what the sequential call would return at
+    that moment -- the model unchanged (``_model_version``), the GPU sampler's counter and the global
+    RNG's raw state equal to those before call j -- and then moves the global RNG (under its lock, so no
+    other thread's draw can fall between the check and the move) and the counter to where call j leaves
+    them.  A random pick (and its warning) is made only when served, from the configspace's own RNG, as
+    the sequential call makes it."""
+
+    def __init__(self, gen, entries, states, counters, version):
+        self.gen, self.entries, self.states, self.counters, self.version = gen, entries, states, counters, version
+        self.mt = _global_mt()
         self.served = 0
-        _rng_set(gen, before)  # nothing consumed yet: pop() moves the RNGs call by call
 
-    def valid(self):
-        """The next result is exactly the sequential call's: same model, RNGs where the last call left them."""
+    def __len__(self):
+        return len(self.entries)
+
+    def _valid_at(self, j):
         g = self.gen
-        if self.served >= len(self.out) or g._model_version != self.version:
-            return False
-        if self.served == 0:
-            return True
-        return _rng_same(_rng_snapshot(g), self.after[self.served - 1])
+        return g._model_version == self.version and g._sample_counter == self.counters[j]
 
-    def pop(self):
-        r = self.out[self.served]
-        _rng_set(self.gen, self.after[self.served])
+    def take(self):
+        """The next result, or None when it is not the sequential call's (or the batch is used up)."""
+        j = self.served
+        if j >= len(self.entries) or not self._valid_at(j):
+            return None
+        mt = self.mt
+        with mt.lock:
+            if mt.snap() != self.states[j]:
+                return None
+            mt.load(self.states[j + 1])
+        self.gen._sample_counter = self.counters[j + 1]
         self.served += 1
-        return r
+        return self.gen._serve(self.entries[j])
+
+    def continues(self):
+        """Every result served and nothing changed since: a longer batch would have stayed valid."""
+        j = self.served
+        return j == len(self.entries) and self._valid_at(j) and self.mt.snap() == self.states[j]
 
 
 class BOHB(base_config_generator):
     def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
                  random_fraction=1 / 3, bandwidth_factor=3, device=None, sampler="host", sampler_seed=None,
-                 **kwargs):
+                 speculative="auto", **kwargs):
         super().__init__(**kwargs)
+        # speculative batches (SuccessiveHalving serving a stage's back-to-back requests from one batched
+        # acquisition): 'auto' = with the GPU sampler only (the host sampler's scipy draws cost ~100x the
+        # acquisition, so batching them gains nothing and risks drawing for calls never served),
+        # 'always', 'never'
+        if speculative not in ("auto", "always", "never"):
+            raise ValueError("speculative must be 'auto', 'always' or 'never'")
+        self.speculative = speculative
         # sampler 'host': the reference's draws from the global numpy RNG (seeded runs reproduce the
         # reference's proposals); 'gpu': the same rule drawn on the GPU from a Philox stream
         # (distributional parity; for large num_samples, where host sampling dominates)
@@ -122,23 +166,26 @@ class BOHB(base_config_generator):
         self._model_version = 0  # bumped whenever kde_models changes (speculative batches check it)
 
     # -- candidates ---------------------------------------------------------------------------
-    def sample_candidates(self, kde_good, num_samples):
+    def sample_candidates(self, kde_good, num_samples, rng=None):
         """bohb.py:133-147: around a random good observation, truncnorm per continuous dim (bounds
-        from bw, scale bandwidth_factor * bw), keep-or-resample per categorical dim.  Global RNG."""
+        from bw, scale bandwidth_factor * bw), keep-or-resample per categorical dim.  Global RNG (or
+        ``rng``, a RandomState drawn from in the same order)."""
+        R = np.random.mtrand._rand if rng is None else rng
         D = len(self.vartypes)
         cands = np.empty((num_samples, D), dtype=np.float64)
         data = kde_good.data
         bws = kde_good.bw
         for i in range(num_samples):
-            idx = np.random.randint(0, len(data))
+            idx = R.randint(0, len(data))
             for d, (m, bw, t) in enumerate(zip(data[idx], bws, self.vartypes)):
                 if t == 0:
-                    cands[i, d] = sps.truncnorm.rvs(-m / bw, (1 - m) / bw, loc=m, scale=self.bw_factor * bw)
+                    cands[i, d] = sps.truncnorm.rvs(-m / bw, (1 - m) / bw, loc=m, scale=self.bw_factor * bw,
+                                                    random_state=R)
                 else:
-                    if np.random.rand() < (1 - bw):
+                    if R.rand() < (1 - bw):
                         cands[i, d] = m
                     else:
-                        cands[i, d] = np.random.randint(t)
+                        cands[i, d] = R.randint(t)
         return cands
 
     def draw_candidates(self, pair, num_samples):
@@ -187,95 +234,133 @@ class BOHB(base_config_generator):
                 info_dict['model_based_pick'] = False
         return sample, info_dict
 
-    def get_config_batch_spec(self, budget, k):
-        """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass), handed out one at a
-        time by the returned SpeculativeBatch -- each only while it is exactly what the sequential call
-        would return at that moment: the model unchanged (no refit since, ``_model_version``) and every
-        RNG the calls consume (numpy's global one, the configspace's, the GPU sampler's counter) in the
-        state the previous call left.  The RNGs are rewound to the state after call 1 at once, so
-        anything else drawing in between (a worker, another generator) sees the sequential stream."""
-        before = _rng_snapshot(self)
-        after = []
-        out = self.get_config_batch(budget, k, _snapshots=after)
-        spec = SpeculativeBatch(self, out, before, after, self._model_version)
-        return spec
+    # -- several get_config calls in one GPU pass ----------------------------
+    def speculation_enabled(self):
+        return self.speculative == "always" or (self.speculative == "auto" and self.sampler == "gpu")
 
-    def get_config_batch(self, budget, k, _snapshots=None):
+    def spec_fingerprint(self):
+        """(model version, GPU sampler counter, raw global RNG state): equal before and after an interval
+        iff a get_config at its end returns what one at its start would have."""
+        mt = _global_mt()
+        return (self._model_version, self._sample_counter, mt.snap() if mt is not None else None)
+
+    def get_config_batch_spec(self, budget, k):
+        """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass) from a private copy of
+        the global RNG, handed out one at a time by the returned SpeculativeBatch -- each only while it is
+        exactly what the sequential call would return at that moment (see SpeculativeBatch).  Returns None
+        when the global RNG cannot be copied (not a legacy MT19937 RandomState)."""
+        g = _global_mt()
+        if g is None:
+            return None
+        rs = getattr(self, "_spec_rs", None)
+        if rs is None:
+            rs = self._spec_rs = np.random.RandomState()
+            self._spec_mt = _MT(rs)
+        pm = self._spec_mt
+        states = [g.snap()]
+        pm.load(states[0])
+        counters = [self._sample_counter]
+        version = self._model_version
+        entries = self._batch_entries(k, rs, states, counters, pm)
+        return SpeculativeBatch(self, entries, states, counters, version)
+
+    def get_config_batch(self, budget, k):
         """``[self.get_config(budget) for _ in range(k)]`` with one GPU pass for all model-based calls.
 
         Valid while no result arrives in between (the model is fixed): an SH stage's first
         ``num_configs[0]`` samples (HB_iteration.py:136-138).  The global numpy RNG is consumed in the
         same order as k sequential calls (the draws of a call do not depend on earlier calls' scores)
-        and the configspace RNG is consumed in call order, so the returned list is identical to the
-        sequential one.
+        and the configspace RNG in call order, so the returned list is identical to the sequential one.
         """
-        plan = []  # per call: None (random pick) or the row offset of its candidates
+        return [self._serve(e) for e in self._batch_entries(k, np.random.mtrand._rand)]
+
+    def _batch_entries(self, k, R, states=None, counters=None, mt=None):
+        """The draws of k calls from RandomState R (and the GPU sampler's counter), their candidates scored
+        in one batched acquisition.  Per call an entry: ('model', best vector, score) or ('random', log
+        level, message) -- the random configuration itself is drawn from the configspace's RNG when the
+        entry is served.  With ``states`` / ``counters``: R's raw state (``mt``) and the counter after
+        every call are appended."""
+        plan = []  # per call: None (random pick), ('err', message) or the row offset of its candidates
         blocks = []
         pair = None
-        g_after = []  # numpy's global RNG state after each call's draws (speculative batches)
-        counter0 = self._sample_counter
+        counter = self._sample_counter
         for _ in range(int(k)):
-            if _snapshots is not None and plan:
-                g_after.append(np.random.get_state())
-            if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
+            if len(self.kde_models.keys()) == 0 or R.rand() < self.random_fraction:
                 plan.append(None)
-                continue
-            if pair is None:
-                pair = self.kde_models[max(self.kde_models.keys())]  # bohb.py:124
-            if self.sampler == "gpu":
-                plan.append(len(blocks) * self.num_samples)
-                blocks.append(None)
-                continue
-            try:  # a sampling error falls back to a random configuration for this call only, after
-                # consuming the global RNG exactly as the sequential call would (bohb.py:163-166)
-                block = self.sample_candidates(pair['good'], self.num_samples)
-            except Exception:
-                self.logger.warning("Sampling based optimization with %i samples failed\n %s \nUsing random "
-                                    "configuration" % (self.num_samples, traceback.format_exc()))
-                plan.append(None)
-                continue
-            plan.append(len(blocks) * self.num_samples)
-            blocks.append(block)
-        if _snapshots is not None and plan:
-            g_after.append(np.random.get_state())
-        results, bad = [], None
-        if blocks:
-            if self.sampler == "gpu":  # one draw for all calls: same Philox counters as call by call
-                cands, err = self.draw_candidates(pair, len(blocks) * self.num_samples)
-                bad = err.view(len(blocks), self.num_samples).any(dim=1).cpu().numpy()
             else:
-                cands = np.concatenate(blocks, axis=0)
-            results = pair.acquire_batch(cands, self.num_samples)
-        out = []
-        nmodel = 0
-        for i, off in enumerate(plan):
-            if _snapshots is not None and i > 0:  # call i-1 is complete: every RNG's state after it
-                _snapshots.append((g_after[i - 1], self.configspace.random.get_state(),
-                                   counter0 + nmodel * self.num_samples))
-            if off is not None:
-                nmodel += 1
+                if pair is None:
+                    pair = self.kde_models[max(self.kde_models.keys())]  # bohb.py:124
+                if self.sampler == "gpu":
+                    plan.append(len(blocks) * self.num_samples)
+                    blocks.append(None)
+                    counter += self.num_samples
+                else:
+                    try:  # a sampling error falls back to a random configuration for this call only, after
+                        # consuming the RNG exactly as the sequential call would (bohb.py:163-166)
+                        block = self.sample_candidates(pair['good'], self.num_samples, rng=R)
+                        plan.append(len(blocks) * self.num_samples)
+                        blocks.append(block)
+                    except Exception:
+                        plan.append(("err", "Sampling based optimization with %i samples failed\n %s \nUsing random "
+                                            "configuration" % (self.num_samples, traceback.format_exc())))
+            if states is not None:
+                states.append(mt.snap())
+                counters.append(counter)
+        entries = []
+        if not blocks:
+            return [("random", None, None) if p is None else ("random", "warning", p[1]) for p in plan]
+        if self.sampler == "gpu":  # one draw for all calls: the same Philox counters as call by call
+            cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, len(blocks) * self.num_samples,
+                                                self.sampler_seed, self._sample_counter if states is None
+                                                else counters[0])
+            if states is None:
+                self._sample_counter += len(blocks) * self.num_samples
+        else:
+            cands, err = np.concatenate(blocks, axis=0), None
+        results = pair.acquire_batch(cands, self.num_samples)
+        # the winners' rows in one gather (one device-to-host copy for a device candidate set)
+        win = [off + results[off // self.num_samples].index for off in plan
+               if type(off) is int and results[off // self.num_samples].index >= 0]
+        if err is not None:
+            import torch
+            bad = err.view(len(blocks), self.num_samples).any(dim=1).cpu().numpy()
+            rows = cands[torch.as_tensor(win, dtype=torch.int64, device=cands.device)].cpu().numpy() if win else None
+        else:
+            bad, rows = None, cands[win] if win else None
+        w = 0
+        for off in plan:
             if off is None:
-                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
-                continue
-            res = results[off // self.num_samples]
-            if bad is not None and bad[off // self.num_samples]:
-                self.logger.warning("Sampling based optimization with %i samples failed (truncnorm domain error)"
-                                    "\nUsing random configuration" % self.num_samples)
-                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
-            elif res.index < 0:
-                self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
-                                  % self.num_samples)
-                out.append((self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}))
+                entries.append(("random", None, None))
+            elif type(off) is tuple:
+                entries.append(("random", "warning", off[1]))
             else:
-                vec = cands[off + res.index]
-                if bad is not None:
-                    vec = vec.cpu().numpy()
-                out.append((ConfigSpace.Configuration(self.configspace, vector=vec).get_dictionary(),
-                            {'model_based_pick': True}))
-        if _snapshots is not None and plan:
-            _snapshots.append((g_after[-1], self.configspace.random.get_state(),
-                               counter0 + nmodel * self.num_samples))
-        return out
+                res = results[off // self.num_samples]
+                if bad is not None and bad[off // self.num_samples]:
+                    if res.index >= 0:
+                        w += 1
+                    entries.append(("random", "warning", "Sampling based optimization with %i samples failed "
+                                                         "(truncnorm domain error)\nUsing random configuration"
+                                                         % self.num_samples))
+                elif res.index < 0:
+                    entries.append(("random", "debug", "Sampling based optimization with %i samples failed -> "
+                                                       "using random configuration" % self.num_samples))
+                else:
+                    entries.append(("model", rows[w], res.score))
+                    w += 1
+        return entries
+
+    def _serve(self, e):
+        """One get_config result from a batch entry (the logging and random draws of bohb.py:124-169 happen
+        here, when the result is handed out)."""
+        if e[0] == "model":
+            self.logger.debug('best_vector: {}, {}'.format(e[1], e[2]))
+            return (ConfigSpace.Configuration(self.configspace, vector=e[1]).get_dictionary(),
+                    {'model_based_pick': True})
+        if e[1] == "warning":
+            self.logger.warning(e[2])
+        elif e[1] == "debug":
+            self.logger.debug(e[2])
+        return self.configspace.sample_configuration().get_dictionary(), {'model_based_pick': False}
 
     # -- observations ---------------------------------------------------------------------------
     def new_result(self, job):

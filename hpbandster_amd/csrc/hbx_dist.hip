@@ -85,6 +85,15 @@ int hbx_rccl_comm_init(void** comm, int32_t nranks, const void* id, int32_t rank
   return HBX_OK;
 }
 
+// the communicator's rank count as RCCL itself reports it (the bench line's world size)
+int hbx_rccl_comm_count(void* comm, int32_t* count) {
+  if (!comm || !count) return hbx_fail(HBX_ERR_ARG, "hbx_rccl_comm_count: null");
+  int c = 0;
+  HBX_RCCL(ncclCommCount((ncclComm_t)comm, &c));
+  *count = c;
+  return HBX_OK;
+}
+
 int hbx_rccl_comm_destroy(void* comm) {
   if (comm) HBX_RCCL(ncclCommDestroy((ncclComm_t)comm));
   return HBX_OK;

@@ -117,9 +117,6 @@ __device__ __forceinline__ uint64_t sel_key(double x) {
 __device__ __forceinline__ double sel_val(uint64_t k) {
   return __longlong_as_double((long long)((k >> 63) ? (k ^ 0x8000000000000000ull) : ~k));
 }
-#ifndef HBX_SEL_QS
-#define HBX_SEL_QS 0  // 1: the last <= 64 keys by quickselect (ablation: 6 % slower at config #5)
-#endif
 // a uniform 64-bit value into scalar registers (the bracket ends: the loops over them run in SALU)
 __device__ __forceinline__ uint64_t sel_uniform(uint64_t x) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
@@ -272,43 +269,6 @@ __device__ __forceinline__ bool sh_select_wave(const double* __restrict__ lossp,
     const uint64_t key1 = lane < cH - cL ? sel_key(cb[lane]) : ~0ull;
     Lk = sel_uniform(Lk);
     Hk = sel_uniform(Hk);
-#if HBX_SEL_QS
-    // quickselect of the j-th smallest key (j = kk - c0, 1 <= j < m) among the m lanes: the pivot is the
-    // middle candidate BY POSITION (position-sorted brackets pivot on their median), every pass drops the
-    // pivot from the candidate range [lo, hi), which always holds the j-th key -- about log2 m passes
-    // where the bisection below needs one per key bit (up to ~50); measured slower all the same: the
-    // bisection's passes are scalar work, each quickselect pass four dependent ballots and two readlanes
-    {
-      const int m = cH - cL, j = kk - c0;
-      const bool valid = lane < m;
-      uint64_t lo = Lk, hi = Hk, p = 0;
-      int cless = 0, cle = 0;
-      for (;;) {
-        const bool in = valid && key1 >= lo && key1 < hi;
-        const uint64_t cm = __builtin_amdgcn_ballot_w64(in);
-        const int half = (int)__popcll(cm) >> 1;
-        const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-        const uint64_t pm = __builtin_amdgcn_ballot_w64(in && rk == half);
-        const int pl = (int)__builtin_ctzll(pm);
-        p = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key1 >> 32), pl) << 32) |
-            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key1, pl);
-        cless = (int)__popcll(__builtin_amdgcn_ballot_w64(valid && key1 < p));
-        cle = (int)__popcll(__builtin_amdgcn_ballot_w64(valid && key1 <= p));
-        if (cless >= j) hi = p;
-        else if (cle >= j) break;  // p is the j-th key
-        else lo = p + 1ull;
-      }
-      if (cle == j) {  // exactly kk keys up to p: the threshold is the next key
-        Lk = p + 1ull;
-        cL = c0 + cle;
-      } else {  // copies of p straddle the k-th place
-        Lk = p;
-        Hk = p + 1ull;
-        cL = c0 + cless;
-        cH = c0 + cle;
-      }
-    }
-#endif
     while (HBX_SEL_OPEN) {
       const int bt = 63 - __clzll((long long)(Lk ^ (Hk - 1ull)));
       const uint64_t M = (Lk & ~((2ull << bt) - 1ull)) | (1ull << bt);
@@ -553,15 +513,22 @@ int hbx_sh_advance_state(int64_t* state, int64_t n, double k, void* stream) {
   state[5] = seq;
   double* pin = (double*)(intptr_t)state[0];
   uint8_t* pout = (uint8_t*)(intptr_t)state[1];
-  return hbx_sh_advance_mapped(pin, n, k, pout, pin, pout, (int32_t*)(intptr_t)state[2], seq,
-                               (void*)(intptr_t)state[3], (int32_t)state[4], stream);
+  const int dev = (int)state[6];
+  int cur = dev;
+  HBX_HIP(hipGetDevice(&cur));  // a dispatcher thread's current device may be another GPU
+  if (cur != dev) HBX_HIP(hipSetDevice(dev));
+  const int rc = hbx_sh_advance_mapped(pin, n, k, pout, pin, pout, (int32_t*)(intptr_t)state[2], seq,
+                                       (void*)(intptr_t)state[3], (int32_t)state[4], stream);
+  if (cur != dev) HBX_HIP(hipSetDevice(cur));
+  return rc;
 }
 
 // pinned host memory the device reads and writes directly (coherent, mapped): the drop-in promotion's
-// losses and mask travel with the kernel's own loads and stores, no copies
+// losses and mask travel with the kernel's own loads and stores, no copies.  Portable: mapped for every
+// device of the process, whichever is current when it is allocated
 int hbx_host_alloc(int64_t bytes, void** out) {
   if (!out || bytes <= 0) return hbx_fail(HBX_ERR_ARG, "hbx_host_alloc: %lld bytes", (long long)bytes);
-  HBX_HIP(hipHostMalloc(out, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  HBX_HIP(hipHostMalloc(out, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
   void* dp = nullptr;  // the engine passes the host address itself to kernels: it must be the device's too
   HBX_HIP(hipHostGetDevicePointer(&dp, *out, 0));
   if (dp != *out) {

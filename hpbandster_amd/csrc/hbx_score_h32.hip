@@ -38,9 +38,6 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define H32_CMAX 30000.f    // |shifted c_i| limit of the three-piece split (else: rescue pass)
-#ifndef HBX_PK_SUM
-#define HBX_PK_SUM 0        // 1: a tile's exp2 terms summed with packed f32 adds (A/B: tools/build_variant.sh)
-#endif
 
 // sparse index words of one tile: KS dwords (one ds_read).  KS = 1: both lane halves read the row's two
 // dwords and take theirs (ds_read_b64 banks over 64 dwords, b32 over 32: 4-way on these rows)
@@ -86,8 +83,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   static_assert(!SG || KP > 0, "signed sums come from categorical dims");
   static_assert(!FAST || KP > 0, "the fast instance drops the one-hot lo parts");
   static_assert(!CO || !SG, "the coarse instance is built for unsigned sums");
-  static_assert(CT == 1 || ((CT == 2 || (CT >= 3 && H32C_SNAKE)) && CO),
-                "several candidate column tiles per wave: the coarse instance (three: snake order)");
+  static_assert(CT == 1 || (CT == 2 && CO), "two candidate column tiles per wave: the coarse instance");
   constexpr int HW = CO ? H32C_WAVES : H16_WAVES;  // waves per block, 32 CT candidates each
   constexpr int AUXF = HW * 32 * CT * 4;  // per candidate: c_i, bound term, shift, rescue flag
   // LDS ring: 4 buffers (3 chunks in flight) when two blocks' rings fit in the 160 KB, else 3
@@ -349,35 +345,17 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   auto tile_sum = [&](const f32x16& a, const f32x16& ap, float& sn) -> float {
     float e[16];
 #pragma unroll
-#ifdef HBX_ABL_NOEXP
-    for (int r = 0; r < 16; ++r) e[r] = fabsf(a[r]);  // ablation: no exp2 (positive sums, no rescue)
-#else
     for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(a[r]);
-#endif
     if constexpr (SG) {
       sn = __builtin_amdgcn_fractf(ap[0]) * e[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) sn = fmaf(__builtin_amdgcn_fractf(ap[r]), e[r], sn);
     }
-#if HBX_PK_SUM
-    // packed pairwise tree (v_pk_add_f32: two adds per lane per instruction): lanes of the pair (r, r + 8),
-    // then (r, r + 4), (r, r + 2), (r, r + 1) -- depth 4 like the scalar tree, 7 packed adds + 1 add
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    f32x2 p[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) p[r] = f32x2{e[r], e[r + 8]};
-#pragma unroll
-    for (int w = 4; w >= 1; w >>= 1)
-#pragma unroll
-      for (int r = 0; r < w; ++r) p[r] = p[r] + p[r + w];
-    return p[0][0] + p[0][1];
-#else
 #pragma unroll
     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
       for (int r = 0; r < w; ++r) e[r] = e[2 * r] + e[2 * r + 1];
     return e[0];
-#endif
   };
   auto schedule = [&]() {
     SgbH32<0, NMT, 32, (KS > 0 ? 2 : 1)>::run();
@@ -426,36 +404,13 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     if constexpr (SG) Snb = tn;
     schedule();
   };
-  // two column tiles (unsigned sums): four phases per chunk, each one tile x one column tile; the
-  // fragments of a tile feed column tile 0 and then column tile 1, whose instructions re-read them for
-  // the next tile.  accA holds column tile 0's products, accB column tile 1's; each phase sums the
-  // accumulator the previous phase filled.  Per column tile the sums keep chunk1's association.
-  auto chunk2 = [&](int cc, int b) {
-    const float* buf = lds + b * CHF;
-    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
-    float tn;
-    issue(cc + PD, (b + PD) % NBUF, 0);
-    mma(accA, 0);                           // (T0(cc), 0)
-    Sb[CT - 1] += tile_sum(accB, accpB, tn);  // (T1(cc-1), 1): chunk cc-1 complete for column tile 1
-    S[CT - 1] += Sb[CT - 1];
-    schedule_nr();
-    mma_rd(accB, accpB, buf, 1);  // (T0(cc), 1); fragments of T1(cc)
-    Sb[0] = tile_sum(accA, accpA, tn);  // (T0(cc), 0)
-    schedule();
-    issue(cc + PD, (b + PD) % NBUF, 1);
-    mma(accA, 0);                           // (T1(cc), 0)
-    Sb[CT - 1] = tile_sum(accB, accpB, tn);  // (T0(cc), 1)
-    schedule_nr();
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
-    __builtin_amdgcn_s_barrier();
-    mma_rd(accB, accpB, nbuf, 0);  // (T1(cc), 1); fragments of T0(cc+1)
-    Sb[0] += tile_sum(accA, accpA, tn);  // (T1(cc), 0): chunk cc complete for column tile 0
-    S[0] += Sb[0];
-    schedule();
-  };
-  // the same in "snake" order: (T0, 0), (T0, 1), (T1, 1), (T1, 0), so every matrix instruction group shares
-  // one operand with the group before it (the A fragments, or column tile's B operands).  accA: the odd
-  // phases, accB: the even ones; column tile 0's T1 is summed in the next chunk's first phase
+  // two column tiles (unsigned sums): four phases per chunk, each one tile x one column tile, in "snake"
+  // order (T0, 0), (T0, 1), (T1, 1), (T1, 0), so every matrix instruction group shares one operand with
+  // the group before it (the A fragments, or the column tile's B operands); the fragments of a tile feed
+  // both column tiles, the second one's instructions re-reading them for the next tile.  accA: the odd
+  // phases, accB: the even ones; each phase sums the accumulator the previous phase filled, and per
+  // column tile the sums keep chunk1's association.  Column tile 0's T1 is summed in the next chunk's
+  // first phase
   auto chunk2s = [&](int cc, int b) {
     const float* buf = lds + b * CHF;
     const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
@@ -479,46 +434,9 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     S[CT - 1] += Sb[CT - 1];
     schedule();
   };
-  // any CT >= 2, snake order (the build uses it for CT >= 3: an ablation): phase p < CT is (T0, p), phase p >= CT is (T1, 2 CT - 1 - p); even phases fill
-  // accA, odd ones accB, each phase sums the one before (a T0 term opens the column tile's chunk sum, a T1
-  // term closes it).  The loop is fully unrolled: every index below is a constant
-  auto chunkNs = [&](int cc, int b) {
-    const float* buf = lds + b * CHF;
-    const float* nbuf = lds + ((b + 1) % NBUF) * CHF;
-    float tn;
-#pragma unroll
-    for (int p = 0; p < 2 * CT; ++p) {
-      const int t = p < CT ? p : 2 * CT - 1 - p;                 // this phase's column tile
-      const int q = p > 0 ? p - 1 : 2 * CT - 1;                  // the phase summed beside it
-      const int tq = q < CT ? q : 2 * CT - 1 - q;
-      if (p == 0 || p == CT) issue(cc + PD, (b + PD) % NBUF, p == 0 ? 0 : 1);
-      if (p == 2 * CT - 1) {
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GW * (PD - 1)) : "memory");
-        __builtin_amdgcn_s_barrier();
-      }
-      f32x16& acc = (p & 1) ? accB : accA;
-      f32x16& accp = (p & 1) ? accpB : accpA;
-      f32x16& prv = (p & 1) ? accA : accB;
-      f32x16& prvp = (p & 1) ? accpA : accpB;
-      if (p == CT - 1) mma_rd(acc, accp, buf, 1, t);           // last use of T0(cc): fragments of T1(cc)
-      else if (p == 2 * CT - 1) mma_rd(acc, accp, nbuf, 0, t);  // last use of T1(cc): fragments of T0(cc+1)
-      else mma(acc, t);
-      const float v = tile_sum(prv, prvp, tn);
-      if (q < CT) {
-        Sb[tq] = v;  // a T0 term: opens the column tile's chunk sum
-      } else {
-        Sb[tq] += v;  // a T1 term: the column tile's chunk complete
-        S[tq] += Sb[tq];
-      }
-      if (p == CT - 1 || p == 2 * CT - 1) schedule();
-      else schedule_nr();
-    }
-  };
   auto chunk = [&](int cc, int b) {
     if constexpr (CT == 1) chunk1(cc, b);
-    else if constexpr (CT >= 3) chunkNs(cc, b);
-    else if constexpr (H32C_SNAKE) chunk2s(cc, b);
-    else chunk2(cc, b);
+    else chunk2s(cc, b);
   };
   int cc = 0;
   for (; cc + NBUF <= nchunks; cc += NBUF) {
@@ -530,7 +448,7 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   for (; cc < nchunks; ++cc) chunk(cc, cc % NBUF);
   {
     float tn;
-    constexpr int tl = (CT > 1 && H32C_SNAKE) ? 0 : CT - 1;  // the column tile of the last phase
+    constexpr int tl = 0;  // the column tile of the last phase (CT = 2: snake order ends on column tile 0)
     Sb[tl] += tile_sum(accB, accpB, tn);  // T1(last)
     S[tl] += Sb[tl];
     if constexpr (SG) Sn += Snb + tn;

@@ -156,6 +156,16 @@ class WinnerExchange(object):
                 N.check(L.hbx_argmax_records(N.ptr(self.gather), self.world, N.ptr(self.out), sh))
         return self.out
 
+    def rccl_world_size(self):
+        """The rank count of libhbx's communicator as RCCL reports it (ncclCommCount); None for the
+        records transport."""
+        if self.comm is None:
+            return None
+        import ctypes
+        c = ctypes.c_int32(0)
+        N.check(N.lib().hbx_rccl_comm_count(self.comm, ctypes.addressof(c)))
+        return int(c.value)
+
     def records(self):
         raw = self.gather.cpu().numpy().tobytes()
         return [_unpack(raw[r * REC_BYTES:(r + 1) * REC_BYTES]) for r in range(self.world)]

@@ -10,6 +10,7 @@ losses straddle the k-th place are re-ranked in that order.  ``ties='stable'`` r
 """
 
 import ctypes
+import math
 import threading
 
 import numpy as np
@@ -71,9 +72,10 @@ class _Staging(object):
         self.cap = 0
         self._ptrs = []
         self.fn = N.lib().hbx_sh_advance_state
-        self.fast = _fast_module()
-        # hbx_sh_advance_state's block: {pin, pout, done, scratch, order_mode, seq}
-        self.state = (ctypes.c_int64 * 6)()
+        # hbx_sh_advance_state's block: {pin, pout, done, scratch, order_mode, seq, device}; the native call
+        # launches on `device` whatever device is current on the calling thread
+        self.state = (ctypes.c_int64 * 7)()
+        self.state[6] = self.index
         self.state_addr = ctypes.addressof(self.state)
         self.mode = None
         self.stream_of = _current_stream_fn()
@@ -85,7 +87,7 @@ class _Staging(object):
             cap = max(1024, 1 << (int(n) - 1).bit_length())
             self._release()
             pin, pout = ctypes.c_void_p(), ctypes.c_void_p()
-            N.check(L.hbx_host_alloc(8 * cap, ctypes.addressof(pin)))
+            N.check(L.hbx_host_alloc(8 * cap, ctypes.addressof(pin)))  # portable: mapped for every device
             N.check(L.hbx_host_alloc(cap + 64, ctypes.addressof(pout)))
             self._ptrs = [pin.value, pout.value]
             self.pin, self.pout = pin.value, pout.value
@@ -117,27 +119,6 @@ class _Staging(object):
 
 
 _tls = threading.local()
-_fast = None
-
-
-def _fast_module():
-    """_hbxfast (hbx_pyfast.c): advance_mask's call into hbx_sh_advance_state through the buffer protocol
-    instead of ctypes, with HBX_PYFAST=1 (not yet measured on the GPU: off by default); None otherwise or
-    when it was not built (the ctypes call then makes the same GPU call)."""
-    global _fast
-    if _fast is None:
-        import importlib.util
-        import os
-        from . import build as B
-        path = B.pyfast_path()
-        mod = False
-        if os.path.exists(path) and os.environ.get("HBX_PYFAST", "0") != "0":
-            spec = importlib.util.spec_from_file_location("hpbandster_amd._hbxfast", path)
-            mod = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(mod)
-            mod.set_entry(ctypes.cast(N.lib().hbx_sh_advance_state, ctypes.c_void_p).value)
-        _fast = mod
-    return _fast or None
 
 
 def _staging(device):
@@ -176,20 +157,68 @@ def _current_stream_fn():
 _MODES = {"numpy": N.ORDER_NUMPY, "stable": N.ORDER_STABLE, N.ORDER_NUMPY: N.ORDER_NUMPY,
           N.ORDER_STABLE: N.ORDER_STABLE}
 
+# one-bracket size policy (bench ``promote_dropin``, profiles/r04/promote_policy): up to HOST_MAX
+# configurations a bracket whose k-th and (k+1)-th smallest losses differ is ranked on the host -- every
+# sort gives the same first k then, so the mask is the reference's bit for bit -- because one kernel round
+# trip (launch, PCIe reads of the losses, the completion word: >= 8.3 us) costs more than numpy's sort of
+# a few hundred values.  Brackets with a tie straddling the k-th place (numpy 1.26.4's unstable order
+# decides them: restated on the device only), non-finite losses, and larger brackets go to the GPU.
+HOST_MAX = 4096
+_SORT_MAX = 256  # below: one argsort; above: np.partition (O(n))
 
-def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
+
+def _threshold(k, n):
+    """Number of ranks r in [0, n) with r < k (HB_iteration.py:180: ``ranks < k``; k may be fractional,
+    SuccessiveResampling's num_configs * (1 - rate)); NaN or k <= 0: none."""
+    if not k > 0:
+        return 0
+    return n if k >= n else int(math.ceil(k))
+
+
+def _host_rank(losses, kk, n):
+    """The mask of a tie-free bracket on the host, or None when the GPU must rank it (a tie across the
+    k-th place, a non-finite loss)."""
+    if kk == 0 or kk == n:
+        if not math.isfinite(float(losses.sum())):
+            return None
+        return np.full(n, kk == n, dtype=bool)
+    if n <= _SORT_MAX:
+        o = losses.argsort()
+        a, b = losses[o[kk - 1]], losses[o[kk]]
+        # finite: argsort puts -inf first and +inf / NaN last
+        if not (a < b and math.isfinite(losses[o[0]]) and math.isfinite(losses[o[n - 1]])):
+            return None
+        m = np.zeros(n, dtype=bool)
+        m[o[:kk]] = True
+        return m
+    p = np.partition(losses, (kk - 1, kk))
+    a, b = p[kk - 1], p[kk]
+    if not (a < b and math.isfinite(float(losses.sum()))):
+        return None
+    return losses <= a
+
+
+def advance_mask(losses, k, device=None, stream=None, ties="numpy", policy="auto"):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
-    What SuccessiveHalving.process_results calls once per bracket: the losses are copied into
-    device-mapped host memory, ONE host call into libhbx (hbx_sh_advance_mapped) launches the one-kernel
-    promotion (the selection, and the numpy-order re-rank when tied losses straddle the k-th place), spins
-    on the kernel's completion word (stored last) instead of synchronising the stream, and copies the
-    mask out."""
-    if type(losses) is not np.ndarray or losses.ndim != 1:
+    What SuccessiveHalving.process_results calls once per bracket.  ``policy='auto'``: brackets of at most
+    HOST_MAX configurations whose k-th place is not inside a run of tied losses are ranked on the host
+    (identical mask, see HOST_MAX); the rest -- and everything with ``policy='gpu'`` -- on the GPU: the
+    losses are copied into device-mapped host memory, ONE host call into libhbx (hbx_sh_advance_state)
+    launches the one-kernel promotion (the selection, and the numpy-order re-rank when tied losses straddle
+    the k-th place), spins on the kernel's completion word (stored last) instead of synchronising the
+    stream, and the mask is copied out."""
+    if type(losses) is not np.ndarray or losses.ndim != 1 or losses.dtype != np.float64:
         losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
     if n == 0:
         return np.zeros(0, dtype=bool)
+    if policy == "auto" and n <= HOST_MAX:
+        m = _host_rank(losses, _threshold(k, n), n)
+        if m is not None:
+            return m
+    elif policy not in ("auto", "gpu"):
+        raise ValueError("policy must be 'auto' or 'gpu'")
     if n > 1024:
         return promote_segments(losses, np.array([0, n], dtype=np.int64), [k], device=device, stream=stream,
                                 ties=ties)
@@ -200,13 +229,6 @@ def advance_mask(losses, k, device=None, stream=None, ties="numpy"):
     h = stream.cuda_stream if stream is not None else st.stream_of(st.index)
     if mode != st.mode:
         st.state[4] = st.mode = mode
-    if st.fast is not None:  # the same call without ctypes (losses in / mask out through the buffer protocol)
-        mask = np.empty(n, dtype=np.bool_)
-        rc = st.fast.advance(st.state_addr, st.cap, losses, mask, float(k), h)
-        if rc <= 0:
-            if rc:
-                N.check(rc)
-            return mask
     st.pin_v[:n] = losses  # straight into the mapped buffer the kernel reads
     rc = st.fn(st.state_addr, n, float(k), h)  # the sequence number advances in the state block
     if rc:

@@ -296,6 +296,8 @@ int hbx_kde_cv_terms(const double* X, int64_t n, int32_t D, const int32_t* varty
 int64_t hbx_rccl_unique_id_bytes(void);
 int hbx_rccl_get_unique_id(void* id_out);
 int hbx_rccl_comm_init(void** comm, int32_t nranks, const void* id, int32_t rank, int32_t device);
+/* the communicator's rank count as RCCL reports it (ncclCommCount) */
+int hbx_rccl_comm_count(void* comm, int32_t* count);
 int hbx_rccl_comm_destroy(void* comm);
 int64_t hbx_argmax_gather_bytes(int32_t nranks);
 int hbx_argmax_allreduce(const void* local, void* gather, void* out, int32_t nranks, void* rccl_comm, void* stream);
@@ -343,9 +345,10 @@ int hbx_sh_promote_one(const double* loss, int64_t n, double k, uint8_t* advance
 int hbx_sh_advance_mapped(const double* losses, int64_t n, double k, uint8_t* mask, double* pin, uint8_t* pout,
                           int32_t* done, int32_t seq, void* scratch, int32_t order_mode, void* stream);
 /* hbx_sh_advance_mapped with its buffers in a state block (4 arguments: what a per-call FFI hop costs, the
- * drop-in's advance_mask pays on every bracket): state = int64[6] {pin, pout, done, scratch, order_mode,
- * seq}.  The caller has written the losses into pin; the mask is left in pout; seq is advanced by the call
- * (1 ... 2^31 - 2, wrapping). */
+ * drop-in's advance_mask pays on every bracket): state = int64[7] {pin, pout, done, scratch, order_mode,
+ * seq, device}.  The caller has written the losses into pin; the mask is left in pout; seq is advanced by
+ * the call (1 ... 2^31 - 2, wrapping).  The launch runs on `device` (the scratch's; the stream must be one
+ * of its streams) whichever device is current on the calling thread, which is left as it was. */
 int hbx_sh_advance_state(int64_t* state, int64_t n, double k, void* stream);
 /* Pinned, device-mapped, coherent host memory (hipHostMalloc) and its release. */
 int hbx_host_alloc(int64_t bytes, void** out);

@@ -58,12 +58,16 @@ class _SyncDispatcher(object):
         return job
 
 
-def test_toy_function_run_matches_reference(device, tmp_path):
+def _toy_run(device, tmp_path, wrapped, speculative="auto"):
+    """HpBandSter.run(4) + GPU BOHB on the toy function.  wrapped: get_config behind a plain function (the
+    drop-in then calls it once per request); else the bound method itself, so SuccessiveHalving serves
+    back-to-back requests from speculative batches (the drop-in's default path), the calls recorded by an
+    iteration class around SuccessiveHalving._sample."""
     from hpbandster_amd import configspace as CS
+    from hpbandster_amd.HB_iteration import SuccessiveHalving
     from hpbandster_amd.HB_master import HpBandSter
     from hpbandster_amd.config_generators import BOHB
 
-    records, ref = G.load_e2e()
     space = CS.ConfigurationSpace(seed=5)
     space.add_hyperparameter(CS.UniformFloatHyperparameter("x", lower=0, upper=1))
     noise = np.random.RandomState(17)
@@ -75,21 +79,33 @@ def test_toy_function_run_matches_reference(device, tmp_path):
         return {"loss": float(np.mean(res)), "info": res}
 
     np.random.seed(123)
-    cg = BOHB(space, device=device)
+    cg = BOHB(space, device=device, speculative=speculative)
     calls = []
-    orig = cg.get_config
+    kw = {}
+    if wrapped:
+        orig = cg.get_config
 
-    def get_config(budget):
-        cfg, info = orig(budget)
-        calls.append((budget, cfg["x"], bool(info["model_based_pick"])))
-        return cfg, info
-
-    cg.get_config = get_config
+        def get_config(budget):
+            cfg, info = orig(budget)
+            calls.append((budget, cfg["x"], bool(info["model_based_pick"])))
+            return cfg, info
+        cg.get_config = get_config
+    else:
+        class RecordingSH(SuccessiveHalving):
+            def _sample(self, budget):
+                cfg, info = super()._sample(budget)
+                calls.append((budget, cfg["x"], bool(info["model_based_pick"])))
+                return cfg, info
+        kw["iteration_class"] = RecordingSH
     hb = HpBandSter(run_id="0", config_generator=cg, working_directory=str(tmp_path), eta=2, min_budget=1,
                     max_budget=64, dispatcher=_SyncDispatcher(compute))
-    res = hb.run(4)
+    res = hb.run(4, **kw)
     hb.shutdown()
+    return calls, res
 
+
+def _check_against_reference(calls, res):
+    records, ref = G.load_e2e()
     assert len(calls) == len(records)
     assert sum(bool(r["model_based"]) for r in records) > 0  # the KDE path is exercised
     for (b, x, mb), r in zip(calls, records):
@@ -112,3 +128,29 @@ def test_toy_function_run_matches_reference(device, tmp_path):
         np.testing.assert_allclose(got[3], w[3], rtol=0, atol=1e-12)
     inc = res.get_incumbent_id()
     assert (None if inc is None else list(inc)) == ref["incumbent"]
+
+
+def test_toy_function_run_matches_reference(device, tmp_path):
+    calls, res = _toy_run(device, tmp_path, wrapped=True)
+    _check_against_reference(calls, res)
+
+
+@pytest.mark.parametrize("speculative", ["auto", "always"])
+def test_toy_function_run_default_drop_in_path(device, tmp_path, monkeypatch, speculative):
+    """The drop-in's default path: cg.get_config passed unwrapped, so SuccessiveHalving may
+    serve requests from speculative batches ('always': also with the host sampler the fixture uses; at
+    least one batched pass must run) -- and the run still reproduces the reference's own run."""
+    from hpbandster_amd import kde
+    orig = kde.KDEPair.acquire_batch
+    n = [0]
+
+    def acquire_batch(selfp, *a, **k):
+        n[0] += 1
+        return orig(selfp, *a, **k)
+    monkeypatch.setattr(kde.KDEPair, "acquire_batch", acquire_batch)
+    calls, res = _toy_run(device, tmp_path, wrapped=False, speculative=speculative)
+    _check_against_reference(calls, res)
+    if speculative == "always":
+        assert n[0] > 0
+    else:
+        assert n[0] == 0  # the host sampler: no speculation by default

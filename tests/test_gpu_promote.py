@@ -8,14 +8,53 @@ from tests import golden_cases as G
 pytestmark = pytest.mark.gpu
 
 
-def test_promotion_matches_reference(device):
+@pytest.mark.parametrize("policy", ["gpu", "auto"])
+def test_promotion_matches_reference(device, policy):
     from hpbandster_amd import promote
     for c in G.load_sh():
         losses = np.where(c["crashed"], np.nan, c["losses"])
-        adv = promote.advance_mask(losses, c["k"], device=device)
+        adv = promote.advance_mask(losses, c["k"], device=device, policy=policy)
         np.testing.assert_array_equal(adv, c["sh_adv"])
-        adv = promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device)
+        adv = promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device, policy=policy)
         np.testing.assert_array_equal(adv, c["sr_adv"])
+
+
+def test_size_policy_equals_gpu_path(device):
+    """advance_mask's size policy (host ranking of tie-free brackets up to HOST_MAX) gives the GPU path's
+    masks: tie-free, straddling and non-straddling ties, -0.0 against 0.0, non-finite losses, fractional,
+    zero, NaN and oversized k, at sizes across the argsort / partition switch and past 1024."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(77)
+    for n in (1, 2, 3, 27, 81, 255, 256, 257, 700, 1024, 1025, 3000):
+        for trial in range(4):
+            if trial == 0:
+                losses = rs.rand(n)
+            elif trial == 1:
+                losses = np.round(rs.rand(n) * 5) / 5
+            elif trial == 2:
+                losses = rs.rand(n)
+                losses[rs.rand(n) < 0.1] = rs.choice([np.inf, -np.inf, np.nan, -0.0, 0.0])
+            else:
+                losses = rs.randn(n) * 10.0 ** rs.randint(-3, 3, n)
+            for k in (n // 3, max(1, n // 2) + 0.5, 0, n, n + 4, float("nan"), 1):
+                want = promote.advance_mask(losses, k, device=device, policy="gpu")
+                got = promote.advance_mask(losses, k, device=device, policy="auto")
+                np.testing.assert_array_equal(got, want, err_msg="n=%d trial=%d k=%r" % (n, trial, k))
+
+
+def test_advance_mask_on_a_non_current_device():
+    """The one-bracket state entry launches on the staging's device whatever device is current on the
+    calling thread (a dispatcher thread's is 0): needs two visible GPUs."""
+    import torch
+    from hpbandster_amd import promote
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    d1 = torch.device("cuda", 1)
+    losses = np.random.RandomState(3).rand(500)
+    want = np.argsort(np.argsort(losses)) < 166
+    with torch.cuda.device(0):
+        np.testing.assert_array_equal(promote.advance_mask(losses, 166, device=d1, policy="gpu"), want)
+        assert torch.cuda.current_device() == 0
 
 
 @pytest.mark.parametrize("B,n", [(1, 1), (3, 5000), (64, 1000), (1000, 81), (7, 4097)])
@@ -38,7 +77,7 @@ def test_batched_promotion_matches_oracle(device, B, n):
 def test_promotion_ties_stable_and_numpy(device):
     from hpbandster_amd import promote
     loss = np.array([1.0] * 40 + [0.5] * 10)
-    adv = promote.advance_mask(loss, 15, device=device, ties="stable")
+    adv = promote.advance_mask(loss, 15, device=device, ties="stable", policy="gpu")
     assert adv[40:].all() and adv[:5].all() and not adv[5:40].any()
     # numpy 1.26.4's argsort of this array starts [40..45, 48, 49, 46, 47, 0, 1, 4, 5, 2, 3, ...]
     adv = promote.advance_mask(loss, 15, device=device)
@@ -58,7 +97,7 @@ def test_one_bracket_entries_agree(device):
     for losses, k in cases:
         n = len(losses)
         for ties, mode in (("numpy", N.ORDER_NUMPY), ("stable", N.ORDER_STABLE)):
-            want = promote.advance_mask(losses, k, device=device, ties=ties)
+            want = promote.advance_mask(losses, k, device=device, ties=ties, policy="gpu")
             assert want.sum() == min(k, n)
             ld = torch.from_numpy(losses).to(device)
             ad = torch.full((n,), 7, dtype=torch.uint8, device=device)
@@ -78,7 +117,7 @@ def test_advance_state_sequence_wraps(device):
     on either side of the wrap still yields numpy's masks."""
     from hpbandster_amd import promote
     tie = np.array([1.0] * 40 + [0.5] * 10)
-    want_tie = promote.advance_mask(tie, 15, device=device)
+    want_tie = promote.advance_mask(tie, 15, device=device, policy="gpu")
     assert sorted(np.nonzero(want_tie)[0].tolist()) == [0, 1, 2, 4, 5] + list(range(40, 50))
     rnd = np.random.RandomState(5).rand(700)
     want_rnd = np.argsort(np.argsort(rnd)) < 233
@@ -87,7 +126,8 @@ def test_advance_state_sequence_wraps(device):
     seqs = []
     for i in range(6):
         losses, k, want = (tie, 15, want_tie) if i % 2 else (rnd, 233, want_rnd)
-        np.testing.assert_array_equal(promote.advance_mask(losses, k, device=device), want, err_msg="call %d" % i)
+        np.testing.assert_array_equal(promote.advance_mask(losses, k, device=device, policy="gpu"), want,
+                                      err_msg="call %d" % i)
         seqs.append(int(st.state[5]))
     assert seqs == [0x7ffffffe - 1, 0x7ffffffe, 1, 2, 3, 4], seqs
 

@@ -121,9 +121,11 @@ def test_promotion_masks_on_ties(device, which):
     cases = G.load_sh(which)
     for c in cases:
         losses = np.where(c["crashed"], np.nan, c["losses"])
-        np.testing.assert_array_equal(promote.advance_mask(losses, c["k"], device=device), c["sh_adv"])
-        np.testing.assert_array_equal(promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device),
-                                      c["sr_adv"])
+        for policy in ("gpu", "auto"):
+            np.testing.assert_array_equal(promote.advance_mask(losses, c["k"], device=device, policy=policy),
+                                          c["sh_adv"])
+            np.testing.assert_array_equal(promote.advance_mask(losses, max(1, c["k"] * (1 - 0.5)), device=device,
+                                                               policy=policy), c["sr_adv"])
     loss = np.concatenate([np.where(c["crashed"], np.nan, c["losses"]) for c in cases])
     seg = np.concatenate([[0], np.cumsum([c["losses"].size for c in cases])]).astype(np.int64)
     k = np.array([c["k"] for c in cases], dtype=np.float64)

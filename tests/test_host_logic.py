@@ -201,3 +201,28 @@ def test_rccl_uid_broadcast_in_a_subgroup_without_global_rank0():
     for p in ps:
         p.join(60)
     assert out == {1: b"uid-of-rank-1", 2: b"uid-of-rank-1"}
+
+
+def test_promotion_size_policy_host_rank():
+    """advance_mask's host ranking (tie-free brackets up to HOST_MAX): the reference's argsort(argsort) < k
+    mask (HB_iteration.py:180) wherever the k-th and (k+1)-th smallest losses differ; None -- the GPU's
+    numpy-order path -- where tied losses straddle the k-th place or a loss is not finite."""
+    from hpbandster_amd import promote as P
+    rs = np.random.RandomState(9)
+    for n in (1, 2, 5, 81, 256, 257, 1000, 4096):
+        x = rs.rand(n)
+        for k in (0, 1, n // 3, n // 2 + 0.5, n - 1, n, n + 3, float("nan"), -1.0):
+            m = P._host_rank(x, P._threshold(k, n), n)
+            assert m is not None
+            want = (np.argsort(np.argsort(x)) < k) if k == k and k > 0 else np.zeros(n, bool)
+            np.testing.assert_array_equal(m, want, err_msg="n=%d k=%r" % (n, k))
+    tie = np.array([1.0] * 40 + [0.5] * 10)
+    assert P._host_rank(tie, 15, 50) is None            # straddling tie: numpy 1.26.4's order decides
+    assert P._host_rank(tie, 10, 50) is not None        # the tie is wholly above the k-th place
+    assert P._host_rank(np.array([-0.0, 0.0, 1.0]), 1, 3) is None  # -0.0 == 0.0 ties
+    for bad in (np.inf, -np.inf, np.nan):
+        y = rs.rand(300)
+        y[17] = bad
+        assert P._host_rank(y, 100, 300) is None
+        assert P._host_rank(y[:100], 30, 100) is None
+    assert P._threshold(4.5, 10) == 5 and P._threshold(3, 10) == 3 and P._threshold(20, 10) == 10

@@ -27,15 +27,24 @@ def per_call(fn, reps):
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
+    for n in [int(a) for a in (sys.argv[1] if len(sys.argv) > 1 else "1000").split(",")]:
+        one(n, int(sys.argv[2]) if len(sys.argv) > 2 else 2000)
+
+
+def one(n, reps):
     dev = torch.device("cuda", 0)
     losses = np.random.RandomState(3).rand(n)
     k = n // 3
     want = np.argsort(np.argsort(losses)) < k
+    assert (promote.advance_mask(losses, k, device=dev, policy="gpu") == want).all()
     assert (promote.advance_mask(losses, k, device=dev) == want).all()
     host = per_call(lambda: np.argsort(np.argsort(losses)) < k, reps)
-    drop = per_call(lambda: promote.advance_mask(losses, k, device=dev), reps)
+    drop = per_call(lambda: promote.advance_mask(losses, k, device=dev, policy="gpu"), reps)
+    policy = per_call(lambda: promote.advance_mask(losses, k, device=dev), reps)
+    if n > 1024:  # the one-bracket kernels take n <= 1024; larger brackets go through promote_segments
+        print({"n": n, "reps": reps, "host_numpy_us": round(host, 2), "advance_mask_gpu_us": round(drop, 2),
+               "size_policy_us": round(policy, 2)})
+        return
     st = promote._staging(dev).get(n)
     stream = torch.cuda.current_stream(dev).cuda_stream
     mask = np.empty(n, dtype=np.bool_)
@@ -79,7 +88,7 @@ def main():
     launch_side = per_call(lambda: one(st._ptrs[0], n, float(k), st._ptrs[1], st.scr_ptr, N.ORDER_NUMPY, None, 0, hs),
                            200)
     side.synchronize()
-    drop_side = per_call(lambda: promote.advance_mask(losses, k, device=dev, stream=side), reps)
+    drop_side = per_call(lambda: promote.advance_mask(losses, k, device=dev, stream=side, policy="gpu"), reps)
     # the floor of any one-launch round trip: hbx_fetch of 8 bytes (launch, a one-wave kernel storing them and
     # its completion word into mapped memory, the host spin) -- no losses read, no selection
     src = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -103,6 +112,7 @@ def main():
     torch.cuda.synchronize()
     assert (ad.cpu().numpy().astype(bool) == want).all()
     print({"n": n, "reps": reps, "fetch8_floor_us": round(floor_us, 2), "device_resident_us": round(devres_us, 2), "host_numpy_us": round(host, 2), "advance_mask_us": round(drop, 2),
+           "size_policy_us": round(policy, 2),
            "native_call_us": round(native, 2), "state_call_us": round(state_us, 2), "launch_only_us": round(launch_us, 2),
            "launch_sync_us": round(sync_us, 2), "stream": stream,
            "side_stream": {"advance_mask_us": round(drop_side, 2), "native_call_us": round(native_side, 2),
