@@ -17,13 +17,11 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <atomic>
 #include <vector>
 
 #include "hbx_common.h"
 #include <hip/hip_ext.h>
 #include "hbx_kde_impl.h"
-#include "hbx_combine.h"
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -660,9 +658,14 @@ static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s)
 // with a true maximum (two passes over the observations), one candidate per thread on the VALU.
 // Continuous coordinates come from the table's f32 part, categorical codes straight from the data.
 template <int DCP, bool SIGNED>
-__device__ __forceinline__ void kde_rescue_one(const double* __restrict__ cand, int64_t i, int32_t D,
-                                               const KdeParams* __restrict__ P, KdeEst* __restrict__ out) {
+__device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                const KdeParams* __restrict__ P, const float* __restrict__ table,
+                                                KdeEst* __restrict__ out, const unsigned blk) {
   constexpr int NC = DCP > 0 ? DCP : 1;
+  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
+  const bool need = i < Nc && out[i].err == -1.f;
+  if (!__any(need)) return;
+  if (!need) return;
   const double* x = cand + i * (int64_t)D;
   const int n = P->n, dc = P->dc, du = P->du;
   const double* __restrict__ Xo = P->X;
@@ -723,17 +726,6 @@ __device__ __forceinline__ void kde_rescue_one(const double* __restrict__ cand, 
 }
 
 template <int DCP, bool SIGNED>
-__device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
-                                                const KdeParams* __restrict__ P, const float* __restrict__ table,
-                                                KdeEst* __restrict__ out, const unsigned blk) {
-  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
-  const bool need = i < Nc && out[i].err == -1.f;
-  if (!__any(need)) return;
-  if (!need) return;
-  kde_rescue_one<DCP, SIGNED>(cand, i, D, P, out);
-}
-
-template <int DCP, bool SIGNED>
 __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                          const KdeParams* __restrict__ P,
                                                          const float* __restrict__ table,
@@ -775,25 +767,6 @@ __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __re
   }
 }
 
-// The rescue pass of a fused single acquisition (the scoring blocks combined every candidate without a
-// marker): grid-stride over candidates, each thread rescuing its candidate's marked estimate(s) of either KDE
-// and then combining it (hbx_combine.h); exits at once when the scoring kernel counted no marker.  Its first
-// workgroup initialises what the fused tail does not touch (shortlist count, result record).
-template <int DCP, bool SIGNED>
-__global__ __launch_bounds__(256) void kde_rescue_combine_kernel(const double* __restrict__ cand, int64_t Nc,
-                                                                 int32_t D, KdePairArgs a) {
-  if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)
-    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
-  if (__hip_atomic_load(a.rescue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < Nc; i += (int64_t)gridDim.x * 256) {
-    const bool ng = a.out0[i].err == -1.f, nl = a.out1[i].err == -1.f;  // out0: g (bad KDE), out1: l
-    if (!ng && !nl) continue;
-    if (ng) kde_rescue_one<DCP, SIGNED>(cand, i, D, a.P0, a.out0);
-    if (nl) kde_rescue_one<DCP, SIGNED>(cand, i, D, a.P1, a.out1);
-    fz_candidate(combine_one(a.out1[i], a.out0[i]), i, a.fuse.lo, a.fuse.hi, a.fuse.words, a.fuse.seq);
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // score intervals, shortlist, exact re-score, final argmin
 
@@ -817,6 +790,20 @@ __global__ void acq_init_batch_kernel(int64_t B, uint32_t* __restrict__ U, int32
     best[b] = ~0ull;
     key[b] = ~0ull;
   }
+}
+
+// ln-pdf interval [lo, hi] and point estimate from (ln S+, ln S-, relative bound); -inf means pdf <= 0
+__device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* hi, float* pt) {
+  const float m = fmaxf(e.lpos, e.lneg);
+  if (m == -INFINITY) {
+    *lo = *hi = *pt = -INFINITY;
+    return;
+  }
+  const float a = __expf(e.lpos - m), b = __expf(e.lneg - m);
+  const float S = a - b, E = e.err * (a + b) + 1e-6f * (a + b);
+  *pt = S > 0.f ? m + __logf(S) : -INFINITY;
+  *hi = (S + E) > 0.f ? m + __logf(S + E) + 1e-6f * fabsf(m) + 1e-5f : -INFINITY;
+  *lo = (S - E) > 0.f ? m + __logf(S - E) - 1e-6f * fabsf(m) - 1e-5f : -INFINITY;
 }
 
 // Candidates [b*seg, (b+1)*seg) form acquisition b (seg = Nc: one acquisition).  U[b] = min over the
@@ -863,14 +850,44 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
     bool one = false;
     const uint32_t sg = (uint32_t)(i < Nc ? i : Nc - 1) / seg;
     if (i < Nc) {
-      const CandScore cs = combine_one(ea[r], eb[r]);
-      h = cs.h;
-      one = cs.one;
-      if (logl) logl[i] = cs.lpt;
-      if (logg) logg[i] = cs.gpt;
-      lo[i] = cs.slo;
-      hi[i] = cs.shi;
-      if (cs.of) atomicOr(flags + sg, 1);
+      const KdeEst a = ea[r], b = eb[r];
+      const float C = (float)HBX_LN_CLAMP;
+      float slo, shi;
+      bool of = false;
+      float llo, lhi, lpt, glo, ghi, gpt;
+      if (a.lpos != a.lpos) {  // l NaN -> max(l, 1e-8) is NaN -> score NaN (never selected)
+        slo = shi = NAN;
+        lpt = NAN;
+        est_interval(b, &glo, &ghi, &gpt);
+        if (b.lpos != b.lpos) gpt = NAN;
+      } else {
+        est_interval(a, &llo, &lhi, &lpt);
+        float Glo, Ghi;
+        if (b.lpos != b.lpos) {  // g NaN -> max(1e-8, g) == 1e-8
+          Glo = Ghi = C;
+          gpt = NAN;
+        } else {
+          est_interval(b, &glo, &ghi, &gpt);
+          Glo = fmaxf(glo, C);
+          Ghi = fmaxf(ghi, C);
+          of = ghi > 700.f;
+        }
+        of = of || lhi > 700.f;
+        slo = Glo - fmaxf(lhi, C);
+        shi = Ghi - fmaxf(llo, C);
+        h = shi;
+        const float C1 = C - 1e-4f;  // margin for the rounding of ln(1e-8) to float
+        if (lhi < C1 && (b.lpos != b.lpos || ghi < C1)) {  // both clamped: score exactly 1 (ln 0)
+          one = true;
+          slo = NAN;  // excluded from the shortlist unless it is the segment's first exact tie
+          shi = h = 0.f;
+        }
+      }
+      if (logl) logl[i] = lpt;
+      if (logg) logg[i] = gpt;
+      lo[i] = slo;
+      hi[i] = shi;
+      if (of) atomicOr(flags + sg, 1);
     }
     // min of hi and first exact tie per segment.  Same-address atomics serialise in L2 (~10 ns each),
     // so: block reduction when the block lies in one segment (the common case), one wave-level atomic
@@ -937,33 +954,14 @@ __global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restr
                                                             int32_t* __restrict__ list,
                                                             int32_t* __restrict__ count,
                                                             int32_t* __restrict__ segcnt,
-                                                            const int32_t* __restrict__ first1,
-                                                            const uint64_t* __restrict__ fzw = nullptr,
-                                                            uint32_t fz_seq = 0, int32_t* fz_flags = nullptr,
-                                                            int32_t* fz_rescue = nullptr) {
+                                                            const int32_t* __restrict__ first1) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  float u;
-  bool all;
-  int32_t f1;
-  if (fzw) {  // a fused single acquisition: its sequence-tagged words (hbx_combine.h)
-    u = hbx_ord2f(fz_read(fzw + FZ_U, fz_seq, hbx_f2ord(INFINITY)));
-    const int32_t fl = (int32_t)fz_read(fzw + FZ_FLAGS, fz_seq, 0u);
-    all = (fl & 1) != 0;
-    f1 = (int32_t)fz_read(fzw + FZ_FIRST1, fz_seq, (uint32_t)INT32_MAX);
-    if (i == 0) {
-      *fz_flags = fl;   // what the final kernel reports
-      *fz_rescue = 0;   // the rescue pass has run: the next acquisition's marker count starts at 0
-    }
-  }
   if (i >= Nc) return;
   const uint32_t sg = (uint32_t)i / seg;
-  if (!fzw) {
-    u = hbx_ord2f(U[sg]);
-    all = (flags[sg] & 1) != 0;
-    f1 = first1[sg];
-  }
+  const float u = hbx_ord2f(U[sg]);
+  const bool all = (flags[sg] & 1) != 0;
   const float l = lo[i];
-  if ((l == l && (all || l <= u)) || (int32_t)i == f1) {
+  if ((l == l && (all || l <= u)) || (int32_t)i == first1[sg]) {
     const int pos = atomicAdd(count, 1);
     list[pos] = (int32_t)i;
     if (segcnt) atomicAdd(segcnt + sg, 1);
@@ -1528,7 +1526,6 @@ struct ScoreFns {
   int threads;
   logpdf_pair_fn pair;  // the same kernel over both KDEs in one grid (hmode 16x16 only), or nullptr
   logpdf_pair_fn rescue_pair;
-  logpdf_pair_fn rescue_fused;  // 32x32 pair kernels: the rescue pass of the fused combine (else nullptr)
 };
 
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
@@ -1536,22 +1533,6 @@ struct ScoreFns {
 static bool pair_enabled() {
   const char* e = getenv("HBX_SCORE_PAIR");
   return !(e && atoi(e) == 0);
-}
-
-// HBX_FUSE_COMBINE=0: the separate combine kernel instead of the scoring blocks' fused tail (A/B)
-static bool fuse_enabled() {
-  const char* e = getenv("HBX_FUSE_COMBINE");
-  return !(e && atoi(e) == 0);
-}
-
-// sequence numbers of fused acquisitions (hbx_combine.h): unique per call in this process, never 0
-static uint32_t next_fuse_seq() {
-  static std::atomic<uint32_t> seq{0};
-  uint32_t v;
-  do {
-    v = seq.fetch_add(1, std::memory_order_relaxed) + 1;
-  } while (v == 0);
-  return v;
 }
 
 template <bool SG>
@@ -1564,18 +1545,6 @@ static logpdf_pair_fn pick_rescue_pair(int dc_pad) {
     case 24: return kde_rescue_pair_kernel<24, SG>;
     case 32: return kde_rescue_pair_kernel<32, SG>;
     case 64: return kde_rescue_pair_kernel<64, SG>;
-  }
-  return nullptr;
-}
-
-template <bool SG>
-static logpdf_pair_fn pick_rescue_fused(int dc_pad) {
-  switch (dc_pad) {
-    case 8: return kde_rescue_combine_kernel<8, SG>;
-    case 16: return kde_rescue_combine_kernel<16, SG>;
-    case 24: return kde_rescue_combine_kernel<24, SG>;
-    case 32: return kde_rescue_combine_kernel<32, SG>;
-    case 64: return kde_rescue_combine_kernel<64, SG>;
   }
   return nullptr;
 }
@@ -1614,8 +1583,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     const int hw = co ? H32C_WAVES : H16_WAVES;
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
-            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad),
-            sg ? pick_rescue_fused<true>(dc_pad) : pick_rescue_fused<false>(dc_pad)};
+            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1645,21 +1613,14 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
                          int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s,
-                         KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr,
-                         KdePairArgs::AcqFuse fuse = {}, bool* fused = nullptr) {
+                         KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr) {
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
-  // the combine fused into the scoring blocks: a single acquisition on the 32x32 pair kernels
-  const bool fz = pair && fuse.tile && rescue_cnt && f0.rescue_fused && f0.rescue_fused == f1.rescue_fused &&
-                  fuse_enabled();
-  if (fused) *fused = fz;
-  if (!fz) fuse = KdePairArgs::AcqFuse{};
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
-    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt, {},
-                  fuse};
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt, {}};
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
       hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
@@ -1670,10 +1631,7 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
     if (inited) *inited = init.U != nullptr;
     // the rescue pass: grid-stride, exits at once unless the scoring kernel counted a marker
     const unsigned grr = rescue_cnt ? (2 * gr < 1024u ? 2 * gr : 1024u) : 2 * gr;
-    if (fz)  // per candidate: its marked estimates, then its score interval
-      hipLaunchKernelGGL(f0.rescue_fused, dim3(gr < 1024u ? gr : 1024u), dim3(256), 0, s, cand, Nc, D, a);
-    else
-      hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
+    hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }
@@ -1690,8 +1648,8 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
 // of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
 // comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t res, U, count, flags, segcnt, segnear, best, key, first1, rescue, fz, tile, est_l, est_g, lo, hi, list, near,
-      exact_l, exact_g, part, total;
+  size_t res, U, count, flags, segcnt, segnear, best, key, first1, rescue, est_l, est_g, lo, hi, list, near, exact_l,
+      exact_g, part, total;
 };
 
 static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
@@ -1712,8 +1670,6 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.key = take(8 * B);
   w.first1 = take(4 * B);
   w.rescue = take(4);
-  w.fz = take(8 * 3);                              // fused single acquisition: tagged words (hbx_combine.h)
-  w.tile = take(8 * (size_t)((Nc + 255) / 256));  // ... and the per-tile arrival words
   w.est_l = take(sizeof(KdeEst) * Nc);
   w.est_g = take(sizeof(KdeEst) * Nc);
   w.lo = take(4 * Nc);
@@ -1977,17 +1933,12 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   // it while the host is still enqueueing the rest
   const bool scored = Nc > 0 && !exact_only;
   bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
-  bool fused = false;   // ... and, on the 32x32 kernels, the scoring blocks combine the candidates
-  KdePairArgs::AcqFuse fz{};
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
-    if (!batch_res) {
-      ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res};
-      if (fast) fz = KdePairArgs::AcqFuse{(uint64_t*)(ws + w.tile), (uint64_t*)(ws + w.fz), lo, hi, next_fuse_seq()};
-    }
+    if (!batch_res) ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res};
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
-                                 (int32_t*)(ws + w.rescue), s, ip, &inited, fz, &fused);
+                                 (int32_t*)(ws + w.rescue), s, ip, &inited);
     if (rc) return rc;
   }
   if (batch_res) {
@@ -2004,20 +1955,14 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     if (exact_only) {
       hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
       HBX_LAUNCH_CHECK();
-    } else if (!fused) {
+    } else {
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
                          dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
                          flags, first1, (int32_t*)(ws + w.rescue));
       HBX_LAUNCH_CHECK();
     }
-    if (fused)  // the fused tail's tagged words: decoded here, flags left for the final kernel
-      hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
-                         (int32_t*)nullptr, first1, (const uint64_t*)fz.words, fz.seq, flags,
-                         (int32_t*)(ws + w.rescue));
-    else
-      hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
-                         batch_res ? segcnt : (int32_t*)nullptr, first1, (const uint64_t*)nullptr, 0u,
-                         (int32_t*)nullptr, (int32_t*)nullptr);
+    hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
+                       batch_res ? segcnt : (int32_t*)nullptr, first1);
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
     hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,

@@ -264,16 +264,6 @@ struct KdePairArgs {
     int32_t* first1;
     struct AcqResult* res;
   } init;
-  // single acquisition, 32x32 kernels (nullable tile): the combine fused into the scoring blocks' tail
-  // (hbx_combine.h fz_tile_tail): per-tile arrival words, the acquisition's sequence-tagged words, the
-  // score intervals
-  struct AcqFuse {
-    uint64_t* tile;
-    uint64_t* words;
-    float* lo;
-    float* hi;
-    uint32_t seq;
-  } fuse;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
 

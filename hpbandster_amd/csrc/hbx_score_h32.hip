@@ -32,7 +32,6 @@
 //   MFMAs of T1(c), fragments re-read for T0(c+1) | exp2/sum of T0(c) beside them.
 #include "hbx_common.h"
 #include "hbx_kde_impl.h"
-#include "hbx_combine.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -72,10 +71,7 @@ template <int NSC, int KP, bool SG, bool FAST, bool CO = false, int CT = 1>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
-                                                    const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr,
-                                                    const KdePairArgs::AcqFuse fz = {},
-                                                    const KdeEst* __restrict__ est_l = nullptr,
-                                                    const KdeEst* __restrict__ est_g = nullptr) {
+                                                    const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr) {
   // CO: the coarse pre-screen (hbx_kde_impl.h coarse layout): one product per continuous dim, no lo parts
   constexpr int ND = CO ? h32c_nd(NSC) : h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + per dim)
   constexpr int KS = KP;                     // sparse 32-wide K-steps (one-hot positions), hi parts
@@ -499,8 +495,6 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     }
   }
   }
-  // a single acquisition: the second of the tile's two blocks combines the tile (hbx_combine.h)
-  if (fz.tile) fz_tile_tail(fz, blk, cbase - (int64_t)wave * 32 * CT, HW * 32 * CT, Nc, est_l, est_g, lds);
 }
 
 // unsigned sums: 128 VGPRs, 4 waves per SIMD (two blocks per CU); the coarse instance: H32C_WAVES-wave
@@ -519,7 +513,7 @@ __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
                                                 second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
-                                                a.rescue, a.fuse, a.out1, a.out0);
+                                                a.rescue);
 }
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
@@ -537,7 +531,7 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
   const bool second = blockIdx.x >= a.nblk0;
   kde_logpdf_h32_body<NSC, KP, true, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
                                            second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
-                                           a.rescue, a.fuse, a.out1, a.out0);
+                                           a.rescue);
 }
 
 // instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part; CO (coarse) for unsigned sums

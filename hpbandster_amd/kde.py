@@ -322,6 +322,13 @@ class KDEPair(object):
                           N.ptr(bad.rows_dev), bad.variant, good.dc_pad, good.du_pad, self.nmax)
         self._wsb = {}
         self._roff = None
+        # the synchronous fast path's constants (acquire: a call on the model's own device)
+        torch = _torch()
+        self._dev_index = torch.device(good.device).index
+        self._cur_dev = getattr(torch._C, "_cuda_getDevice", None)
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        self._host_fn = N.lib().hbx_kde_acquire_host
+        self._ws_cache = {}  # (thread, Nc) -> workspace of synchronous calls made without one
 
     def __getitem__(self, key):  # cg.kde_models[b]['good'] like the reference dict
         if key == "good":
@@ -359,8 +366,48 @@ class KDEPair(object):
         """
         if ties not in ("pinned", "process"):
             raise ValueError("ties must be 'pinned' or 'process'")
+        if (sync and not logs and stream is None and self._cur_dev is not None and self._raw_stream is not None
+                and self._cur_dev() == self._dev_index):
+            r = self._acquire_sync(cands, index_base, workspace, events)
+            if r is not None:
+                if ties == "process" and r.flags & ACQ_NEAR_TIE:
+                    with N.on_device(self.good.device):
+                        ws = workspace if workspace is not None else self._ws_cache[(threading.get_ident(), len(cands))]
+                        self._resolve(r, ws, len(cands), len(cands), cands, int(index_base))
+                return r
         with N.on_device(self.good.device, stream):
             return self._acquire(cands, index_base, logs, stream, workspace, sync, events, ties)
+
+    def _acquire_sync(self, cands, index_base, workspace, events):
+        """The drop-in's common call -- synchronous, the winner only, on the model's device and its current
+        stream, which is this thread's current device (no device switch): one native call
+        (hbx_kde_acquire_host) with the fewest host steps around it; a workspace is kept per thread and
+        candidate count when none is given.  None when the candidates need staging (host arrays, other
+        dtypes): the general path then runs."""
+        torch = _torch()
+        if type(cands) is not torch.Tensor or cands.dtype is not torch.float64 or not cands.is_cuda:
+            return None
+        D = self.good.k_vars
+        if cands.dim() != 2 or cands.shape[1] != D or not cands.is_contiguous() or \
+                cands.device.index != self._dev_index:
+            return None
+        Nc = cands.shape[0]
+        wsb = self._wsb.get(Nc)
+        if wsb is None:
+            wsb = self.workspace_bytes(Nc)
+        if workspace is None:
+            key = (threading.get_ident(), Nc)
+            workspace = self._ws_cache.get(key)
+            if workspace is None:
+                workspace = self._ws_cache[key] = torch.empty(wsb, dtype=torch.uint8, device=cands.device)
+        n = workspace.numel()
+        if n < wsb:
+            raise N.HbxError("workspace too small")
+        rec = _record_buffer()
+        N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
+                              events.address if events is not None else None, self._raw_stream(self._dev_index),
+                              rec))
+        return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):
         torch = _torch()

@@ -258,7 +258,7 @@ def test_sh_stage_with_results_between_requests_stays_sequential(device, monkeyp
 def test_speculation_off_for_the_host_sampler_by_default(device, monkeypatch):
     """speculative='auto' batches only with the GPU sampler: the host sampler's scipy draws dominate a call."""
     _, _, cnt, _ = _stage(device, 11, True, False, monkeypatch, speculative="auto")
-    assert cnt.n == {"acquire": 27, "acquire_batch": 0}
+    assert cnt.n["acquire_batch"] == 0 and cnt.n["acquire"] >= 10  # one per model-based call
 
 
 def test_draw_while_a_batch_is_built_is_never_replayed(device, monkeypatch):

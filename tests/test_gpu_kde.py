@@ -681,13 +681,10 @@ def test_coarse_two_column_tiles_ragged(device, nc, monkeypatch):
 @pytest.mark.parametrize("dc,du,nobs,nc,far", [(24, 8, 3000, 512, True), (24, 8, 10000, 4099, False),
                                                (16, 0, 700, 1, False), (16, 4, 1500, 513, True),
                                                (8, 12, 2000, 1025, False), (32, 4, 900, 2048, True)])
-def test_fused_combine_identical_to_combine_kernel(device, dc, du, nobs, nc, far, monkeypatch):
-    """A single acquisition on the 32x32 pair kernels combines each candidate tile in the tail of the
-    tile's second scoring block (hbx_combine.h: sequence-tagged minimum / first-clamped / flag words, no
-    combine launch); candidates with a rescue marker are combined by the rescue pass.  Records equal the
-    separate combine kernel's (HBX_FUSE_COMBINE=0) field by field, at every tile fill, with rescue markers
-    (far candidates), signed KDEs and a reused workspace (stale words of earlier acquisitions), and the
-    winner is the oracle's."""
+def test_acquire_reused_workspace_and_ragged_tiles(device, dc, du, nobs, nc, far):
+    """One workspace reused across acquisitions (over other candidates in between) gives the records of
+    fresh workspaces field by field, at every tile fill, with rescue markers (far candidates); the winner
+    is the oracle's."""
     import torch
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
@@ -699,21 +696,16 @@ def test_fused_combine_identical_to_combine_kernel(device, dc, du, nobs, nc, far
         C[min(5, nc - 1), 0] = 1000.0
         C[nc // 2, dc - 1] = -400.0
     pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
-    ws = torch.empty(pair.workspace_bytes(nc), dtype=torch.uint8, device=device)
 
     def rec(r):
         return (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist, r.flags, r.near, r.rel)
-    monkeypatch.setenv("HBX_FUSE_COMBINE", "0")
-    ref = rec(pair.acquire(C, workspace=ws))
-    monkeypatch.setenv("HBX_FUSE_COMBINE", "1")
-    for rep in range(3):  # the same workspace again: the tagged words of the earlier calls lose
-        got = rec(pair.acquire(C, workspace=ws))
-        assert got == ref, (rep, got, ref)
-    C2 = C[::-1].copy()  # other candidates in the reused workspace
-    monkeypatch.setenv("HBX_FUSE_COMBINE", "0")
-    ref2 = rec(pair.acquire(C2, workspace=ws))
-    monkeypatch.setenv("HBX_FUSE_COMBINE", "1")
-    assert rec(pair.acquire(C2, workspace=ws)) == ref2
+    ref = rec(pair.acquire(C))
+    C2 = C[::-1].copy()
+    ref2 = rec(pair.acquire(C2))
+    ws = torch.full((pair.workspace_bytes(nc),), 0xA5, dtype=torch.uint8, device=device)
+    for rep in range(2):
+        assert rec(pair.acquire(C, workspace=ws)) == ref, rep
+        assert rec(pair.acquire(C2, workspace=ws)) == ref2, rep
     if nc * nobs > 4e6:
         return
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
