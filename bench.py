@@ -22,6 +22,7 @@ basis, 157.3 TFLOP/s, beside it).  cpu_baseline: the C oracle
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -34,6 +35,7 @@ sys.path.insert(0, ROOT)
 METRIC = "candidate KDE evals/sec (cand×obs pairs) at D=32, 1/2/4/8 MI355X; % VALU peak"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 PEAK_F16_MFMA_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense BF16/FP16 MFMA (~2.5 PF; no sparsity credit)
+PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector peak (AMD spec; not in MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4            # spec engine clock (the chip holds ~2.0-2.1 GHz under this load)
 N_SIMD = 1024              # 256 CUs x 4 SIMDs
 
@@ -153,22 +155,25 @@ def host_info():
                     break
     except OSError:
         pass
-    quota = None
+    quota, qcpus = None, None
     try:  # the job's cgroup CPU quota ("max" or "<quota_us> <period_us>")
         with open("/sys/fs/cgroup/cpu.max") as fh:
             q = fh.read().split()
-        quota = q[0] if q[0] == "max" else "%.1f cpus" % (int(q[0]) / int(q[1]))
-    except (OSError, ValueError, IndexError):
+        if q[0] != "max":
+            qcpus = int(q[0]) / int(q[1])
+        quota = q[0] if q[0] == "max" else "%.1f cpus" % qcpus
+    except (OSError, ValueError, IndexError, ZeroDivisionError):
         pass
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_max": quota}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_max": quota, "cgroup_cpus": qcpus}
 
 
 def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     """CPU baselines on the host cores, bounded samples of the same workload:
     * value: the C oracle (oracle/kde_oracle.c, fp64, the reference's arithmetic, OpenMP over
-      candidates) with one thread per host core this process may run on (the affinity mask; the box's
-      OMP_NUM_THREADS and cgroup quota are recorded beside it);
+      candidates) with one thread per host core this process may run on: the affinity mask, capped by the
+      job's cgroup CPU quota when there is one (the GPU box's lease grants 16 of its 256 cores: 256 threads
+      under a 16-CPU quota measured 6.0e7 pairs/s against 1.5e8 with 16, profiles/r04/bench.json notes);
     * reference_as_called: the reference's own path, KDEMultivariate.pdf for l and g per candidate
       (bohb.py:149), single core -- statsmodels is not installed on the box, so its numpy restatement
       oracle.kde_oracle.pdf stands in (bit-identical to statsmodels on every golden fixture), level
@@ -177,6 +182,8 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     from oracle import kde_oracle as O
     hi = host_info()
     threads = hi["affinity"] or 1
+    if hi["cgroup_cpus"]:
+        threads = max(1, min(threads, int(math.ceil(hi["cgroup_cpus"]))))
     Xg, Xb = X[good_rows], X[bad_rows]
     args_g = (Xg, pair.good.bw, var_type, pair.good.nlev)
     args_b = (Xb, pair.bad.bw, var_type, pair.bad.nlev)
@@ -192,8 +199,8 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     nobs = Xg.shape[0] + Xb.shape[0]
     out = {"value": n * nobs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
            "sample": "%d of the %d candidates x %d observations (D=%d), fp64 C oracle (reference arithmetic), "
-                     "%d OpenMP threads = the affinity mask (cgroup quota %s), %.1f s"
-                     % (n, cands.shape[0], nobs, X.shape[1], threads, hi["cgroup_cpu_max"], dt)}
+                     "%d OpenMP threads = the affinity mask (%d cores) capped by the job's cgroup quota (%s), %.1f s"
+                     % (n, cands.shape[0], nobs, X.shape[1], threads, hi["affinity"], hi["cgroup_cpu_max"], dt)}
     out.update(hi)
     m, t_ref = 0, 0.0
     t0 = time.perf_counter()
@@ -641,10 +648,12 @@ def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
     rate = pairs / (t * 1e-3)
     W = 92  # SURVEY 8d algorithmic flops per pair at 24c + 8u
     return {"workload": "kde_logpdf_rtol%g_d32_obs%d_cand%d" % (rtol, pair.good.nobs + pair.bad.nobs, Nc),
-            "value": rate, "unit": "pairs/s", "ms_l_plus_g": t, "rtol": rtol, "kernel": name, "per_kde": res,
-            "roofline": {"bound": "mfma", "achieved": W * rate / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": W * rate / 1e12 / PEAK_F16_MFMA_TFLOPS,
-                         "basis": "whole hbx_kde_logpdf_rtol call (scoring launch + classify + fp64 re-evaluation)"}}
+            "value": rate, "unit": "pairs/s", "ms_l_plus_g": t, "rtol": rtol, "fp64_kernel": "kde_logpdf_tiled_kernel" if os.environ.get("HBX_LOGPDF_TILED", "1") != "0" else "kde_logpdf_exact_kernel", "kernel": name, "per_kde": res,
+            "roofline": {"bound": "valu_f64", "achieved": W * rate / 1e12, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": W * rate / 1e12 / PEAK_FP64_TFLOPS,
+                         "basis": "W = 92 algorithmic flops per pair over the whole hbx_kde_logpdf_rtol call (f16 estimate "
+                                  "launch + classify + the fp64 log-space re-evaluation, which dominates when every "
+                                  "candidate is re-evaluated) vs the fp64 vector peak (AMD spec)"}}
 
 
 def config2_line(device, reps=50):
@@ -1042,7 +1051,7 @@ def main():
         except Exception as e:
             out["sh_stage"] = {"error": repr(e)}
         try:
-            out["sh_stage_interleaved"] = sh_stage_line(device, interleaved=True, reps=3)
+            out["sh_stage_interleaved"] = sh_stage_line(device, interleaved=True, reps=7)
         except Exception as e:
             out["sh_stage_interleaved"] = {"error": repr(e)}
         try:

@@ -52,7 +52,7 @@ class SuccessiveHalving(object):
             self._next = min(2 * len(self._spec), self.MAX_BATCH) if cont else 1
             self._spec = None
         elif self._fp is not None:
-            self._next = 2 if gen.spec_fingerprint() == self._fp else 1
+            self._next = 2 if gen.spec_unchanged(self._fp) else 1
         self._fp = None
         remaining = self.num_configs[self.SH_iter] - self.actual_num_configs[self.SH_iter]
         size = min(remaining, self._next)

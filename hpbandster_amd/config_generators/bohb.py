@@ -244,6 +244,13 @@ class BOHB(base_config_generator):
         mt = _global_mt()
         return (self._model_version, self._sample_counter, mt.snap() if mt is not None else None)
 
+    def spec_unchanged(self, fp):
+        """spec_fingerprint() == fp, the cheap fields first (a refit in between is the common change)."""
+        if fp[0] != self._model_version or fp[1] != self._sample_counter:
+            return False
+        mt = _global_mt()
+        return mt is not None and mt.snap() == fp[2]
+
     def get_config_batch_spec(self, budget, k):
         """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass) from a private copy of
         the global RNG, handed out one at a time by the returned SpeculativeBatch -- each only while it is

@@ -2082,6 +2082,131 @@ int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* p
 
 // ln pdf within rtol * max(1, |ln p|) of the reference's (the north-star contract), per candidate: the
 // fp32 estimate where its rigorous bound guarantees it, else queued for an fp64 evaluation
+// ln pdf in fp64 log space, tiled: the same value as kde_logpdf_exact_kernel (per pair the direct
+// differences -((x - X) / (h sqrt 2))^2 per continuous dim, ln(1 - h) or ln(h / (c - 1)) per categorical
+// dim, SM:kernels.py:23-65 in log form), but one candidate per thread and the observations staged in LDS
+// 64 at a time for the whole block -- each observation row is read once per 256 candidates, where the
+// per-point kernel re-read every row for every candidate (2.6 TB of L2 traffic for 1e6 x 1e4 at D = 32).
+// Per thread the pair terms go into a running logsumexp: the running maximum m and S = sum 2^(t' - m')
+// (t' = t log2 e), each term 2^(t' - m') evaluated by v_exp_f32 on the fp32-rounded exponent.  Error of a
+// term <= ln2 |t' - m'| 2^-24 + 2^-22 relative: below 3e-6 for the terms with |t' - m'| <= 60 and a
+// contribution < 1e4 x 2^-60 for the rest, so |ln S_est - ln S| < 4e-6 -- inside rtol for rtol >= 1e-5
+// (EXP64: fp64 exp2 for tighter rtol).  The sums, the maximum and the pair terms are fp64.
+// DC / DU: continuous / categorical slots (the KDE's dims padded with zero terms); candidates list[0, *count)
+// (or all Np), outputs at their own index.  Only for KDEs without negative categorical factors, structural
+// NaN or single-level categorical dims (kde_pdf_exact_kernel takes those).
+template <int DC, int DU, bool EXP64>
+__global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __restrict__ pts, int64_t Np,
+                                                              int32_t D, const KdeParams* __restrict__ P,
+                                                              const double* __restrict__ X,
+                                                              const int64_t* __restrict__ rows,
+                                                              double* __restrict__ out,
+                                                              const int32_t* __restrict__ list,
+                                                              const int32_t* __restrict__ count) {
+  constexpr int OB = 64;  // observations per staged chunk
+  constexpr int DUS = DU > 0 ? DU : 1;
+  __shared__ double xs_c[2][OB][DC];
+  __shared__ double xs_u[2][OB][DUS];
+  __shared__ double sa[DC], sdl[DUS];
+  __shared__ int32_t scol[DC + DUS];
+  __shared__ double lconst;
+  const int n = P->n, dc = P->dc, du = P->du;
+  const int64_t np = list ? (int64_t)*count : Np;
+  const int64_t i0 = (int64_t)blockIdx.x * 256;
+  if (i0 >= np) return;  // uniform
+  const int tid = threadIdx.x;
+  if (P->has_neg || P->nan_all || P->nconst) {  // kde_pdf_exact_kernel writes these (ln of the exact pdf)
+    if (i0 + tid < np) out[list ? (int64_t)list[i0 + tid] : i0 + tid] = NAN;
+    return;
+  }
+  // per-dim constants: a_c = 1 / (h sqrt 2) (finite: a zero bandwidth is nan_all); categorical: the term is
+  // ln(h / (c - 1)) + [match] (ln(1 - h) - ln(h / (c - 1))), the first part summed into the constant
+  if (tid < DC) {
+    const bool act = tid < dc;
+    const int d = act ? P->cont_dim[tid] : 0;
+    sa[tid] = act ? 1.0 / (P->bw[d] * 1.4142135623730951) : 0.0;
+    scol[tid] = d;
+  }
+  if (tid < DU) {
+    const bool act = tid < du;
+    const int d = act ? P->cat_dim[tid] : 0;
+    const double h = act ? P->bw[d] : 0.0;
+    sdl[tid] = act ? log(1. - h) - log(h / (double)(P->nlev[d] - 1)) : 0.0;
+    scol[DC + tid] = d;
+  }
+  if (tid == 0) {
+    double lc = -log((double)n);
+    for (int k = 0; k < dc; ++k) lc -= log(P->bw[P->cont_dim[k]]) + 0.91893853320467274178;  // ln(h sqrt(2 pi))
+    for (int k = 0; k < du; ++k) {
+      const int d = P->cat_dim[k];
+      lc += log(P->bw[d] / (double)(P->nlev[d] - 1));
+    }
+    lconst = lc;
+  }
+  __syncthreads();
+  const int64_t pi = i0 + tid;
+  const bool valid = pi < np;
+  const int64_t p = valid ? (list ? (int64_t)list[pi] : pi) : 0;
+  const double* x = pts + p * (int64_t)D;
+  double xc[DC], xu[DUS];  // the candidate: scaled continuous coordinates, categorical codes
+#pragma unroll
+  for (int k = 0; k < DC; ++k) xc[k] = (k < dc && valid) ? x[scol[k]] * sa[k] : 0.0;
+#pragma unroll
+  for (int k = 0; k < DUS; ++k) xu[k] = (k < du && valid) ? x[scol[DC + k]] : 0.0;
+  // stage chunk c into buffer b: scaled coordinates and codes of 64 observations (padding dims 0; an
+  // observation past n gets an infinite first coordinate: its term is exp(-inf) = 0)
+  auto stage = [&](int c, int b) {
+    const int j0 = c * OB;
+    for (int e = tid; e < OB * (DC + DU); e += 256) {
+      const int jj = e / (DC + DU), k = e - jj * (DC + DU);
+      const int j = j0 + jj;
+      double v = 0.0;
+      if (j < n) {
+        if (k < DC) {
+          if (k < dc) v = X[rows[j] * (int64_t)D + scol[k]] * sa[k];
+        } else if (k - DC < du) {
+          v = X[rows[j] * (int64_t)D + scol[k]];
+        }
+      } else if (k == 0) {
+        v = __builtin_inf();
+      }
+      if (k < DC) xs_c[b][jj][k] = v;
+      else xs_u[b][jj][k - DC] = v;
+    }
+  };
+  const int nch = (n + OB - 1) / OB;
+  double m = -INFINITY, S = 0.0;
+  bool nan = false;
+  stage(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // chunk c staged; every thread done with chunk c - 1's buffer
+    if (c + 1 < nch) stage(c + 1, (c + 1) & 1);
+    const int b = c & 1;
+    const int jn = min(OB, n - c * OB);
+    for (int jj = 0; jj < jn; ++jj) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < DC; ++k) {
+        const double d = xc[k] - xs_c[b][jj][k];
+        t = fma(-d, d, t);
+      }
+#pragma unroll
+      for (int k = 0; k < DU; ++k) t += (xu[k] == xs_u[b][jj][k]) ? sdl[k] : 0.0;
+      const double tl = t * 1.4426950408889634;  // log2 units
+      if (tl > m) {
+        S = (m > -INFINITY ? S * (EXP64 ? exp2(m - tl) : (double)__builtin_amdgcn_exp2f((float)(m - tl))) : 0.0) + 1.0;
+        m = tl;
+      } else if (tl > -INFINITY) {
+        S += EXP64 ? exp2(tl - m) : (double)__builtin_amdgcn_exp2f((float)(tl - m));
+      } else if (tl != tl) {
+        nan = true;
+      }
+    }
+  }
+  if (valid)
+    out[p] = nan ? NAN : (m > -INFINITY ? (m + log2(S)) * 0.69314718055994531 + lconst : -INFINITY);
+}
+
 __global__ __launch_bounds__(256) void kde_logpdf_classify_kernel(const KdeEst* __restrict__ est, int64_t Nc,
                                                                  double rtol, int exact_all, double* __restrict__ out,
                                                                  int32_t* __restrict__ list,
@@ -2101,6 +2226,49 @@ __global__ __launch_bounds__(256) void kde_logpdf_classify_kernel(const KdeEst* 
     if (ok) out[i] = pt;
   }
   if (!ok) list[atomicAdd(count, 1)] = (int32_t)i;
+}
+
+extern "C" {
+
+}  // extern "C"
+
+typedef void (*logpdf_tiled_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*,
+                                double*, const int32_t*, const int32_t*);
+
+// HBX_LOGPDF_TILED=0: the per-point fp64 kernel for every re-evaluated candidate (A/B)
+static bool tiled_enabled() {
+  const char* e = getenv("HBX_LOGPDF_TILED");
+  return !(e && atoi(e) == 0);
+}
+
+template <int DC, bool E64>
+static logpdf_tiled_fn pick_tiled_du(int du_pad) {
+  switch (du_pad) {
+    case 0: return kde_logpdf_tiled_kernel<DC, 0, E64>;
+    case 4:
+    case 8: return kde_logpdf_tiled_kernel<DC, 8, E64>;
+    case 16: return kde_logpdf_tiled_kernel<DC, 16, E64>;
+    case 32: return kde_logpdf_tiled_kernel<DC, 32, E64>;
+  }
+  return nullptr;
+}
+
+template <bool E64>
+static logpdf_tiled_fn pick_tiled_e(int dc_pad, int du_pad) {
+  switch (dc_pad) {
+    case 0:
+    case 4:
+    case 8: return pick_tiled_du<8, E64>(du_pad);
+    case 16: return pick_tiled_du<16, E64>(du_pad);
+    case 24: return pick_tiled_du<24, E64>(du_pad);
+    case 32: return pick_tiled_du<32, E64>(du_pad);
+  }
+  return nullptr;  // 64 continuous slots: the per-point kernel
+}
+
+// the tiled fp64 log-space kernel of a bucket (dc_pad, du_pad), fp64 exponentials for rtol < 1e-5
+static logpdf_tiled_fn pick_logpdf_tiled(int dc_pad, int du_pad, bool exp64) {
+  return exp64 ? pick_tiled_e<true>(dc_pad, du_pad) : pick_tiled_e<false>(dc_pad, du_pad);
 }
 
 extern "C" {
@@ -2134,9 +2302,15 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
                      exact_only ? 1 : 0, out, list, count);
   HBX_LAUNCH_CHECK();
   const unsigned grid = (unsigned)(Nc < EXACT_GRID ? Nc : EXACT_GRID);
-  // the rest in fp64: log space (positive factors) ...
-  hipLaunchKernelGGL(kde_logpdf_exact_kernel, dim3(grid), dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params, X,
-                     rows, out, list, count);
+  // the rest in fp64 log space (positive factors): tiled over candidates where the bucket has an instance,
+  // else one block per point (its kernel exits for KDEs the tiled one would mis-handle: see below)
+  const logpdf_tiled_fn tf = exact_only || !tiled_enabled() ? nullptr : pick_logpdf_tiled(dc_pad, du_pad, rtol < 1e-5);
+  if (tf)
+    hipLaunchKernelGGL(tf, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params,
+                       X, rows, out, list, count);
+  else
+    hipLaunchKernelGGL(kde_logpdf_exact_kernel, dim3(grid), dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params, X,
+                       rows, out, list, count);
   HBX_LAUNCH_CHECK();
   // ... or ln of the exact pdf (negative categorical factors, structural NaN: every block exits otherwise)
   hipLaunchKernelGGL(kde_pdf_exact_kernel, dim3(grid), dim3(EXACT_THREADS), 0, s, cand, Nc, D,

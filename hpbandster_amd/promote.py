@@ -157,13 +157,16 @@ def _current_stream_fn():
 _MODES = {"numpy": N.ORDER_NUMPY, "stable": N.ORDER_STABLE, N.ORDER_NUMPY: N.ORDER_NUMPY,
           N.ORDER_STABLE: N.ORDER_STABLE}
 
-# one-bracket size policy (bench ``promote_dropin``, profiles/r04/promote_policy): up to HOST_MAX
+# one-bracket size policy (bench ``promote_dropin``, profiles/r04/promote_latency.txt): up to HOST_MAX
 # configurations a bracket whose k-th and (k+1)-th smallest losses differ is ranked on the host -- every
 # sort gives the same first k then, so the mask is the reference's bit for bit -- because one kernel round
 # trip (launch, PCIe reads of the losses, the completion word: >= 8.3 us) costs more than numpy's sort of
-# a few hundred values.  Brackets with a tie straddling the k-th place (numpy 1.26.4's unstable order
-# decides them: restated on the device only), non-finite losses, and larger brackets go to the GPU.
-HOST_MAX = 4096
+# a few hundred values (n = 81: 1.9 us against 12.0 us for the GPU round trip and 2.5 us for the reference's
+# argsort(argsort); n = 1000: 3.8 / 12.6 / 12.2 us; n = 4096: 7.2 us against 291 us through the sorting
+# kernels brackets > 1024 take).  Brackets with a tie straddling the k-th place (numpy 1.26.4's unstable
+# order decides them: restated on the device only -- this process's numpy orders 65 of 206 recorded arrays
+# differently), non-finite losses, and larger brackets go to the GPU.
+HOST_MAX = 1 << 16
 _SORT_MAX = 256  # below: one argsort; above: np.partition (O(n))
 
 

@@ -577,8 +577,9 @@ def _capi_logpdf_rtol(k, C, rtol=1e-5):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("case", ["outlier", "d46", "signed", "d32m"])
-def test_capi_logpdf_rtol_contract(device, case):
+@pytest.mark.parametrize("tiled", ["1", "0"])
+@pytest.mark.parametrize("case", ["outlier", "d46", "signed", "d32m", "far24c8u", "cat_only"])
+def test_capi_logpdf_rtol_contract(device, case, tiled, monkeypatch):
     """The north-star ln-pdf contract at the C-ABI (not through DeviceKDE): within 1e-5 * max(1, |ln p|)
     of the reference's ln pdf for every candidate where that is finite, NaN where it is NaN -- next to an
     outlying observation (the fp32 estimates there are off by up to 5e-2), at D = 46 (3e-5), on a KDE with
@@ -603,9 +604,22 @@ def test_capi_logpdf_rtol_contract(device, case):
     elif case == "signed":
         c = G.load_kde_case("hgt1")
         X, Lo, vt, C = c["X"], c["eff_losses"], c["var_type"], c["cands"]
+    elif case == "far24c8u":  # config #3's dims, uniform candidates: every one re-evaluated in fp64
+        X = S.make_observations(1500, 24, 8, 4, seed=24)
+        Lo = S.make_losses(1500, seed=25)
+        vt = S.var_type_string(24, 8)
+        C = S.make_candidates(700, 24, 8, 4, seed=26)  # 2 full + 1 ragged block of the tiled kernel
+        C[3, 5] = 40.0  # far outside the data
+        C[9, 30] = 7.5  # a code no observation has
+    elif case == "cat_only":
+        X = S.make_observations(300, 0, 6, 5, seed=27)
+        Lo = S.make_losses(300, seed=28)
+        vt = S.var_type_string(0, 6)
+        C = S.make_candidates(300, 0, 6, 5, seed=29)
     else:
         c = G.load_kde_case("d32m")
         X, Lo, vt, C = c["X"], c["eff_losses"], c["var_type"], c["cands"][:96]
+    monkeypatch.setenv("HBX_LOGPDF_TILED", tiled)  # the tiled fp64 kernel, or the per-point one
     pair = kde.fit_pair(X, Lo, vt, len(vt) + 1, device=device)
     for k in (pair.good, pair.bad):
         lref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
