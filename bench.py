@@ -805,7 +805,7 @@ def kde_result_bytes():
     return kde.RESULT_BYTES
 
 
-PROFILE_SET = "profiles/r03"
+PROFILE_SET = "profiles/r04"
 
 
 def load_traffic(workload):

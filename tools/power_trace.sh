@@ -6,6 +6,7 @@ set -o pipefail
 O=${1:-gpurun_out/power}
 SEC=${2:-8}
 mkdir -p $O
+timeout 10 amd-smi static -l -g 0 > $O/limits.txt 2>&1 || true   # the power cap
 timeout -k 10 120 python -u tools/power_probe.py $SEC > $O/probe.log 2>&1 &
 P=$!
 sleep 4   # the probe's fit and first launches

@@ -35,4 +35,8 @@ cp $(ls $OUT/trace/*kernel_stats.csv | head -1) $OUT/kernel_stats.csv
 rm -rf $OUT/pmc[0-9]/ $OUT/trace/*kernel_trace.csv
 head -8 $OUT/kernel_steady.txt
 cat $OUT/trace_vs_line.txt
+
+# package power / clock while the scoring launch runs back to back (is it held at the power limit?)
+bash tools/power_trace.sh $OUT/power 8 > $OUT/power.log 2>&1 || { echo "power trace failed"; tail -5 $OUT/power.log; }
+grep -i -E "power|sclk|gfx_clk|clock|temp" $OUT/power/samples.txt | head -40
 echo profile done
