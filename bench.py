@@ -594,10 +594,11 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
         return time.perf_counter() - t0, cfgs
 
     res = {}
-    for batch in (False, True) * reps:  # alternated, best of reps each
-        t, c = run(batch)
-        if batch not in res or t < res[batch][0]:
-            res[batch] = (t, c)
+    for r in range(reps):  # alternated, either one first in turn, best of reps each
+        for batch in ((False, True) if r % 2 == 0 else (True, False)):
+            t, c = run(batch)
+            if batch not in res or t < res[batch][0]:
+                res[batch] = (t, c)
     return {"workload": "sh_stage_%d_get_next_run_d32_obs%d%s" % (stage, n_obs, "_interleaved" if interleaved else ""),
             "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
             "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],

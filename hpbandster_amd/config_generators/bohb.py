@@ -46,6 +46,10 @@ class _MT(object):
     def load(self, raw):
         ctypes.memmove(self.addr, raw, self.NB)
 
+    def tag(self):
+        """(position, first key word): changes with every draw, for a cheap hint (not a check)."""
+        return (ctypes.c_int32.from_address(self.addr + 624 * 4).value, ctypes.c_uint32.from_address(self.addr).value)
+
 
 _GLOBAL = [None]
 
@@ -239,17 +243,18 @@ class BOHB(base_config_generator):
         return self.speculative == "always" or (self.speculative == "auto" and self.sampler == "gpu")
 
     def spec_fingerprint(self):
-        """(model version, GPU sampler counter, raw global RNG state): equal before and after an interval
-        iff a get_config at its end returns what one at its start would have."""
+        """(model version, GPU sampler counter, global RNG position tag): the same before and after an
+        interval in which nothing a get_config depends on changed.  A hint for SuccessiveHalving's batch
+        sizes only -- every speculative result is checked against the full RNG state when served."""
         mt = _global_mt()
-        return (self._model_version, self._sample_counter, mt.snap() if mt is not None else None)
+        return (self._model_version, self._sample_counter, mt.tag() if mt is not None else None)
 
     def spec_unchanged(self, fp):
         """spec_fingerprint() == fp, the cheap fields first (a refit in between is the common change)."""
         if fp[0] != self._model_version or fp[1] != self._sample_counter:
             return False
         mt = _global_mt()
-        return mt is not None and mt.snap() == fp[2]
+        return mt is not None and mt.tag() == fp[2]
 
     def get_config_batch_spec(self, budget, k):
         """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass) from a private copy of

@@ -507,7 +507,52 @@ __device__ inline void nps_sort_segment(const double* __restrict__ x, int n, boo
   }
 }
 
-// One segment re-ranked in numpy's order by the whole workgroup (the flagged segments of a stable order).
+// Which positions numpy's argsort puts first: the first kk of A[0..n) after the same quicksort, without
+// finishing it -- after a partition only the child range holding the boundary between places kk - 1 and
+// kk decides anything more (the other child's keys lie wholly before or after it, in whatever order), so
+// the walk follows that one range, a quickselect along numpy's own partition sequence, and ends in its
+// network, its std::sort (depth budget spent) or a partition point at the boundary.  One wave; NaN-free
+// keys (the promotion's finite losses).  The whole workgroup calls it (a barrier at the end).
+__device__ inline void nps_select_segment(const double* __restrict__ x, int n, int kk, int32_t* A, int32_t* T,
+                                          int32_t* W) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave == 0 && n > 1 && kk > 0 && kk < n) {
+    if (n <= 64) {
+      nps_leaf(x, A, 0, n, lane);
+    } else {
+      int L = 0, R = n, it = 2 * (31 - __clz(n));  // 2 * (int64_t)log2(arrsize), as nps_sort_segment
+      for (;;) {
+        double pivot, sm, bg;
+        const int pidx = nps_partition(x, A, T, W, L, R, lane, &pivot, &sm, &bg);
+        int cL, cR;
+        bool want;
+        if (kk < pidx) {
+          cL = L, cR = pidx, want = pivot != sm;
+        } else if (kk > pidx) {
+          cL = pidx, cR = R, want = pivot != bg;
+        } else {
+          break;  // the boundary is the partition point
+        }
+        --it;
+        if (!want || cR - cL <= 1) break;
+        if (it <= 0) {  // depth budget spent: std_argsort on the range
+          if (lane == 0) nps_std_sort(A, cL, cR, NpsLess{x, false});
+          break;
+        }
+        if (cR - cL <= 64) {
+          nps_leaf(x, A, cL, cR - cL, lane);
+          break;
+        }
+        L = cL;
+        R = cR;
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+}
+
+// One segment re-ranked in numpy's order by the whole workgroup// One segment re-ranked in numpy's order by the whole workgroup (the flagged segments of a stable order).
 //   promote = 0 (argsort): every position is ranked; out_order[r] = the r-th position.
 //   promote = 1 (SH promotion ranks, HB_iteration.py:179-182): the finite losses' positions, in position
 //     order, are ranked; advance[pos] = rank < kk (kk = min(#finite, ceil(kb)), kb <= 0: none) for the
@@ -542,13 +587,16 @@ __device__ inline void nps_order_segment(const double* __restrict__ x, int n, in
   __threadfence_block();
   __syncthreads();
   const int m = promote ? m_sh : n;
-  nps_sort_segment(x, m, nan_any != 0, A, T, W, (NpsRange*)Lst, (n / 3) / 2);
+  const int kk = kb > 0.0 ? (kb >= (double)m ? m : (int)ceil(kb)) : 0;
+  if (promote && !out_order)  // the mask alone: only which positions come first (finite keys: no NaN path)
+    nps_select_segment(x, m, kk, A, T, W);
+  else
+    nps_sort_segment(x, m, nan_any != 0, A, T, W, (NpsRange*)Lst, (n / 3) / 2);
   __threadfence_block();
   __syncthreads();
   if (!promote) {
     for (int i = tid; i < n; i += NPS_THREADS) out_order[i] = A[i];
   } else {
-    const int kk = kb > 0.0 ? (kb >= (double)m ? m : (int)ceil(kb)) : 0;
     for (int r = tid; r < m; r += NPS_THREADS) {
       advance[A[r]] = r < kk ? 1 : 0;
       if (out_order) out_order[r] = A[r];

@@ -349,10 +349,20 @@ __global__ __launch_bounds__(64) void sh_promote_one_kernel(const double* __rest
 __global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double* __restrict__ loss, int n, double kb,
                                                                      uint8_t* __restrict__ advance, int32_t* __restrict__ scr,
                                                                      int force, int32_t* done, int32_t seq) {
+  constexpr int NM = 64 * PW_PER_LANE;  // n <= 1024
   __shared__ int go;
+  __shared__ double xl[NM];              // the bracket's losses
+  __shared__ int32_t wk[4 * NM];         // the sort's position arrays and range lists
   if (threadIdx.x == 0) go = force || scr[0];
-  __syncthreads();  // every thread has the flag before the re-rank overwrites the scratch
-  if (go) nps_order_segment(loss, n, 1, kb, scr, scr + n, scr + 2 * n, scr + 3 * n, nullptr, advance);
+  __syncthreads();
+  if (go) {  // uniform
+    // the sort reads and rewrites its keys and positions at random, many times over: all of it in LDS --
+    // the losses may be mapped host memory (the drop-in's), the scratch is global memory; reading them in
+    // place made a 1000-config bracket of quantised losses cost 0.43-0.5 ms
+    for (int i = threadIdx.x; i < n; i += blockDim.x) xl[i] = loss[i];
+    __syncthreads();
+    nps_order_segment(xl, n, 1, kb, wk, wk + n, wk + 2 * n, wk + 3 * n, nullptr, advance);
+  }
   if (done) {
     __threadfence_system();
     __syncthreads();
