@@ -46,10 +46,6 @@ class _MT(object):
     def load(self, raw):
         ctypes.memmove(self.addr, raw, self.NB)
 
-    def tag(self):
-        """(position, first key word): changes with every draw, for a cheap hint (not a check)."""
-        return (ctypes.c_int32.from_address(self.addr + 624 * 4).value, ctypes.c_uint32.from_address(self.addr).value)
-
 
 _GLOBAL = [None]
 
@@ -243,18 +239,14 @@ class BOHB(base_config_generator):
         return self.speculative == "always" or (self.speculative == "auto" and self.sampler == "gpu")
 
     def spec_fingerprint(self):
-        """(model version, GPU sampler counter, global RNG position tag): the same before and after an
-        interval in which nothing a get_config depends on changed.  A hint for SuccessiveHalving's batch
-        sizes only -- every speculative result is checked against the full RNG state when served."""
-        mt = _global_mt()
-        return (self._model_version, self._sample_counter, mt.tag() if mt is not None else None)
+        """(model version, GPU sampler counter): the same before and after an interval in which no result
+        refitted the model.  A hint for SuccessiveHalving's batch sizes only -- every speculative result is
+        checked against the full RNG state when served, and a batch cut short by another draw from the
+        global RNG drops the sizes back to one."""
+        return (self._model_version, self._sample_counter)
 
     def spec_unchanged(self, fp):
-        """spec_fingerprint() == fp, the cheap fields first (a refit in between is the common change)."""
-        if fp[0] != self._model_version or fp[1] != self._sample_counter:
-            return False
-        mt = _global_mt()
-        return mt is not None and mt.tag() == fp[2]
+        return fp[0] == self._model_version and fp[1] == self._sample_counter
 
     def get_config_batch_spec(self, budget, k):
         """k get_config calls drawn and scored now (ONE hbx_kde_acquire_batch pass) from a private copy of

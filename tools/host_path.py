@@ -64,16 +64,29 @@ def main():
     from hpbandster_amd import synthetic as S
     dev = torch.device("cuda", 0)
     out = {}
+    variants = [v for v in os.environ.get("HOST_PATH_AB", "").split(",") if v]  # e.g. HBX_RESCUE_PASS=1
     X = S.make_observations(1000, 8, 0, 0)
     pair = kde.fit_pair(X, S.make_losses(1000), S.var_type_string(8, 0), 9, device=dev)
     C = torch.from_numpy(S.make_candidates(100_000, 8, 0, 0)).to(dev)
     out["config2"] = measure(pair, C, a.reps)
+    for v in variants:
+        k, val = v.split("=")
+        old = os.environ.get(k)
+        os.environ[k] = val
+        out["config2_" + v] = measure(pair, C, a.reps)
+        os.environ.pop(k) if old is None else os.environ.__setitem__(k, old)
     X = S.make_observations(10000, 24, 8, 4)
     pair = kde.fit_pair(X, S.make_losses(10000), S.var_type_string(24, 8), 33, device=dev)
     C = torch.from_numpy(S.make_candidates(64, 24, 8, 4)).to(dev)
     out["get_config_64"] = measure(pair, C, a.reps)
     C = torch.from_numpy(S.make_candidates(1000000, 24, 8, 4)).to(dev)
     out["config3"] = measure(pair, C, 40)
+    for v in variants:
+        k, val = v.split("=")
+        old = os.environ.get(k)
+        os.environ[k] = val
+        out["config3_" + v] = measure(pair, C, 40)
+        os.environ.pop(k) if old is None else os.environ.__setitem__(k, old)
     print(json.dumps(out))
 
 

@@ -1,11 +1,10 @@
 #!/bin/bash
-# round-4 check set on one GPU box: the changed parity tests, the default bench line, the one-bracket
+# round-4 check set on one GPU box: every GPU parity test, the default bench line, the one-bracket
 # promotion latency sweep, and the gloo 2-rank rehearsal launched as a bare `bench.py --gpus 2`
 set -o pipefail
 O=gpurun_out/${1:-r04a}
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_promote.py \
-  tests/test_gpu_ties.py tests/test_gpu_batch.py tests/test_gpu_e2e.py tests/test_gpu_sample.py tests/test_gpu_dist.py tests/test_gpu_kde.py tests/test_gpu_fetch.py \
+timeout -k 10 600 python -u -m pytest -x -q -m gpu --timeout 120 --timeout-method thread tests/ \
   > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
