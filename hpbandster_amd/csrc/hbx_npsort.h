@@ -27,6 +27,13 @@
 #define NPS_WAVES 4
 #define NPS_THREADS (64 * NPS_WAVES)
 
+#ifdef NPS_TIMING  // diagnostic builds only (tools/build_variant.sh): stage stamps of the last re-rank
+__device__ unsigned long long nps_dbg[64];
+#define NPS_STAMP(k) do { if ((threadIdx.x & 63) == 0 && (k) < 64) nps_dbg[(k)] = wall_clock64(); } while (0)
+#else
+#define NPS_STAMP(k) do { } while (0)
+#endif
+
 struct NpsRange {
   int32_t L, R, it;  // [L, R), remaining depth budget
 };
@@ -517,6 +524,8 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
                                           int32_t* W) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (wave == 0 && n > 1 && kk > 0 && kk < n) {
+    int st = 1;
+    NPS_STAMP(0);
     if (n <= 64) {
       nps_leaf(x, A, 0, n, lane);
     } else {
@@ -524,6 +533,8 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
       for (;;) {
         double pivot, sm, bg;
         const int pidx = nps_partition(x, A, T, W, L, R, lane, &pivot, &sm, &bg);
+        NPS_STAMP(st);
+        ++st;
         int cL, cR;
         bool want;
         if (kk < pidx) {
@@ -547,6 +558,8 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
         R = cR;
       }
     }
+    NPS_STAMP(st);
+    NPS_STAMP(63);
   }
   __threadfence_block();
   __syncthreads();

@@ -359,9 +359,12 @@ __global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double
     // the sort reads and rewrites its keys and positions at random, many times over: all of it in LDS --
     // the losses may be mapped host memory (the drop-in's), the scratch is global memory; reading them in
     // place made a 1000-config bracket of quantised losses cost 0.43-0.5 ms
+    NPS_STAMP(40);
     for (int i = threadIdx.x; i < n; i += blockDim.x) xl[i] = loss[i];
     __syncthreads();
+    NPS_STAMP(41);
     nps_order_segment(xl, n, 1, kb, wk, wk + n, wk + 2 * n, wk + 3 * n, nullptr, advance);
+    NPS_STAMP(42);
   }
   if (done) {
     __threadfence_system();
@@ -371,6 +374,10 @@ __global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double
 }
 
 extern "C" {
+
+#ifdef NPS_TIMING
+int hbx_debug_nps(void* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(nps_dbg), sizeof(nps_dbg)) == hipSuccess ? 0 : 1; }
+#endif
 
 int64_t hbx_sort_scratch_bytes(int64_t N);
 
