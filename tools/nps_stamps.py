@@ -15,6 +15,8 @@ def main():
     from hpbandster_amd import promote
     dev = torch.device("cuda", 0)
     L = N.lib()
+    L.hbx_debug_nps.argtypes = [ctypes.c_void_p]
+    L.hbx_debug_nps.restype = ctypes.c_int
     for digits in (1, 2, 3):
         x = np.round(np.random.RandomState(3).rand(1000), digits)
         promote.advance_mask(x, 333, device=dev)
