@@ -676,8 +676,22 @@ def config2_line(device, reps=50):
         r = pair.acquire(c_dev, workspace=ws)
     el = (time.perf_counter() - t0) / reps
     pairs = Nc * (pair.good.nobs + pair.bad.nobs)
+    # the scoring launch's own time (HIP events at its start and end, separate calls after the timed ones)
+    ev = kde.ScoreEvents()
+    launch = []
+    for _ in range(20):
+        pair.acquire(c_dev, workspace=ws, events=ev)
+        launch.append(ev.elapsed_ms(True)[0])
+    lm = float(np.median(launch))
+    fpp = 3 * 8 + 4  # 3 Dc + 2 Du + 4 flops per pair
+    tf = fpp * pairs / (lm * 1e-3) / 1e12
     return {"workload": "kde_acquisition_d8_8c_obs1000_cand100000", "value": pairs / el, "unit": "pairs/s",
-            "ms_per_step": el * 1e3, "winner": r.index, "variant": int(pair.bad.variant)}
+            "ms_per_step": el * 1e3, "winner": r.index, "variant": int(pair.bad.variant),
+            "scoring_launch_ms": lm, "step_minus_scoring_ms": el * 1e3 - lm,
+            "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tf / PEAK_F16_MFMA_TFLOPS, "flops_per_pair": fpp,
+                         "kernel": "kde_logpdf_h32_pair_kernel<1,0,false,true> (l and g in one launch)",
+                         "timing": "median of 20 launches' start/end events"}}
 
 
 def refit_line(X, losses, var_type, device, reps=20):

@@ -35,14 +35,16 @@ class SuccessiveHalving(object):
         self._spec = None
         self._fp = None   # after a single call: the generator's state fingerprint (BOHB.spec_fingerprint)
         self._next = 1    # size of the next speculative batch
+        gen = getattr(config_sampler, "__self__", None)  # resolved once: the sampler is fixed per instance
+        ok = (batch_sampling and getattr(config_sampler, "__name__", "") == "get_config"
+              and getattr(gen, "get_config_batch_spec", None) is not None)
+        self._gen = gen if ok else None
 
     MAX_BATCH = 128
 
     def _sample(self, budget):
-        gen = getattr(self.config_sampler, "__self__", None)
-        spec_fn = getattr(gen, "get_config_batch_spec", None) if self.batch_sampling else None
-        if (spec_fn is None or getattr(self.config_sampler, "__name__", "") != "get_config"
-                or not gen.speculation_enabled()):
+        gen = self._gen
+        if gen is None or not gen.speculation_enabled():
             return self.config_sampler(budget)
         if self._spec is not None:
             r = self._spec.take()
@@ -57,7 +59,7 @@ class SuccessiveHalving(object):
         remaining = self.num_configs[self.SH_iter] - self.actual_num_configs[self.SH_iter]
         size = min(remaining, self._next)
         if size > 1:
-            spec = spec_fn(budget, size)
+            spec = gen.get_config_batch_spec(budget, size)
             r = spec.take() if spec is not None else None
             if r is not None:
                 self._spec = spec

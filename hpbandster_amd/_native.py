@@ -11,6 +11,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HBX_LIB_PATH: load another build of the same library (diagnostic ablation builds, tools/ablate.sh)
 LIB_PATH = os.environ.get("HBX_LIB_PATH") or os.path.join(_HERE, "_lib", "libhbx.so")
+DIAGNOSTIC_BUILD = bool(os.environ.get("HBX_LIB_PATH"))
 
 _lock = threading.Lock()
 _lib = None
@@ -46,6 +47,10 @@ SIGNATURES = {
                                      c_vp, c_vp, c_vp, c_vp, c_i32,
                                      c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
                                      c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "hbx_kde_pair_bind": (c_vp, [c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
+                                 c_i64]),
+    "hbx_kde_acquire_bound": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_pair_free": (None, [c_vp]),
     "hbx_kde_batch_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "hbx_kde_acquire_batch": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i64,
                                       c_vp, c_vp, c_vp, c_vp, c_i32,
@@ -127,6 +132,8 @@ def lib():
         import torch  # noqa: F401
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if DIAGNOSTIC_BUILD and not hasattr(L, name):  # an older build under A/B: entries it lacks stay absent
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -329,6 +329,22 @@ class KDEPair(object):
         self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         self._host_fn = N.lib().hbx_kde_acquire_host
         self._ws_cache = {}  # (thread, Nc) -> workspace of synchronous calls made without one
+        # the fixed arguments bound once on the native side: the synchronous call converts 8 arguments
+        # instead of 22 (hbx_kde_acquire_bound)
+        L = N.lib()
+        self._bound = None
+        if N.DIAGNOSTIC_BUILD and not hasattr(L, "hbx_kde_pair_bind"):
+            return  # an older diagnostic build (A/B runs): the unbound call
+        self._bound_fn = L.hbx_kde_acquire_bound
+        self._free_fn = L.hbx_kde_pair_free
+        self._bound = L.hbx_kde_pair_bind(good.k_vars, *self._kde_args)
+        if not self._bound:
+            raise N.HbxError("hbx_kde_pair_bind: %s" % L.hbx_last_error().decode())
+
+    def __del__(self):
+        b, self._bound = getattr(self, "_bound", None), None
+        if b:
+            self._free_fn(b)
 
     def __getitem__(self, key):  # cg.kde_models[b]['good'] like the reference dict
         if key == "good":
@@ -404,9 +420,12 @@ class KDEPair(object):
         if n < wsb:
             raise N.HbxError("workspace too small")
         rec = _record_buffer()
-        N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
-                              events.address if events is not None else None, self._raw_stream(self._dev_index),
-                              rec))
+        if events is None and self._bound:
+            N.check(self._bound_fn(self._bound, cands.data_ptr(), Nc, int(index_base), workspace.data_ptr(), n,
+                                   self._raw_stream(self._dev_index), rec))
+        else:
+            N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
+                                  events.address, self._raw_stream(self._dev_index), rec))
         return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):

@@ -162,6 +162,20 @@ int hbx_kde_acquire_host(const double* cand, int64_t Nc, int32_t D, int64_t inde
                          int64_t nmax, void* workspace, int64_t ws_bytes, void* events, void* stream,
                          void* rec_out);
 
+/* hbx_kde_acquire_host with the KDE pair's fixed arguments (params_good .. nmax, and D) bound once: the
+ * drop-in binds each model it fits (bohb.py:248-251 replaces the pair on every refit) and its get_config
+ * passes only what changes per call -- 8 arguments for the FFI to convert instead of 22 (about 2 us of host
+ * time per acquisition, on the critical path of every call).  The handle holds the pointers only: the caller
+ * keeps the KDEs' device buffers alive while it is in use, and frees it with hbx_kde_pair_free.  NULL on
+ * bad arguments (hbx_last_error). */
+void* hbx_kde_pair_bind(int32_t D, const void* params_good, const float* table_good, const double* X_good,
+                        const int64_t* rows_good, int32_t variant_good, const void* params_bad,
+                        const float* table_bad, const double* X_bad, const int64_t* rows_bad, int32_t variant_bad,
+                        int32_t dc_pad, int32_t du_pad, int64_t nmax);
+int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int64_t index_base, void* workspace,
+                          int64_t ws_bytes, void* stream, void* rec_out);
+void hbx_kde_pair_free(void* pair);
+
 /* Batched acquisition: B = ceil(Nc / seg) independent get_config calls against the same model in one
  * pass (replaces B sequential runs of the bohb.py:124-169 loop, as an SH stage issues
  * them back to back, HB_iteration.py:136-138).  Candidates [b*seg, min((b+1)*seg, Nc)) belong to call b;

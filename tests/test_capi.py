@@ -72,3 +72,19 @@ def test_philox_known_answers(ctr, key, want):
     c, k, o = np.array(ctr, np.uint32), np.array(key, np.uint32), np.zeros(4, np.uint32)
     N.check(N.lib().hbx_philox4x32_10(N.ptr(c), N.ptr(k), N.ptr(o)))
     assert [int(v) for v in o] == want
+
+
+def test_pair_binding_host_side():
+    """hbx_kde_pair_bind keeps the fixed arguments of a KDE pair (no GPU: host memory only); bad ones give
+    NULL and the error text, and the bound call refuses a NULL pair."""
+    from hpbandster_amd import _native as N
+    L = N.lib()
+    h = L.hbx_kde_pair_bind(32, 1, 2, 3, 4, 0, 5, 6, 7, 8, 0, 24, 8, 10000)
+    assert h
+    L.hbx_kde_pair_free(h)
+    assert not L.hbx_kde_pair_bind(0, 1, 2, 3, 4, 0, 5, 6, 7, 8, 0, 24, 8, 10000)
+    assert b"hbx_kde_pair_bind" in L.hbx_last_error()
+    assert not L.hbx_kde_pair_bind(32, None, 2, 3, 4, 0, 5, 6, 7, 8, 0, 24, 8, 10000)
+    rec = ctypes.create_string_buffer(64)
+    assert L.hbx_kde_acquire_bound(None, None, 0, 0, None, 0, None, rec) != 0
+    L.hbx_kde_pair_free(None)

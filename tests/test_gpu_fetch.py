@@ -64,3 +64,30 @@ def test_acquire_host_record_equals_workspace_record(device):
                (r_host.index, r_host.score, r_host.pdf_l, r_host.pdf_g, r_host.shortlist, r_host.flags)
     empty = pair.acquire(C[:0], workspace=ws)
     assert empty.index == -1
+
+
+def test_bound_pair_record_equals_unbound(device):
+    """hbx_kde_acquire_bound (the drop-in's synchronous call: the pair's fixed arguments bound once) stores
+    the same 48 bytes as hbx_kde_acquire_host with every argument passed, and the record published to mapped
+    memory equals the workspace's -- over many back-to-back calls (the completion word per call)."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(1200, 24, 8, 4, seed=15)
+    pair = kde.fit_pair(X, S.make_losses(1200, seed=16), S.var_type_string(24, 8), 33, device=device)
+    C = torch.from_numpy(S.make_candidates(20000, 24, 8, 4, seed=17)).to(device)
+    ws = torch.empty(pair.workspace_bytes(20000), dtype=torch.uint8, device=device)
+    L = N.lib()
+    sh = N.stream_handle(None, device)
+    off = pair.result_offset()
+    for base in (0, 5, 1 << 33):
+        a, b = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
+        N.check(L.hbx_kde_acquire_bound(pair._bound, C.data_ptr(), 20000, base, ws.data_ptr(), ws.numel(), sh, a))
+        w = ws[off:off + kde.RESULT_BYTES].cpu().numpy().tobytes()
+        N.check(L.hbx_kde_acquire_host(C.data_ptr(), 20000, 32, base, *pair._kde_args, ws.data_ptr(), ws.numel(),
+                                       None, sh, b))
+        assert a.raw[:kde.RESULT_BYTES] == b.raw[:kde.RESULT_BYTES] == w
+        assert kde.AcqResult.from_bytes(a.raw[:kde.RESULT_BYTES]).index >= base
+    seen = {pair.acquire(C[i * 1000:(i + 1) * 1000]).index for i in range(20)}
+    assert len(seen) > 1 and min(seen) >= 0
