@@ -122,7 +122,6 @@ struct AcqResult {
 };
 // flags: HBX_ACQ_OVERFLOW / HBX_ACQ_NEAR_TIE / HBX_ACQ_RESOLVED (include/hbx.h)
 
-// float <-> order-preserving uint32 (for atomicMin on floats of either sign)
 // Publish `words` 32-bit words of this thread (or, called by every lane, of this wave) to device-mapped
 // coherent host memory, then the completion word the host polls.  The words go out as system-scope relaxed
 // stores (coherent, not held in the L2), the wave waits until every one is acknowledged, then stores the
@@ -136,18 +135,7 @@ __device__ __forceinline__ void hbx_publish_done(int32_t* done, int32_t seq) {
   __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Device-coherent fp64 store / load (agent-scope relaxed atomics): data one workgroup hands to another of
-// the same launch, across the XCDs' non-coherent L2s, ordered by a wait for the store's acknowledgement
-// and an atomic ticket instead of agent-scope fences (each of which writes back and invalidates a whole
-// L2 on this part)
-__device__ __forceinline__ void hbx_st_co(double* p, double v) {
-  __hip_atomic_store((uint64_t*)p, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double hbx_ld_co(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
+// float <-> order-preserving uint32 (for atomicMin on floats of either sign)
 __device__ __forceinline__ uint32_t hbx_f2ord(float f) {
   uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);

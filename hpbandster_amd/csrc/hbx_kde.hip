@@ -17,9 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <vector>
-
 #include <new>
+#include <vector>
 
 #include "hbx_common.h"
 #include <hip/hip_ext.h>
@@ -737,8 +736,7 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
 
 // a single acquisition's state before its combine / shortlist / exact / final steps
 __device__ __forceinline__ void acq_init_state(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1,
-                                               AcqResult* res, int32_t* ticket) {
-  *ticket = 0;  // kde_exact_final_kernel's workgroup count
+                                               AcqResult* res) {
   *U = hbx_f2ord(INFINITY);
   *first1 = INT32_MAX;
   *count = 0;
@@ -761,7 +759,7 @@ template <int DCP, bool SIGNED>
 __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                               KdePairArgs a) {
   if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)  // a single acquisition's state (acq_init's work)
-    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res, a.init.ticket);
+    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
   if (a.rescue && __hip_atomic_load(a.rescue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   for (unsigned b = blockIdx.x; b < 2 * a.nblk0; b += gridDim.x) {
     const bool second = b >= a.nblk0;
@@ -773,9 +771,8 @@ __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __re
 // ------------------------------------------------------------------------------------------
 // score intervals, shortlist, exact re-score, final argmin
 
-__global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1, AcqResult* res,
-                                int32_t* ticket) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) acq_init_state(U, count, flags, first1, res, ticket);
+__global__ void acq_init_kernel(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1, AcqResult* res) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) acq_init_state(U, count, flags, first1, res);
 }
 
 // batched acquisition: per-segment bound, flags, shortlist count, best score and (index, position) key
@@ -821,7 +818,7 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
                                                           const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
-                                                          float* __restrict__ lo, float* __restrict__ hi,
+                                                          float* __restrict__ lo,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                                           int32_t* __restrict__ first1,
                                                           int32_t* __restrict__ rescue_cnt) {
@@ -889,8 +886,7 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
       }
       if (logl) logl[i] = lpt;
       if (logg) logg[i] = gpt;
-      lo[i] = slo;
-      hi[i] = shi;
+      lo[i] = slo;  // (the upper bound only enters the segment minimum below)
       if (of) atomicOr(flags + sg, 1);
     }
     // min of hi and first exact tie per segment.  Same-address atomics serialise in L2 (~10 ns each),
@@ -1045,78 +1041,6 @@ __device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64
   return acc / (double)n;  // valid in thread 0
 }
 
-// One unit of the split re-score at D <= 32 (exact_setup + exact_unit's arithmetic, same operations in the
-// same order), its loads issued by dependency level instead of in order of use: (1) the shortlist entry,
-// this thread's row index of the unit and the KDE's per-dim constants, (2) the point's coordinates and the
-// thread's whole observation row, into registers.  The block then waits about three memory latencies
-// before its arithmetic (the count, (1), (2)) where exact_setup + exact_unit waited about six (count,
-// entry, point, row index, then the row in 8-dim batches between the exps).
-__device__ double exact_unit32(const double* __restrict__ cand, int32_t D, const int32_t* __restrict__ entry,
-                               const KdeParams* __restrict__ P, const double* __restrict__ X,
-                               const int64_t* __restrict__ rows, int first, int len, ExactShared* sh) {
-  const int tid = threadIdx.x;
-  const int32_t q = *entry;
-  const bool has0 = tid < len;
-  const int64_t r0 = has0 ? rows[first + tid] : 0;
-  double h = 0.0;
-  int32_t vt = 0, nl = 2;
-  if (tid < D) {
-    h = P->bw[tid];
-    vt = P->vartype[tid];
-    nl = P->nlev[tid];
-  }
-  const double pbc = P->prod_bw_c;
-  const double xv = tid < D ? cand[(int64_t)q * D + tid] : 0.0;
-  const double* xr = X + r0 * (int64_t)D;
-  double v[32];
-#pragma unroll
-  for (int d = 0; d < 32; ++d) v[d] = (has0 && d < D) ? xr[d] : 0.0;
-  if (tid < D) {
-    const bool c = vt == 0;
-    sh->cont[tid] = c;
-    sh->c0[tid] = c ? (h * h) * 2. : 1. - h;
-    sh->c1[tid] = c ? 0. : h / (double)(nl - 1);
-    sh->xd[tid] = xv;
-  }
-  __syncthreads();
-  if (has0) {
-    double p = 1.0;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) {
-      if (d < D) {
-        const double xd = sh->xd[d];
-        double k;
-        if (sh->cont[d]) {
-          const double diff = v[d] - xd;
-          k = HBX_INV_SQRT_2PI * hbx_npexp::exp(-(diff * diff) / sh->c0[d]);  // numpy's exp, bit for bit
-        } else {
-          k = (v[d] == xd) ? sh->c0[d] : sh->c1[d];
-        }
-        p = (d == 0) ? k : p * k;
-      }
-    }
-    sh->dens[tid] = p / pbc;
-  }
-  for (int j = tid + (int)blockDim.x; j < len; j += blockDim.x) {  // units longer than the block (<= 263)
-    const double* xj = X + rows[first + j] * (int64_t)D;
-    double p = 1.0;
-    for (int d = 0; d < D; ++d) {
-      const double w = xj[d], xd = sh->xd[d];
-      double k;
-      if (sh->cont[d]) {
-        const double diff = w - xd;
-        k = HBX_INV_SQRT_2PI * hbx_npexp::exp(-(diff * diff) / sh->c0[d]);
-      } else {
-        k = (w == xd) ? sh->c0[d] : sh->c1[d];
-      }
-      p = (d == 0) ? k : p * k;
-    }
-    sh->dens[j] = p / pbc;
-  }
-  __syncthreads();
-  return np_pairwise_block<PW_SPLIT_LEVELS>(sh->dens, len, sh->nsum);
-}
-
 // Exact re-score of the shortlist.  Small shortlists (<= EXACT_SPLIT_CAP): one work item per
 // (candidate, KDE, 8192-buffer, unit) so one candidate spreads over many CUs; the unit sums go to
 // `part` and kde_final combines them.  Larger: one item per (candidate, KDE), all units in turn.
@@ -1125,18 +1049,14 @@ __device__ double exact_unit32(const double* __restrict__ cand, int32_t D, const
 #ifndef EXACT_ACQ_THREADS
 #define EXACT_ACQ_THREADS 256
 #endif
-// The exact re-score's work items of this block; returns the number of items of the launch (a block
-// with blockIdx.x < items took at least one).  CO: results stored device-coherently (kde_exact_final_kernel's
-// last workgroup reads them without a kernel boundary in between).
-template <bool CO>
-__device__ int64_t exact_items(const double* __restrict__ cand, int32_t D, const KdeParams* __restrict__ Pg,
-                               const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
-                               const KdeParams* __restrict__ Pb, const double* __restrict__ Xb,
-                               const int64_t* __restrict__ rows_b, const int32_t* __restrict__ list,
-                               const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
-                               double* __restrict__ exact_l, double* __restrict__ exact_g, ExactShared& sh) {
+__global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
+    const double* __restrict__ cand, int32_t D,
+    const KdeParams* __restrict__ Pg, const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
+    const KdeParams* __restrict__ Pb, const double* __restrict__ Xb, const int64_t* __restrict__ rows_b,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
+    double* __restrict__ exact_l, double* __restrict__ exact_g) {
+  __shared__ ExactShared sh;
   const int cnt = *count;
-  const int n_g = Pg->n, n_b = Pb->n;  // loaded beside the count
   const bool split = cnt <= EXACT_SPLIT_CAP;
   const int per = split ? nbuf * PW_SPLIT_UNITS : 1;  // items per (candidate, KDE)
   const int64_t items = (int64_t)cnt * 2 * per;
@@ -1149,43 +1069,21 @@ __device__ int64_t exact_items(const double* __restrict__ cand, int32_t D, const
     const int64_t* rows = isl ? rows_g : rows_b;
     if (split) {
       const int r = (int)(item % per), b = r / PW_SPLIT_UNITS, u = r % PW_SPLIT_UNITS;
-      const int n = isl ? n_g : n_b, c = b * PW_BUF;
+      const int n = P->n, c = b * PW_BUF;
       if (c >= n) continue;
       const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
       int off, len;
       if (!pw_unit<PW_SPLIT_CUT>(m, u, &off, &len)) continue;
-      double v;
-      if (D <= 32) {
-        v = exact_unit32(cand, D, list + p, P, X, rows, c + off, len, &sh);
-      } else {
-        exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
-        v = exact_unit<PW_SPLIT_LEVELS>(X, D, rows, P, c + off, len, &sh);
-      }
-      if (threadIdx.x == 0) {
-        if (CO) hbx_st_co(part + pk * per + r, v);
-        else part[pk * per + r] = v;
-      }
+      exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
+      const double v = exact_unit<PW_SPLIT_LEVELS>(X, D, rows, P, c + off, len, &sh);
+      if (threadIdx.x == 0) part[pk * per + r] = v;
     } else {
       exact_setup(P, D, cand + (int64_t)list[p] * D, &sh);
       const double v = exact_pdf(X, D, rows, P, &sh);
-      if (threadIdx.x == 0) {
-        if (CO) hbx_st_co((isl ? exact_l : exact_g) + p, v);
-        else (isl ? exact_l : exact_g)[p] = v;
-      }
+      if (threadIdx.x == 0) (isl ? exact_l : exact_g)[p] = v;
     }
     __syncthreads();
   }
-  return items;
-}
-
-__global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
-    const double* __restrict__ cand, int32_t D,
-    const KdeParams* __restrict__ Pg, const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
-    const KdeParams* __restrict__ Pb, const double* __restrict__ Xb, const int64_t* __restrict__ rows_b,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
-    double* __restrict__ exact_l, double* __restrict__ exact_g) {
-  __shared__ ExactShared sh;
-  exact_items<false>(cand, D, Pg, Xg, rows_g, Pb, Xb, rows_b, list, count, nbuf, part, exact_l, exact_g, sh);
 }
 
 // split mode: pdf of every (shortlisted candidate, KDE) from its unit sums; one thread each
@@ -1361,12 +1259,6 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
 
 // the final argmin of one acquisition (256 threads): the split re-score's unit sums -> pdfs, strict '<'
 // first-index argmin over the shortlist, the near set, the result record
-template <bool CO>
-__device__ __forceinline__ double ld_maybe_co(const double* p) {
-  return CO ? hbx_ld_co(p) : *p;
-}
-
-template <bool CO>
 __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* __restrict__ count,
                                const double* exact_l,  // (written here through exact_lw / _gw)
                                const double* exact_g, const int32_t* __restrict__ flags, int64_t index_base,
@@ -1396,12 +1288,11 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
       double acc = 0.0;
       for (int c = 0, b = 0; c < n; c += PW_BUF, ++b) {
         const int m = (n - c) < PW_BUF ? (n - c) : PW_BUF;
-        acc = acc + pw_combine_units_wave<PW_SPLIT_CUT, CO>(m, us + b * PW_SPLIT_UNITS);
+        acc = acc + pw_combine_units_wave<PW_SPLIT_CUT>(m, us + b * PW_SPLIT_UNITS);
       }
       if ((threadIdx.x & 63) == 0) {
         const double pdf = acc / (double)n;
-        if (CO) hbx_st_co((isl ? exact_lw : exact_gw) + (pk >> 1), pdf);
-        else (isl ? exact_lw : exact_gw)[pk >> 1] = pdf;
+        (isl ? exact_lw : exact_gw)[pk >> 1] = pdf;
         if (small) (isl ? exl : exg)[pk >> 1] = pdf;
       }
     }
@@ -1409,8 +1300,8 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     __syncthreads();
   } else if (small) {  // pdfs written by another kernel: one global read each
     if (tp < cnt) {
-      exl[tp] = ld_maybe_co<CO>(exact_l + tp);
-      exg[tp] = ld_maybe_co<CO>(exact_g + tp);
+      exl[tp] = exact_l[tp];
+      exg[tp] = exact_g[tp];
     }
     __syncthreads();
   }
@@ -1421,7 +1312,7 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
   for (int p = threadIdx.x; p < cnt; p += 256) {
     // bohb.py:129 with Python max(): max(1e-8, g) keeps 1e-8 unless g > 1e-8 (NaN -> 1e-8);
     // max(l, 1e-8) keeps l unless 1e-8 > l (NaN -> NaN)
-    const double g = small ? exg[p] : ld_maybe_co<CO>(exact_g + p), l = small ? exl[p] : ld_maybe_co<CO>(exact_l + p);
+    const double g = small ? exg[p] : exact_g[p], l = small ? exl[p] : exact_l[p];
     const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
     const int64_t idx = small ? my_idx : list[p];
     // valid iff s < +inf (bohb.py:150 'val < best' with best = inf); strict '<', first index wins
@@ -1459,7 +1350,7 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     const double sb = bs[0];
     if (!small) rb = score_rel(Pg, Pb, el, eg, list[wp]);
     for (int p = threadIdx.x; p < cnt; p += 256) {
-      const double g = small ? exg[p] : ld_maybe_co<CO>(exact_g + p), l = small ? exl[p] : ld_maybe_co<CO>(exact_l + p);
+      const double g = small ? exg[p] : exact_g[p], l = small ? exl[p] : exact_l[p];
       const double s = ((g > 1e-8) ? g : 1e-8) / ((1e-8 > l) ? 1e-8 : l);
       const int64_t ip = small ? my_idx : list[p];
       if (p == wp || near_best(s, small ? my_rel : score_rel(Pg, Pb, el, eg, ip), sb, rb))
@@ -1478,8 +1369,8 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     if (wp >= 0) {
       r.index = bi[0] + index_base;
       r.score = bs[0];
-      r.pdf_l = small ? exl[wp] : ld_maybe_co<CO>(exact_l + wp);
-      r.pdf_g = small ? exg[wp] : ld_maybe_co<CO>(exact_g + wp);
+      r.pdf_l = small ? exl[wp] : exact_l[wp];
+      r.pdf_g = small ? exg[wp] : exact_g[wp];
     }
     *res = r;
     if (host_res) {  // hbx_kde_acquire_host: the record to mapped host memory, then the completion word
@@ -1503,43 +1394,8 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
                                                         int32_t nbuf, const double* __restrict__ part,
                                                         double* exact_lw, double* exact_gw, AcqResult* host_res,
                                                         int32_t* done, int32_t seq) {
-  kde_final_body<false>(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
-                        exact_lw, exact_gw, host_res, done, seq);
-}
-
-// The exact re-score with the final argmin run by its last workgroup (a single acquisition): each
-// workgroup that took work items stores its results device-coherently, waits for their acknowledgement and
-// takes a ticket; the one that takes the last ticket runs kde_final_body over coherent loads.  One launch
-// instead of two and no agent-scope fence (an earlier ticket scheme with release/acquire fences measured
-// 20 us slower than the separate final launch).  An empty shortlist: workgroup 0 runs the final.  The
-// ticket is zeroed with the rest of the acquisition state (acq_init_state).
-static_assert(EXACT_ACQ_THREADS == 256, "kde_final_body runs on 256 threads");
-__global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_final_kernel(
-    const double* __restrict__ cand, int32_t D, const KdeParams* __restrict__ Pg, const double* __restrict__ Xg,
-    const int64_t* __restrict__ rows_g, const KdeParams* __restrict__ Pb, const double* __restrict__ Xb,
-    const int64_t* __restrict__ rows_b, const int32_t* __restrict__ list, const int32_t* __restrict__ count,
-    int32_t nbuf, double* __restrict__ part, double* exact_l, double* exact_g, const int32_t* __restrict__ flags,
-    int64_t index_base, const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg, int32_t* __restrict__ near_list,
-    AcqResult* __restrict__ res, AcqResult* host_res, int32_t* done, int32_t seq, int32_t* ticket) {
-  __shared__ ExactShared sh;
-  __shared__ int is_last;
-  const int64_t items =
-      exact_items<true>(cand, D, Pg, Xg, rows_g, Pb, Xb, rows_b, list, count, nbuf, part, exact_l, exact_g, sh);
-  const int64_t active = items < (int64_t)gridDim.x ? items : (int64_t)gridDim.x;
-  if (threadIdx.x == 0) {
-    if (active == 0) {
-      is_last = blockIdx.x == 0;
-    } else if ((int64_t)blockIdx.x < active) {
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's results acknowledged
-      is_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
-    } else {
-      is_last = 0;
-    }
-  }
-  __syncthreads();
-  if (!is_last) return;  // uniform
-  kde_final_body<true>(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
-                       exact_l, exact_g, host_res, done, seq);
+  kde_final_body(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
+                 exact_lw, exact_gw, host_res, done, seq);
 }
 
 // Batched argmin, three passes over the shortlist: (1) per-segment minimum of the exact score,
@@ -1679,13 +1535,6 @@ struct ScoreFns {
   logpdf_pair_fn rescue_pair;
 };
 
-// the exact re-score and the final argmin of a single acquisition in one launch (kde_exact_final_kernel);
-// HBX_EXACT_FINAL=0 keeps two launches (read per call: tests switch it in-process)
-static bool exact_final_enabled() {
-  const char* e = getenv("HBX_EXACT_FINAL");
-  return !(e && atoi(e) == 0);
-}
-
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
 // HBX_SCORE_PAIR=0 keeps two launches (read per call: tests switch it in-process)
 static bool pair_enabled() {
@@ -1806,7 +1655,7 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
 // of acquisitions (segments) of a batched call (1 for hbx_kde_acquire).  The single result record
 // comes first so its offset does not depend on the sizes.
 struct WsLayout {
-  size_t res, U, count, flags, segcnt, segnear, best, key, first1, rescue, est_l, est_g, lo, hi, list, near, exact_l,
+  size_t res, U, count, flags, segcnt, segnear, best, key, first1, rescue, est_l, est_g, lo, list, near, exact_l,
       exact_g, part, total;
 };
 
@@ -1831,7 +1680,6 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.est_l = take(sizeof(KdeEst) * Nc);
   w.est_g = take(sizeof(KdeEst) * Nc);
   w.lo = take(4 * Nc);
-  w.hi = take(4 * Nc);
   w.list = take(4 * Nc);
   w.near = take(4 * Nc);
   w.exact_l = take(8 * Nc);
@@ -2075,12 +1923,10 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   uint64_t* best = (uint64_t*)(ws + w.best);
   uint64_t* key = (uint64_t*)(ws + w.key);
   int32_t* first1 = (int32_t*)(ws + w.first1);
-  int32_t* ticket = (int32_t*)(ws + w.rescue + 64);  // in the rescue counter's 256-byte slot
   AcqResult* res = (AcqResult*)(ws + w.res);
   KdeEst* el = (KdeEst*)(ws + w.est_l);
   KdeEst* eg = (KdeEst*)(ws + w.est_g);
   float* lo = (float*)(ws + w.lo);
-  float* hi = (float*)(ws + w.hi);
   int32_t* list = (int32_t*)(ws + w.list);
   double* exact_l = (double*)(ws + w.exact_l);
   double* exact_g = (double*)(ws + w.exact_g);
@@ -2095,7 +1941,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
-    if (!batch_res) ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res, ticket};
+    if (!batch_res) ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res};
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
                                  (int32_t*)(ws + w.rescue), s, ip, &inited);
     if (rc) return rc;
@@ -2105,7 +1951,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                        segcnt, best, key, first1, count, segnear);
     HBX_LAUNCH_CHECK();
   } else if (!inited) {
-    hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res, ticket);
+    hipLaunchKernelGGL(acq_init_kernel, dim3(1), dim3(64), 0, s, U, count, flags, first1, res);
     HBX_LAUNCH_CHECK();
   }
   const dim3 grid((unsigned)((Nc + 255) / 256));
@@ -2116,7 +1962,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
       HBX_LAUNCH_CHECK();
     } else {
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
-                         dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, hi, U,
+                         dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, U,
                          flags, first1, (int32_t*)(ws + w.rescue));
       HBX_LAUNCH_CHECK();
     }
@@ -2124,21 +1970,12 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                        batch_res ? segcnt : (int32_t*)nullptr, first1);
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
-    // single acquisition: the final argmin combines the unit sums itself (one launch less) -- and runs as
-    // the exact re-score's last workgroup (kde_exact_final_kernel)
-    fuse_combine = !batch_res && !(exact_only && (logl_out || logg_out));
-    if (fuse_combine && exact_final_enabled()) {
-      hipLaunchKernelGGL(kde_exact_final_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,
-                         (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
-                         rows_bad, list, count, nbuf, part, exact_l, exact_g, flags, index_base, el, eg, near, res,
-                         host_res, done, seq, ticket);
-      HBX_LAUNCH_CHECK();
-      return HBX_OK;
-    }
     hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,
                        (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
                        rows_bad, list, count, nbuf, part, exact_l, exact_g);
     HBX_LAUNCH_CHECK();
+    // single acquisition: the final kernel combines the unit sums itself (one launch less)
+    fuse_combine = !batch_res && !(exact_only && (logl_out || logg_out));
     if (!fuse_combine) {
       hipLaunchKernelGGL(kde_exact_combine_kernel, dim3((2 * EXACT_SPLIT_CAP + 3) / 4), dim3(256), 0, s,
                          (const KdeParams*)params_good, (const KdeParams*)params_bad, count, nbuf, part, exact_l,

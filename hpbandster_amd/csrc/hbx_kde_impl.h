@@ -263,7 +263,6 @@ struct KdePairArgs {
     int32_t* flags;
     int32_t* first1;
     struct AcqResult* res;
-    int32_t* ticket;
   } init;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);

@@ -84,8 +84,7 @@ __device__ inline double pw_combine_units(int m, const double* us) {
 
 // The same by one wave: lane t holds node (lev, t) of each level in turn, its children read from lanes 2t
 // and 2t+1 of the level below -- the same additions in the same order; every lane returns the root.
-// CO: the unit sums were stored device-coherently by other workgroups of the same launch (hbx_ld_co)
-template <int CUT, bool CO = false>
+template <int CUT>
 __device__ inline double pw_combine_units_wave(int m, const double* us) {
   static_assert((1 << CUT) <= 64, "one node per lane");
   const int t = threadIdx.x & 63;
@@ -94,7 +93,7 @@ __device__ inline double pw_combine_units_wave(int m, const double* us) {
     const double c0 = __shfl(v, (2 * t) & 63), c1 = __shfl(v, (2 * t + 1) & 63);
     int off, len;
     if (t < (1 << lev) && pw_node(m, lev, t, &off, &len))
-      v = (lev == CUT || len <= 128) ? (CO ? hbx_ld_co(us + (t << (CUT - lev))) : us[t << (CUT - lev)]) : c0 + c1;
+      v = (lev == CUT || len <= 128) ? us[t << (CUT - lev)] : c0 + c1;
   }
   return __shfl(v, 0);
 }

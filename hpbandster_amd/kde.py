@@ -425,7 +425,8 @@ class KDEPair(object):
                                    self._raw_stream(self._dev_index), rec))
         else:
             N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
-                                  events.address, self._raw_stream(self._dev_index), rec))
+                                  events.address if events is not None else None,
+                                  self._raw_stream(self._dev_index), rec))
         return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):

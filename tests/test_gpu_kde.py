@@ -725,3 +725,37 @@ def test_acquire_reused_workspace_and_ragged_tiles(device, dc, du, nobs, nc, far
     l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
     g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
     assert ref[0] == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("nc", [300, 2500])
+def test_large_shortlists_through_the_synchronous_call(device, nc):
+    """The drop-in's synchronous call (hbx_kde_acquire_bound: the record published to mapped memory without a
+    system fence) at shortlists past the in-LDS 256 (300) and past the split cap (2500: one work item per
+    candidate, all units in turn) picks the C oracle's candidate with its pdfs; repeated on one workspace,
+    forward and reversed (the previous call's state and record must not leak)."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    from oracle import c_oracle
+    dc = 70
+    X = S.make_observations(320, dc, 0, 0, seed=81)
+    vt = S.var_type_string(dc, 0)
+    pair = kde.fit_pair(X, S.make_losses(320, seed=82), vt, dc + 1, device=device)
+    assert pair.good.exact_only  # every candidate re-scored: the shortlist is the whole set
+    C = S.make_candidates(nc, dc, 0, 0, seed=83)
+    C[:40] = X[pair.good.rows_dev.cpu().numpy()[:40]] + 1e-3
+    Cd = torch.from_numpy(C).to(device)
+    ws = torch.empty(pair.workspace_bytes(nc), dtype=torch.uint8, device=device)
+
+    def rec(r):
+        return (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist, r.flags, r.near, r.rel)
+    first = rec(pair.acquire(Cd, workspace=ws))
+    for _ in range(3):
+        back = pair.acquire(torch.flip(Cd, [0]).contiguous(), workspace=ws)
+        assert back.score == first[1] and back.shortlist == nc
+        assert rec(pair.acquire(Cd, workspace=ws)) == first
+    assert first[4] == nc
+    l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+    g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    want, _ = O.select(l, g)
+    assert first[0] == want and (first[2], first[3]) == (l[want], g[want])
