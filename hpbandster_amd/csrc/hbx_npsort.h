@@ -39,11 +39,14 @@ struct NpsRange {
 };
 
 // ---- libstdc++ std::sort (bits/stl_algo.h, bits/stl_heap.h) on one lane ----------------------------
+// Elements T: positions (int32, keys read through x) or (key, position) pairs (NpsKV: the key travels
+// with its position, so a comparison is one LDS read instead of two dependent ones).  The same
+// comparisons in the same order either way, so the same arrangement of positions.
 struct NpsLess {
   const double* x;
   bool nan_last;
-  __device__ bool operator()(int32_t a, int32_t b) const {
-    const double u = x[a], v = x[b];
+  __device__ bool operator()(int32_t a, int32_t b) const { return less(x[a], x[b]); }
+  __device__ bool less(double u, double v) const {
     if (!nan_last) return u < v;
     if (u == u && v == v) return u < v;
     if (u != u) return false;
@@ -51,13 +54,25 @@ struct NpsLess {
   }
 };
 
-__device__ inline void nps_swap(int32_t* a, int i, int j) {
-  const int32_t t = a[i];
+struct NpsKV {
+  double k;
+  int32_t i, pad;
+};
+
+struct NpsKVLess {
+  bool nan_last;
+  __device__ bool operator()(const NpsKV& a, const NpsKV& b) const { return NpsLess{nullptr, nan_last}.less(a.k, b.k); }
+};
+
+template <class T>
+__device__ inline void nps_swap(T* a, int i, int j) {
+  const T t = a[i];
   a[i] = a[j];
   a[j] = t;
 }
 
-__device__ inline void nps_move_median_to_first(int32_t* a, int res, int p, int q, int r, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_move_median_to_first(T* a, int res, int p, int q, int r, const C& lt) {
   if (lt(a[p], a[q])) {
     if (lt(a[q], a[r])) nps_swap(a, res, q);
     else if (lt(a[p], a[r])) nps_swap(a, res, r);
@@ -71,7 +86,8 @@ __device__ inline void nps_move_median_to_first(int32_t* a, int res, int p, int 
   }
 }
 
-__device__ inline int nps_unguarded_partition(int32_t* a, int first, int last, int pivot, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline int nps_unguarded_partition(T* a, int first, int last, int pivot, const C& lt) {
   while (true) {
     while (lt(a[first], a[pivot])) ++first;
     --last;
@@ -82,7 +98,8 @@ __device__ inline int nps_unguarded_partition(int32_t* a, int first, int last, i
   }
 }
 
-__device__ inline void nps_adjust_heap(int32_t* a, int first, int hole, int len, int32_t value, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_adjust_heap(T* a, int first, int hole, int len, T value, const C& lt) {
   const int top = hole;
   int child = hole;
   while (child < (len - 1) / 2) {
@@ -105,7 +122,8 @@ __device__ inline void nps_adjust_heap(int32_t* a, int first, int hole, int len,
   a[first + hole] = value;
 }
 
-__device__ inline void nps_heap_sort(int32_t* a, int first, int last, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_heap_sort(T* a, int first, int last, const C& lt) {
   const int n = last - first;
   if (n >= 2)
     for (int parent = (n - 2) / 2;; --parent) {
@@ -114,16 +132,17 @@ __device__ inline void nps_heap_sort(int32_t* a, int first, int last, const NpsL
     }
   while (last - first > 1) {
     --last;
-    const int32_t value = a[last];
+    const T value = a[last];
     a[last] = a[first];
     nps_adjust_heap(a, first, 0, last - first, value, lt);
   }
 }
 
-__device__ inline void nps_insertion_sort(int32_t* a, int first, int last, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_insertion_sort(T* a, int first, int last, const C& lt) {
   if (first == last) return;
   for (int i = first + 1; i < last; ++i) {
-    const int32_t val = a[i];
+    const T val = a[i];
     if (lt(val, a[first])) {
       for (int j = i; j > first; --j) a[j] = a[j - 1];
       a[first] = val;
@@ -138,9 +157,10 @@ __device__ inline void nps_insertion_sort(int32_t* a, int first, int last, const
   }
 }
 
-__device__ inline void nps_unguarded_insertion_sort(int32_t* a, int first, int last, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_unguarded_insertion_sort(T* a, int first, int last, const C& lt) {
   for (int i = first; i < last; ++i) {
-    const int32_t val = a[i];
+    const T val = a[i];
     int j = i;
     while (lt(val, a[j - 1])) {
       a[j] = a[j - 1];
@@ -153,7 +173,8 @@ __device__ inline void nps_unguarded_insertion_sort(int32_t* a, int first, int l
 // std::sort(a + first, a + last, lt): __introsort_loop (threshold 16, depth 2 floor(log2 n)) made
 // iterative -- the right part of each cut on a stack with its depth, the loop on the left part; the
 // ranges are disjoint, so the order they are finished in does not matter -- then __final_insertion_sort
-__device__ inline void nps_std_sort(int32_t* a, int first, int last, const NpsLess& lt) {
+template <class T, class C>
+__device__ inline void nps_std_sort(T* a, int first, int last, const C& lt) {
   if (last - first < 2) return;
   struct Fr {
     int f, l, d;
@@ -181,6 +202,23 @@ __device__ inline void nps_std_sort(int32_t* a, int first, int last, const NpsLe
   } else {
     nps_insertion_sort(a, first, last, lt);
   }
+}
+
+// std::sort of the positions A[first, last) by keys x (NaN-free) with each key carried beside its
+// position in kv (>= last - first pairs of LDS scratch): the wave stages the pairs, lane 0 sorts them, the
+// wave writes the positions back.  Whole wave.
+__device__ inline void nps_std_sort_staged(const double* __restrict__ x, int32_t* A, int first, int last, NpsKV* kv,
+                                           int lane) {
+  const int m = last - first;
+  for (int j = lane; j < m; j += 64) {
+    const int32_t p = A[first + j];
+    kv[j] = NpsKV{x[p], p, 0};
+  }
+  __threadfence_block();
+  if (lane == 0) nps_std_sort(kv, 0, m, NpsKVLess{false});
+  __threadfence_block();
+  for (int j = lane; j < m; j += 64) A[first + j] = kv[j].i;
+  __threadfence_block();
 }
 
 // ---- the bitonic key/index networks (x86-simd-sort argsort_{8,16,32,64}_64bit) on one wave ----------
@@ -290,6 +328,15 @@ __device__ inline void nps_leaf(const double* __restrict__ x, int32_t* A, int L,
 
 // ---- the quicksort partition of one range by one wave ----------------------------------------------
 
+// lane `src` (wave-uniform) of v, through the scalar unit (v_readlane: no LDS round trip as __shfl takes)
+__device__ __forceinline__ int32_t nps_rl(int32_t v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ double nps_rl(double v, int src) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // packed >= pivot counts of the U blocks of 8 of group g (4 bits per block): one lane's share of a window
 __device__ __forceinline__ uint32_t nps_group_counts(const double* __restrict__ x, const int32_t* A, int Lp, int g,
                                                      int U, double pivot) {
@@ -316,11 +363,11 @@ __device__ inline int nps_partition(const double* __restrict__ x, int32_t* A, in
   int rank = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const double o = __shfl(sv, q);
+    const double o = nps_rl(sv, q);
     rank += (o < sv) || (o == sv && q < lane);
   }
   const uint64_t at4 = __ballot(lane < 8 && rank == 4);
-  const double pivot = __shfl(sv, __ffsll((long long)at4) - 1);
+  const double pivot = nps_rl(sv, __ffsll((long long)at4) - 1);
   // the range's min / max (the recursion stops on a side whose extreme equals the pivot)
   double mn = __builtin_inf(), mx = -__builtin_inf();
   for (int i = L + lane; i < R; i += 64) {
@@ -346,12 +393,12 @@ __device__ inline int nps_partition(const double* __restrict__ x, int32_t* A, in
     double kv = x[id];
     for (int t = 0; t < p; ++t) {
       const int sl = left - L;
-      const double kl = __shfl(kv, sl);
+      const double kl = nps_rl(kv, sl);
       if (!(kl < pivot)) {
         --right;
         const int sr = right - (R - 64);
-        const double kr = __shfl(kv, sr);
-        const int32_t il = __shfl(id, sl), ir = __shfl(id, sr);
+        const double kr = nps_rl(kv, sr);
+        const int32_t il = nps_rl(id, sl), ir = nps_rl(id, sr);
         if (lane == sl) {
           kv = kr;
           id = ir;
@@ -415,7 +462,7 @@ __device__ inline int nps_partition(const double* __restrict__ x, int32_t* A, in
       }
       slot = g - wl;
     }
-    store_group(g, (uint32_t)__shfl((int)win, slot));
+    store_group(g, (uint32_t)nps_rl((int32_t)win, slot));
   }
   {  // the held-back first and last groups
     uint32_t pk0 = 0, pk1 = 0;
@@ -423,8 +470,8 @@ __device__ inline int nps_partition(const double* __restrict__ x, int32_t* A, in
       pk0 = nps_group_counts(x, A, Lp, 0, U, pivot);
       pk1 = nps_group_counts(x, A, Lp, G - 1, U, pivot);
     }
-    store_group(0, (uint32_t)__shfl((int)pk0, 0));
-    store_group(G - 1, (uint32_t)__shfl((int)pk1, 0));
+    store_group(0, (uint32_t)nps_rl((int32_t)pk0, 0));
+    store_group(G - 1, (uint32_t)nps_rl((int32_t)pk1, 0));
   }
   __threadfence_block();
   // the compress-stores, all at once: block b's keys >= pivot end at W[2b+1], the rest start at W[2b]
@@ -520,8 +567,9 @@ __device__ inline void nps_sort_segment(const double* __restrict__ x, int n, boo
 // the walk follows that one range, a quickselect along numpy's own partition sequence, and ends in its
 // network, its std::sort (depth budget spent) or a partition point at the boundary.  One wave; NaN-free
 // keys (the promotion's finite losses).  The whole workgroup calls it (a barrier at the end).
+// kv (nullable): LDS scratch of kv_cap (key, position) pairs for a std::sort finish that fits
 __device__ inline void nps_select_segment(const double* __restrict__ x, int n, int kk, int32_t* A, int32_t* T,
-                                          int32_t* W) {
+                                          int32_t* W, NpsKV* kv = nullptr, int kv_cap = 0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (wave == 0 && n > 1 && kk > 0 && kk < n) {
     int st = 1;
@@ -547,7 +595,8 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
         --it;
         if (!want || cR - cL <= 1) break;
         if (it <= 0) {  // depth budget spent: std_argsort on the range
-          if (lane == 0) nps_std_sort(A, cL, cR, NpsLess{x, false});
+          if (kv && cR - cL <= kv_cap) nps_std_sort_staged(x, A, cL, cR, kv, lane);
+          else if (lane == 0) nps_std_sort(A, cL, cR, NpsLess{x, false});
           break;
         }
         if (cR - cL <= 64) {
@@ -565,7 +614,7 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
   __syncthreads();
 }
 
-// One segment re-ranked in numpy's order by the whole workgroup// One segment re-ranked in numpy's order by the whole workgroup (the flagged segments of a stable order).
+// One segment re-ranked in numpy's order by the whole workgroup (the flagged segments of a stable order).
 //   promote = 0 (argsort): every position is ranked; out_order[r] = the r-th position.
 //   promote = 1 (SH promotion ranks, HB_iteration.py:179-182): the finite losses' positions, in position
 //     order, are ranked; advance[pos] = rank < kk (kk = min(#finite, ceil(kb)), kb <= 0: none) for the
@@ -573,7 +622,7 @@ __device__ inline void nps_select_segment(const double* __restrict__ x, int n, i
 // A / T / W: n int32 of scratch each; Lst: n int32 (two range lists of n / 6).
 __device__ inline void nps_order_segment(const double* __restrict__ x, int n, int promote, double kb, int32_t* A,
                                          int32_t* T, int32_t* W, int32_t* Lst, int64_t* __restrict__ out_order,
-                                         uint8_t* __restrict__ advance) {
+                                         uint8_t* __restrict__ advance, NpsKV* kv = nullptr, int kv_cap = 0) {
   __shared__ int nan_any, m_sh;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -602,7 +651,7 @@ __device__ inline void nps_order_segment(const double* __restrict__ x, int n, in
   const int m = promote ? m_sh : n;
   const int kk = kb > 0.0 ? (kb >= (double)m ? m : (int)ceil(kb)) : 0;
   if (promote && !out_order)  // the mask alone: only which positions come first (finite keys: no NaN path)
-    nps_select_segment(x, m, kk, A, T, W);
+    nps_select_segment(x, m, kk, A, T, W, kv, kv_cap);
   else
     nps_sort_segment(x, m, nan_any != 0, A, T, W, (NpsRange*)Lst, (n / 3) / 2);
   __threadfence_block();

@@ -353,6 +353,7 @@ __global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double
   __shared__ int go;
   __shared__ double xl[NM];              // the bracket's losses
   __shared__ int32_t wk[4 * NM];         // the sort's position arrays and range lists
+  __shared__ NpsKV kv[NM];                // a std::sort finish's (key, position) pairs
   if (threadIdx.x == 0) go = force || scr[0];
   __syncthreads();
   if (go) {  // uniform
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(NPS_THREADS) void sh_rerank_one_kernel(const double
     for (int i = threadIdx.x; i < n; i += blockDim.x) xl[i] = loss[i];
     __syncthreads();
     NPS_STAMP(41);
-    nps_order_segment(xl, n, 1, kb, wk, wk + n, wk + 2 * n, wk + 3 * n, nullptr, advance);
+    nps_order_segment(xl, n, 1, kb, wk, wk + n, wk + 2 * n, wk + 3 * n, nullptr, advance, kv, NM);
     NPS_STAMP(42);
   }
   if (done) {
