@@ -562,13 +562,13 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
         j.result = {"loss": float(loss), "info": None}
         return j
 
-    def make():
+    def make(spec):
         space = CS.ConfigurationSpace(seed=3)
         for i in range(24):
             space.add_hyperparameter(CS.UniformFloatHyperparameter("x%02d" % i, lower=0, upper=1))
         for i in range(8):
             space.add_hyperparameter(CS.CategoricalHyperparameter("y%02d" % i, ["a", "b", "c", "d"]))
-        cg = BOHB(space, device=device, sampler="gpu", sampler_seed=77)
+        cg = BOHB(space, device=device, sampler="gpu", sampler_seed=77, speculative=spec)
         X = S.make_observations(n_obs, 24, 8, 4, seed=51)
         Lo = S.make_losses(n_obs, seed=52)
         for i in range(n_obs):
@@ -576,7 +576,7 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
         return cg, space
 
     def run(batch):
-        cg, space = make()
+        cg, space = make("auto" if batch else "never")
         np.random.seed(5)
         space.seed(6)
         sh = SuccessiveHalving(0, [stage, stage // 3, stage // 9, 3, 1], [1.0, 3.0, 9.0, 27.0, 81.0], cg.get_config,
@@ -601,11 +601,14 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
                 res[batch] = (t, c)
     return {"workload": "sh_stage_%d_get_next_run_d32_obs%d%s" % (stage, n_obs, "_interleaved" if interleaved else ""),
             "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
+            "sequential_is": "speculative='never': one draw + acquisition per call, nothing computed ahead",
             "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],
             "note": ("SuccessiveHalving.get_next_run x %d, each followed by its result (new_result + refit); "
-                     "batched = speculative batching on" % stage) if interleaved else
+                     "batched = the default drop-in: each call's acquisition launched ahead by the refit before "
+                     "it" % stage) if interleaved else
                     ("SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
-                     "batched = speculative batches of 1, 2, 4, ... (hbx_kde_acquire_batch)" % stage)}
+                     "batched = the default drop-in: speculative batches of 1, 2, 4, ... (hbx_kde_acquire_batch), "
+                     "the first call computed ahead" % stage)}
 
 
 def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):

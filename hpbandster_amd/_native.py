@@ -23,6 +23,7 @@ SIGNATURES = {
     "hbx_last_error": (ctypes.c_char_p, []),
     "hbx_version": (ctypes.c_char_p, []),
     "hbx_kde_param_bytes": (c_i64, []),
+    "hbx_kde_param_bw_offset": (c_i64, []),
     "hbx_kde_est_bytes": (c_i64, []),
     "hbx_acq_result_bytes": (c_i64, []),
     "hbx_max_dims": (c_i32, []),
@@ -51,6 +52,8 @@ SIGNATURES = {
                                  c_i64]),
     "hbx_kde_acquire_bound": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_pair_free": (None, [c_vp]),
+    "hbx_kde_acquire_ahead": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp]),
+    "hbx_wait_word": (c_i32, [c_vp, c_i32, c_vp]),
     "hbx_kde_batch_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "hbx_kde_acquire_batch": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i64,
                                       c_vp, c_vp, c_vp, c_vp, c_i32,

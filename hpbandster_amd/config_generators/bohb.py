@@ -16,13 +16,14 @@ reference's order), so a seeded run proposes the same configurations.  What move
 """
 
 import ctypes
+import threading
 import traceback
 
 import numpy as np
 import scipy.stats as sps
 
 from .. import _native
-from ..kde import ObservationStore
+from ..kde import AcqResult, ObservationStore, RESULT_BYTES
 from .base import base_config_generator
 from ._cs import ConfigSpace
 
@@ -105,6 +106,21 @@ class SpeculativeBatch(object):
         return j == len(self.entries) and self._valid_at(j) and self.mt.snap() == self.states[j]
 
 
+# layout of a pick published by hbx_kde_acquire_ahead (include/hbx.h HBX_PICK_*)
+PICK_ERR, PICK_DONE, PICK_ROW = 48, 52, 64
+
+
+class _Ahead(object):
+    """One get_config call's acquisition enqueued before the call (BOHB._launch_ahead): the model it was
+    drawn from, the sampler counter it starts at, the model version, the completion word's value, the
+    device tensors it uses, its mapped output buffer and what launched it ('get_config' / 'new_result')."""
+    __slots__ = ("pair", "counter", "version", "seq", "keep", "buf", "source", "calls")
+
+    def __init__(self, pair, counter, version, seq, keep, buf, source, calls):
+        self.pair, self.counter, self.version, self.seq = pair, counter, version, seq
+        self.keep, self.buf, self.source, self.calls = keep, buf, source, calls
+
+
 class BOHB(base_config_generator):
     def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
                  random_fraction=1 / 3, bandwidth_factor=3, device=None, sampler="host", sampler_seed=None,
@@ -164,6 +180,21 @@ class BOHB(base_config_generator):
         self.kde_models = dict()
         self._stores = dict()  # budget -> ObservationStore: the budget's rows resident in HBM
         self._model_version = 0  # bumped whenever kde_models changes (speculative batches check it)
+        # the next get_config's acquisition computed ahead (GPU sampler: its candidates depend only on the
+        # model and the sampler's counter, not on the global RNG) -- launched after a refit or a served
+        # call, served when the call finds the same model and counter.  A source whose last one went unused
+        # (a result arrived first, a batch took over, a burst of results) pauses until the pattern it serves
+        # shows up again: a call right after a call (no refit between) for 'get_config', a call after a
+        # result for 'new_result'
+        self._ahead = None
+        self._ahead_lock = threading.Lock()
+        self._ahead_on = {"get_config": True, "new_result": True}
+        self._last_call_version = None
+        self._ahead_stats = {"launched": 0, "served": 0, "dropped": 0}
+        self._calls = 0  # get_config calls so far
+        self._pick_free = []     # mapped output buffers ready for reuse
+        self._pick_pending = []  # (buffer, seq, tensors) of dropped ones the device may still write
+        self._pick_seq = 0
 
     # -- candidates ---------------------------------------------------------------------------
     def sample_candidates(self, kde_good, num_samples, rng=None):
@@ -201,6 +232,9 @@ class BOHB(base_config_generator):
     def get_config(self, budget):
         sample = None
         info_dict = {}
+        self._calls += 1
+        if self._last_call_version is not None:  # the pattern since the previous call re-enables its source
+            self._ahead_on["get_config" if self._last_call_version == self._model_version else "new_result"] = True
         if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
             sample = self.configspace.sample_configuration().get_dictionary()
             info_dict['model_based_pick'] = False
@@ -209,19 +243,28 @@ class BOHB(base_config_generator):
             try:
                 budget = max(self.kde_models.keys())  # always the largest-budget model (bohb.py:124)
                 pair = self.kde_models[budget]        # immutable snapshot (new_result swaps entries)
-                cands, err = self.draw_candidates(pair, self.num_samples)
-                res = pair.acquire(cands)
-                if err is not None and bool(err.any()):
-                    raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
+                a = self._take_ahead(pair) if self._ahead is not None else None
+                if a is not None:  # this call's draws and acquisition, computed ahead on the same counter
+                    res, bad, best_vector = self._serve_ahead(a)
+                    self._sample_counter += self.num_samples
+                    if bad:
+                        raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
+                else:
+                    cands, err = self.draw_candidates(pair, self.num_samples)
+                    res = pair.acquire(cands)
+                    if err is not None and bool(err.any()):
+                        raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
+                    best_vector = None
                 if res.index < 0:
                     self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
                                       % self.num_samples)
                     sample = self.configspace.sample_configuration().get_dictionary()
                     info_dict['model_based_pick'] = False
                 else:
-                    best_vector = cands[res.index]
-                    if err is not None:
-                        best_vector = best_vector.cpu().numpy()
+                    if best_vector is None:
+                        best_vector = cands[res.index]
+                        if err is not None:
+                            best_vector = best_vector.cpu().numpy()
                     self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
                     sample = ConfigSpace.Configuration(self.configspace, vector=best_vector).get_dictionary()
                     info_dict['model_based_pick'] = True
@@ -232,7 +275,134 @@ class BOHB(base_config_generator):
                                     % (self.num_samples, traceback.format_exc()))
                 sample = self.configspace.sample_configuration().get_dictionary()
                 info_dict['model_based_pick'] = False
+        self._last_call_version = self._model_version
+        self._launch_ahead("get_config")
         return sample, info_dict
+
+    # -- the next call computed ahead (GPU sampler) ----------------------------------------------
+    def _ahead_enabled(self):
+        return self.sampler == "gpu" and self.speculative != "never"
+
+    def _launch_ahead(self, source):
+        """Enqueue the next get_config call's draws and acquisition (hbx_kde_acquire_ahead, no wait) on the
+        current model and sampler counter, unless that one is in flight already."""
+        if not self._ahead_enabled() or not self.kde_models:
+            return
+        import torch
+        if self.random_fraction > 0 and self._next_call_is_random():
+            return
+        with self._ahead_lock:
+            if not self._ahead_on[source]:
+                return
+            pair = self.kde_models[max(self.kde_models.keys())]
+            counter, version = self._sample_counter, self._model_version
+            a = self._ahead
+            if a is not None:
+                if a.pair is pair and a.counter == counter and a.version == version:
+                    return
+                self._drop_ahead(a)
+            if not getattr(pair, "_bound", None):
+                return
+            buf, keep = self._pick_buffer(pair)
+            self._pick_seq = self._pick_seq % 0x7FFFFFFF + 1
+            cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
+                                                counter, out=keep[:3])
+            pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
+            self._ahead = _Ahead(pair, counter, version, self._pick_seq, keep, buf, source, self._calls)
+            self._ahead_stats["launched"] += 1
+
+    def _next_call_is_random(self):
+        """A hint only: the next get_config's first draw (bohb.py:124, np.random.rand() < random_fraction)
+        read from a private copy of the global RNG as it stands -- a random pick would not use an
+        acquisition computed ahead.  Another draw before that call makes the hint wrong, never a result."""
+        g = _global_mt()
+        if g is None:
+            return False
+        pm = getattr(self, "_peek_mt", None)
+        if pm is None:
+            pm = self._peek_mt = _MT(np.random.RandomState())
+        pm.load(g.snap())
+        return pm.rs.rand() < self.random_fraction
+
+    def _drop_ahead(self, a):  # under the lock
+        """An unused one: wasted if nothing could have served it -- launched by a call (the next was a batch
+        or followed a result), or by a refit with no call since (a burst of results); a refit's that met
+        only random picks (bohb.py:124's random_fraction) was just not needed."""
+        self._ahead = None
+        self._pick_pending.append((a.buf, a.seq, a.keep))
+        if a.source == "get_config" or self._calls == a.calls:
+            self._ahead_on[a.source] = False
+        self._ahead_stats["dropped"] += 1
+
+    def _pick_buffer(self, pair):  # under the lock
+        """A mapped output buffer and device tensors (candidates, datum, error flags, workspace) for one
+        computed-ahead call: reused once the device is done with them (a served call, or a dropped one whose
+        completion word has landed) -- no allocation per call."""
+        import torch
+        still = []
+        for buf, seq, keep in self._pick_pending:  # the device has finished with a dropped one
+            if ctypes.c_int32.from_address(buf + PICK_DONE).value == seq:
+                self._pick_free.append((buf, keep))
+            else:
+                still.append((buf, seq, keep))
+        self._pick_pending = still
+        wsb = pair.workspace_bytes(self.num_samples)
+        dev = pair.good.device
+        if self._pick_free:
+            buf, keep = self._pick_free.pop()
+        else:
+            p = ctypes.c_void_p()
+            _native.check(_native.lib().hbx_host_alloc(PICK_ROW + 8 * len(self.vartypes), ctypes.addressof(p)))
+            buf, keep = p.value, None
+        if keep is None or keep[3].numel() < wsb or keep[0].device != torch.device(dev):
+            n, D = self.num_samples, len(self.vartypes)
+            keep = (torch.empty((n, D), dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
+                    torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(wsb, dtype=torch.uint8, device=dev))
+        ctypes.c_int32.from_address(buf + PICK_DONE).value = 0
+        return buf, keep
+
+    def _take_ahead(self, pair):
+        """The computed-ahead acquisition when it is exactly this call's (same model, version and counter)."""
+        with self._ahead_lock:
+            a = self._ahead
+            if a is None:
+                return None
+            if a.pair is pair and a.counter == self._sample_counter and a.version == self._model_version:
+                self._ahead = None
+                return a
+            self._drop_ahead(a)
+            return None
+
+    def _serve_ahead(self, a):
+        """(record, any domain error, winning row) of a computed-ahead acquisition, once the device is done."""
+        L = _native.lib()
+        _native.check(L.hbx_wait_word(a.buf + PICK_DONE, a.seq, _native.stream_handle(None, a.pair.good.device)))
+        res = AcqResult.from_bytes(ctypes.string_at(a.buf, RESULT_BYTES))
+        bad = ctypes.c_int32.from_address(a.buf + PICK_ERR).value != 0
+        row = None
+        if res.index >= 0:
+            row = np.frombuffer(ctypes.string_at(a.buf + PICK_ROW, 8 * len(self.vartypes)), dtype=np.float64).copy()
+        with self._ahead_lock:
+            self._pick_free.append((a.buf, a.keep))
+            self._ahead_on[a.source] = True
+            self._ahead_stats["served"] += 1
+        return res, bad, row
+
+    def __del__(self):
+        bufs = [b for b, _ in getattr(self, "_pick_free", [])] + [b for b, _, _ in getattr(self, "_pick_pending", [])]
+        a = getattr(self, "_ahead", None)
+        if a is not None:
+            bufs.append(a.buf)
+        if not bufs:
+            return
+        try:
+            import torch
+            torch.cuda.synchronize(self.device)  # nothing may still write them
+            L = _native.lib()
+            for b in bufs:
+                L.hbx_host_free(ctypes.c_void_p(b))
+        except Exception:
+            pass
 
     # -- several get_config calls in one GPU pass (SURVEY 8f row 1) ----------------------------
     def speculation_enabled(self):
@@ -396,6 +566,7 @@ class BOHB(base_config_generator):
             return
         self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
         self._model_version += 1
+        self._launch_ahead("new_result")
         self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
                           'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,
                                                        np.min(store.losses_host)))

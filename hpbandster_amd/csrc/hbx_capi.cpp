@@ -1,4 +1,5 @@
 // hbx_capi.cpp -- error plumbing and introspection entry points of libhbx.so (see include/hbx.h).
+#include <cstddef>
 #include <stdarg.h>
 #include <stdio.h>
 
@@ -21,6 +22,7 @@ const char* hbx_last_error(void) { return g_err; }
 const char* hbx_version(void) { return "hbx 0.1.0 gfx950"; }
 
 int64_t hbx_kde_param_bytes(void) { return (int64_t)HBX_PARAM_BYTES; }
+int64_t hbx_kde_param_bw_offset(void) { return (int64_t)offsetof(KdeParams, bw); }
 
 int64_t hbx_kde_est_bytes(void) { return (int64_t)sizeof(KdeEst); }
 

@@ -2483,6 +2483,49 @@ int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int6
 
 void hbx_kde_pair_free(void* pair) { delete (KdePairBinding*)pair; }
 
+// One get_config's pick to device-mapped host memory, with no host wait: the acquisition's record, whether
+// any of its candidates hit a sampler domain error (bohb.py:163-166's exception path), and the winning
+// candidate's row -- then the completion word.  One wave.  Layout of `out` (HBX_PICK_* in include/hbx.h).
+__global__ __launch_bounds__(64) void pick_publish_kernel(const AcqResult* __restrict__ rec,
+                                                          const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                          const uint8_t* __restrict__ err, char* out, int32_t seq) {
+  const int lane = threadIdx.x;
+  bool e = false;
+  if (err)
+    for (int64_t i = lane; i < Nc; i += 64) e = e || err[i] != 0;
+  const bool any = __any(e);
+  const int64_t idx = rec->index;  // relative to the candidate set (index_base 0)
+  uint32_t* o = (uint32_t*)out;
+  if (lane < (int)(sizeof(AcqResult) / 4)) hbx_publish_store(o + lane, ((const uint32_t*)rec)[lane]);
+  if (lane == 0) hbx_publish_store(o + HBX_PICK_ERR / 4, any ? 1u : 0u);
+  if (idx >= 0 && idx < Nc)
+    for (int w = lane; w < 2 * D; w += 64)
+      hbx_publish_store(o + HBX_PICK_ROW / 4 + w, ((const uint32_t*)(cand + idx * D))[w]);
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's words acknowledged (one wave)
+  if (lane == 0) hbx_publish_done((int32_t*)(out + HBX_PICK_DONE), seq);
+}
+
+int hbx_kde_acquire_ahead(const void* pair, const double* cand, int64_t Nc, void* workspace, int64_t ws_bytes,
+                          const uint8_t* err, void* out, int32_t seq, void* stream) {
+  if (!pair || !out || Nc < 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_ahead: bad arguments");
+  const KdePairBinding& b = *(const KdePairBinding*)pair;
+  int rc = acquire_impl("hbx_kde_acquire_ahead", cand, Nc, Nc > 0 ? Nc : 1, b.D, 0, b.params_good, b.table_good,
+                        b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad,
+                        b.variant_bad, b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes,
+                        nullptr, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(pick_publish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const AcqResult*)((char*)workspace + ws_layout(0, 0).res), cand, Nc, b.D, err, (char*)out,
+                     seq);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
+int hbx_wait_word(const void* word, int32_t seq, void* stream) {
+  if (!word) return hbx_fail(HBX_ERR_ARG, "hbx_wait_word: null word");
+  return wait_done((int32_t*)word, seq, (hipStream_t)stream, "hbx_wait_word");
+}
+
 // numpy's float64 exp (hbx_npexp.h) element-wise: the known-answer check of the exact re-score's exp
 __global__ void np_exp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;

@@ -204,28 +204,29 @@ class DeviceKDE(object):
                                         sb, N.stream_handle(stream, self.device)))
             return np.squeeze(out.cpu().numpy())
 
-    def sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id=0, stream=None, table=None):
+    def sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id=0, stream=None, table=None, out=None):
         """BOHB's candidate rule around this (good) KDE's observations, on the GPU (bohb.py:133-147).
 
         ``levels``: per dim 0 (continuous) or the number of choices.  Candidate i draws from the
         Philox stream (seed, counter_base + i, stream_id).  Returns (cands [Nc, D] f64, datum [Nc] i64,
-        domain_err [Nc] u8) device tensors."""
+        domain_err [Nc] u8) device tensors (``out``: those three tensors to fill instead of new ones)."""
         with N.on_device(self.device, stream):
-            return self._sample(levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table)
+            return self._sample(levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table, out)
 
-    def _sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table):
+    def _sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id, stream, table, out=None):
         torch = _torch()
         L = N.lib()
         D = self.k_vars
         sh = N.stream_handle(stream, self.device)
-        if getattr(self, "_bw_dev", None) is None:
-            self._bw_dev = torch.from_numpy(np.ascontiguousarray(self.bw, dtype=np.float64)).to(self.device)
+        # the bandwidths the sampler reads: the prepared parameter block's own fp64 bw[D] (bit-identical
+        # to self.bw, which was read back from it) -- no upload per refit
+        bw_ptr = N.ptr(self.params) + int(L.hbx_kde_param_bw_offset())
         lv = np.ascontiguousarray(np.asarray(levels, dtype=np.int32))
         if lv.shape != (D,):
             raise N.HbxError("levels must have %d entries" % D)
         key = lv.tobytes()
         if getattr(self, "_lv_key", None) != key:
-            self._lv_dev, self._lv_key = torch.from_numpy(lv).to(self.device), key
+            self._lv_dev, self._lv_key = _levels_on_device(key, lv, self.device), key
             self._tab = None
         Nc = int(Nc)
         if table is None:
@@ -236,12 +237,17 @@ class DeviceKDE(object):
                 self._tab = torch.empty(int(L.hbx_kde_sample_table_bytes(self.nobs, D)) // 8, dtype=torch.float64,
                                         device=self.device)
                 N.check(L.hbx_kde_sample_table(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs,
-                                               N.ptr(self._bw_dev), N.ptr(self._lv_dev), N.ptr(self._tab), sh))
+                                               bw_ptr, N.ptr(self._lv_dev), N.ptr(self._tab), sh))
             tab = self._tab
-        cands = torch.empty((Nc, D), dtype=torch.float64, device=self.device)
-        datum = torch.empty(Nc, dtype=torch.int64, device=self.device)
-        err = torch.empty(Nc, dtype=torch.uint8, device=self.device)
-        N.check(L.hbx_kde_sample(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs, N.ptr(self._bw_dev),
+        if out is not None:
+            cands, datum, err = out
+            if tuple(cands.shape) != (Nc, D) or datum.numel() < Nc or err.numel() < Nc:
+                raise N.HbxError("sample: output tensors of the wrong size")
+        else:
+            cands = torch.empty((Nc, D), dtype=torch.float64, device=self.device)
+            datum = torch.empty(Nc, dtype=torch.int64, device=self.device)
+            err = torch.empty(Nc, dtype=torch.uint8, device=self.device)
+        N.check(L.hbx_kde_sample(N.ptr(self.X_dev), D, N.ptr(self.rows_dev), self.nobs, bw_ptr,
                                  N.ptr(self._lv_dev), N.ptr(tab), float(bw_factor), int(seed) & (2 ** 64 - 1),
                                  int(counter_base) & (2 ** 64 - 1), int(stream_id) & 0xFFFFFFFF, Nc, N.ptr(cands),
                                  N.ptr(datum), N.ptr(err), sh))
@@ -299,6 +305,16 @@ class DeviceKDE(object):
                                      N.stream_handle(stream, self.device)))
             e = est.cpu().numpy()
         return e[:, 0], e[:, 1], e[:, 2]
+
+
+_LEVELS = {}  # (device, level bytes) -> the level counts on the device (one upload per space and device)
+
+
+def _levels_on_device(key, lv, device):
+    t = _LEVELS.get((str(device), key))
+    if t is None:
+        t = _LEVELS[(str(device), key)] = _torch().from_numpy(lv.copy()).to(device)
+    return t
 
 
 class KDEPair(object):
@@ -507,6 +523,20 @@ class KDEPair(object):
             if pick is not None:
                 r.index, r.score, r.pdf_l, r.pdf_g = pick[0] - b * seg, pick[1], pick[2], pick[3]
             r.flags |= ACQ_RESOLVED
+
+    def acquire_ahead(self, cands, err, workspace, out, seq):
+        """Enqueue the acquisition of ``cands`` (a device [Nc, D] f64 tensor) without waiting: the device
+        stores into ``out`` (device-mapped host memory, hbx_host_alloc) the record, the domain-error flag
+        of ``err`` (the sampler's per-candidate flags, or None) and the winning row, then the completion
+        word ``seq`` (include/hbx.h hbx_kde_acquire_ahead).  The tensors and ``out`` stay in use until the
+        word is seen."""
+        if not self._bound:
+            raise N.HbxError("acquire_ahead needs the bound pair entry")
+        with N.on_device(self.good.device):
+            N.check(N.lib().hbx_kde_acquire_ahead(self._bound, cands.data_ptr(), int(cands.shape[0]),
+                                                  workspace.data_ptr(), workspace.numel(),
+                                                  err.data_ptr() if err is not None else None, out, int(seq),
+                                                  N.stream_handle(None, self.good.device)))
 
     def batch_workspace_bytes(self, Nc, seg):
         return int(N.lib().hbx_kde_batch_workspace_bytes(int(Nc), int(seg), self.nmax))

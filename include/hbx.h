@@ -43,6 +43,7 @@ extern "C" {
 const char* hbx_last_error(void);
 const char* hbx_version(void);
 int64_t hbx_kde_param_bytes(void);     /* bytes of one prepared KDE parameter block (device) */
+int64_t hbx_kde_param_bw_offset(void); /* byte offset of the KDE's fp64 bandwidths bw[D] in that block */
 int64_t hbx_kde_est_bytes(void);       /* bytes per candidate of hbx_kde_logpdf output */
 int64_t hbx_acq_result_bytes(void);    /* bytes of the acquisition result record */
 int32_t hbx_max_dims(void);            /* largest D accepted */
@@ -175,6 +176,23 @@ void* hbx_kde_pair_bind(int32_t D, const void* params_good, const float* table_g
 int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int64_t index_base, void* workspace,
                           int64_t ws_bytes, void* stream, void* rec_out);
 void hbx_kde_pair_free(void* pair);
+
+/* One get_config's acquisition enqueued AHEAD of the call (bohb.py:124-169 computed before it is asked for:
+ * BOHB launches the next call's acquisition right after a refit or a served call, and serves it only if the
+ * model and the sampler's counter are unchanged when the call comes).  Returns once enqueued on `stream`;
+ * the device then stores into `out` (device-mapped host memory, hbx_host_alloc, >= HBX_PICK_ROW + 8 D
+ * bytes): the 48-byte record (index relative to the candidate set), at HBX_PICK_ERR an int32 = 1 when any
+ * err[0 .. Nc) byte is set (err nullable: the GPU sampler's domain-error flags), the winning row's D
+ * doubles at HBX_PICK_ROW, and last the completion word `seq` at HBX_PICK_DONE.  The workspace, the
+ * candidates and `out` stay in use until that word is seen (hbx_wait_word). */
+#define HBX_PICK_ERR 48
+#define HBX_PICK_DONE 52
+#define HBX_PICK_ROW 64
+int hbx_kde_acquire_ahead(const void* pair, const double* cand, int64_t Nc, void* workspace, int64_t ws_bytes,
+                          const uint8_t* err, void* out, int32_t seq, void* stream);
+/* Spin until the int32 at `word` (device-mapped host memory) equals seq; bounded, then `stream` is
+ * synchronised and the word checked once more (error if it still differs). */
+int hbx_wait_word(const void* word, int32_t seq, void* stream);
 
 /* Batched acquisition: B = ceil(Nc / seg) independent get_config calls against the same model in one
  * pass (replaces B sequential runs of the bohb.py:124-169 loop, as an SH stage issues

@@ -307,3 +307,75 @@ def test_threaded_worker_draws_are_never_duplicated(device):
         t.join()
     assert len(vals) > 100
     assert len(set(vals)) == len(vals)
+
+
+def test_computed_ahead_calls_equal_sequential(device):
+    """The next get_config computed ahead (GPU sampler: launched after a refit or a served call, served when
+    the model, its version and the sampler counter are unchanged) proposes exactly what the call computed
+    on the spot proposes (speculative='never'), in every interleaving: back-to-back calls, one result before
+    each call, bursts of results, a batch in between -- with the global RNG and the counter left in the same
+    place; the computed-ahead path serves most model-based calls."""
+    def drive(spec):
+        cg, space = _fitted_bohb(device, 21, sampler="gpu", sampler_seed=9, speculative=spec)
+        np.random.seed(3)
+        space.seed(4)
+        out, k = [], 0
+        def result(cfg):
+            nonlocal k
+            cg.new_result(_job((1, 0, k), cfg, 1.0, np.random.RandomState(100 + k).rand()))
+            k += 1
+        for _ in range(8):  # back to back
+            out.append(cg.get_config(1.0))
+        for _ in range(8):  # one result before each call (one worker)
+            result(out[-1][0])
+            out.append(cg.get_config(1.0))
+        for _ in range(4):  # bursts
+            result(out[-1][0])
+            result(out[-2][0])
+            out.append(cg.get_config(1.0))
+        if spec != "never":
+            out.extend(cg.get_config_batch(1.0, 5))
+        else:
+            out.extend(cg.get_config(1.0) for _ in range(5))
+        for _ in range(6):
+            out.append(cg.get_config(1.0))
+        return out, np.random.get_state(), cg._sample_counter, cg._ahead_stats
+    ref, st_ref, c_ref, _ = drive("never")
+    got, st_got, c_got, stats = drive("auto")
+    assert sum(i["model_based_pick"] for _, i in ref) >= 12
+    assert [(c, i) for c, i in ref] == [(c, i) for c, i in got]
+    np.testing.assert_array_equal(st_ref[1], st_got[1])
+    assert st_ref[2] == st_got[2] and c_ref == c_got
+    assert stats["served"] >= 10, stats
+
+
+def test_computed_ahead_with_results_from_another_thread(device):
+    """new_result on a dispatcher thread while the main thread calls get_config (the drop-in's threading):
+    every model-based pick is the acquisition of the model the call saw -- re-scored here on the same
+    candidates -- and no call fails."""
+    import threading
+    from hpbandster_amd import configspace as CS
+    cg, space = _fitted_bohb(device, 23, sampler="gpu", sampler_seed=11, speculative="auto")
+    stop = threading.Event()
+    errs = []
+
+    def worker():
+        k = 0
+        try:
+            while not stop.is_set():
+                cfg = space.sample_configuration().get_dictionary()
+                cg.new_result(_job((2, 0, k), cfg, 1.0, np.random.RandomState(k).rand()))
+                k += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+    t = threading.Thread(target=worker)
+    t.start()
+    try:
+        picks = [cg.get_config(1.0) for _ in range(60)]
+    finally:
+        stop.set()
+        t.join()
+    assert not errs
+    assert sum(i["model_based_pick"] for _, i in picks) >= 20
+    for c, _ in picks:
+        CS.Configuration(space, c)  # a valid configuration of the space
