@@ -249,6 +249,15 @@ class BOHB(base_config_generator):
                     self._sample_counter += self.num_samples
                     if bad:
                         raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
+                elif self.sampler == "gpu" and getattr(pair, "_bound", None):
+                    # on the spot, one wait: the draws, the acquisition, the error flag and the winning row
+                    # published together (no separate device reduction and row copy)
+                    with self._ahead_lock:
+                        a = self._enqueue_pick(pair, self._sample_counter, self._model_version, None)
+                    res, bad, best_vector = self._serve_ahead(a)
+                    self._sample_counter += self.num_samples
+                    if bad:
+                        raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
                 else:
                     cands, err = self.draw_candidates(pair, self.num_samples)
                     res = pair.acquire(cands)
@@ -303,13 +312,17 @@ class BOHB(base_config_generator):
                 self._drop_ahead(a)
             if not getattr(pair, "_bound", None):
                 return
-            buf, keep = self._pick_buffer(pair)
-            self._pick_seq = self._pick_seq % 0x7FFFFFFF + 1
-            cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
-                                                counter, out=keep[:3])
-            pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
-            self._ahead = _Ahead(pair, counter, version, self._pick_seq, keep, buf, source, self._calls)
+            self._ahead = self._enqueue_pick(pair, counter, version, source)
             self._ahead_stats["launched"] += 1
+
+    def _enqueue_pick(self, pair, counter, version, source):  # under the lock
+        """One call's draws on `counter` and its acquisition, published to a pooled mapped buffer."""
+        buf, keep = self._pick_buffer(pair)
+        self._pick_seq = self._pick_seq % 0x7FFFFFFF + 1
+        cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
+                                            counter, out=keep[:3])
+        pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
+        return _Ahead(pair, counter, version, self._pick_seq, keep, buf, source, self._calls)
 
     def _next_call_is_random(self):
         """A hint only: the next get_config's first draw (bohb.py:124, np.random.rand() < random_fraction)
@@ -384,8 +397,9 @@ class BOHB(base_config_generator):
             row = np.frombuffer(ctypes.string_at(a.buf + PICK_ROW, 8 * len(self.vartypes)), dtype=np.float64).copy()
         with self._ahead_lock:
             self._pick_free.append((a.buf, a.keep))
-            self._ahead_on[a.source] = True
-            self._ahead_stats["served"] += 1
+            if a.source is not None:  # computed ahead (None: the call's own)
+                self._ahead_on[a.source] = True
+                self._ahead_stats["served"] += 1
         return res, bad, row
 
     def __del__(self):
