@@ -16,6 +16,7 @@ reference's order), so a seeded run proposes the same configurations.  What move
 """
 
 import ctypes
+import logging
 import threading
 import traceback
 
@@ -274,7 +275,8 @@ class BOHB(base_config_generator):
                         best_vector = cands[res.index]
                         if err is not None:
                             best_vector = best_vector.cpu().numpy()
-                    self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
+                    if self.logger.isEnabledFor(logging.DEBUG):  # (formatting the vector costs ~0.1 ms)
+                        self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
                     sample = ConfigSpace.Configuration(self.configspace, vector=best_vector).get_dictionary()
                     info_dict['model_based_pick'] = True
             except _native.HbxError:
@@ -541,7 +543,8 @@ class BOHB(base_config_generator):
         """One get_config result from a batch entry (the logging and random draws of bohb.py:124-169 happen
         here, when the result is handed out)."""
         if e[0] == "model":
-            self.logger.debug('best_vector: {}, {}'.format(e[1], e[2]))
+            if self.logger.isEnabledFor(logging.DEBUG):
+                self.logger.debug('best_vector: {}, {}'.format(e[1], e[2]))
             return (ConfigSpace.Configuration(self.configspace, vector=e[1]).get_dictionary(),
                     {'model_based_pick': True})
         if e[1] == "warning":
@@ -581,6 +584,7 @@ class BOHB(base_config_generator):
         self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
         self._model_version += 1
         self._launch_ahead("new_result")
-        self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
-                          'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,
-                                                       np.min(store.losses_host)))
+        if self.logger.isEnabledFor(logging.DEBUG):
+            self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
+                              'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,
+                                                           np.min(store.losses_host)))
