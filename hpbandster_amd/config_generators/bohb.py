@@ -321,10 +321,38 @@ class BOHB(base_config_generator):
         """One call's draws on `counter` and its acquisition, published to a pooled mapped buffer."""
         buf, keep = self._pick_buffer(pair)
         self._pick_seq = self._pick_seq % 0x7FFFFFFF + 1
-        cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
-                                            counter, out=keep[:3])
-        pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
+        if not self._enqueue_pick_direct(pair, counter, keep, buf):
+            cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
+                                                counter, out=keep[:3])
+            pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
         return _Ahead(pair, counter, version, self._pick_seq, keep, buf, source, self._calls)
+
+    def _enqueue_pick_direct(self, pair, counter, keep, buf):
+        """The same two native calls (hbx_kde_sample, hbx_kde_acquire_ahead) without the wrappers' device
+        switch and argument checks, when they are not needed: the calling thread's current device is the
+        model's and the draw needs no Phi table.  False: take the wrapped path."""
+        g = pair.good
+        n = self.num_samples
+        if (pair._cur_dev is None or pair._raw_stream is None or pair._cur_dev() != pair._dev_index
+                or n >= 4 * g.nobs or not pair._bound):
+            return False
+        from ..kde import _levels_on_device
+        L = _native.lib()
+        lvb = getattr(self, "_lv_bytes", None)
+        if lvb is None:
+            self._lv_np = np.ascontiguousarray(self.vartypes, dtype=np.int32)
+            lvb = self._lv_bytes = self._lv_np.tobytes()
+            self._bw_off = int(L.hbx_kde_param_bw_offset())
+        lvd = _levels_on_device(lvb, self._lv_np, g.device)
+        cands, datum, err, ws = keep
+        sh = pair._raw_stream(pair._dev_index)
+        _native.check(L.hbx_kde_sample(g.X_dev.data_ptr(), g.k_vars, g.rows_dev.data_ptr(), g.nobs,
+                                       g.params.data_ptr() + self._bw_off, lvd.data_ptr(), None, float(self.bw_factor),
+                                       int(self.sampler_seed) & (2 ** 64 - 1), int(counter) & (2 ** 64 - 1), 0, n,
+                                       cands.data_ptr(), datum.data_ptr(), err.data_ptr(), sh))
+        _native.check(L.hbx_kde_acquire_ahead(pair._bound, cands.data_ptr(), n, ws.data_ptr(), ws.numel(),
+                                              err.data_ptr(), buf, self._pick_seq, sh))
+        return True
 
     def _next_call_is_random(self):
         """A hint only: the next get_config's first draw (bohb.py:124, np.random.rand() < random_fraction)

@@ -1257,6 +1257,16 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
   return s < INFINITY && s <= best * (1.0 + 1.0001 * (rp + rb));
 }
 
+// A get_config pick published to device-mapped host memory by the final argmin (hbx_kde_acquire_ahead):
+// the record, whether any of the call's candidates hit a sampler domain error, the winning row
+struct PickOut {
+  const double* cand;
+  const uint8_t* err;  // nullable
+  int64_t Nc;
+  int32_t D;
+  char* out;  // null: no pick
+};
+
 // the final argmin of one acquisition (256 threads): the split re-score's unit sums -> pdfs, strict '<'
 // first-index argmin over the shortlist, the near set, the result record
 __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* __restrict__ count,
@@ -1266,14 +1276,21 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
                                const KdeEst* __restrict__ el, const KdeEst* __restrict__ eg,
                                int32_t* __restrict__ near_list, AcqResult* __restrict__ res, int32_t nbuf,
                                const double* part, double* exact_lw, double* exact_gw, AcqResult* host_res,
-                               int32_t* done, int32_t seq) {
+                               int32_t* done, int32_t seq, PickOut pick = PickOut{}) {
   __shared__ double bs[256];
+  __shared__ AcqResult rec_sh;
   __shared__ int64_t bi[256];
   __shared__ int32_t bp[256];
   __shared__ double exl[256], exg[256];  // the exact pdfs of a shortlist of <= 256 (no global re-read)
   __shared__ double rb_sh;
   __shared__ int32_t nnear;
   const int cnt = *count;
+  int err_any = 0;
+  if (pick.out && pick.err) {  // uniform
+    bool e = false;
+    for (int64_t i = threadIdx.x; i < pick.Nc; i += 256) e = e || pick.err[i] != 0;
+    err_any = __syncthreads_or(e);
+  }
   // shortlists of <= 256 (the common case): thread p owns candidate p -- its index and bound are loaded
   // first, beside the unit sums' combination, and its pdfs come back through LDS
   const bool small = cnt <= 256;
@@ -1373,14 +1390,23 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
       r.pdf_g = small ? exg[wp] : exact_g[wp];
     }
     *res = r;
-    if (host_res) {  // hbx_kde_acquire_host: the record to mapped host memory, then the completion word
-      static_assert(sizeof(AcqResult) % 4 == 0, "record of whole words");
-      uint32_t w[sizeof(AcqResult) / 4];
-      __builtin_memcpy(w, &r, sizeof(AcqResult));
-#pragma unroll
-      for (int i = 0; i < (int)(sizeof(AcqResult) / 4); ++i) hbx_publish_store((uint32_t*)host_res + i, w[i]);
-      hbx_publish_done(done, seq);
+    rec_sh = r;
+  }
+  if (host_res || pick.out) {  // uniform: the record to mapped host memory, then the completion word
+    static_assert(sizeof(AcqResult) % 4 == 0, "record of whole words");
+    __syncthreads();
+    uint32_t* out = pick.out ? (uint32_t*)pick.out : (uint32_t*)host_res;
+    if (threadIdx.x < (int)(sizeof(AcqResult) / 4)) hbx_publish_store(out + threadIdx.x, ((const uint32_t*)&rec_sh)[threadIdx.x]);
+    if (pick.out) {  // hbx_kde_acquire_ahead: + the domain-error flag and the winning row
+      if (threadIdx.x == 0) hbx_publish_store(out + HBX_PICK_ERR / 4, err_any ? 1u : 0u);
+      const int64_t idx = rec_sh.index - index_base;
+      if (rec_sh.index >= 0 && idx < pick.Nc)
+        for (int w = threadIdx.x; w < 2 * pick.D; w += 256)
+          hbx_publish_store(out + HBX_PICK_ROW / 4 + w, ((const uint32_t*)(pick.cand + idx * pick.D))[w]);
     }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words acknowledged
+    __syncthreads();                                       // ... and every wave's
+    if (threadIdx.x == 0) hbx_publish_done(pick.out ? (int32_t*)(pick.out + HBX_PICK_DONE) : done, seq);
   }
 }
 
@@ -1393,9 +1419,9 @@ __global__ __launch_bounds__(256) void kde_final_kernel(const int32_t* __restric
                                                         int32_t* __restrict__ near_list, AcqResult* __restrict__ res,
                                                         int32_t nbuf, const double* __restrict__ part,
                                                         double* exact_lw, double* exact_gw, AcqResult* host_res,
-                                                        int32_t* done, int32_t seq) {
+                                                        int32_t* done, int32_t seq, PickOut pick) {
   kde_final_body(list, count, exact_l, exact_g, flags, index_base, Pg, Pb, el, eg, near_list, res, nbuf, part,
-                 exact_lw, exact_gw, host_res, done, seq);
+                 exact_lw, exact_gw, host_res, done, seq, pick);
 }
 
 // Batched argmin, three passes over the shortlist: (1) per-segment minimum of the exact score,
@@ -1894,7 +1920,8 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                         const float* table_bad, const double* X_bad, const int64_t* rows_bad, int32_t variant_bad,
                         int32_t dc_pad, int32_t du_pad, int64_t nmax, float* logl_out, float* logg_out,
                         AcqResult* batch_res, void* workspace, int64_t ws_bytes, void* events, void* stream,
-                        AcqResult* host_res = nullptr, int32_t* done = nullptr, int32_t seq = 0) {
+                        AcqResult* host_res = nullptr, int32_t* done = nullptr, int32_t seq = 0,
+                        PickOut pick = PickOut{}) {
   if ((!cand && Nc > 0) || !params_good || !table_good || !X_good || !rows_good || !params_bad || !table_bad ||
       !X_bad || !rows_bad || !workspace)
     return hbx_fail(HBX_ERR_ARG, "%s: null pointer", who);
@@ -1992,7 +2019,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     hipLaunchKernelGGL(kde_final_kernel, dim3(1), dim3(256), 0, s, list, count, exact_l, exact_g, flags,
                        index_base, (const KdeParams*)params_good, (const KdeParams*)params_bad, el, eg, near, res,
                        (int32_t)((nmax + PW_BUF - 1) / PW_BUF), fuse_combine ? part : (const double*)nullptr,
-                       exact_l, exact_g, host_res, done, seq);
+                       exact_l, exact_g, host_res, done, seq, pick);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }
@@ -2483,42 +2510,15 @@ int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int6
 
 void hbx_kde_pair_free(void* pair) { delete (KdePairBinding*)pair; }
 
-// One get_config's pick to device-mapped host memory, with no host wait: the acquisition's record, whether
-// any of its candidates hit a sampler domain error (bohb.py:163-166's exception path), and the winning
-// candidate's row -- then the completion word.  One wave.  Layout of `out` (HBX_PICK_* in include/hbx.h).
-__global__ __launch_bounds__(64) void pick_publish_kernel(const AcqResult* __restrict__ rec,
-                                                          const double* __restrict__ cand, int64_t Nc, int32_t D,
-                                                          const uint8_t* __restrict__ err, char* out, int32_t seq) {
-  const int lane = threadIdx.x;
-  bool e = false;
-  if (err)
-    for (int64_t i = lane; i < Nc; i += 64) e = e || err[i] != 0;
-  const bool any = __any(e);
-  const int64_t idx = rec->index;  // relative to the candidate set (index_base 0)
-  uint32_t* o = (uint32_t*)out;
-  if (lane < (int)(sizeof(AcqResult) / 4)) hbx_publish_store(o + lane, ((const uint32_t*)rec)[lane]);
-  if (lane == 0) hbx_publish_store(o + HBX_PICK_ERR / 4, any ? 1u : 0u);
-  if (idx >= 0 && idx < Nc)
-    for (int w = lane; w < 2 * D; w += 64)
-      hbx_publish_store(o + HBX_PICK_ROW / 4 + w, ((const uint32_t*)(cand + idx * D))[w]);
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's words acknowledged (one wave)
-  if (lane == 0) hbx_publish_done((int32_t*)(out + HBX_PICK_DONE), seq);
-}
-
 int hbx_kde_acquire_ahead(const void* pair, const double* cand, int64_t Nc, void* workspace, int64_t ws_bytes,
                           const uint8_t* err, void* out, int32_t seq, void* stream) {
   if (!pair || !out || Nc < 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_ahead: bad arguments");
   const KdePairBinding& b = *(const KdePairBinding*)pair;
-  int rc = acquire_impl("hbx_kde_acquire_ahead", cand, Nc, Nc > 0 ? Nc : 1, b.D, 0, b.params_good, b.table_good,
-                        b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad,
-                        b.variant_bad, b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes,
-                        nullptr, stream);
-  if (rc) return rc;
-  hipLaunchKernelGGL(pick_publish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                     (const AcqResult*)((char*)workspace + ws_layout(0, 0).res), cand, Nc, b.D, err, (char*)out,
-                     seq);
-  HBX_LAUNCH_CHECK();
-  return HBX_OK;
+  // the final argmin publishes the pick itself (record, error flag, winning row, completion word)
+  return acquire_impl("hbx_kde_acquire_ahead", cand, Nc, Nc > 0 ? Nc : 1, b.D, 0, b.params_good, b.table_good,
+                      b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad,
+                      b.variant_bad, b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes,
+                      nullptr, stream, nullptr, nullptr, seq, PickOut{cand, err, Nc, b.D, (char*)out});
 }
 
 int hbx_wait_word(const void* word, int32_t seq, void* stream) {
