@@ -539,7 +539,7 @@ def batched(pair, device, dc, du, levels, calls=81, per_call=64, reps=20):
             "get_config_per_s_batched": calls / res["batched"], "speedup": res["sequential"] / res["batched"]}
 
 
-def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
+def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False, sampler="gpu", dims=(24, 8)):
     """Side measurement (SURVEY 8f row 1 through the drop-in): the first stage of an eta=3 bracket -- 81
     configurations requested through SuccessiveHalving.get_next_run, as HpBandSter.run requests them --
     from BOHB (config #3's dims, 24c + 8u, GPU sampler, num_samples=64) with speculative batching (batches
@@ -564,12 +564,12 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
 
     def make(spec):
         space = CS.ConfigurationSpace(seed=3)
-        for i in range(24):
+        for i in range(dims[0]):
             space.add_hyperparameter(CS.UniformFloatHyperparameter("x%02d" % i, lower=0, upper=1))
-        for i in range(8):
+        for i in range(dims[1]):
             space.add_hyperparameter(CS.CategoricalHyperparameter("y%02d" % i, ["a", "b", "c", "d"]))
-        cg = BOHB(space, device=device, sampler="gpu", sampler_seed=77, speculative=spec)
-        X = S.make_observations(n_obs, 24, 8, 4, seed=51)
+        cg = BOHB(space, device=device, sampler=sampler, sampler_seed=77, speculative=spec)
+        X = S.make_observations(n_obs, dims[0], dims[1], 4, seed=51)
         Lo = S.make_losses(n_obs, seed=52)
         for i in range(n_obs):
             cg.new_result(job((0, 0, i), CS.Configuration(space, vector=X[i]).get_dictionary(), Lo[i]))
@@ -599,13 +599,16 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False):
             t, c = run(batch)
             if batch not in res or t < res[batch][0]:
                 res[batch] = (t, c)
-    return {"workload": "sh_stage_%d_get_next_run_d32_obs%d%s" % (stage, n_obs, "_interleaved" if interleaved else ""),
+    return {"workload": "sh_stage_%d_get_next_run_d%d_obs%d%s%s" % (stage, sum(dims), n_obs,
+                                                                  "_interleaved" if interleaved else "",
+                                                                  "_host_sampler" if sampler == "host" else ""),
             "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
             "sequential_is": "speculative='never': one draw + acquisition per call, nothing computed ahead",
             "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],
             "note": ("SuccessiveHalving.get_next_run x %d, each followed by its result (new_result + refit); "
-                     "batched = the default drop-in: each call's acquisition launched ahead by the refit before "
-                     "it" % stage) if interleaved else
+                     "batched = the default drop-in (GPU sampler: a call's acquisition launched ahead by the refit "
+                     "before it when the caller leaves time to hide it; host sampler: no speculation)" % stage)
+            if interleaved else
                     ("SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
                      "batched = the default drop-in: speculative batches of 1, 2, 4, ... (hbx_kde_acquire_batch), "
                      "the first call computed ahead" % stage)}
@@ -1072,6 +1075,11 @@ def main():
             out["sh_stage_interleaved"] = sh_stage_line(device, interleaved=True, reps=7)
         except Exception as e:
             out["sh_stage_interleaved"] = {"error": repr(e)}
+        try:  # results between requests with the default (host, scipy) sampler
+            out["sh_stage_interleaved_host_sampler"] = sh_stage_line(device, n_obs=100, stage=27, reps=3,
+                                                                     interleaved=True, sampler="host", dims=(4, 2))
+        except Exception as e:
+            out["sh_stage_interleaved_host_sampler"] = {"error": repr(e)}
         try:
             out["gpu_sampler"] = sampler_line(pair, device, a.dc, a.du, a.levels, Nc, ws)
         except Exception as e:

@@ -18,6 +18,7 @@ reference's order), so a seeded run proposes the same configurations.  What move
 import ctypes
 import logging
 import threading
+import time
 import traceback
 
 import numpy as np
@@ -191,6 +192,11 @@ class BOHB(base_config_generator):
         self._ahead_lock = threading.Lock()
         self._ahead_on = {"get_config": True, "new_result": True}
         self._last_call_version = None
+        # a refit's launch pays only when the caller leaves time before the next call to hide the device
+        # work in (HB_master: the dispatcher thread's callback, then a hand-off to the master loop): the
+        # gap from a new_result's end to the next call, smoothed; below AHEAD_MIN_GAP_S refits launch nothing
+        self._result_end = None
+        self._gap = None
         self._ahead_stats = {"launched": 0, "served": 0, "dropped": 0}
         self._calls = 0  # get_config calls so far
         self._pick_free = []     # mapped output buffers ready for reuse
@@ -236,6 +242,11 @@ class BOHB(base_config_generator):
         self._calls += 1
         if self._last_call_version is not None:  # the pattern since the previous call re-enables its source
             self._ahead_on["get_config" if self._last_call_version == self._model_version else "new_result"] = True
+        t_end = self._result_end
+        if t_end is not None:  # a result came before this call: how long after it
+            self._result_end = None
+            gap = time.perf_counter() - t_end
+            self._gap = gap if self._gap is None else 0.75 * self._gap + 0.25 * gap
         if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
             sample = self.configspace.sample_configuration().get_dictionary()
             info_dict['model_based_pick'] = False
@@ -291,15 +302,15 @@ class BOHB(base_config_generator):
         return sample, info_dict
 
     # -- the next call computed ahead (GPU sampler) ----------------------------------------------
+    AHEAD_MIN_GAP_S = 40e-6  # ~ the device time of a 64-candidate draw + acquisition
     def _ahead_enabled(self):
         return self.sampler == "gpu" and self.speculative != "never"
 
     def _launch_ahead(self, source):
         """Enqueue the next get_config call's draws and acquisition (hbx_kde_acquire_ahead, no wait) on the
         current model and sampler counter, unless that one is in flight already."""
-        if not self._ahead_enabled() or not self.kde_models:
+        if not self._ahead_enabled() or not self.kde_models or not self._ahead_on[source]:
             return
-        import torch
         if self.random_fraction > 0 and self._next_call_is_random():
             return
         with self._ahead_lock:
@@ -611,7 +622,9 @@ class BOHB(base_config_generator):
             return
         self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
         self._model_version += 1
-        self._launch_ahead("new_result")
+        if self._gap is None or self._gap >= self.AHEAD_MIN_GAP_S:
+            self._launch_ahead("new_result")
+        self._result_end = time.perf_counter()
         if self.logger.isEnabledFor(logging.DEBUG):
             self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
                               'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,

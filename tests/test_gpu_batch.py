@@ -317,6 +317,7 @@ def test_computed_ahead_calls_equal_sequential(device):
     place; the computed-ahead path serves most model-based calls."""
     def drive(spec):
         cg, space = _fitted_bohb(device, 21, sampler="gpu", sampler_seed=9, speculative=spec)
+        cg.AHEAD_MIN_GAP_S = 0.0  # launch after every refit (this loop leaves no time between result and call)
         np.random.seed(3)
         space.seed(4)
         out, k = [], 0

@@ -18,6 +18,9 @@ def main():
         elif name == "sh_stage":
             out["sh_stage"] = bench.sh_stage_line(dev)
             out["sh_stage_interleaved"] = bench.sh_stage_line(dev, interleaved=True, reps=7)
+            out["sh_stage_interleaved_host_sampler"] = bench.sh_stage_line(dev, n_obs=100, stage=27, reps=3,
+                                                                           interleaved=True, sampler="host",
+                                                                           dims=(4, 2))
         elif name == "config2":
             out["config2"] = bench.config2_line(dev)
         print(json.dumps({name: {k: v for k, v in out.items()}}), flush=True)
