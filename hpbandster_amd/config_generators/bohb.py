@@ -112,6 +112,44 @@ class SpeculativeBatch(object):
 PICK_ERR, PICK_DONE, PICK_ROW = 48, 52, 64
 
 
+class _PickBuffers(object):
+    """Device-mapped host buffers for published picks, shared by every BOHB of the process: hipHostMalloc
+    is slow (and a generator's buffers would otherwise be freed -- after a device synchronisation -- when
+    it is collected, at whatever moment the garbage collector picks).  A buffer the device may still
+    write (a dropped pick) waits in `pending` until its completion word shows its sequence number."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.free = {}     # bytes -> [buffer]
+        self.pending = []  # (buffer, seq, bytes)
+
+    def get(self, nbytes):
+        with self.lock:
+            still = []
+            for buf, seq, nb in self.pending:
+                if ctypes.c_int32.from_address(buf + PICK_DONE).value == seq:
+                    self.free.setdefault(nb, []).append(buf)
+                else:
+                    still.append((buf, seq, nb))
+            self.pending = still
+            lst = self.free.get(nbytes)
+            if lst:
+                return lst.pop()
+        p = ctypes.c_void_p()
+        _native.check(_native.lib().hbx_host_alloc(nbytes, ctypes.addressof(p)))
+        return p.value
+
+    def put(self, buf, nbytes, seq=None):
+        with self.lock:
+            if seq is None:
+                self.free.setdefault(nbytes, []).append(buf)
+            else:
+                self.pending.append((buf, seq, nbytes))
+
+
+_PICKS = _PickBuffers()
+
+
 class _Ahead(object):
     """One get_config call's acquisition enqueued before the call (BOHB._launch_ahead): the model it was
     drawn from, the sampler counter it starts at, the model version, the completion word's value, the
@@ -405,9 +443,7 @@ class BOHB(base_config_generator):
         if self._pick_free:
             buf, keep = self._pick_free.pop()
         else:
-            p = ctypes.c_void_p()
-            _native.check(_native.lib().hbx_host_alloc(PICK_ROW + 8 * len(self.vartypes), ctypes.addressof(p)))
-            buf, keep = p.value, None
+            buf, keep = _PICKS.get(PICK_ROW + 8 * len(self.vartypes)), None
         if keep is None or keep[3].numel() < wsb or keep[0].device != torch.device(dev):
             n, D = self.num_samples, len(self.vartypes)
             keep = (torch.empty((n, D), dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
@@ -443,19 +479,16 @@ class BOHB(base_config_generator):
                 self._ahead_stats["served"] += 1
         return res, bad, row
 
-    def __del__(self):
-        bufs = [b for b, _ in getattr(self, "_pick_free", [])] + [b for b, _, _ in getattr(self, "_pick_pending", [])]
-        a = getattr(self, "_ahead", None)
-        if a is not None:
-            bufs.append(a.buf)
-        if not bufs:
-            return
+    def __del__(self):  # the mapped buffers back to the process-wide pool (no synchronisation)
         try:
-            import torch
-            torch.cuda.synchronize(self.device)  # nothing may still write them
-            L = _native.lib()
-            for b in bufs:
-                L.hbx_host_free(ctypes.c_void_p(b))
+            nb = PICK_ROW + 8 * len(self.vartypes)
+            for b, _ in getattr(self, "_pick_free", []):
+                _PICKS.put(b, nb)
+            for b, seq, _ in getattr(self, "_pick_pending", []):
+                _PICKS.put(b, nb, seq)
+            a = getattr(self, "_ahead", None)
+            if a is not None:
+                _PICKS.put(a.buf, nb, a.seq)
         except Exception:
             pass
 
