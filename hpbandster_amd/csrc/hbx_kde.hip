@@ -661,10 +661,13 @@ static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s)
 template <int DCP, bool SIGNED>
 __device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                 const KdeParams* __restrict__ P, const float* __restrict__ table,
-                                                KdeEst* __restrict__ out, const unsigned blk) {
+                                                KdeEst* __restrict__ out, const unsigned blk,
+                                                const int nsplit = 1) {
   constexpr int NC = DCP > 0 ? DCP : 1;
   const int64_t i = (int64_t)blk * 256 + threadIdx.x;
-  const bool need = i < Nc && out[i].err == -1.f;
+  bool need = false;  // a marker in any observation split's partial estimate
+  if (i < Nc)
+    for (int r = 0; r < nsplit; ++r) need = need || out[(int64_t)r * Nc + i].err == -1.f;
   if (!__any(need)) return;
   if (!need) return;
   const double* x = cand + i * (int64_t)D;
@@ -723,7 +726,8 @@ __device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand,
   } else {
     mx = 0.f;
   }
-  out[i] = finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);
+  out[i] = finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);  // the whole sum in split 0
+  for (int r = 1; r < nsplit; ++r) out[(int64_t)r * Nc + i] = kde_est_neutral();
 }
 
 template <int DCP, bool SIGNED>
@@ -764,7 +768,7 @@ __global__ __launch_bounds__(256) void kde_rescue_pair_kernel(const double* __re
   for (unsigned b = blockIdx.x; b < 2 * a.nblk0; b += gridDim.x) {
     const bool second = b >= a.nblk0;
     kde_rescue_body<DCP, SIGNED>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                 second ? a.out1 : a.out0, second ? b - a.nblk0 : b);
+                                 second ? a.out1 : a.out0, second ? b - a.nblk0 : b, second ? a.nsplit1 : a.nsplit0);
   }
 }
 
@@ -812,16 +816,41 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 // Candidates whose l and g are both certainly below 1e-8 score exactly 1e-8/1e-8 = 1 (bohb.py:129):
 // they tie, so only the first of them per segment (first1[b]) can win and needs the exact re-score
 // (BOHB's own sampler puts most candidates there at D = 32: the truncnorm scale is 3 bw).
+// Candidate i's estimate merged over its nsplit observation-split partials (hbx_score_h32.hip): the sums
+// add (log domain, fp32); each partial's relative bound holds for the total too (sums of positive terms),
+// plus per merge its own rounding: 2^-18 for the fp32 exp / log / addition, and the rounding of the merged
+// ln S to fp32 (<= |ln S| 2^-23 absolute, counted as 2^-22 |ln S| relative on S)
+__device__ __forceinline__ KdeEst merge_splits(const KdeEst* __restrict__ e, int64_t Nc, int64_t i, int nsplit) {
+  KdeEst a = e[i];
+  auto lae = [](float x, float y) {
+    const float m = fmaxf(x, y);
+    return m == -INFINITY ? m : m + __logf(__expf(x - m) + __expf(y - m));
+  };
+  for (int r = 1; r < nsplit; ++r) {
+    const KdeEst b = e[(int64_t)r * Nc + i];
+    if (a.lpos != a.lpos || b.lpos != b.lpos) {  // structural NaN (every split carries it)
+      a.lpos = NAN;
+      continue;
+    }
+    a.lpos = lae(a.lpos, b.lpos);
+    a.lneg = lae(a.lneg, b.lneg);
+    const float ml = fmaxf(a.lpos > -INFINITY ? fabsf(a.lpos) : 0.f, a.lneg > -INFINITY ? fabsf(a.lneg) : 0.f);
+    a.err = fmaxf(a.err, b.err) + 0x1p-18f + ml * 0x1p-22f;
+  }
+  return a;
+}
+
 #ifndef COMBINE_SUB
 #define COMBINE_SUB 2  // 256-candidate sub-blocks per block of kde_combine_kernel (2: 13-15 us at 1e6, 4: 15-17, 8: 19)
 #endif
-__global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
-                                                          const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
+__global__ __launch_bounds__(256) void kde_combine_kernel(KdeEst* __restrict__ el,
+                                                          KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                                           int32_t* __restrict__ first1,
-                                                          int32_t* __restrict__ rescue_cnt) {
+                                                          int32_t* __restrict__ rescue_cnt, int32_t nsplit_l = 1,
+                                                          int32_t nsplit_g = 1) {
   // the rescue pass of this acquisition has run: its marker count starts the next one at 0
   if (rescue_cnt && blockIdx.x == 0 && threadIdx.x == 0) *rescue_cnt = 0;
   // COMBINE_SUB consecutive 256-candidate sub-blocks per block: every sub-block's loads are issued first
@@ -831,8 +860,15 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
   for (int r = 0; r < COMBINE_SUB; ++r) {
     const int64_t i = ((int64_t)blockIdx.x * COMBINE_SUB + r) * 256 + threadIdx.x;
     if (i < Nc) {
-      ea[r] = el[i];
-      eb[r] = eg[i];
+      if (nsplit_l > 1 || nsplit_g > 1) {  // observation splits: merged, and kept for the later steps
+        ea[r] = merge_splits(el, Nc, i, nsplit_l);
+        eb[r] = merge_splits(eg, Nc, i, nsplit_g);
+        el[i] = ea[r];
+        eg[i] = eb[r];
+      } else {
+        ea[r] = el[i];
+        eb[r] = eg[i];
+      }
     }
   }
   __shared__ float rh[COMBINE_SUB][4];
@@ -1559,7 +1595,30 @@ struct ScoreFns {
   int threads;
   logpdf_pair_fn pair;  // the same kernel over both KDEs in one grid (hmode 16x16 only), or nullptr
   logpdf_pair_fn rescue_pair;
+  bool split_ok = false;  // the pair kernel takes observation splits (the 32x32-tile instances)
 };
+
+// Observation splits of a pair launch with `tiles` candidate tiles per KDE over <= nmax observations: a
+// few candidates against many observations would otherwise be a handful of blocks each walking every
+// chunk (64 candidates x 1e4 observations: 2 blocks, 123 us); while both KDEs' tiles are at most one block
+// per CU, split until they fill the chip about twice, each range >= 4 chunks, at most 16 (the combine
+// kernel merges the partial sums).
+// HBX_OBS_SPLIT=0: no splits (read per call).  ws_sizing: the workspace's bound (no switch, the largest
+// tile size).
+#define OBS_SPLIT_MAX 16
+static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
+  if (!ws_sizing) {
+    const char* e = getenv("HBX_OBS_SPLIT");
+    if (e && atoi(e) == 0) return 1;
+  }
+  const int64_t nch = (nmax + OBS_CHUNK - 1) / OBS_CHUNK;
+  if (2 * (int64_t)tiles > 256) return 1;  // one block per CU or more already (config #2: 392 blocks, a
+                                           // split measured 4 us slower: more prologues, the merge)
+  int64_t sp = (512 + 2 * (int64_t)tiles - 1) / (2 * (int64_t)(tiles > 0 ? tiles : 1));
+  if (sp > nch / 4) sp = nch / 4;
+  if (sp > OBS_SPLIT_MAX) sp = OBS_SPLIT_MAX;
+  return sp < 1 ? 1 : (int)sp;
+}
 
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
 // HBX_SCORE_PAIR=0 keeps two launches (read per call: tests switch it in-process)
@@ -1616,7 +1675,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     const int hw = co ? H32C_WAVES : H16_WAVES;
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
-            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad)};
+            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1646,18 +1705,25 @@ static int launch_score(ScoreFns f, const double* cand, int64_t Nc, int32_t D, c
 static int launch_score2(ScoreFns f0, const void* params0, const float* table0, KdeEst* est0, ScoreFns f1,
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
                          int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s,
-                         KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr) {
+                         KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr, int64_t nmax = 0,
+                         int32_t* nsplit_out = nullptr) {
+  if (nsplit_out) *nsplit_out = 1;
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
-    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm, rescue_cnt, {}};
+    const int ns = (f0.split_ok && nsplit_out && nmax > 0) ? obs_splits(gm, nmax) : 1;
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns,
+                  rescue_cnt, {}};
+    a.tiles = gm;
+    a.nsplit0 = a.nsplit1 = ns;
+    if (nsplit_out) *nsplit_out = ns;
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
-      hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
+      hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm * ns), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
-      hipLaunchKernelGGL(f0.pair, dim3(2 * gm), dim3(f0.threads), 0, s, cand, Nc, D, a);
+      hipLaunchKernelGGL(f0.pair, dim3(2 * gm * ns), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
     a.init = init;  // the acquisition state, set by the rescue pass's first workgroup
@@ -1703,8 +1769,10 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.key = take(8 * B);
   w.first1 = take(4 * B);
   w.rescue = take(4);
-  w.est_l = take(sizeof(KdeEst) * Nc);
-  w.est_g = take(sizeof(KdeEst) * Nc);
+  // estimates: one per candidate and observation split (the launch's splits never exceed this bound)
+  const int sp = obs_splits((unsigned)((Nc + 511) / 512), nmax, true);
+  w.est_l = take(sizeof(KdeEst) * Nc * sp);
+  w.est_g = take(sizeof(KdeEst) * Nc * sp);
   w.lo = take(4 * Nc);
   w.list = take(4 * Nc);
   w.near = take(4 * Nc);
@@ -1965,12 +2033,15 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   // it while the host is still enqueueing the rest
   const bool scored = Nc > 0 && !exact_only;
   bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
+  int32_t nsplit = 1;   // the scoring launch's observation splits (the combine merges them)
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
     if (!batch_res) ip = KdePairArgs::AcqInitPtrs{U, count, flags, first1, res};
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
-                                 (int32_t*)(ws + w.rescue), s, ip, &inited);
+                                 (int32_t*)(ws + w.rescue), s, ip, &inited,
+                                 fast ? nmax : 0,  // splits for the pick only: reported ln-pdfs stay unsplit
+                                 &nsplit);
     if (rc) return rc;
   }
   if (batch_res) {
@@ -1990,7 +2061,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     } else {
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
                          dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, U,
-                         flags, first1, (int32_t*)(ws + w.rescue));
+                         flags, first1, (int32_t*)(ws + w.rescue), nsplit, nsplit);
       HBX_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,

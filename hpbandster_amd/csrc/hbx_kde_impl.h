@@ -264,8 +264,31 @@ struct KdePairArgs {
     int32_t* first1;
     struct AcqResult* res;
   } init;
+  // observation splits (h32 pair kernels, acquisitions only): KDE k's blocks are `tiles` candidate tiles x
+  // nsplit_k chunk ranges; range r writes its partial estimate to out_k + r Nc (the combine kernel merges
+  // them).  1: one block covers all of the KDE's observations.
+  unsigned tiles = 0;
+  int32_t nsplit0 = 1, nsplit1 = 1;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
+
+// A partial estimate over an empty chunk range (S = 0): merging it changes nothing
+__host__ __device__ inline KdeEst kde_est_neutral() {
+  KdeEst e;
+  e.lpos = -INFINITY;
+  e.lneg = -INFINITY;
+  e.err = 0.f;
+  e.pad = 0.f;
+  return e;
+}
+
+// Chunk range [c0, c0 + nch) of observation split r of nsplit over nchunks chunks (nch <= 0: empty)
+__host__ __device__ inline void obs_split_range(int nchunks, int r, int nsplit, int* c0, int* nch) {
+  const int per = (nchunks + nsplit - 1) / nsplit;
+  *c0 = r * per;
+  const int e = (*c0 + per) < nchunks ? (*c0 + per) : nchunks;
+  *nch = e - *c0;
+}
 
 // host-side pickers of the scoring kernel instances (nullptr when the bucket has none)
 logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip

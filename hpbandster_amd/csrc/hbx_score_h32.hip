@@ -71,7 +71,8 @@ template <int NSC, int KP, bool SG, bool FAST, bool CO = false, int CT = 1>
 __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
                                                     const KdeParams* __restrict__ P,
                                                     const float* __restrict__ table, KdeEst* __restrict__ out,
-                                                    const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr) {
+                                                    const unsigned blk, int32_t* __restrict__ rescue_cnt = nullptr,
+                                                    const int split = 0, const int nsplit = 1) {
   // CO: the coarse pre-screen (hbx_kde_impl.h coarse layout): one product per continuous dim, no lo parts
   constexpr int ND = CO ? h32c_nd(NSC) : h32_nd(NSC);  // dense 16-wide K-steps (C_j / c_i pieces + per dim)
   constexpr int KS = KP;                     // sparse 32-wide K-steps (one-hot positions), hi parts
@@ -95,12 +96,25 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
   __shared__ __align__(16) float lds[NBUF * CHF + AUXF];  // the kernel's only LDS object
   float* aux = lds + NBUF * CHF;
   if constexpr (CO) table += P->coarse_off;  // the coarse layout follows the precise table
+  // observation split: this block's chunk range, its partial estimates at out + split Nc
+  int c0 = 0, nchunks = (P->n + OBS_CHUNK - 1) / OBS_CHUNK;
+  if (nsplit > 1) {
+    obs_split_range(nchunks, split, nsplit, &c0, &nchunks);
+    out += (int64_t)split * Nc;
+    if (nchunks <= 0) {  // more splits than chunks: this range is empty
+      const int64_t cb = (int64_t)blk * HW * 32 * CT;
+      for (int k = threadIdx.x; k < HW * 32 * CT; k += blockDim.x)
+        if (cb + k < Nc) out[cb + k] = kde_est_neutral();
+      return;
+    }
+    table += (int64_t)c0 * CHF;
+  }
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, h = lane >> 5;
   const int64_t cbase = ((int64_t)blk * HW + wave) * 32 * CT;
   const bool xpiece = wave < NX;
-  const int n = P->n, dc = P->dc;
+  const int dc = P->dc;
 
   // per-dim parameters and the block's candidate rows staged in the (not yet used) ring
   struct ContPrm { double scale, center; float xmax; int32_t col; };
@@ -207,7 +221,6 @@ __device__ __forceinline__ void kde_logpdf_h32_body(const double* __restrict__ c
     asm volatile("" ::: "memory");
   }
 
-  const int nchunks = (n + OBS_CHUNK - 1) / OBS_CHUNK;
   // LDS-DMA of chunk cc into ring slot `slot`; part p issues the pieces g with g % 2 == p.  Every wave
   // issues GL + 1 pieces when GP is not a multiple of HW: the waves without an extra piece load their
   // first one again (same bytes to the same place), so the loop body has no branch -- a branch would
@@ -511,9 +524,12 @@ template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
+  const unsigned loc = second ? blockIdx.x - a.nblk0 : blockIdx.x;
+  const int ns = second ? a.nsplit1 : a.nsplit0;
+  const unsigned tile = ns > 1 ? loc % a.tiles : loc;  // blocks of one chunk range are consecutive
+  const int split = ns > 1 ? (int)(loc / a.tiles) : 0;
   kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                                second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
-                                                a.rescue);
+                                                second ? a.out1 : a.out0, tile, a.rescue, split, ns);
 }
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
@@ -529,9 +545,12 @@ template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
   const bool second = blockIdx.x >= a.nblk0;
+  const unsigned loc = second ? blockIdx.x - a.nblk0 : blockIdx.x;
+  const int ns = second ? a.nsplit1 : a.nsplit0;
+  const unsigned tile = ns > 1 ? loc % a.tiles : loc;
+  const int split = ns > 1 ? (int)(loc / a.tiles) : 0;
   kde_logpdf_h32_body<NSC, KP, true, FAST>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                           second ? a.out1 : a.out0, second ? blockIdx.x - a.nblk0 : blockIdx.x,
-                                           a.rescue);
+                                           second ? a.out1 : a.out0, tile, a.rescue, split, ns);
 }
 
 // instances: h32_ok (hbx_kde_impl.h); FAST where there is a one-hot part; CO (coarse) for unsigned sums
