@@ -759,3 +759,38 @@ def test_large_shortlists_through_the_synchronous_call(device, nc):
     g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
     want, _ = O.select(l, g)
     assert first[0] == want and (first[2], first[3]) == (l[want], g[want])
+
+
+@pytest.mark.parametrize("nc,nobs,far", [(64, 10000, False), (64, 10000, True), (700, 4000, False), (5000, 3000, True)])
+def test_observation_splits_pick_like_one_range(device, monkeypatch, nc, nobs, far):
+    """Few candidates against many observations: the scoring blocks split the observations into chunk
+    ranges whose partial estimates the combine kernel merges (HBX_OBS_SPLIT=1, the default) -- the exact
+    pick, its score and both pdfs equal the unsplit launch's, with rescue markers in some ranges (far
+    candidates) too; and the winner is the oracle's."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(nobs, 24, 8, 4, seed=91)
+    vt = S.var_type_string(24, 8)
+    pair = kde.fit_pair(X, S.make_losses(nobs, seed=92), vt, 33, device=device)
+    C = S.make_candidates(nc, 24, 8, 4, seed=93)
+    if far:
+        C[3, 0] = 900.0
+        C[nc // 2, 5] = -300.0
+    Cd = torch.from_numpy(C).to(device)
+
+    def rec(r):
+        return (r.index, r.score, r.pdf_l, r.pdf_g)
+    monkeypatch.setenv("HBX_OBS_SPLIT", "0")
+    one = pair.acquire(Cd)
+    monkeypatch.setenv("HBX_OBS_SPLIT", "1")
+    for _ in range(2):
+        assert rec(pair.acquire(Cd)) == rec(one)
+    rb = pair.acquire_batch(Cd, max(1, nc // 4))
+    monkeypatch.setenv("HBX_OBS_SPLIT", "0")
+    rb0 = pair.acquire_batch(Cd, max(1, nc // 4))
+    assert [rec(a) for a in rb] == [rec(b) for b in rb0]
+    if nc * nobs <= 1e6:
+        l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+        g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+        assert one.index == O.select(l, g)[0]
