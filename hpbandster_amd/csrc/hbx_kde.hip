@@ -1606,14 +1606,15 @@ struct ScoreFns {
 // HBX_OBS_SPLIT=0: no splits (read per call).  ws_sizing: the workspace's bound (no switch, the largest
 // tile size).
 #define OBS_SPLIT_MAX 16
+static bool obs_split_enabled() {
+  const char* e = getenv("HBX_OBS_SPLIT");
+  return !(e && atoi(e) == 0);
+}
 static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
-  if (!ws_sizing) {
-    const char* e = getenv("HBX_OBS_SPLIT");
-    if (e && atoi(e) == 0) return 1;
-  }
+  if (!ws_sizing && !obs_split_enabled()) return 1;
   const int64_t nch = (nmax + OBS_CHUNK - 1) / OBS_CHUNK;
-  if (2 * (int64_t)tiles > 256) return 1;  // one block per CU or more already (config #2: 392 blocks, a
-                                           // split measured 4 us slower: more prologues, the merge)
+  if (2 * (int64_t)tiles > 256) return 1;  // one block per CU or more already (config #2: 392 blocks; both
+                                           // KDEs split in two measured 4 us slower: a second round)
   int64_t sp = (512 + 2 * (int64_t)tiles - 1) / (2 * (int64_t)(tiles > 0 ? tiles : 1));
   if (sp > nch / 4) sp = nch / 4;
   if (sp > OBS_SPLIT_MAX) sp = OBS_SPLIT_MAX;
@@ -1707,23 +1708,32 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
                          int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s,
                          KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr, int64_t nmax = 0,
                          int32_t* nsplit_out = nullptr) {
-  if (nsplit_out) *nsplit_out = 1;
+  if (nsplit_out) nsplit_out[0] = nsplit_out[1] = 1;
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
     const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
-    const int ns = (f0.split_ok && nsplit_out && nmax > 0) ? obs_splits(gm, nmax) : 1;
-    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns,
+    const bool can = f0.split_ok && nsplit_out && nmax > 0;
+    // segment 0 = params1 (the bad KDE), 1 = params0.  (At about one block per CU -- config #2, 2 x 196
+    // blocks -- splitting only the bad KDE's longer walks in two measured 3-5 us slower, like splitting
+    // both: each range repeats the block's prologue, and the merge reads twice the estimates.)
+    const int ns0 = can ? obs_splits(gm, nmax) : 1, ns1 = ns0;
+    KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns0,
                   rescue_cnt, {}};
     a.tiles = gm;
-    a.nsplit0 = a.nsplit1 = ns;
-    if (nsplit_out) *nsplit_out = ns;
+    a.nsplit0 = ns0;
+    a.nsplit1 = ns1;
+    if (nsplit_out) {
+      nsplit_out[0] = ns1;  // params0's (the first KDE argument's) splits
+      nsplit_out[1] = ns0;
+    }
+    const unsigned grid = gm * (unsigned)(ns0 + ns1);
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
-      hipExtLaunchKernelGGL(f0.pair, dim3(2 * gm * ns), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
+      hipExtLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
-      hipLaunchKernelGGL(f0.pair, dim3(2 * gm * ns), dim3(f0.threads), 0, s, cand, Nc, D, a);
+      hipLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
     a.init = init;  // the acquisition state, set by the rescue pass's first workgroup
@@ -2033,7 +2043,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   // it while the host is still enqueueing the rest
   const bool scored = Nc > 0 && !exact_only;
   bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
-  int32_t nsplit = 1;   // the scoring launch's observation splits (the combine merges them)
+  int32_t nsplit[2] = {1, 1};  // the scoring launch's observation splits, good / bad (the combine merges them)
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
@@ -2041,7 +2051,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
                                  (int32_t*)(ws + w.rescue), s, ip, &inited,
                                  fast ? nmax : 0,  // splits for the pick only: reported ln-pdfs stay unsplit
-                                 &nsplit);
+                                 nsplit);
     if (rc) return rc;
   }
   if (batch_res) {
@@ -2061,7 +2071,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     } else {
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
                          dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, U,
-                         flags, first1, (int32_t*)(ws + w.rescue), nsplit, nsplit);
+                         flags, first1, (int32_t*)(ws + w.rescue), nsplit[0], nsplit[1]);
       HBX_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
