@@ -1,5 +1,5 @@
-"""Host-side pieces of one BOHB refit (ObservationStore.refit at config #3's 1e4 x 32), GPU box:
-    python tools/refit_host.py
+"""Host-side pieces of one BOHB refit (ObservationStore.refit at config #3's 1e4 x 32, or n x 32), GPU box:
+    python tools/refit_host.py [n]
 Wall time per refit, the native hbx_kde_refit call's own host time, and the stream time (events)."""
 import json
 import os
@@ -17,8 +17,9 @@ def main():
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
     dev = torch.device("cuda", 0)
-    X = S.make_observations(10000, 24, 8, 4)
-    losses = S.make_losses(10000)
+    nobs = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    X = S.make_observations(nobs, 24, 8, 4)
+    losses = S.make_losses(nobs)
     D = 32
     reps = 30
     n0 = X.shape[0] - reps - 1
