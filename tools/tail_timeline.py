@@ -13,6 +13,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CONFIGS = {"config2": (8, 0, 0, 1000, 100_000, 9), "config3": (24, 8, 4, 10000, 1_000_000, 33)}
+if os.environ.get("TAIL_SMALL"):  # get_config-sized calls: 64 candidates against 400 / 10000 observations
+    CONFIGS = {"config2": (24, 8, 4, 400, 64, 33), "config3": (24, 8, 4, 10000, 64, 33)}
 
 
 def run(reps=40):
