@@ -816,41 +816,62 @@ __device__ __forceinline__ void est_interval(const KdeEst e, float* lo, float* h
 // Candidates whose l and g are both certainly below 1e-8 score exactly 1e-8/1e-8 = 1 (bohb.py:129):
 // they tie, so only the first of them per segment (first1[b]) can win and needs the exact re-score
 // (BOHB's own sampler puts most candidates there at D = 32: the truncnorm scale is 3 bw).
+#define OBS_SPLIT_MAX 16  // observation splits of one scoring launch at most (obs_splits)
+
 // Candidate i's estimate merged over its nsplit observation-split partials (hbx_score_h32.hip): the sums
 // add (log domain, fp32); each partial's relative bound holds for the total too (sums of positive terms),
 // plus per merge its own rounding: 2^-18 for the fp32 exp / log / addition, and the rounding of the merged
 // ln S to fp32 (<= |ln S| 2^-23 absolute, counted as 2^-22 |ln S| relative on S)
 __device__ __forceinline__ KdeEst merge_splits(const KdeEst* __restrict__ e, int64_t Nc, int64_t i, int nsplit) {
-  KdeEst a = e[i];
+  // every partial's load issued before the first merge (a load per dependent merge step cost 14 us for 16
+  // splits of 64 candidates); fixed-size and fully unrolled, so the partials stay in registers
+  KdeEst p[OBS_SPLIT_MAX];
+#pragma unroll
+  for (int r = 0; r < OBS_SPLIT_MAX; ++r) p[r] = r < nsplit ? e[(int64_t)r * Nc + i] : kde_est_neutral();
   auto lae = [](float x, float y) {
     const float m = fmaxf(x, y);
     return m == -INFINITY ? m : m + __logf(__expf(x - m) + __expf(y - m));
   };
-  for (int r = 1; r < nsplit; ++r) {
-    const KdeEst b = e[(int64_t)r * Nc + i];
-    if (a.lpos != a.lpos || b.lpos != b.lpos) {  // structural NaN (every split carries it)
-      a.lpos = NAN;
-      continue;
+  KdeEst a = p[0];
+#pragma unroll
+  for (int r = 1; r < OBS_SPLIT_MAX; ++r) {
+    if (r < nsplit) {
+      const KdeEst b = p[r];
+      if (a.lpos != a.lpos || b.lpos != b.lpos) {  // structural NaN (every split carries it)
+        a.lpos = NAN;
+      } else {
+        a.lpos = lae(a.lpos, b.lpos);
+        a.lneg = lae(a.lneg, b.lneg);
+        const float ml = fmaxf(a.lpos > -INFINITY ? fabsf(a.lpos) : 0.f, a.lneg > -INFINITY ? fabsf(a.lneg) : 0.f);
+        a.err = fmaxf(a.err, b.err) + 0x1p-18f + ml * 0x1p-22f;
+      }
     }
-    a.lpos = lae(a.lpos, b.lpos);
-    a.lneg = lae(a.lneg, b.lneg);
-    const float ml = fmaxf(a.lpos > -INFINITY ? fabsf(a.lpos) : 0.f, a.lneg > -INFINITY ? fabsf(a.lneg) : 0.f);
-    a.err = fmaxf(a.err, b.err) + 0x1p-18f + ml * 0x1p-22f;
   }
   return a;
+}
+
+// observation splits: each candidate's partial estimates merged into its first slot, for the combine and
+// every later step (one thread per candidate and KDE; launched only when the scoring launch split)
+__global__ __launch_bounds__(256) void kde_merge_splits_kernel(KdeEst* __restrict__ el, KdeEst* __restrict__ eg,
+                                                               int64_t Nc, int32_t ns_l, int32_t ns_g) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * Nc) return;
+  const bool g = t >= Nc;
+  const int64_t i = g ? t - Nc : t;
+  const int ns = g ? ns_g : ns_l;
+  if (ns > 1) (g ? eg : el)[i] = merge_splits(g ? eg : el, Nc, i, ns);
 }
 
 #ifndef COMBINE_SUB
 #define COMBINE_SUB 2  // 256-candidate sub-blocks per block of kde_combine_kernel (2: 13-15 us at 1e6, 4: 15-17, 8: 19)
 #endif
-__global__ __launch_bounds__(256) void kde_combine_kernel(KdeEst* __restrict__ el,
-                                                          KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
+__global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
+                                                          const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
                                                           float* __restrict__ logl, float* __restrict__ logg,
                                                           float* __restrict__ lo,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
                                                           int32_t* __restrict__ first1,
-                                                          int32_t* __restrict__ rescue_cnt, int32_t nsplit_l = 1,
-                                                          int32_t nsplit_g = 1) {
+                                                          int32_t* __restrict__ rescue_cnt) {
   // the rescue pass of this acquisition has run: its marker count starts the next one at 0
   if (rescue_cnt && blockIdx.x == 0 && threadIdx.x == 0) *rescue_cnt = 0;
   // COMBINE_SUB consecutive 256-candidate sub-blocks per block: every sub-block's loads are issued first
@@ -860,15 +881,8 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(KdeEst* __restrict__ e
   for (int r = 0; r < COMBINE_SUB; ++r) {
     const int64_t i = ((int64_t)blockIdx.x * COMBINE_SUB + r) * 256 + threadIdx.x;
     if (i < Nc) {
-      if (nsplit_l > 1 || nsplit_g > 1) {  // observation splits: merged, and kept for the later steps
-        ea[r] = merge_splits(el, Nc, i, nsplit_l);
-        eb[r] = merge_splits(eg, Nc, i, nsplit_g);
-        el[i] = ea[r];
-        eg[i] = eb[r];
-      } else {
-        ea[r] = el[i];
-        eb[r] = eg[i];
-      }
+      ea[r] = el[i];
+      eb[r] = eg[i];
     }
   }
   __shared__ float rh[COMBINE_SUB][4];
@@ -1605,7 +1619,6 @@ struct ScoreFns {
 // kernel merges the partial sums).
 // HBX_OBS_SPLIT=0: no splits (read per call).  ws_sizing: the workspace's bound (no switch, the largest
 // tile size).
-#define OBS_SPLIT_MAX 16
 static bool obs_split_enabled() {
   const char* e = getenv("HBX_OBS_SPLIT");
   return !(e && atoi(e) == 0);
@@ -2043,7 +2056,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   // it while the host is still enqueueing the rest
   const bool scored = Nc > 0 && !exact_only;
   bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
-  int32_t nsplit[2] = {1, 1};  // the scoring launch's observation splits, good / bad (the combine merges them)
+  int32_t nsplit[2] = {1, 1};  // the scoring launch's observation splits, good / bad (merged before the combine)
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
@@ -2069,9 +2082,14 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
       hipLaunchKernelGGL(kde_exact_only_init_kernel, grid, dim3(256), 0, s, Nc, sg, el, eg, lo, flags);
       HBX_LAUNCH_CHECK();
     } else {
+      if (nsplit[0] > 1 || nsplit[1] > 1) {  // the scoring launch's observation splits merged first
+        hipLaunchKernelGGL(kde_merge_splits_kernel, dim3((unsigned)((2 * Nc + 255) / 256)), dim3(256), 0, s, el, eg,
+                           Nc, nsplit[0], nsplit[1]);
+        HBX_LAUNCH_CHECK();
+      }
       hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
                          dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, U,
-                         flags, first1, (int32_t*)(ws + w.rescue), nsplit[0], nsplit[1]);
+                         flags, first1, (int32_t*)(ws + w.rescue));
       HBX_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
