@@ -658,25 +658,29 @@ static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s)
 // Rescue (rare): candidates whose every term sits far below the static bound M0 are recomputed
 // with a true maximum (two passes over the observations), one candidate per thread on the VALU.
 // Continuous coordinates come from the table's f32 part, categorical codes straight from the data.
-template <int DCP, bool SIGNED>
-__device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
-                                                const KdeParams* __restrict__ P, const float* __restrict__ table,
-                                                KdeEst* __restrict__ out, const unsigned blk,
-                                                const int nsplit = 1) {
-  constexpr int NC = DCP > 0 ? DCP : 1;
-  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
-  bool need = false;  // a marker in any observation split's partial estimate
-  if (i < Nc)
-    for (int r = 0; r < nsplit; ++r) need = need || out[(int64_t)r * Nc + i].err == -1.f;
-  if (!__any(need)) return;
-  if (!need) return;
+// LOWREG (the combine kernel's copy): the same operations in the same order over k < dc only (the padded
+// k >= dc terms add exact zeros), candidate and observation coordinates recomputed per pair instead of held
+// in DCP-long register arrays -- the combine kernel keeps its occupancy (29-32 VGPRs, not up to 170)
+template <int DCP, bool SIGNED, bool LOWREG = false>
+__device__ __forceinline__ KdeEst kde_rescue_one(const double* __restrict__ cand, int64_t i, int32_t D,
+                                                 const KdeParams* __restrict__ P) {
+  constexpr int NC = DCP > 0 && !LOWREG ? DCP : 1;
   const double* x = cand + i * (int64_t)D;
   const int n = P->n, dc = P->dc, du = P->du;
   const double* __restrict__ Xo = P->X;
   const int64_t* __restrict__ rows = P->rows;
   float xs[NC], ci = 0.f, bnd = 0.f;
+  auto coord = [&](const double* r, int k) { return (float)(P->cont_scale[k] * (r[P->cont_dim[k]] - P->center[k])); };
+  if constexpr (LOWREG) {
+#pragma unroll 1
+    for (int k = 0; k < dc; ++k) {
+      const float v = coord(x, k);
+      ci = fmaf(-v, v, ci);
+      bnd = fmaf(fabsf(2.f * v), P->xmax[k], bnd);
+    }
+  }
 #pragma unroll
-  for (int k = 0; k < DCP; ++k) {
+  for (int k = 0; k < (LOWREG ? 0 : DCP); ++k) {
     float v = 0.f;
     if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
     ci = fmaf(-v, v, ci);
@@ -688,8 +692,15 @@ __device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand,
     const double* xo = Xo + rows[j] * (int64_t)D;
     float Xp[NC];
     double Cd = 0.0;
+    if constexpr (LOWREG) {
+#pragma unroll 1
+      for (int k = 0; k < dc; ++k) {
+        const float v = coord(xo, k);
+        Cd -= (double)v * (double)v;
+      }
+    }
 #pragma unroll
-    for (int k = 0; k < DCP; ++k) {
+    for (int k = 0; k < (LOWREG ? 0 : DCP); ++k) {
       float v = 0.f;
       if (k < dc) v = (float)(P->cont_scale[k] * (xo[P->cont_dim[k]] - P->center[k]));
       Cd -= (double)v * (double)v;
@@ -698,8 +709,12 @@ __device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand,
     const float Cj = (float)(Cd + P->lb_sum - P->m0_log2);
     float t = fmaf(1.f, Cj, 0.f);
     t = fmaf(ci, 1.f, t);
+    if constexpr (LOWREG) {
+#pragma unroll 1
+      for (int k = 0; k < dc; ++k) t = fmaf(2.f * coord(x, k), coord(xo, k), t);
+    }
 #pragma unroll
-    for (int k = 0; k < DCP; ++k) t = fmaf(xs[k], Xp[k], t);
+    for (int k = 0; k < (LOWREG ? 0 : DCP); ++k) t = fmaf(xs[k], Xp[k], t);
     par = 0.f;
     for (int u = 0; u < du; ++u) {
       const int d = P->cat_dim[u];
@@ -726,7 +741,21 @@ __device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand,
   } else {
     mx = 0.f;
   }
-  out[i] = finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);  // the whole sum in split 0
+  return finish_est(P, S, Sn, mx, false, ci, bnd, SIGNED, OBS_CHUNK);
+}
+
+template <int DCP, bool SIGNED>
+__device__ __forceinline__ void kde_rescue_body(const double* __restrict__ cand, int64_t Nc, int32_t D,
+                                                const KdeParams* __restrict__ P, const float* __restrict__ table,
+                                                KdeEst* __restrict__ out, const unsigned blk,
+                                                const int nsplit = 1) {
+  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
+  bool need = false;  // a marker in any observation split's partial estimate
+  if (i < Nc)
+    for (int r = 0; r < nsplit; ++r) need = need || out[(int64_t)r * Nc + i].err == -1.f;
+  if (!__any(need)) return;
+  if (!need) return;
+  out[i] = kde_rescue_one<DCP, SIGNED>(cand, i, D, P);  // the whole sum in split 0
   for (int r = 1; r < nsplit; ++r) out[(int64_t)r * Nc + i] = kde_est_neutral();
 }
 
@@ -738,22 +767,6 @@ __global__ __launch_bounds__(256) void kde_rescue_kernel(const double* __restric
   kde_rescue_body<DCP, SIGNED>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
-// a single acquisition's state before its combine / shortlist / exact / final steps
-__device__ __forceinline__ void acq_init_state(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1,
-                                               AcqResult* res) {
-  *U = hbx_f2ord(INFINITY);
-  *first1 = INT32_MAX;
-  *count = 0;
-  *flags = 0;
-  res->index = -1;
-  res->score = NAN;
-  res->pdf_l = NAN;
-  res->pdf_g = NAN;
-  res->shortlist = 0;
-  res->flags = 0;
-  res->near = 0;
-  res->rel = 0.f;
-}
 
 // both KDEs' rescue passes in one launch (blocks [0, nblk0) KDE 0, the rest KDE 1)
 // grid-stride over the 2 nblk0 logical blocks; with the scoring kernel's marker count available and 0
@@ -865,17 +878,28 @@ __global__ __launch_bounds__(256) void kde_merge_splits_kernel(KdeEst* __restric
 #ifndef COMBINE_SUB
 #define COMBINE_SUB 2  // 256-candidate sub-blocks per block of kde_combine_kernel (2: 13-15 us at 1e6, 4: 15-17, 8: 19)
 #endif
-__global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restrict__ el,
-                                                          const KdeEst* __restrict__ eg, int64_t Nc, uint32_t seg,
-                                                          float* __restrict__ logl, float* __restrict__ logg,
-                                                          float* __restrict__ lo,
+// RESCUE: the rescue pass done here (a single acquisition scored by a 32x32 pair launch without splits):
+// with the scoring launch's marker count non-zero, a thread re-scores its own marked candidates before
+// combining them (kde_rescue_one, the rescue kernel's arithmetic) and stores them for the later steps --
+// one launch less per acquisition (a rescue launch took 4.8 us even when it exited at once)
+struct CombineRescue {
+  const double* cand;
+  int32_t D;
+  const KdeParams* Pl;  // the KDEs behind el / eg
+  const KdeParams* Pg;
+  const int32_t* cnt;   // the scoring launch's marker count
+};
+template <bool SIGNED, bool RESCUE>
+__global__ __launch_bounds__(256) void kde_combine_kernel(KdeEst* __restrict__ el, KdeEst* __restrict__ eg,
+                                                          int64_t Nc, uint32_t seg, float* __restrict__ logl,
+                                                          float* __restrict__ logg, float* __restrict__ lo,
                                                           uint32_t* __restrict__ U, int32_t* __restrict__ flags,
-                                                          int32_t* __restrict__ first1,
-                                                          int32_t* __restrict__ rescue_cnt) {
-  // the rescue pass of this acquisition has run: its marker count starts the next one at 0
-  if (rescue_cnt && blockIdx.x == 0 && threadIdx.x == 0) *rescue_cnt = 0;
+                                                          int32_t* __restrict__ first1, CombineRescue rs) {
   // COMBINE_SUB consecutive 256-candidate sub-blocks per block: every sub-block's loads are issued first
   // (the kernel is latency-bound with one candidate per thread), then each runs as its own block would
+  // the marker count, final since the scoring launch ended: a plain (scalar) load, like the estimates'
+  int32_t nres = 0;
+  if constexpr (RESCUE) nres = *rs.cnt;
   KdeEst ea[COMBINE_SUB], eb[COMBINE_SUB];
 #pragma unroll
   for (int r = 0; r < COMBINE_SUB; ++r) {
@@ -883,6 +907,22 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
     if (i < Nc) {
       ea[r] = el[i];
       eb[r] = eg[i];
+    }
+  }
+  if constexpr (RESCUE) {
+    if (nres != 0) {  // rare
+#pragma unroll
+      for (int r = 0; r < COMBINE_SUB; ++r) {
+        const int64_t i = ((int64_t)blockIdx.x * COMBINE_SUB + r) * 256 + threadIdx.x;
+        if (i < Nc && ea[r].err == -1.f) {
+          ea[r] = kde_rescue_one<0, SIGNED, true>(rs.cand, i, rs.D, rs.Pl);
+          el[i] = ea[r];
+        }
+        if (i < Nc && eb[r].err == -1.f) {
+          eb[r] = kde_rescue_one<0, SIGNED, true>(rs.cand, i, rs.D, rs.Pg);
+          eg[i] = eb[r];
+        }
+      }
     }
   }
   __shared__ float rh[COMBINE_SUB][4];
@@ -998,13 +1038,19 @@ __global__ __launch_bounds__(256) void kde_combine_kernel(const KdeEst* __restri
   }
 }
 
+typedef void (*combine_fn)(KdeEst*, KdeEst*, int64_t, uint32_t, float*, float*, float*, uint32_t*, int32_t*,
+                           int32_t*, CombineRescue);
+
 __global__ __launch_bounds__(256) void kde_shortlist_kernel(const float* __restrict__ lo, int64_t Nc, uint32_t seg,
                                                             const uint32_t* __restrict__ U,
                                                             const int32_t* __restrict__ flags,
                                                             int32_t* __restrict__ list,
                                                             int32_t* __restrict__ count,
                                                             int32_t* __restrict__ segcnt,
-                                                            const int32_t* __restrict__ first1) {
+                                                            const int32_t* __restrict__ first1,
+                                                            int32_t* __restrict__ rescue_cnt) {
+  // the rescue of this acquisition is done (its pass or the combine): the marker count starts the next at 0
+  if (rescue_cnt && blockIdx.x == 0 && threadIdx.x == 0) *rescue_cnt = 0;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= Nc) return;
   const uint32_t sg = (uint32_t)i / seg;
@@ -1609,7 +1655,9 @@ struct ScoreFns {
   int threads;
   logpdf_pair_fn pair;  // the same kernel over both KDEs in one grid (hmode 16x16 only), or nullptr
   logpdf_pair_fn rescue_pair;
-  bool split_ok = false;  // the pair kernel takes observation splits (the 32x32-tile instances)
+  bool split_ok = false;  // the pair kernel takes observation splits and initialises a single acquisition's
+                          // state (the 32x32-tile instances)
+  combine_fn combine_rescue = nullptr;  // the combine kernel doing the rescue pass of this instance
 };
 
 // Observation splits of a pair launch with `tiles` candidate tiles per KDE over <= nmax observations: a
@@ -1632,6 +1680,13 @@ static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
   if (sp > nch / 4) sp = nch / 4;
   if (sp > OBS_SPLIT_MAX) sp = OBS_SPLIT_MAX;
   return sp < 1 ? 1 : (int)sp;
+}
+
+// the rescue pass done by the combine kernel where it can (HBX_COMBINE_RESCUE=0: its own launch; read per
+// call: tests switch it in-process)
+static bool combine_rescue_enabled() {
+  const char* e = getenv("HBX_COMBINE_RESCUE");
+  return !(e && atoi(e) == 0);
 }
 
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
@@ -1689,7 +1744,8 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     const int hw = co ? H32C_WAVES : H16_WAVES;
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
-            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true};
+            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true,
+            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1720,8 +1776,9 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
                          const void* params1, const float* table1, KdeEst* est1, const double* cand, int64_t Nc,
                          int32_t D, hipEvent_t* ev, int32_t* rescue_cnt, hipStream_t s,
                          KdePairArgs::AcqInitPtrs init = {}, bool* inited = nullptr, int64_t nmax = 0,
-                         int32_t* nsplit_out = nullptr) {
+                         int32_t* nsplit_out = nullptr, bool* rescue_inline = nullptr) {
   if (nsplit_out) nsplit_out[0] = nsplit_out[1] = 1;
+  if (rescue_inline) *rescue_inline = false;
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
@@ -1743,14 +1800,21 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
       nsplit_out[1] = ns0;
     }
     const unsigned grid = gm * (unsigned)(ns0 + ns1);
+    const bool pinit = f0.split_ok && HBX_PAIR_INIT;
+    if (pinit) a.init = init;  // the 32x32 pair kernel's first workgroup sets the acquisition state
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
       hipExtLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
       hipLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
-    a.init = init;  // the acquisition state, set by the rescue pass's first workgroup
+    a.init = pinit ? KdePairArgs::AcqInitPtrs{} : init;  // else set by the rescue pass's first workgroup
     if (inited) *inited = init.U != nullptr;
+    if (rescue_inline && pinit && f0.combine_rescue && rescue_cnt && ns0 == 1 && ns1 == 1 &&
+        combine_rescue_enabled()) {
+      *rescue_inline = true;  // the combine kernel re-scores the marked candidates
+      return HBX_OK;
+    }
     // the rescue pass: grid-stride, exits at once unless the scoring kernel counted a marker
     const unsigned grr = rescue_cnt ? (2 * gr < 1024u ? 2 * gr : 1024u) : 2 * gr;
     hipLaunchKernelGGL(f0.rescue_pair, dim3(grr), dim3(256), 0, s, cand, Nc, D, a);
@@ -2057,6 +2121,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
   const bool scored = Nc > 0 && !exact_only;
   bool inited = false;  // a single acquisition's pair launch: its rescue pass initialises the state
   int32_t nsplit[2] = {1, 1};  // the scoring launch's observation splits, good / bad (merged before the combine)
+  bool rescue_inline = false;  // the rescue pass left to the combine kernel
   if (scored) {
     hipEvent_t* ev = (hipEvent_t*)events;  // optional: [before l, between, after g] for timing
     KdePairArgs::AcqInitPtrs ip{};
@@ -2064,7 +2129,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
     const int rc = launch_score2(fg, params_good, table_good, el, fb, params_bad, table_bad, eg, cand, Nc, D, ev,
                                  (int32_t*)(ws + w.rescue), s, ip, &inited,
                                  fast ? nmax : 0,  // splits for the pick only: reported ln-pdfs stay unsplit
-                                 nsplit);
+                                 nsplit, batch_res ? nullptr : &rescue_inline);
     if (rc) return rc;
   }
   if (batch_res) {
@@ -2087,13 +2152,15 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                            Nc, nsplit[0], nsplit[1]);
         HBX_LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(kde_combine_kernel, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))),
-                         dim3(256), 0, s, el, eg, Nc, sg, logl_out, logg_out, lo, U,
-                         flags, first1, (int32_t*)(ws + w.rescue));
+      const CombineRescue rs{cand, D, (const KdeParams*)params_good, (const KdeParams*)params_bad,
+                             (const int32_t*)(ws + w.rescue)};
+      const combine_fn cf = rescue_inline ? fg.combine_rescue : kde_combine_kernel<false, false>;
+      hipLaunchKernelGGL(cf, dim3((unsigned)((Nc + 256 * COMBINE_SUB - 1) / (256 * COMBINE_SUB))), dim3(256), 0, s, el,
+                         eg, Nc, sg, logl_out, logg_out, lo, U, flags, first1, rs);
       HBX_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
-                       batch_res ? segcnt : (int32_t*)nullptr, first1);
+                       batch_res ? segcnt : (int32_t*)nullptr, first1, (int32_t*)(ws + w.rescue));
     HBX_LAUNCH_CHECK();
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
     hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,

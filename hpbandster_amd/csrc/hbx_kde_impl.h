@@ -244,6 +244,10 @@ typedef _Float16 f16x16 __attribute__((ext_vector_type(16)));
 typedef void (*logpdf_fn)(const double*, int64_t, int32_t, const KdeParams*, const float*, KdeEst*);
 
 // kernel arguments of the two-KDE (l and g in one grid) hmode launch
+#ifndef HBX_PAIR_INIT
+#define HBX_PAIR_INIT 1  // the 32x32 pair kernel initialises a single acquisition's state (0: A/B builds only)
+#endif
+
 struct KdePairArgs {
   const KdeParams* P0;
   const KdeParams* P1;
@@ -253,10 +257,11 @@ struct KdePairArgs {
   KdeEst* out1;
   unsigned nblk0;
   // acquisition workspace counter of rescue-marked candidates (nullable): the scoring kernel counts its
-  // markers, the rescue pass exits at once on 0, the combine kernel zeroes it for the next acquisition
+  // markers, the rescue pass (or the combine kernel doing it) exits at once on 0, the shortlist kernel
+  // zeroes it for the next acquisition
   int32_t* rescue;
-  // single acquisition (nullable): the per-acquisition state the rescue pass initialises in its first
-  // block (acq_init's work, one launch less): U, count, flags, first1, the result record
+  // single acquisition (nullable): the per-acquisition state the 32x32 pair kernel or the rescue pass
+  // initialises in its first block (acq_init's work, one launch less): U, count, flags, first1, the record
   struct AcqInitPtrs {
     uint32_t* U;
     int32_t* count;
@@ -271,6 +276,23 @@ struct KdePairArgs {
   int32_t nsplit0 = 1, nsplit1 = 1;
 };
 typedef void (*logpdf_pair_fn)(const double*, int64_t, int32_t, KdePairArgs);
+
+// a single acquisition's state before its combine / shortlist / exact / final steps
+__device__ __forceinline__ void acq_init_state(uint32_t* U, int32_t* count, int32_t* flags, int32_t* first1,
+                                               AcqResult* res) {
+  *U = hbx_f2ord(INFINITY);
+  *first1 = INT32_MAX;
+  *count = 0;
+  *flags = 0;
+  res->index = -1;
+  res->score = NAN;
+  res->pdf_l = NAN;
+  res->pdf_g = NAN;
+  res->shortlist = 0;
+  res->flags = 0;
+  res->near = 0;
+  res->rel = 0.f;
+}
 
 // A partial estimate over an empty chunk range (S = 0): merging it changes nothing
 __host__ __device__ inline KdeEst kde_est_neutral() {

@@ -523,6 +523,10 @@ __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((
 template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+#if HBX_PAIR_INIT
+  if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)  // a single acquisition's state (acq_init's work)
+    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
+#endif
   const bool second = blockIdx.x >= a.nblk0;  // uniform per block: scalar selects
   const unsigned loc = second ? blockIdx.x - a.nblk0 : blockIdx.x;
   const int ns = second ? a.nsplit1 : a.nsplit0;
@@ -544,6 +548,10 @@ __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(
 template <int NSC, int KP, bool FAST>
 __global__ __launch_bounds__(64 * H16_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void kde_logpdf_h32s_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+#if HBX_PAIR_INIT
+  if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)
+    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
+#endif
   const bool second = blockIdx.x >= a.nblk0;
   const unsigned loc = second ? blockIdx.x - a.nblk0 : blockIdx.x;
   const int ns = second ? a.nsplit1 : a.nsplit0;

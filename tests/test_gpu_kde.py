@@ -794,3 +794,44 @@ def test_observation_splits_pick_like_one_range(device, monkeypatch, nc, nobs, f
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
         assert one.index == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("nc,nobs", [(512, 3000), (64, 300), (2100, 1500)])
+def test_rescue_in_the_combine_kernel_equals_its_own_launch(device, monkeypatch, nc, nobs):
+    """A single acquisition scored by the 32x32 pair kernel leaves the rescue pass to the combine kernel
+    (one launch less; a copy of the rescue arithmetic without register arrays).  With far candidates
+    (markers in both KDEs) the record and both ln-pdf estimate arrays equal, bit for bit, those of the
+    separate rescue launch (HBX_COMBINE_RESCUE=0) and of two single-KDE launches (HBX_SCORE_PAIR=0); the
+    winner is the oracle's."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    vt = S.var_type_string(24, 8)
+    X = S.make_observations(nobs, 24, 8, 4, seed=101)
+    pair = kde.fit_pair(X, S.make_losses(nobs, seed=102), vt, 33, device=device)
+    assert (pair.good.variant >> 6) & 1 and (pair.bad.variant >> 6) & 1
+    C = S.make_candidates(nc, 24, 8, 4, seed=103)
+    C[min(5, nc - 1), 0] = 1000.0
+    C[nc // 2, 3] = -400.0
+    C[nc - 1, 23] = 2500.0
+    Cd = torch.from_numpy(C).to(device)
+
+    def rec(r):
+        return (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist, r.flags, r.near, r.rel)
+
+    def run():
+        res, logl, logg = pair.acquire(Cd, logs=True)
+        return rec(res), np.asarray(logl).tobytes(), np.asarray(logg).tobytes(), rec(pair.acquire(Cd))
+    inline = run()
+    monkeypatch.setenv("HBX_COMBINE_RESCUE", "0")
+    assert run() == inline
+    monkeypatch.setenv("HBX_SCORE_PAIR", "0")
+    assert run()[:3] == inline[:3]
+    monkeypatch.delenv("HBX_SCORE_PAIR")
+    monkeypatch.delenv("HBX_COMBINE_RESCUE")
+    lref = O.log_pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+    assert np.isfinite(lref[[min(5, nc - 1), nc // 2, nc - 1]]).sum() >= 2  # far, yet finite: rescued
+    if nc * nobs <= 2e6:
+        l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+        g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+        assert inline[0][0] == O.select(l, g)[0]

@@ -18,5 +18,7 @@ import json, sys, glob
 for f in sorted(glob.glob(sys.argv[1] + "/*_?.json")):
     d = json.loads(open(f).read().strip().splitlines()[-1])
     s = d["roofline"]["launch_ms_stats"]
-    print("%-16s median %.4f mean %.4f shortlist %s" % (f.split("/")[-1], s["median"], s["mean"], d["config"]["shortlist"]))
+    c2 = d.get("config2", {})
+    print("%-16s median %.4f mean %.4f shortlist %s step %.4f config2 step %s" % (f.split("/")[-1], s["median"], s["mean"],
+          d["config"]["shortlist"], d["ms_per_step"], c2.get("ms_per_step")))
 PY
