@@ -1145,14 +1145,72 @@ __device__ double exact_pdf(const double* __restrict__ X, int32_t D, const int64
 #ifndef EXACT_ACQ_THREADS
 #define EXACT_ACQ_THREADS 256
 #endif
+// SCAN (a single acquisition of <= EXACT_SCAN_MAX candidates): no shortlist launch before this one -- every
+// block restates kde_shortlist_kernel's predicate over the whole candidate set itself, in index order (a
+// ballot prefix per wave), into its own LDS list; block 0 stores the list, its length and the zeroed marker
+// count for the later kernels.  The final pick does not depend on the list's order (the atomics of the
+// shortlist kernel give none).
+#define EXACT_SCAN_MAX 1024
+struct ExactScan {
+  const float* lo;
+  int64_t Nc;
+  const uint32_t* U;
+  const int32_t* flags;
+  const int32_t* first1;
+  int32_t* list;
+  int32_t* count;
+  int32_t* rescue_cnt;
+};
+template <bool SCAN>
 __global__ __launch_bounds__(EXACT_ACQ_THREADS) void kde_exact_kernel(
     const double* __restrict__ cand, int32_t D,
     const KdeParams* __restrict__ Pg, const double* __restrict__ Xg, const int64_t* __restrict__ rows_g,
     const KdeParams* __restrict__ Pb, const double* __restrict__ Xb, const int64_t* __restrict__ rows_b,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
-    double* __restrict__ exact_l, double* __restrict__ exact_g) {
+    const int32_t* __restrict__ list_in, const int32_t* __restrict__ count, int32_t nbuf, double* __restrict__ part,
+    double* __restrict__ exact_l, double* __restrict__ exact_g, ExactScan sc) {
   __shared__ ExactShared sh;
-  const int cnt = *count;
+  __shared__ int32_t slist[SCAN ? EXACT_SCAN_MAX : 1];
+  __shared__ int32_t swc[EXACT_ACQ_THREADS / 64];
+  int cnt;
+  const int32_t* list = list_in;
+  if constexpr (SCAN) {
+    const float u = hbx_ord2f(sc.U[0]);
+    const bool all = (sc.flags[0] & 1) != 0;
+    const int32_t f1 = sc.first1[0];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int base = 0;
+    for (int64_t c0 = 0; c0 < sc.Nc; c0 += EXACT_ACQ_THREADS) {
+      const int64_t i = c0 + threadIdx.x;
+      bool in = false;
+      if (i < sc.Nc) {
+        const float l = sc.lo[i];
+        in = (l == l && (all || l <= u)) || (int32_t)i == f1;
+      }
+      const uint64_t b = __ballot(in);
+      if (lane == 0) swc[wv] = __popcll(b);
+      __syncthreads();
+      int off = base, tot = 0;
+#pragma unroll
+      for (int w = 0; w < EXACT_ACQ_THREADS / 64; ++w) {
+        off += w < wv ? swc[w] : 0;
+        tot += swc[w];
+      }
+      if (in) slist[off + __popcll(b & ((1ull << lane) - 1))] = (int32_t)i;
+      base += tot;
+      __syncthreads();
+    }
+    cnt = base;
+    list = slist;
+    if (blockIdx.x == 0) {
+      for (int k = threadIdx.x; k < cnt; k += EXACT_ACQ_THREADS) sc.list[k] = slist[k];
+      if (threadIdx.x == 0) {
+        *sc.count = cnt;
+        if (sc.rescue_cnt) *sc.rescue_cnt = 0;
+      }
+    }
+  } else {
+    cnt = *count;
+  }
   const bool split = cnt <= EXACT_SPLIT_CAP;
   const int per = split ? nbuf * PW_SPLIT_UNITS : 1;  // items per (candidate, KDE)
   const int64_t items = (int64_t)cnt * 2 * per;
@@ -1682,6 +1740,13 @@ static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
   return sp < 1 ? 1 : (int)sp;
 }
 
+// the shortlist done by the exact re-score's blocks for few candidates (HBX_EXACT_SCAN=0: its own launch;
+// read per call)
+static bool exact_scan_enabled() {
+  const char* e = getenv("HBX_EXACT_SCAN");
+  return !(e && atoi(e) == 0);
+}
+
 // the rescue pass done by the combine kernel where it can (HBX_COMBINE_RESCUE=0: its own launch; read per
 // call: tests switch it in-process)
 static bool combine_rescue_enabled() {
@@ -2159,13 +2224,19 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
                          eg, Nc, sg, logl_out, logg_out, lo, U, flags, first1, rs);
       HBX_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
-                       batch_res ? segcnt : (int32_t*)nullptr, first1, (int32_t*)(ws + w.rescue));
-    HBX_LAUNCH_CHECK();
+    // a single acquisition of few candidates: the exact re-score's blocks shortlist for themselves
+    const bool scan = !batch_res && Nc <= EXACT_SCAN_MAX && exact_scan_enabled();
+    if (!scan) {
+      hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
+                         batch_res ? segcnt : (int32_t*)nullptr, first1, (int32_t*)(ws + w.rescue));
+      HBX_LAUNCH_CHECK();
+    }
     const int nbuf = (int)((nmax + PW_BUF - 1) / PW_BUF);
-    hipLaunchKernelGGL(kde_exact_kernel, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,
+    const ExactScan esc{lo, Nc, U, flags, first1, list, count, (int32_t*)(ws + w.rescue)};
+    auto ek = scan ? kde_exact_kernel<true> : kde_exact_kernel<false>;
+    hipLaunchKernelGGL(ek, dim3(EXACT_GRID), dim3(EXACT_ACQ_THREADS), 0, s, cand, D,
                        (const KdeParams*)params_good, X_good, rows_good, (const KdeParams*)params_bad, X_bad,
-                       rows_bad, list, count, nbuf, part, exact_l, exact_g);
+                       rows_bad, list, count, nbuf, part, exact_l, exact_g, esc);
     HBX_LAUNCH_CHECK();
     // single acquisition: the final kernel combines the unit sums itself (one launch less)
     fuse_combine = !batch_res && !(exact_only && (logl_out || logg_out));

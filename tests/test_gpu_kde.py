@@ -835,3 +835,44 @@ def test_rescue_in_the_combine_kernel_equals_its_own_launch(device, monkeypatch,
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
         assert inline[0][0] == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("case", ["mixed", "exact_only", "far", "one", "full"])
+def test_exact_scan_equals_the_shortlist_launch(device, monkeypatch, case):
+    """A single acquisition of <= 1024 candidates has no shortlist launch: every exact re-score block
+    shortlists for itself (the shortlist kernel's predicate in index order).  Records, ln-pdf estimates and
+    the exact pdfs equal those of the shortlist launch (HBX_EXACT_SCAN=0) field by field -- every
+    candidate re-scored (exact_only), rescue markers (far), one candidate, the 1024 cap -- and the winner
+    is the oracle's."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, nobs, nc = {"mixed": (24, 8, 3000, 64), "exact_only": (70, 0, 320, 300), "far": (16, 4, 1500, 513),
+                        "one": (8, 4, 900, 1), "full": (8, 12, 2000, 1024)}[case]
+    vt = S.var_type_string(dc, du)
+    X = S.make_observations(nobs, dc, du, 4 if du else 0, seed=111 + dc)
+    pair = kde.fit_pair(X, S.make_losses(nobs, seed=112), vt, dc + du + 1, device=device)
+    C = S.make_candidates(nc, dc, du, 4 if du else 0, seed=113 + nc)
+    if case == "far":
+        C[5, 0] = 1000.0
+        C[nc // 2, dc - 1] = -400.0
+    if case == "exact_only":
+        assert pair.good.exact_only
+        C[:20] = X[pair.good.rows_dev.cpu().numpy()[:20]] + 1e-3
+    Cd = torch.from_numpy(C).to(device)
+
+    def rec(r):
+        return (r.index, r.score, r.pdf_l, r.pdf_g, r.shortlist, r.flags, r.near, r.rel)
+
+    def run():
+        res, logl, logg = pair.acquire(Cd, logs=True)
+        return rec(res), np.asarray(logl).tobytes(), np.asarray(logg).tobytes(), rec(pair.acquire(Cd))
+    scan = run()
+    monkeypatch.setenv("HBX_EXACT_SCAN", "0")
+    assert run() == scan
+    monkeypatch.delenv("HBX_EXACT_SCAN")
+    assert run() == scan  # the workspace after a shortlist launch
+    if nc * nobs <= 2e6:
+        l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
+        g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
+        assert scan[0][0] == O.select(l, g)[0]
