@@ -99,6 +99,12 @@ SIGNATURES = {
     "hbx_kde_logpdf_rtol": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, ctypes.c_double,
                                     c_vp, c_vp, c_i64, c_vp]),
     "hbx_host_free": (c_i32, [c_vp]),
+    "hbx_np_argsort_host": (c_i32, [c_vp, c_i64, c_vp]),
+    "hbx_sh_advance_host": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "hbx_mt_state_bytes": (c_i64, []),
+    "hbx_mt_draw": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp]),
+    "hbx_bohb_draw": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, ctypes.c_double, c_i64, c_vp, c_vp, c_vp, c_vp,
+                              c_vp]),
 }
 
 # tie order of the sorts (include/hbx.h): numpy's unstable argsort (the reference's) or by position

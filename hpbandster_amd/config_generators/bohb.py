@@ -34,7 +34,9 @@ class _MT(object):
     """The raw MT19937 state (key[624] words + position: 2500 bytes) of a legacy ``RandomState`` -- a
     snapshot, compare or restore in ~1 us, where ``get_state`` / ``set_state`` cost ~60 us each (they
     build and parse the state tuple).  The Gaussian cache of the legacy generator is not part of it:
-    BOHB's draws (``rand``, ``randint``, scipy's truncnorm by inversion of a uniform) never touch it."""
+    BOHB's draws (``rand``, ``randint``, scipy's truncnorm by inversion of a uniform) never touch it.
+    The layout is numpy's ``mt19937_state``; ``mt_layout_ok()`` checks it against ``get_state`` /
+    ``set_state`` once per process before anything relies on it."""
     NB = 624 * 4 + 4
 
     def __init__(self, rs):
@@ -50,19 +52,154 @@ class _MT(object):
         ctypes.memmove(self.addr, raw, self.NB)
 
 
+_LAYOUT = [None]
+
+
+def mt_layout_ok():
+    """Once per process: the raw bytes at the bit generator's state address are get_state()'s key words
+    and position, and load() of another state's bytes gives that state's get_state() (and its next
+    draws).  False (never raising) when numpy's layout is not the one assumed: the raw-state users then
+    step aside -- speculative batches are not made, the host draws take scipy's per-element path."""
+    if _LAYOUT[0] is None:
+        try:
+            a, b = np.random.RandomState(20240917), np.random.RandomState(77)
+            a.random_sample(700)  # position off the block boundary
+            ma, mb = _MT(a), _MT(b)
+            st = a.get_state(legacy=True)
+            ok = ma.snap() == np.asarray(st[1], dtype="<u4").tobytes() + np.int32(st[2]).tobytes()
+            mb.load(ma.snap())
+            sb = b.get_state(legacy=True)
+            ok = ok and np.array_equal(sb[1], st[1]) and sb[2] == st[2]
+            ok = ok and np.array_equal(a.random_sample(3), b.random_sample(3))
+            _LAYOUT[0] = bool(ok)
+        except Exception:
+            _LAYOUT[0] = False
+        if not _LAYOUT[0]:
+            logging.getLogger('hpbandster').warning(
+                "numpy's MT19937 state layout is not the assumed one: speculative batches and the fast host draws "
+                "are off (results unchanged)")
+    return _LAYOUT[0]
+
+
 _GLOBAL = [None]
 
 
 def _global_mt():
-    """_MT of numpy's global RandomState (the one np.random.rand / randint / scipy's rvs draw from)."""
+    """_MT of numpy's global RandomState (the one np.random.rand / randint / scipy's rvs draw from), or
+    None when its raw state cannot be used."""
     R = np.random.mtrand._rand
     g = _GLOBAL[0]
     if g is None or g.rs is not R:
+        if not mt_layout_ok():
+            return None
         try:
             g = _GLOBAL[0] = _MT(R)
         except (TypeError, AttributeError):
             return None
     return g
+
+
+_HOSTDRAW = [None]
+
+
+def host_draw_ok():
+    """Once per process: hbx_bohb_draw (libhbx's restatement of the draws, on numpy's own state) agrees with
+    numpy and scipy -- random_sample and randint streams, and a small get_config draw against the
+    per-element scipy path, values and final state bit for bit.  False (never raising) otherwise: the
+    per-element path then runs."""
+    if _HOSTDRAW[0] is None:
+        ok = False
+        try:
+            ok = mt_layout_ok() and int(_native.lib().hbx_mt_state_bytes()) == _MT.NB
+            if ok:
+                L = _native.lib()
+                a, b = np.random.RandomState(5), np.random.RandomState(5)
+                ma = _MT(a)
+                out = np.empty(1500)
+                _native.check(L.hbx_mt_draw(ma.addr, 0, out.size, 0, out.ctypes.data))
+                ok = np.array_equal(out, b.random_sample(out.size))
+                for high in (1, 2, 3, 4, 7, 100, 1000, 65537, 2 ** 31 + 5):
+                    o = np.empty(64)
+                    _native.check(L.hbx_mt_draw(ma.addr, 1, o.size, high, o.ctypes.data))
+                    ok = ok and np.array_equal(o, [b.randint(0, high) for _ in range(o.size)])
+                ok = ok and ma.snap() == _MT(b).snap()
+            if ok:
+                rs = np.random.RandomState(11)
+                data = np.column_stack([rs.rand(9, 3), rs.randint(0, 3, (9, 2))]).astype(np.float64)
+                data[4, 0], data[2, 1] = 0.0, 1.0
+                kde = _HostModel(data, np.array([0.2, 0.05, 0.6, 0.4, 0.9]))
+                lv = np.array([0, 0, 0, 3, 4])
+                a, b = np.random.RandomState(6), np.random.RandomState(6)
+                fast = _draw_fast(kde, lv, 3, 16, a, _MT(a))
+                slow = _draw_rvs(kde, lv, 3, 16, b)
+                ok = np.array_equal(fast, slow) and _MT(a).snap() == _MT(b).snap()
+        except Exception:
+            ok = False
+        _HOSTDRAW[0] = bool(ok)
+        if not ok:
+            logging.getLogger('hpbandster').warning(
+                "hbx_bohb_draw disagrees with numpy/scipy here: BOHB draws candidates element by element")
+    return _HOSTDRAW[0]
+
+
+class _HostModel(object):
+    """The two fields of a KDE the draws read (``data`` rows and ``bw``)."""
+
+    def __init__(self, data, bw):
+        self.data, self.bw = data, bw
+
+
+def _draw_rvs(kde_good, levels, bw_factor, num_samples, R):
+    """bohb.py:133-147 element by element: R.randint for the datum, one scipy truncnorm.rvs per continuous
+    dim (bounds from bw, scale bw_factor * bw), keep-or-resample per categorical dim."""
+    D = len(levels)
+    cands = np.empty((num_samples, D), dtype=np.float64)
+    data = kde_good.data
+    bws = kde_good.bw
+    for i in range(num_samples):
+        idx = R.randint(0, len(data))
+        for d, (m, bw, t) in enumerate(zip(data[idx], bws, levels)):
+            if t == 0:
+                cands[i, d] = sps.truncnorm.rvs(-m / bw, (1 - m) / bw, loc=m, scale=bw_factor * bw, random_state=R)
+            else:
+                if R.rand() < (1 - bw):
+                    cands[i, d] = m
+                else:
+                    cands[i, d] = R.randint(t)
+    return cands
+
+
+def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt):
+    """The same draws in one native call on R's own MT19937 state (hbx_bohb_draw, the reference's
+    consumption order), then ONE vectorised ``truncnorm._ppf`` over the call's uniforms and rvs's
+    ``* scale + loc`` -- the arithmetic rvs applies to each uniform, elementwise, so the values are the
+    per-element path's bit for bit (checked by host_draw_ok and tests/test_host_draw.py).  A domain error
+    raises ValueError with R left where scipy's raise leaves it."""
+    data = kde_good.data
+    if not (isinstance(data, np.ndarray) and data.dtype == np.float64 and data.flags.c_contiguous):
+        data = np.ascontiguousarray(data, dtype=np.float64)
+    bws = np.ascontiguousarray(kde_good.bw, dtype=np.float64)
+    lv = np.ascontiguousarray(levels, dtype=np.int64)
+    n, D = data.shape
+    vals = np.empty((num_samples, D))
+    uni = np.empty((num_samples, D))
+    need = np.empty((num_samples, D), dtype=np.uint8)
+    stop = ctypes.c_int64(-1)
+    with mt.lock:
+        rc = _native.lib().hbx_bohb_draw(mt.addr, data.ctypes.data, n, D, bws.ctypes.data, lv.ctypes.data,
+                                         float(bw_factor), num_samples, vals.ctypes.data, uni.ctypes.data,
+                                         need.ctypes.data, None, ctypes.addressof(stop))
+    if rc == 1:
+        raise ValueError("Domain error in arguments (truncnorm bounds of candidate %d, dim %d; bohb.py:141)"
+                         % divmod(stop.value, D))
+    _native.check(rc)
+    m = need.view(np.bool_)
+    if m.any():
+        h = np.broadcast_to(bws, (num_samples, D))[m]
+        loc = vals[m]
+        y = sps.truncnorm._ppf(uni[m], -loc / h, (1 - loc) / h)
+        vals[m] = y * (bw_factor * h) + loc
+    return vals
 
 
 class SpeculativeBatch(object):
@@ -245,24 +382,19 @@ class BOHB(base_config_generator):
     def sample_candidates(self, kde_good, num_samples, rng=None):
         """bohb.py:133-147: around a random good observation, truncnorm per continuous dim (bounds
         from bw, scale bandwidth_factor * bw), keep-or-resample per categorical dim.  Global RNG (or
-        ``rng``, a RandomState drawn from in the same order)."""
+        ``rng``, a RandomState drawn from in the same order).  One native call for every draw of the call
+        plus one vectorised truncnorm inversion (``_draw_fast``); the values and the RNG's state after the
+        call are the reference's per-element path's bit for bit (``_draw_rvs``, which runs instead when
+        host_draw_ok() finds numpy or scipy not as assumed)."""
         R = np.random.mtrand._rand if rng is None else rng
-        D = len(self.vartypes)
-        cands = np.empty((num_samples, D), dtype=np.float64)
-        data = kde_good.data
-        bws = kde_good.bw
-        for i in range(num_samples):
-            idx = R.randint(0, len(data))
-            for d, (m, bw, t) in enumerate(zip(data[idx], bws, self.vartypes)):
-                if t == 0:
-                    cands[i, d] = sps.truncnorm.rvs(-m / bw, (1 - m) / bw, loc=m, scale=self.bw_factor * bw,
-                                                    random_state=R)
-                else:
-                    if R.rand() < (1 - bw):
-                        cands[i, d] = m
-                    else:
-                        cands[i, d] = R.randint(t)
-        return cands
+        if host_draw_ok():
+            mt = _global_mt() if rng is None else getattr(self, "_rng_mt", (None, None))[1]
+            if mt is None or mt.rs is not R:
+                mt = _MT(R)
+                if rng is not None:
+                    self._rng_mt = (R, mt)
+            return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt)
+        return _draw_rvs(kde_good, self.vartypes, self.bw_factor, num_samples, R)
 
     def draw_candidates(self, pair, num_samples):
         """Candidates of one get_config call (or of several back to back): host numpy array, or with

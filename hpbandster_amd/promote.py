@@ -164,8 +164,9 @@ _MODES = {"numpy": N.ORDER_NUMPY, "stable": N.ORDER_STABLE, N.ORDER_NUMPY: N.ORD
 # a few hundred values (n = 81: 1.9 us against 12.0 us for the GPU round trip and 2.5 us for the reference's
 # argsort(argsort); n = 1000: 3.8 / 12.6 / 12.2 us; n = 4096: 7.2 us against 291 us through the sorting
 # kernels brackets > 1024 take).  Brackets with a tie straddling the k-th place (numpy 1.26.4's unstable
-# order decides them: restated on the device only -- this process's numpy orders 65 of 206 recorded arrays
-# differently), non-finite losses, and larger brackets go to the GPU.
+# order decides them -- this process's numpy orders 65 of 206 recorded arrays differently) and non-finite
+# losses are ranked on the host too, by libhbx's host restatement of that sort (hbx_sh_advance_host);
+# larger brackets go to the GPU.
 HOST_MAX = 1 << 16
 _SORT_MAX = 256  # below: one argsort; above: np.partition (O(n))
 
@@ -201,25 +202,68 @@ def _host_rank(losses, kk, n):
     return losses <= a
 
 
+def _host_rank_ordered(losses, kk, n, ties):
+    """A bracket whose tied losses straddle the k-th place, or with non-finite losses, on the host in the
+    requested tie order: numpy 1.26.4's (hbx_sh_advance_host, the x86-simd-sort / introsort restatement in
+    libhbx's host code) or by position.  As on the device, non-finite losses are CRASHED runs: never
+    ranked, never advanced, and the first min(k, finite count) of the finite losses' argsort advance."""
+    fin = None
+    if not math.isfinite(float(losses.sum())):
+        fin = np.isfinite(losses)
+        sub = np.ascontiguousarray(losses[fin])
+        kk = min(kk, sub.shape[0])
+    else:
+        sub = losses if losses.flags.c_contiguous else np.ascontiguousarray(losses)
+    m = sub.shape[0]
+    if kk == 0 or kk == m:
+        adv = np.full(m, kk == m and m > 0, dtype=bool)
+    else:
+        mode = _MODES.get(ties)
+        if mode is None:
+            mode = N.order_mode(ties)
+        if mode == N.ORDER_STABLE:
+            adv = np.zeros(m, dtype=bool)
+            adv[np.argsort(sub, kind="stable")[:kk]] = True
+        else:
+            hb = getattr(_tls, "host", None)
+            if hb is None or hb[0] < m:  # per-thread output and scratch, their addresses taken once
+                cap = max(1024, 1 << (m - 1).bit_length())
+                a, sc = np.empty(cap, dtype=np.bool_), np.empty(cap, dtype=np.int64)
+                hb = _tls.host = (cap, a, sc, a.ctypes.data, sc.ctypes.data, N.lib().hbx_sh_advance_host)
+            rc = hb[5](sub.ctypes.data, m, kk, hb[3], hb[4])
+            if rc:
+                N.check(rc)
+            adv = hb[1][:m].copy()
+    if fin is None:
+        return adv
+    out = np.zeros(n, dtype=bool)
+    out[fin] = adv
+    return out
+
+
 def advance_mask(losses, k, device=None, stream=None, ties="numpy", policy="auto"):
     """Single bracket: bool mask of the configurations that advance (HB_iteration.py:180-182).
 
     What SuccessiveHalving.process_results calls once per bracket.  ``policy='auto'``: brackets of at most
-    HOST_MAX configurations whose k-th place is not inside a run of tied losses are ranked on the host
-    (identical mask, see HOST_MAX); the rest -- and everything with ``policy='gpu'`` -- on the GPU: the
-    losses are copied into device-mapped host memory, ONE host call into libhbx (hbx_sh_advance_state)
-    launches the one-kernel promotion (the selection, and the numpy-order re-rank when tied losses straddle
-    the k-th place), spins on the kernel's completion word (stored last) instead of synchronising the
-    stream, and the mask is copied out."""
+    HOST_MAX configurations are ranked on the host -- tie-free ones by numpy's argsort / partition (any sort
+    gives the same first k), ones with tied losses across the k-th place or non-finite losses by libhbx's
+    host restatement of numpy 1.26.4's sort (hbx_sh_advance_host) -- because one GPU round trip costs more
+    than the sort.  Larger brackets, and everything with ``policy='gpu'``, go to the GPU: the losses are
+    copied into device-mapped host memory, ONE host call into libhbx (hbx_sh_advance_state) launches the
+    one-kernel promotion (the selection, and the numpy-order re-rank when tied losses straddle the k-th
+    place), spins on the kernel's completion word (stored last) instead of synchronising the stream, and the
+    mask is copied out."""
     if type(losses) is not np.ndarray or losses.ndim != 1 or losses.dtype != np.float64:
         losses = np.asarray(losses, dtype=np.float64).reshape(-1)
     n = losses.shape[0]
     if n == 0:
         return np.zeros(0, dtype=bool)
     if policy == "auto" and n <= HOST_MAX:
-        m = _host_rank(losses, _threshold(k, n), n)
-        if m is not None:
-            return m
+        kk = _threshold(k, n)
+        m = _host_rank(losses, kk, n)
+        if m is None:
+            m = _host_rank_ordered(losses, kk, n, ties)
+        return m
     elif policy not in ("auto", "gpu"):
         raise ValueError("policy must be 'auto' or 'gpu'")
     if n > 1024:

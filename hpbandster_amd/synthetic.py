@@ -55,6 +55,26 @@ def make_candidates(n_cand, dc, du, levels, seed=SEED_CAND):
     return make_points(np.random.RandomState(seed), n_cand, dc, du, levels)
 
 
+CAND_BLOCK = 1 << 16
+
+
+def make_candidates_blocked(lo, hi, dc, du, levels, seed=SEED_CAND):
+    """Rows [lo, hi) of an unbounded seeded candidate stream: block b (rows b*CAND_BLOCK ...) is
+    ``make_points(RandomState([seed, b]), CAND_BLOCK, ...)``.  Any slice is reproducible without drawing
+    the rows before it, so every rank of a sharded run draws only its own shard, the weak-scaling set at N
+    ranks (rank r: rows [r Nc, (r+1) Nc)) is a prefix of config #4's 1e7 set, and the oracle's full-size
+    winners (tests/golden/full_winners.json) cover every rank count from one scan."""
+    if hi < lo or lo < 0:
+        raise ValueError("bad row range")
+    out = np.empty((hi - lo, dc + du))
+    b0, b1 = lo // CAND_BLOCK, (hi + CAND_BLOCK - 1) // CAND_BLOCK
+    for b in range(b0, b1):
+        blk = make_points(np.random.RandomState([seed, b]), CAND_BLOCK, dc, du, levels)
+        r0, r1 = max(lo, b * CAND_BLOCK), min(hi, (b + 1) * CAND_BLOCK)
+        out[r0 - lo:r1 - lo] = blk[r0 - b * CAND_BLOCK:r1 - b * CAND_BLOCK]
+    return out
+
+
 def var_type_string(dc, du):
     return "c" * dc + "u" * du
 

@@ -386,6 +386,36 @@ int hbx_sh_advance_state(int64_t* state, int64_t n, double k, void* stream);
 int hbx_host_alloc(int64_t bytes, void** out);
 int hbx_host_free(void* p);
 
+/* ---- numpy's argsort on the host (hbx_npsort_host.cpp) ------------------------------------------------
+ * hbx_np_argsort_host: np.argsort(x) of numpy 1.26.4 on an AVX-512 host (x86-simd-sort avx512_argsort<double>,
+ *   std::sort with NaN last when a NaN is present), ties in its order; host x[n] -> host order[n].
+ * hbx_sh_advance_host: one bracket's HB_iteration.py:180-182 on the host: advance[i] = argsort(argsort(loss))[i]
+ *   < k, i.e. the first k positions of that argsort; host loss[n], advance u8[n], scratch i64[n].
+ *   Replaces np.argsort(np.argsort(losses)) < num_configs[SH_iter] of SuccessiveHalving.process_results for
+ *   one bracket whose tied losses straddle the k-th place (hbx_sh_promote_ex ranks batched brackets). */
+int hbx_np_argsort_host(const double* x, int64_t n, int64_t* order);
+int hbx_sh_advance_host(const double* loss, int64_t n, int64_t k, uint8_t* advance, int64_t* scratch);
+
+/* ---- BOHB's candidate draws on the host (bohb.py:133-147), the reference's RNG stream -------------
+ * Host code (hbx_draw.cpp), no device work.  `state` is the MT19937 state a legacy numpy RandomState
+ * holds (uint32 key[624] followed by int pos: hbx_mt_state_bytes() bytes, e.g. the global generator's
+ * bit_generator.ctypes.state_address, held under that generator's lock); the draws continue its stream
+ * exactly as the reference's calls would.
+ * hbx_mt_draw: n draws of random_sample() (kind 0) or randint(0, high) (kind 1) into out (self-checks).
+ * hbx_bohb_draw: one get_config call's draws -- per candidate randint(0, n) for the datum (bohb.py:135),
+ *   then per dim of data[idx] (host f64[n][D]): levels[d] == 0 (continuous): scipy truncnorm.rvs's domain
+ *   check (a = -m/bw < b = (1-m)/bw, scale = bw_factor bw >= 0; on failure *stop = element, return 1, the
+ *   state left as the reference's raise leaves it), loc returned when scale == 0, else ONE uniform into
+ *   uni[e] with need_ppf[e] = 1 and vals[e] = m (the caller computes truncnorm._ppf(uni, a, b) * scale + m,
+ *   the rest of rvs); levels[d] > 0: rand() < 1 - bw keeps m, else randint(levels[d]) (bohb.py:144-147).
+ *   vals/uni: host f64[num_samples][D]; need_ppf: host u8[num_samples][D]; datum: host i64[num_samples]
+ *   (nullable).  Replaces the scalar draw loop of bohb.py:133-147 (the scoring moved to hbx_kde_acquire). */
+int64_t hbx_mt_state_bytes(void);
+int hbx_mt_draw(void* state, int32_t kind, int64_t n, int64_t high, double* out);
+int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const double* bw, const int64_t* levels,
+                  double bw_factor, int64_t num_samples, double* vals, double* uni, uint8_t* need_ppf,
+                  int64_t* datum, int64_t* stop);
+
 #ifdef __cplusplus
 }
 #endif

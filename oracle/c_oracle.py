@@ -31,6 +31,8 @@ def lib():
         L.oracle_bohb_select.argtypes = [vp, vp, i64, vp]
         L.oracle_bohb_select.restype = i64
         L.oracle_max_threads.restype = i32
+        L.oracle_kde_pdf_screen.argtypes = [vp, i64, i32, vp, vp, vp, vp, i64, vp, vp, i32]
+        L.oracle_kde_pdf_screen.restype = i32
         _lib = L
     return _lib
 
@@ -56,6 +58,24 @@ def kde_pdf(data, bw, var_type, nlev, pts, nthreads=0, exact=False):
                               nlev.ctypes.data, pts.ctypes.data, pts.shape[0], out.ctypes.data, int(nthreads),
                               1 if exact else 0)
     return out
+
+
+def kde_pdf_screen(data, bw, var_type, nlev, pts, nthreads=0):
+    """Screening pdf (one libm exp per pair, kde_oracle.c:oracle_kde_pdf_screen) and its per-point
+    relative bound against the exact mode; None when a categorical kernel is not positive."""
+    data = np.ascontiguousarray(data, dtype=np.float64)
+    pts = np.ascontiguousarray(np.atleast_2d(pts), dtype=np.float64)
+    vt = np.array([0 if c == "c" else 1 for c in var_type], dtype=np.int32)
+    bw = np.ascontiguousarray(bw, dtype=np.float64)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    out = np.empty(pts.shape[0])
+    rel = np.empty(pts.shape[0])
+    rc = lib().oracle_kde_pdf_screen(data.ctypes.data, data.shape[0], data.shape[1], vt.ctypes.data, bw.ctypes.data,
+                                     nlev.ctypes.data, pts.ctypes.data, pts.shape[0], out.ctypes.data,
+                                     rel.ctypes.data, int(nthreads))
+    if rc != 0:
+        return None
+    return out, rel
 
 
 def bohb_select(pdf_l, pdf_g):

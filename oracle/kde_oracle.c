@@ -78,6 +78,65 @@ void oracle_kde_pdf(const double* data, int64_t n, int32_t D, const int32_t* var
   oracle_kde_pdf_mode(data, n, D, vartype, bw, nlev, pts, Np, out, nthreads, 0);
 }
 
+/* Screening pdf for the full-size winner scans (tests/golden/gen_full_winners.py): the same density
+ * with the continuous kernels' exponents summed first and ONE libm exp per pair,
+ *   term_j = exp(sum_c a_jd) * INV_SQRT_2PI^Dc * prod_u k_jd / prod_bw_c,   a_jd as in the exact mode,
+ * sequential sum over j.  Against the exact mode every term differs by a relative
+ * |sum_c a_jd| * (Dc + 2) * 2^-52 + (D + 4) * 2^-52 at most (rounding of the exponent sum and of the
+ * products; 4 ulp allowed per exp), and the sum of same-signed terms keeps the largest term's bound plus the
+ * two summation orders' n ulp each; the bound is returned per point in rel_out (nullable).  Only for KDEs whose categorical kernels are all positive
+ * (1 - h > 0, h > 0): returns -1 otherwise and writes nothing. */
+int32_t oracle_kde_pdf_screen(const double* data, int64_t n, int32_t D, const int32_t* vartype, const double* bw,
+                              const int32_t* nlev, const double* pts, int64_t Np, double* out, double* rel_out,
+                              int32_t nthreads) {
+  int dc = 0, du = 0;
+  int cidx[512], uidx[512];
+  if (D > 512) return -2;
+  double prod_bw_c = 1.0, c_norm = 1.0, inv2h2[512], kmatch[512], kmis[512];
+  for (int d = 0; d < D; ++d) {
+    if (vartype[d] == 0) {
+      prod_bw_c *= bw[d];
+      c_norm *= INV_SQRT_2PI;
+      inv2h2[dc] = (bw[d] * bw[d]) * 2.;
+      cidx[dc++] = d;
+    } else {
+      if (!(bw[d] > 0.0 && 1. - bw[d] > 0.0) || nlev[d] < 2) return -1;
+      kmatch[du] = 1. - bw[d];
+      kmis[du] = bw[d] / (double)(nlev[d] - 1);
+      uidx[du++] = d;
+    }
+  }
+  const double scale = c_norm / prod_bw_c;
+  const double eps = 2.220446049250313e-16;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+  for (int64_t p = 0; p < Np; ++p) {
+    const double* x = pts + p * D;
+    double acc = 0.0, worst = 0.0;
+    for (int64_t j = 0; j < n; ++j) {
+      const double* xr = data + j * D;
+      double a = 0.0, aa = 0.0;
+      for (int k = 0; k < dc; ++k) {
+        const double diff = xr[cidx[k]] - x[cidx[k]];
+        const double t = -(diff * diff) / inv2h2[k];
+        a += t;
+        aa -= t;
+      }
+      double prod = exp(a) * scale;
+      for (int k = 0; k < du; ++k) prod *= (xr[uidx[k]] == x[uidx[k]]) ? kmatch[k] : kmis[k];
+      acc += prod;
+      if (aa > worst) worst = aa;
+    }
+    out[p] = acc / (double)n;
+    /* exponent sum (dc terms) + exp (libm and numpy's, 4 ulp each allowed) + the products (D + 4 roundings)
+       + sequential vs pairwise summation (n ulp each) */
+    if (rel_out) rel_out[p] = worst * (dc + 2) * eps + 4.0 * (D + 4) * eps + 2.0 * (double)n * eps;
+  }
+  return 0;
+}
+
 /* numpy 1.26.4's exp (SVML), element-wise: for the oracle's own known-answer tests */
 void oracle_np_exp(const double* x, int64_t n, double* y) {
   for (int64_t i = 0; i < n; ++i) y[i] = np_exp(x[i]);

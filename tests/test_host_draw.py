@@ -1,0 +1,126 @@
+"""CPU: BOHB's candidate draws on the host (bohb.py:133-147) through hbx_bohb_draw + one vectorised
+truncnorm inversion, against the reference's element-by-element path (np.random.randint / rand and one
+scipy truncnorm.rvs per continuous element): the candidate values bit for bit, the RNG's state after the
+call byte for byte, and domain errors at the same element with the same state."""
+import numpy as np
+import pytest
+
+from hpbandster_amd.config_generators import bohb as B
+
+
+def _model(rs, n, dc, du, levels, bw_c=None, bw_u=None):
+    data = np.column_stack([rs.rand(n, dc)] + [rs.randint(0, l, n) for l in levels]).astype(np.float64)
+    bw = np.concatenate([rs.uniform(0.01, 0.6, dc) if bw_c is None else np.full(dc, bw_c),
+                         rs.uniform(0.05, 1.2, du) if bw_u is None else np.full(du, bw_u)])
+    return B._HostModel(np.ascontiguousarray(data), bw), np.array([0] * dc + list(levels))
+
+
+def _both(kde, lv, ns, seed, bw_factor=3):
+    a, b = np.random.RandomState(seed), np.random.RandomState(seed)
+    ea = eb = None
+    try:
+        fa = B._draw_fast(kde, lv, bw_factor, ns, a, B._MT(a))
+    except ValueError as e:
+        fa, ea = None, e
+    try:
+        fb = B._draw_rvs(kde, lv, bw_factor, ns, b)
+    except ValueError as e:
+        fb, eb = None, e
+    return fa, fb, ea, eb, B._MT(a).snap() == B._MT(b).snap()
+
+
+def test_checks_pass_here():
+    assert B.mt_layout_ok()
+    assert B.host_draw_ok()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_models_bit_identical(seed):
+    rs = np.random.RandomState(100 + seed)
+    dc, du = int(rs.randint(0, 9)), int(rs.randint(0, 5))
+    if dc + du == 0:
+        dc = 1
+    levels = list(rs.randint(1, 6, du))
+    kde, lv = _model(rs, int(rs.randint(1, 60)), dc, du, levels)
+    fa, fb, ea, eb, same_state = _both(kde, lv, int(rs.randint(1, 40)), seed)
+    assert ea is None and eb is None
+    assert np.array_equal(fa, fb)
+    assert same_state
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_config3_dims_bit_identical(seed):
+    """get_config's real size at config #3's dims: 64 candidates, 24c + 8u (4 levels), 400 observations."""
+    rs = np.random.RandomState(7 + seed)
+    kde, lv = _model(rs, 400, 24, 8, [4] * 8)
+    fa, fb, ea, eb, same_state = _both(kde, lv, 64, seed)
+    assert ea is None and eb is None and np.array_equal(fa, fb) and same_state
+
+
+def test_tails_and_edges():
+    """Data at 0 and 1 with tiny and large bandwidths (both tails of truncnorm._ppf), a bandwidth factor
+    other than 3, categorical bandwidths > 1 (always resampled) and = 0 (always kept), one level."""
+    rs = np.random.RandomState(3)
+    data = np.array([[0.0, 1.0, 1e-12, 1 - 1e-12, 2.0, 0.0],
+                     [1.0, 0.0, 0.5, 0.999, 1.0, 0.0],
+                     [0.3, 0.7, 1e-300, 0.5, 0.0, 0.0]])
+    for bwc in (1e-6, 1e-3, 0.3, 5.0, 1e3):
+        kde = B._HostModel(data, np.array([bwc, bwc * 2, bwc / 3, bwc, 1.7, 0.0]))
+        lv = np.array([0, 0, 0, 0, 3, 1])
+        for f in (3, 1, 2.5):
+            fa, fb, ea, eb, same = _both(kde, lv, 50, int(rs.randint(1 << 30)), bw_factor=f)
+            assert ea is None and eb is None and np.array_equal(fa, fb) and same, (bwc, f)
+
+
+@pytest.mark.parametrize("case", ["zero_bw_interior", "zero_bw_at_0", "zero_bw_at_1", "nan_bw"])
+def test_domain_errors_and_zero_scale(case):
+    """scipy's rvs: a zero bandwidth with 0 < m < 1 returns loc without a draw; m = 0 or 1 with a zero
+    bandwidth (a NaN bound) and NaN bandwidths raise before drawing -- at the same element, with the same
+    RNG state left behind, as the reference's loop."""
+    rs = np.random.RandomState(9)
+    data = np.column_stack([rs.rand(20, 3), rs.randint(0, 3, 20)]).astype(np.float64)
+    bw = np.array([0.2, 0.3, 0.1, 0.5])
+    if case == "zero_bw_interior":
+        bw[1] = 0.0
+    elif case == "zero_bw_at_0":
+        bw[1] = 0.0
+        data[::3, 1] = 0.0
+    elif case == "zero_bw_at_1":
+        bw[2] = 0.0
+        data[::4, 2] = 1.0
+    else:
+        bw[0] = np.nan
+    kde = B._HostModel(np.ascontiguousarray(data), bw)
+    lv = np.array([0, 0, 0, 3])
+    with np.errstate(all="ignore"):
+        fa, fb, ea, eb, same = _both(kde, lv, 30, 4)
+    assert same
+    if case == "zero_bw_interior":
+        assert ea is None and eb is None and np.array_equal(fa, fb)
+        assert np.isin(fa[:, 1], data[:, 1]).all()  # loc itself, no draw
+    else:
+        assert ea is not None and eb is not None
+
+
+def test_sample_candidates_uses_the_global_rng_like_the_reference():
+    """BOHB.sample_candidates on the global RNG: the same values and global state as the per-element path
+    on a copy of the global state."""
+    from hpbandster_amd import configspace as CS
+    space = CS.ConfigurationSpace(seed=1)
+    for i in range(5):
+        space.add_hyperparameter(CS.UniformFloatHyperparameter("x%d" % i, lower=0, upper=1))
+    space.add_hyperparameter(CS.CategoricalHyperparameter("y", ["a", "b", "c"]))
+    cg = B.BOHB(space)
+    rs = np.random.RandomState(2)
+    kde = B._HostModel(np.column_stack([rs.rand(30, 5), rs.randint(0, 3, 30)]).astype(np.float64),
+                       np.array([0.1, 0.2, 0.3, 0.15, 0.25, 0.4]))
+    np.random.seed(12)
+    copy = np.random.RandomState(12)
+    got = cg.sample_candidates(kde, 64)
+    want = B._draw_rvs(kde, cg.vartypes, cg.bw_factor, 64, copy)
+    assert np.array_equal(got, want)
+    assert B._global_mt().snap() == B._MT(copy).snap()
+    # and with a private RandomState (the speculative batches' draws)
+    r1, r2 = np.random.RandomState(44), np.random.RandomState(44)
+    assert np.array_equal(cg.sample_candidates(kde, 10, rng=r1), B._draw_rvs(kde, cg.vartypes, 3, 10, r2))
+    assert B._MT(r1).snap() == B._MT(r2).snap()
