@@ -216,6 +216,52 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     return out
 
 
+def reference_loop_baseline(device, n_obs=400, dims=(24, 8), calls=3):
+    """CPU baseline of the one-worker loop at default sizes (VERDICT r04 missing #3), the reference's own
+    arithmetic on one core: a model-based get_config = bohb.py:133-152 -- the per-element draws (one scipy
+    truncnorm.rvs per continuous element, rand / randint per categorical one) and KDEMultivariate.pdf of l
+    and g per candidate (statsmodels is not installed on the box: oracle.kde_oracle.pdf, its numpy
+    restatement, bit-identical on every golden fixture) -- and a refit = bohb.py:220-246 (np.argsort, the
+    good / bad rows, 1.06 std n^(-1/(4+D)), np.unique level counts).  Beside bench's
+    sh_stage_interleaved_host_sampler (the drop-in on the same loop shape)."""
+    from oracle import kde_oracle as O
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    from hpbandster_amd.config_generators import bohb as Bm
+    D = sum(dims)
+    vt = S.var_type_string(*dims)
+    X = S.make_observations(n_obs, dims[0], dims[1], 4, seed=51)
+    Lo = S.make_losses(n_obs, seed=52)
+    pair = kde.fit_pair(X, Lo, vt, D + 1, device=device)
+    good = Bm._HostModel(X[pair.good.rows_dev.cpu().numpy()], pair.good.bw)
+    Xb = X[pair.bad.rows_dev.cpu().numpy()]
+    lv = np.array([0] * dims[0] + [4] * dims[1])
+    R = np.random.RandomState(5)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        cands = Bm._draw_rvs(good, lv, 3, 64, R)
+        best, bi = np.inf, -1
+        for i in range(64):
+            v = O.py_score(O.pdf(good.data, good.bw, vt, cands[i]), O.pdf(Xb, pair.bad.bw, vt, cands[i]))
+            if v < best:
+                best, bi = v, i
+    get_ms = (time.perf_counter() - t0) / calls * 1e3
+    t0 = time.perf_counter()
+    for _ in range(10):
+        idx = np.argsort(Lo)
+        ng, nb = kde.bohb_split_sizes(n_obs, D + 1)
+        for rows, n in ((idx[:ng], ng), (idx[-nb:], nb)):
+            data = X[rows]
+            bw = 1.06 * np.std(data, axis=0) * n ** (-1. / (4 + D))
+            lev = [np.unique(data[:, d]).size for d in range(D) if vt[d] == "u"]
+    refit_ms = (time.perf_counter() - t0) / 10 * 1e3
+    return {"workload": "one_worker_loop_d%d_obs%d_64cand" % (D, n_obs), "cores": 1,
+            "ms_per_model_based_get_config": get_ms, "ms_per_refit": refit_ms,
+            "ms_per_request_at_random_fraction_1_3": 2. / 3 * get_ms + refit_ms,
+            "kind": "reference arithmetic in numpy/scipy on one core (KDEMultivariate.pdf as its numpy restatement)",
+            "sample": "%d model-based get_config calls, 10 refits" % calls}
+
+
 def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     """Secondary line: BASELINE config #5, batched successive-halving promotion (eta=3 -> k=333) over
     B brackets x n configs (fp64 losses resident in HBM) plus one batched KDE refit of every bracket
@@ -349,22 +395,50 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
     return out
 
 
-def device_candidates(total, lo, hi, dc, du, levels, device, seed=44):
-    """Rows [lo, hi) of a seeded set of `total` candidates drawn on the device (U[0,1) continuous,
-    U{0..L-1} categorical): the whole set is drawn on every rank and sliced, so a sharded run scores the
-    same candidates at every rank count (its winner cannot depend on N)."""
+def blocked_candidates(lo, hi, dc, du, levels, device):
+    """Rows [lo, hi) of the seeded candidate stream (synthetic.make_candidates_blocked: U[0,1) continuous,
+    U{0..L-1} categorical, block b of 65536 rows from RandomState([3, b])), drawn on the host and moved to
+    the device.  Any slice is drawn without the rows before it, so every rank draws only its own shard, the
+    weak set at N ranks is the first N x 1e6 rows and config #4 is the first 1e7 -- the sets whose winners
+    the C oracle pinned at full size (tests/golden/full_winners.json)."""
     import torch
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    C = torch.empty((total, dc + du), dtype=torch.float64, device=device)
-    C[:, :dc] = torch.rand((total, dc), dtype=torch.float64, device=device, generator=g)
-    if du:
-        C[:, dc:] = torch.randint(0, levels, (total, du), device=device, generator=g).to(torch.float64)
-    if lo == 0 and hi == total:
-        return C
-    out = C[lo:hi].clone()
-    del C
-    return out
+    from hpbandster_amd import synthetic as S
+    return torch.from_numpy(S.make_candidates_blocked(lo, hi, dc, du, levels)).to(device)
+
+
+_PINNED = [None]
+
+
+def pinned_winners():
+    """tests/golden/full_winners.json (data: the C oracle's full-size winners, tests/golden/gen_full_winners.py)."""
+    if _PINNED[0] is None:
+        try:
+            with open(os.path.join(ROOT, "tests", "golden", "full_winners.json")) as fh:
+                _PINNED[0] = json.load(fh)
+        except (OSError, ValueError):
+            _PINNED[0] = {}
+    return _PINNED[0]
+
+
+def winner_check(entry, index, score, pdf_l=None, pdf_g=None):
+    """The acquisition's winner against a pinned one: index, score (and the pdfs when given) bit for bit.
+    None when nothing is pinned for this workload."""
+    if not entry:
+        return None
+    ok = index == entry["winner"] and float(score).hex() == entry["score_hex"]
+    if pdf_l is not None:
+        ok = ok and float(pdf_l).hex() == entry["pdf_l_hex"] and float(pdf_g).hex() == entry["pdf_g_hex"]
+    return {"winner_ok": bool(ok), "pinned_winner": entry["winner"], "pinned_score": entry["score"],
+            "pinned_margin_rel": entry["margin_rel"], "pinned_by": "tests/golden/full_winners.json (C oracle, %s)"
+                                                                 % ("exact over every candidate" if not entry.get("screen")
+                                                                    else "screen + exact re-score")}
+
+
+def pinned_prefix(n, dc, du, levels, obs):
+    """The pinned entry of the blocked stream's first n rows at config #3's model, if any."""
+    if (dc, du, levels, obs) != (24, 8, 4, 10_000):
+        return None
+    return pinned_winners().get("config3_prefixes", {}).get("prefix_%d" % n)
 
 
 def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
@@ -376,7 +450,7 @@ def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
     import torch
     from hpbandster_amd import kde
     from hpbandster_amd.distributed import reduce_records_host, shard_range
-    C = device_candidates(Nc, 0, Nc, dc, du, levels, device)
+    C = blocked_candidates(0, Nc, dc, du, levels, device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     r = pair.acquire(C, workspace=ws)
     torch.cuda.synchronize()
@@ -393,10 +467,17 @@ def config4_line(pair, device, dc, du, levels, Nc=10_000_000, shards=8, reps=3):
     del C, ws
     torch.cuda.empty_cache()
     pairs = Nc * (pair.good.nobs + pair.bad.nobs)
-    return {"workload": "kde_acquisition_d%d_%dc%du_obs%d_cand%d_one_gpu" % (dc + du, dc, du,
-                                                                           pair.good.nobs + pair.bad.nobs, Nc),
-            "value": pairs / el, "unit": "pairs/s", "ms_per_acquisition": el * 1e3, "winner": r.index,
-            "winner_8_shards": sharded, "winners_identical": r.index == sharded, "shortlist": r.shortlist}
+    out = {"workload": "kde_acquisition_d%d_%dc%du_obs%d_cand%d_one_gpu" % (dc + du, dc, du,
+                                                                          pair.good.nobs + pair.bad.nobs, Nc),
+           "value": pairs / el, "unit": "pairs/s", "ms_per_acquisition": el * 1e3, "winner": r.index,
+           "winner_8_shards": sharded, "winners_identical": r.index == sharded, "shortlist": r.shortlist,
+           "candidates": "rows [0, %d) of synthetic.make_candidates_blocked (seed 3)" % Nc}
+    chk = winner_check(pinned_prefix(Nc, dc, du, levels, pair.good.nobs + pair.bad.nobs), r.index, r.score,
+                       r.pdf_l, r.pdf_g)
+    if chk:
+        chk["winner_ok"] = chk["winner_ok"] and sharded == r.index
+        out.update(chk)
+    return out
 
 
 def strong_line(pair, device, a, rank, world, dist, xchg, reps=10):
@@ -409,7 +490,7 @@ def strong_line(pair, device, a, rank, world, dist, xchg, reps=10):
     from hpbandster_amd.distributed import shard_range
     lo, hi = shard_range(a.strong_total, rank, world)
     Nc = hi - lo
-    C = device_candidates(a.strong_total, lo, hi, a.dc, a.du, a.levels, device)
+    C = blocked_candidates(lo, hi, a.dc, a.du, a.levels, device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
 
     def step():
@@ -433,9 +514,13 @@ def strong_line(pair, device, a, rank, world, dist, xchg, reps=10):
     del C, ws
     torch.cuda.empty_cache()
     pairs = a.strong_total * (pair.good.nobs + pair.bad.nobs)
-    return {"workload": "kde_acquisition_d%d_obs%d_total%d_sharded" % (a.dc + a.du, a.obs, a.strong_total),
-            "scaling": "strong", "value": pairs * reps / el, "unit": "pairs/s", "ms_per_step": el / reps * 1e3,
-            "candidates_per_rank": Nc, "ranks": world, "winner": r.index}
+    out = {"workload": "kde_acquisition_d%d_obs%d_total%d_sharded" % (a.dc + a.du, a.obs, a.strong_total),
+           "scaling": "strong", "value": pairs * reps / el, "unit": "pairs/s", "ms_per_step": el / reps * 1e3,
+           "candidates_per_rank": Nc, "ranks": world, "winner": r.index}
+    chk = winner_check(pinned_prefix(a.strong_total, a.dc, a.du, a.levels, a.obs), r.index, r.score)
+    if chk:
+        out.update(chk)
+    return out
 
 
 def promote_dropin(device, n=1000, reps=50):
@@ -603,6 +688,7 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False, sample
                                                                   "_interleaved" if interleaved else "",
                                                                   "_host_sampler" if sampler == "host" else ""),
             "ms_sequential": res[False][0] * 1e3, "ms_batched": res[True][0] * 1e3,
+            "ms_per_request": res[True][0] * 1e3 / stage,
             "sequential_is": "speculative='never': one draw + acquisition per call, nothing computed ahead",
             "speedup": res[False][0] / res[True][0], "proposals_identical": res[False][1] == res[True][1],
             "note": ("SuccessiveHalving.get_next_run x %d, each followed by its result (new_result + refit); "
@@ -612,6 +698,69 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False, sample
                     ("SuccessiveHalving.get_next_run x %d without results in between (a filled job queue); "
                      "batched = the default drop-in: speculative batches of 1, 2, 4, ... (hbx_kde_acquire_batch), "
                      "the first call computed ahead" % stage)}
+
+
+def _space_and_jobs(dims, levels=4):
+    from hpbandster_amd import configspace as CS
+
+    class Job(object):
+        pass
+
+    def job(cid, cfg, loss):
+        j = Job()
+        j.id, j.exception, j.timestamps = cid, None, {}
+        j.kwargs = {"config": cfg, "budget": 1.0}
+        j.result = {"loss": float(loss), "info": None}
+        return j
+
+    space = CS.ConfigurationSpace(seed=3)
+    for i in range(dims[0]):
+        space.add_hyperparameter(CS.UniformFloatHyperparameter("x%02d" % i, lower=0, upper=1))
+    for i in range(dims[1]):
+        space.add_hyperparameter(CS.CategoricalHyperparameter("y%02d" % i, ["abcdefgh"[j] for j in range(levels)]))
+    return CS, space, job
+
+
+def get_config_line(device, n_obs=400, dims=(24, 8), calls=30, slow_calls=3):
+    """Side line: the DEFAULT drop-in's get_config -- BOHB(space) with the host sampler,
+    num_samples=64, bohb.py's draws from the global numpy RNG -- at config #3's dims (24c + 8u) against a
+    400-observation model, ms per model-based call (random_fraction=0, so every call samples and scores):
+    the draws made by hbx_bohb_draw on numpy's own MT19937 state + one vectorised truncnorm inversion,
+    against the same BOHB with the per-element scipy path the reference runs (bohb.py:133-147: one
+    truncnorm.rvs per continuous element); the proposals and the global RNG's state must be identical."""
+    from hpbandster_amd.config_generators import BOHB
+    from hpbandster_amd.config_generators import bohb as Bm
+    from hpbandster_amd import synthetic as S
+    CS, space, job = _space_and_jobs(dims)
+    cg = BOHB(space, device=device, random_fraction=0.0)
+    X = S.make_observations(n_obs, dims[0], dims[1], 4, seed=51)
+    Lo = S.make_losses(n_obs, seed=52)
+    for i in range(n_obs):
+        cg.new_result(job((0, 0, i), CS.Configuration(space, vector=X[i]).get_dictionary(), Lo[i]))
+
+    def run(k):
+        np.random.seed(5)
+        t0 = time.perf_counter()
+        out = [cg.get_config(1.0)[0] for _ in range(k)]
+        return (time.perf_counter() - t0) / k, out, Bm._global_mt().snap()
+
+    assert Bm.host_draw_ok()
+    run(2)
+    fast, cf, sf = run(calls)
+    saved = Bm._HOSTDRAW[0]
+    try:
+        Bm._HOSTDRAW[0] = False  # the per-element scipy path
+        slow, cs, ss = run(slow_calls)
+    finally:
+        Bm._HOSTDRAW[0] = saved
+    _, cf3, sf3 = run(slow_calls)
+    return {"workload": "get_config_default_d%d_obs%d_64cand" % (sum(dims), n_obs), "ms_per_call": fast * 1e3,
+            "ms_per_call_per_element_draws": slow * 1e3, "speedup": slow / fast,
+            "proposals_identical": cs == cf3, "global_rng_identical": ss == sf3,
+            "model_based_calls": calls,
+            "note": "BOHB defaults (host sampler, num_samples=64) with random_fraction=0; per_element = bohb.py's "
+                    "scipy truncnorm.rvs per continuous element (what the reference's get_config draws), the rest "
+                    "of the call identical (GPU acquisition)"}
 
 
 def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
@@ -691,8 +840,9 @@ def config2_line(device, reps=50):
     lm = float(np.median(launch))
     fpp = 3 * 8 + 4  # 3 Dc + 2 Du + 4 flops per pair
     tf = fpp * pairs / (lm * 1e-3) / 1e12
+    chk = winner_check(pinned_winners().get("config2"), r.index, r.score, r.pdf_l, r.pdf_g) or {}
     return {"workload": "kde_acquisition_d8_8c_obs1000_cand100000", "value": pairs / el, "unit": "pairs/s",
-            "ms_per_step": el * 1e3, "winner": r.index, "variant": int(pair.bad.variant),
+            "ms_per_step": el * 1e3, "winner": r.index, "variant": int(pair.bad.variant), **chk,
             "scoring_launch_ms": lm, "step_minus_scoring_ms": el * 1e3 - lm,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": tf / PEAK_F16_MFMA_TFLOPS, "flops_per_pair": fpp,
@@ -908,12 +1058,10 @@ def main():
     if a.total_candidates:  # strong scaling: this rank's contiguous shard of ONE seeded set, global indices
         lo, hi = shard_range(a.total_candidates, rank, world)
         Nc, base = hi - lo, lo
-        c_dev = device_candidates(a.total_candidates, lo, hi, a.dc, a.du, a.levels, device)
-        cands = None
-    else:
+    else:  # weak: rank r scores rows [r Nc, (r+1) Nc) of the stream -- at N ranks the first N Nc rows
         Nc, base = a.candidates, rank * a.candidates
-        cands = S.make_candidates(Nc, a.dc, a.du, a.levels, seed=S.SEED_CAND + rank)
-        c_dev = torch.from_numpy(cands).to(device)
+    cands = S.make_candidates_blocked(base, base + Nc, a.dc, a.du, a.levels)
+    c_dev = torch.from_numpy(cands).to(device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     ev = kde.ScoreEvents()
     # l and g in one launch of the pair kernel (hbx_kde.hip launch_score2): same hmode instance for both
@@ -1008,10 +1156,13 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": Nc,
                    "total_candidates": a.total_candidates or world * Nc, "observations": a.obs, "n_good": Ng,
                    "n_bad": Nb, "dims": "%dc+%du" % (a.dc, a.du), "levels": a.levels,
-                   "parallelism": "candidate-sharded x%d, %s" % (
-                       world, "one collective: hbx_argmax_allreduce (RCCL all-gather of result records)"
-                       if a.backend == "nccl" else "gloo all_gather of result records (rehearsal)"),
+                   "parallelism": ("one GPU, no collective (the final argmin kernel publishes the record to the host)"
+                                   if world == 1 else "candidate-sharded x%d, %s" % (
+                       world, "one collective per step: hbx_argmax_allreduce (RCCL all-gather of result records)"
+                       if a.backend == "nccl" else "gloo all_gather of result records (rehearsal)")),
                    "winner": winner[0], "shortlist": last.shortlist,
+                   "candidates": "rows [%d, %d) of synthetic.make_candidates_blocked (seed 3) per rank, the first %d "
+                                 "rows in all" % (base, base + Nc, pairs_step // (Ng + Nb)),
                    "world_size_rccl": xchg.rccl_world_size() if xchg is not None else None,
                    "launcher": ("bench.py -> torch.distributed.run" if os.environ.get("HBX_BENCH_SPAWNED") == "1"
                                 else "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")},
@@ -1020,6 +1171,9 @@ def main():
         # the VALU-basis figure SURVEY 8d first proposed are reported beside it
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_MFMA_TFLOPS, "traffic": traffic,
+                     "traffic_source": ("carried, not counted in this run: HBM bytes per launch from the committed PMC "
+                                        "record of this workload (profiles/pmc_traffic.json: rocprofv3 --pmc "
+                                        "FETCH_SIZE / WRITE_SIZE passes, tools/profile_round.sh)") if traffic else None,
                      "valu_basis": {"peak": PEAK_FP32_TFLOPS, "frac": achieved / PEAK_FP32_TFLOPS},
                      "kernel": km["kernel"] + (" (l and g in one launch)" if fused else " (l and g launches)"),
                      "flops_per_pair": W,
@@ -1042,6 +1196,9 @@ def main():
                      "mfma_util": mfma_util, "issue_bound": issue_bound},
         "cpu_baseline": None,
     }
+    chk = winner_check(pinned_prefix(pairs_step // (Ng + Nb), a.dc, a.du, a.levels, a.obs), winner[0], winner[1],
+                       last.pdf_l if world == 1 else None, last.pdf_g if world == 1 else None)
+    out["config"].update(chk or {"winner_ok": None, "pinned_by": "no pinned winner for this workload"})
     if world > 1 and a.strong_total and not a.total_candidates:
         try:  # config #4 beside the weak line: the same total at every N (strong scaling)
             out["strong_config4"] = strong_line(pair, device, a, rank, world, dist, xchg)
@@ -1075,9 +1232,13 @@ def main():
             out["sh_stage_interleaved"] = sh_stage_line(device, interleaved=True, reps=7)
         except Exception as e:
             out["sh_stage_interleaved"] = {"error": repr(e)}
-        try:  # results between requests with the default (host, scipy) sampler
-            out["sh_stage_interleaved_host_sampler"] = sh_stage_line(device, n_obs=100, stage=27, reps=3,
-                                                                     interleaved=True, sampler="host", dims=(4, 2))
+        try:  # the default drop-in's get_config (host sampler) against the per-element draws
+            out["get_config_default"] = get_config_line(device)
+        except Exception as e:
+            out["get_config_default"] = {"error": repr(e)}
+        try:  # one worker with the default (host) sampler at default sizes: request, result, refit
+            out["sh_stage_interleaved_host_sampler"] = sh_stage_line(device, n_obs=400, stage=81, reps=3,
+                                                                     interleaved=True, sampler="host")
         except Exception as e:
             out["sh_stage_interleaved_host_sampler"] = {"error": repr(e)}
         try:
@@ -1104,10 +1265,17 @@ def main():
         try:
             out["cpu_baseline"] = cpu_baseline(X, pair.good.rows_dev.cpu().numpy(), pair.bad.rows_dev.cpu().numpy(),
                                                pair, var_type,
-                                               cands if cands is not None else c_dev[:400_000].cpu().numpy(),
+                                               cands,
                                                a.cpu_seconds)
         except Exception as e:  # the baseline is a side measurement; report why it is missing
             out["cpu_baseline"] = {"error": repr(e)}
+        try:
+            out["cpu_baseline"]["reference_loop"] = reference_loop_baseline(device)
+        except Exception as e:
+            out["cpu_baseline"]["reference_loop"] = {"error": repr(e)}
+    if world > 1:
+        out["cpu_baseline_note"] = ("the CPU baseline is measured on rank 0 at N=1 only (bench contract): see that "
+                                    "line's cpu_baseline")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if xchg is not None:

@@ -2476,6 +2476,287 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
     out[p] = nan ? NAN : (m > -INFINITY ? (m + log2(S)) * 0.69314718055994531 + lconst : -INFINITY);
 }
 
+// ln pdf within rtol by DIRECT DIFFERENCES in fp32 (the ln-pdf contract's first pass, hbx_kde_logpdf_rtol):
+// per pair t' = -sum_k (x'_k - X'_jk)^2 + sum_u delta_u [x_u == X_ju] (log2 units, x' = s (x - mu) as the
+// scoring kernels scale it, s = sqrt(log2 e / 2) / h; SM:kernels.py:23-65,108-125 in log2 form), S' =
+// sum_j 2^(t'_j - m) (m: the largest exponent of the first chunk, raised when a group of terms would
+// overflow), ln p = ln2 (m + log2 S' + lb_sum - M0) + log_norm.  No expansion -|x'|^2 - |X'|^2 + 2 x'X': its
+// terms of ~100 log2 units cancel, and a bound relative to them (the matrix-core estimates') never reaches
+// 1e-5 at D = 32; here every rounding is relative to the pair's own distance.  Packed fp32 VALU: the
+// differences and their squares two dims per v_pk_add_f32 / v_pk_fma_f32, the categorical match as
+// clamp(1 - e^2) of the integer code difference e (v_pk_fma_f32 ... clamp) times delta; observations staged
+// in LDS 64 at a time and read as broadcasts; CPT candidates per thread share each read.
+// Rigorous per-candidate bound of |ln p_est - ln p| (log2 units first):
+//   coordinates: x', X' rounded to fp32, d = fl(x' - X'): |d~ - d| <= dl_k = 2^-23 (1 + 2^-20)(|x'_k| + xmax_k);
+//   squares: |d~^2 - d^2| summed <= 2 sqrt(Q) |dl| + |dl|^2 over the terms that matter (t' >= t'_max - 64,
+//     Q = -m + 64 + sum_u max(delta_u, 0) + slack bounds their sum_k d_k^2; the others add <= n 2^-63);
+//   the accumulation: chains of NCH fma / add steps, each rounding <= 2^-24 (Q + sum|delta|);
+//   delta_u in fp32: <= 2^-24 sum|delta|; the exponent t' - m: 2^-24 (64 + 1);
+//   exp2: v_exp_f32 within 2 ulp (2^-22 relative); sums: 3 x 2^-24 (fp32 groups of 4) + n 2^-52 (fp64).
+// Candidates whose bound stays within 0.99 rtol max(1, |ln p|) are written; the rest go to `list` for the
+// fp64 pass.  KDEs with negative categorical factors, structural NaN or single-level dims: all to `list`.
+template <int DC, int DU, int CPT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 32 ? 4 : 2))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
+                                                           const KdeParams* __restrict__ P,
+                                                           const double* __restrict__ X,
+                                                           const int64_t* __restrict__ rows, double rtol,
+                                                           double* __restrict__ out, int32_t* __restrict__ list,
+                                                           int32_t* __restrict__ count) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int OB = 64;      // observations per staged chunk
+  constexpr int W = DC + DU;  // floats per staged row: DC scaled coordinates, DU codes
+  constexpr int NB = DC / 2, NU = DU / 2;  // packed pairs
+  static_assert(DC % 4 == 0 && DU % 4 == 0, "pairs of pairs");
+  __shared__ __align__(16) float xs[2][OB][W];
+  __shared__ double s_scale[DC > 0 ? DC : 1], s_mu[DC > 0 ? DC : 1];
+  __shared__ int32_t s_col[W > 0 ? W : 1];
+  __shared__ float s_dl[DU > 0 ? DU : 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int n = P->n, dc = P->dc, du = P->du;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 * CPT;
+  if (i0 >= Np) return;  // uniform
+  int64_t cid[CPT];
+  bool valid[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    cid[c] = i0 + c * 256 + tid;
+    valid[c] = cid[c] < Np;
+  }
+  const bool unsupported = P->has_neg || P->nan_all || P->nconst || n <= 0;
+  auto to_list = [&](bool f, int64_t p) __attribute__((always_inline)) {  // one atomic per wave
+    const uint64_t bal = __ballot(f);
+    if (!bal) return;
+    int32_t base = 0;
+    if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(count, __popcll(bal));
+    base = __shfl(base, __ffsll((long long)bal) - 1);
+    if (f) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)p;
+  };
+  if (unsupported) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) to_list(valid[c], cid[c]);
+    return;
+  }
+  for (int k = tid; k < W; k += 256) {
+    if (k < DC) {
+      const bool act = k < dc;
+      s_scale[k] = act ? P->cont_scale[k] : 0.0;
+      s_mu[k] = act ? P->center[k] : 0.0;
+      s_col[k] = act ? P->cont_dim[k] : -1;
+    } else {
+      const int u = k - DC;
+      const bool act = u < du;
+      s_dl[u] = act ? P->cat_delta[u] : 0.f;
+      s_col[k] = act ? P->cat_dim[u] : -1;
+    }
+  }
+  __syncthreads();
+  // the candidates: scaled continuous coordinates and codes in registers, pairs of dims packed
+  f2 xc[CPT][NB > 0 ? NB : 1], xu[CPT][NU > 0 ? NU : 1];
+  float nx2[CPT];  // sum_k (|x'_k| + xmax_k)^2
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const double* x = pts + (valid[c] ? cid[c] : 0) * (int64_t)D;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * q + h;
+        v[h] = s_col[k] >= 0 ? (float)(s_scale[k] * (x[s_col[k]] - s_mu[k])) : 0.f;
+        const float a = fabsf(v[h]) + (k < dc ? P->xmax[k] : 0.f);
+        acc = fmaf(a, a, acc);
+      }
+      xc[c][q] = f2{v[0], v[1]};
+    }
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = DC + 2 * q + h;
+        v[h] = s_col[k] >= 0 ? cand_code(x[s_col[k]]) : 0.f;
+      }
+      xu[c][q] = f2{v[0], v[1]};
+    }
+    nx2[c] = acc;
+  }
+  f2 dl2[NU > 0 ? NU : 1];
+#pragma unroll
+  for (int q = 0; q < NU; ++q) dl2[q] = f2{s_dl[2 * q], s_dl[2 * q + 1]};
+  // stage chunk cc into buffer b (padding dims 0 -- codes 0 against the candidate's 0: a match of delta 0;
+  // an observation past n: first coordinate +inf, its term 2^-inf = 0)
+  // the loads of a chunk are issued into registers before the previous chunk's math and stored after it
+  constexpr int PER = (OB * W + 255) / 256;
+  double pre[PER];
+  auto fetch = [&](int cc) __attribute__((always_inline)) {
+    const int j0 = cc * OB;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = tid + 256 * q;
+      const int jj = e / W, k = e - jj * W;
+      const int j = j0 + jj;
+      pre[q] = (e < OB * W && j < n && s_col[k] >= 0) ? X[rows[j] * (int64_t)D + s_col[k]] : 0.0;
+    }
+  };
+  auto store = [&](int cc, int b) __attribute__((always_inline)) {
+    const int j0 = cc * OB;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = tid + 256 * q;
+      if (e >= OB * W) break;
+      const int jj = e / W, k = e - jj * W;
+      float v = 0.f;
+      if (j0 + jj < n) {
+        if (s_col[k] >= 0) v = k < DC ? (float)(s_scale[k] * (pre[q] - s_mu[k])) : cand_code(pre[q]);
+      } else if (k == 0) {
+        v = __builtin_inf();
+      }
+      xs[b][jj][k] = v;
+    }
+  };
+  auto stage = [&](int cc, int b) __attribute__((always_inline)) {
+    fetch(cc);
+    store(cc, b);
+  };
+  // exponent t' of the pair (candidate c, staged row r): two packed accumulators (four fma chains)
+  auto term = [&](int c, const float* r) __attribute__((always_inline)) -> float {
+    f2 a0 = f2{0.f, 0.f}, a1 = f2{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const f2 X2 = f2{r[2 * q], r[2 * q + 1]};
+      const f2 d = xc[c][q] - X2;
+      if (q < NB / 2) a0 = __builtin_elementwise_fma(-d, d, a0);
+      else a1 = __builtin_elementwise_fma(-d, d, a1);
+    }
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const f2 E2 = f2{r[DC + 2 * q], r[DC + 2 * q + 1]};
+      const f2 e = xu[c][q] - E2;
+      f2 m;  // [x_u == X_u] = clamp(1 - e^2) for integer code differences e
+      asm("v_pk_fma_f32 %0, %1, %2, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0] clamp" : "=v"(m) : "v"(e), "v"(e));
+      if (q < NU / 2) a0 = __builtin_elementwise_fma(dl2[q], m, a0);
+      else a1 = __builtin_elementwise_fma(dl2[q], m, a1);
+    }
+    const f2 a = a0 + a1;
+    return a.x + a.y;
+  };
+  const int nch = (n + OB - 1) / OB;
+  stage(0, 0);
+  __syncthreads();
+  // m: the largest exponent of chunk 0 (every candidate's sum then has a term 2^0)
+  float m[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) m[c] = -INFINITY;
+  const int jn0 = min(OB, n);
+  for (int jj = 0; jj < jn0; ++jj) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) m[c] = fmaxf(m[c], term(c, &xs[0][jj][0]));
+  }
+  double S[CPT];
+  float s4[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    S[c] = 0.0;
+    s4[c] = 0.f;
+    if (!(m[c] > -INFINITY)) m[c] = 0.f;  // no finite term in chunk 0 (or NaN): any reference point
+  }
+  for (int cc = 0; cc < nch; ++cc) {
+    const int b = cc & 1;
+    if (cc + 1 < nch) fetch(cc + 1);
+    const int jn = min(OB, n - cc * OB);
+    // terms summed in fp32 in groups of 4, the groups into the fp64 sums (a chunk's last group: rows past jn
+    // are the padding rows, whose first coordinate is +inf: exact zeros)
+    const int jg = (jn + 3) & ~3;
+    for (int j4 = 0; j4 < jg; j4 += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* r = &xs[b][j4 + q][0];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+          const float t = term(c, r);
+          float e = __builtin_amdgcn_exp2f(t - m[c]);
+          if (!(e < 0x1p100f)) {  // rare: a term far above the reference point (or NaN): move it up to t
+            if (t == t) {
+              S[c] = (S[c] + (double)s4[c]) * exp2((double)m[c] - (double)t);
+              s4[c] = 0.f;
+              m[c] = t;
+              e = 1.f;
+            }
+          }
+          s4[c] += e;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        S[c] += (double)s4[c];
+        s4[c] = 0.f;
+      }
+    }
+    // the other buffer is free since the barrier after chunk cc - 1
+    if (cc + 1 < nch) store(cc + 1, b ^ 1);
+    __syncthreads();  // chunk cc + 1 staged; every thread done with chunk cc's buffer
+  }
+  // the bound (log2 units) and the result
+  float sdp = 0.f, sda = 0.f;
+  for (int u = 0; u < du; ++u) {
+    const float dlt = s_dl[u];
+    if (dlt > -1e29f) {  // a 1 - h == 0 factor's match: 2^-inf, no rounding
+      sdp += fmaxf(dlt, 0.f);
+      sda += fabsf(dlt);
+    }
+  }
+  const double log_c = P->lb_sum - P->m0_log2;
+  const float u24 = 0x1p-24f;
+  constexpr int NCH = (NB + NU) / 2 + 3;  // fma / add steps per chain, with the combining adds
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const float Q = fmaxf(-m[c], 0.f) + 64.f + sdp + 1.f;
+    const float dln = 0x1p-23f * (1.f + 0x1p-20f) * __builtin_sqrtf(nx2[c]) * (1.f + 0x1p-20f);
+    const float Et = 2.f * __builtin_sqrtf(Q) * dln + dln * dln + (float)NCH * u24 * (Q + sda) + u24 * sda +
+                     65.f * u24 + 0x1p-48f * Q;
+    // relative bound of S': 2^Et - 1 per term, the exp, the sums, the terms left out
+    const double rel = exp2((double)Et * (1.0 + 0x1p-20)) - 1.0 + 0x1p-22 + 3.0 * 0x1p-24 + (double)n * 0x1p-52 +
+                       (double)n * 0x1p-63;
+    const double lnS = log(S[c]) + (double)m[c] * 0.69314718055994531;
+    const double lp = lnS + log_c * 0.69314718055994531 + P->log_norm;
+    const double bound = rel / (1.0 - rel) + 0x1p-50 * fabs(lp);
+    const bool ok = valid[c] && S[c] > 0.0 && lp - lp == 0.0 && rel < 0.5 && bound <= 0.99 * rtol * fmax(1.0, fabs(lp));
+    if (ok) out[cid[c]] = lp;
+    to_list(valid[c] && !ok, cid[c]);
+  }
+}
+
+typedef void (*logpdf_dd_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*, double,
+                             double*, int32_t*, int32_t*);
+// candidates per thread: two share each staged row where both fit the register budget
+constexpr int dd_cpt(int dc, int du) { return dc + du <= 16 ? 2 : 1; }
+
+template <int DC>
+static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt) {
+  switch (du_pad) {
+    case 0: *cpt = dd_cpt(DC, 0); return kde_logpdf_dd_kernel<DC, 0, dd_cpt(DC, 0)>;
+    case 4: *cpt = dd_cpt(DC, 4); return kde_logpdf_dd_kernel<DC, 4, dd_cpt(DC, 4)>;
+    case 8: *cpt = dd_cpt(DC, 8); return kde_logpdf_dd_kernel<DC, 8, dd_cpt(DC, 8)>;
+    case 16: *cpt = dd_cpt(DC, 16); return kde_logpdf_dd_kernel<DC, 16, dd_cpt(DC, 16)>;
+    case 32: *cpt = dd_cpt(DC, 32); return kde_logpdf_dd_kernel<DC, 32, dd_cpt(DC, 32)>;
+  }
+  return nullptr;
+}
+
+// the direct-difference fp32 kernel of a bucket (continuous slots rounded up to a multiple of 4)
+static logpdf_dd_fn pick_logpdf_dd(int dc_pad, int du_pad, int* cpt) {
+  switch (dc_pad) {
+    case 0:
+    case 4: return pick_dd_du<4>(du_pad, cpt);
+    case 8: return pick_dd_du<8>(du_pad, cpt);
+    case 16: return pick_dd_du<16>(du_pad, cpt);
+    case 24: return pick_dd_du<24>(du_pad, cpt);
+    case 32: return pick_dd_du<32>(du_pad, cpt);
+  }
+  return nullptr;  // 64 continuous slots: the estimate + fp64 path
+}
+
 __global__ __launch_bounds__(256) void kde_logpdf_classify_kernel(const KdeEst* __restrict__ est, int64_t Nc,
                                                                  double rtol, int exact_all, double* __restrict__ out,
                                                                  int32_t* __restrict__ list,
@@ -2559,17 +2840,27 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
   KdeEst* est = (KdeEst*)(sc + 256);
   int32_t* list = (int32_t*)(sc + 256 + 16 * Nc);
   const bool exact_only = (variant >> 5) & 1;
-  if (!exact_only) {  // the estimate (the precise instance: hbx_kde_logpdf's)
-    if (!table) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: null table");
-    ScoreFns f = pick_logpdf(dc_pad, du_pad, variant);
-    if (!f.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
-    const int rc = launch_score(f, cand, Nc, D, params, table, est, s);
-    if (rc) return rc;
-  }
+  // unsigned KDEs of a bucket with <= 32 continuous slots: the direct-difference fp32 pass writes every
+  // candidate its bound accepts and lists the rest (its kernel lists all of a KDE it does not model)
+  int cpt = 1;
+  const logpdf_dd_fn dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt) : nullptr;
   HBX_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), s));
-  hipLaunchKernelGGL(kde_logpdf_classify_kernel, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, est, Nc, rtol,
-                     exact_only ? 1 : 0, out, list, count);
-  HBX_LAUNCH_CHECK();
+  if (dd) {
+    hipLaunchKernelGGL(dd, dim3((unsigned)((Nc + 256 * cpt - 1) / (256 * cpt))), dim3(256), 0, s, cand, Nc, D,
+                       (const KdeParams*)params, X, rows, rtol, out, list, count);
+    HBX_LAUNCH_CHECK();
+  } else {
+    if (!exact_only) {  // the estimate (the precise instance: hbx_kde_logpdf's)
+      if (!table) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_rtol: null table");
+      ScoreFns f = pick_logpdf(dc_pad, du_pad, variant);
+      if (!f.main) return hbx_fail(HBX_ERR_UNSUPPORTED, "no kernel for dc_pad=%d du_pad=%d", dc_pad, du_pad);
+      const int rc = launch_score(f, cand, Nc, D, params, table, est, s);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(kde_logpdf_classify_kernel, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, est, Nc, rtol,
+                       exact_only ? 1 : 0, out, list, count);
+    HBX_LAUNCH_CHECK();
+  }
   const unsigned grid = (unsigned)(Nc < EXACT_GRID ? Nc : EXACT_GRID);
   // the rest in fp64 log space (positive factors): tiled over candidates where the bucket has an instance,
   // else one block per point (its kernel exits for KDEs the tiled one would mis-handle: see below)

@@ -9,9 +9,6 @@ import struct
 import numpy as np
 import pytest
 
-from oracle import c_oracle
-from oracle import kde_oracle as O
-
 pytestmark = pytest.mark.gpu
 
 
@@ -131,14 +128,17 @@ def test_two_ranks_share_the_gpu_gloo_records():
 
 def test_config4_shape_sharded_8_ways(device):
     """BASELINE config #4 on one MI355X: 1e7 candidates x 1e4 observations (1500 good / 8500 bad),
-    D = 32 (24c + 8u, 4 levels).  The 8 per-rank shards (index_base = shard start) reduced by the
-    exchange's rule give the unsharded winner; the winner and the next best candidates by the fp32
-    estimates are re-scored by the C oracle (reference arithmetic, fp64): the oracle picks the same
-    index among them, and the GPU's exact pdfs of the winner agree with it."""
+    D = 32 (24c + 8u, 4 levels) -- the set whose winner the C oracle pinned by scoring every candidate
+    (tests/golden/full_winners.json, prefix_10000000).  The acquisition that also reports ln-pdfs (the
+    precise scoring instance) and the 8 per-rank shards (index_base = shard start) reduced by the
+    exchange's rule both return the pinned winner, score and pdfs bit for bit."""
+    import json
     import torch
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
     from hpbandster_amd.distributed import reduce_records_host, shard_range
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_winners.json")) as fh:
+        e = json.load(fh)["config3_prefixes"]["prefix_10000000"]
     dc, du, lev = 24, 8, 4
     X = S.make_observations(10000, dc, du, lev)
     L = S.make_losses(10000)
@@ -146,29 +146,16 @@ def test_config4_shape_sharded_8_ways(device):
     pair = kde.fit_pair(X, L, vt, dc + du + 1, device=device)
     assert (pair.good.nobs, pair.bad.nobs) == (1500, 8500)
     Nc = 10_000_000
-    g = torch.Generator(device=device)
-    g.manual_seed(123)
-    C = torch.empty((Nc, dc + du), dtype=torch.float64, device=device)
-    C[:, :dc] = torch.rand((Nc, dc), dtype=torch.float64, device=device, generator=g)
-    C[:, dc:] = torch.randint(0, lev, (Nc, du), device=device, generator=g).to(torch.float64)
+    C = torch.from_numpy(S.make_candidates_blocked(0, Nc, dc, du, lev)).to(device)
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=device)
     res, logl, logg = pair.acquire(C, workspace=ws, logs=True)
-    assert res.index >= 0
     recs = []
     for k in range(8):
         lo, hi = shard_range(Nc, k, 8)
         recs.append(pair.acquire(C[lo:hi], index_base=lo, workspace=ws))
     best, _ = reduce_records_host(recs)
-    assert recs[best].index == res.index and recs[best].score == res.score
-    # winner + runners-up by the fp32 score estimate, re-scored by the C oracle
-    est = np.maximum(logg, np.log(1e-8)) - np.maximum(logl, np.log(1e-8))
-    top = np.unique(np.concatenate([[res.index], np.argsort(est, kind="stable")[:15]]))
-    pts = C[torch.from_numpy(top).to(device)].cpu().numpy()
-    good_rows = pair.good.rows_dev.cpu().numpy()
-    bad_rows = pair.bad.rows_dev.cpu().numpy()
-    pl = c_oracle.kde_pdf(X[good_rows], pair.good.bw, vt, pair.good.nlev, pts)
-    pg = c_oracle.kde_pdf(X[bad_rows], pair.bad.bw, vt, pair.bad.nlev, pts)
-    scores = [O.py_score(a, b) for a, b in zip(pl, pg)]
-    assert top[O.py_argmin(scores)] == res.index
-    w = int(np.nonzero(top == res.index)[0][0])
-    np.testing.assert_allclose([res.pdf_l, res.pdf_g], [pl[w], pg[w]], rtol=1e-13)
+    for r in (res, recs[best]):
+        assert r.index == e["winner"] and float(r.score).hex() == e["score_hex"]
+        assert float(r.pdf_l).hex() == e["pdf_l_hex"] and float(r.pdf_g).hex() == e["pdf_g_hex"]
+    # the reported ln-pdf estimates of the winner agree with its exact pdfs
+    np.testing.assert_allclose([logl[e["winner"]], logg[e["winner"]]], np.log([res.pdf_l, res.pdf_g]), rtol=1e-4)
