@@ -375,7 +375,7 @@ class BOHB(base_config_generator):
         self._ahead_stats = {"launched": 0, "served": 0, "dropped": 0}
         self._calls = 0  # get_config calls so far
         self._pick_free = []     # mapped output buffers ready for reuse
-        self._pick_pending = []  # (buffer, seq, tensors) of dropped ones the device may still write
+        self._pick_pending = []  # (buffer, seq, tensors, pair) of dropped ones the device may still use
         self._pick_seq = 0
 
     # -- candidates ---------------------------------------------------------------------------
@@ -553,7 +553,9 @@ class BOHB(base_config_generator):
         or followed a result), or by a refit with no call since (a burst of results); a refit's that met
         only random picks (bohb.py:124's random_fraction) was just not needed."""
         self._ahead = None
-        self._pick_pending.append((a.buf, a.seq, a.keep))
+        # the pair stays referenced too: the dropped launch may still read its parameters, tables and rows
+        # (allocated on another thread's stream) until its completion word lands
+        self._pick_pending.append((a.buf, a.seq, a.keep, a.pair))
         if a.source == "get_config" or self._calls == a.calls:
             self._ahead_on[a.source] = False
         self._ahead_stats["dropped"] += 1
@@ -564,11 +566,11 @@ class BOHB(base_config_generator):
         completion word has landed) -- no allocation per call."""
         import torch
         still = []
-        for buf, seq, keep in self._pick_pending:  # the device has finished with a dropped one
+        for buf, seq, keep, pr in self._pick_pending:  # the device has finished with a dropped one
             if ctypes.c_int32.from_address(buf + PICK_DONE).value == seq:
                 self._pick_free.append((buf, keep))
             else:
-                still.append((buf, seq, keep))
+                still.append((buf, seq, keep, pr))
         self._pick_pending = still
         wsb = pair.workspace_bytes(self.num_samples)
         dev = pair.good.device
@@ -616,7 +618,7 @@ class BOHB(base_config_generator):
             nb = PICK_ROW + 8 * len(self.vartypes)
             for b, _ in getattr(self, "_pick_free", []):
                 _PICKS.put(b, nb)
-            for b, seq, _ in getattr(self, "_pick_pending", []):
+            for b, seq, _, _ in getattr(self, "_pick_pending", []):
                 _PICKS.put(b, nb, seq)
             a = getattr(self, "_ahead", None)
             if a is not None:

@@ -1921,10 +1921,14 @@ static WsLayout ws_layout(int64_t Nc, int64_t nmax, int64_t B = 1) {
   w.key = take(8 * B);
   w.first1 = take(4 * B);
   w.rescue = take(4);
-  // estimates: one per candidate and observation split (the launch's splits never exceed this bound)
+  // estimates: one per candidate and observation split (the launch's splits never exceed this bound).  The
+  // allowance is non-decreasing in Nc -- a workspace sized for a larger candidate count serves every smaller
+  // one: splits happen only up to 65536 candidates (128 tiles), where Nc x sp <= min(16 Nc, 196608)
   const int sp = obs_splits((unsigned)((Nc + 511) / 512), nmax, true);
-  w.est_l = take(sizeof(KdeEst) * Nc * sp);
-  w.est_g = take(sizeof(KdeEst) * Nc * sp);
+  const int64_t cap16 = 16 * Nc < 196608 ? 16 * Nc : 196608;
+  const int64_t nest = Nc * sp > cap16 ? Nc * sp : cap16;
+  w.est_l = take(sizeof(KdeEst) * nest);
+  w.est_g = take(sizeof(KdeEst) * nest);
   w.lo = take(4 * Nc);
   w.list = take(4 * Nc);
   w.near = take(4 * Nc);

@@ -15,6 +15,10 @@
 //     the end, the next vector taken from the side with less stored room; ranges <= 64 go to the bitonic
 //     key/index networks argsort_{8,16,32,64}_64bit (padding lanes +inf / index 0; equal keys never
 //     swap); std::sort once 2 floor(log2 n) levels are spent.
+// Licences of the restated third-party algorithms: x86-simd-sort is BSD-3-Clause (Intel Corporation), as
+// vendored by numpy (BSD-3-Clause); libstdc++'s std::sort / heap helpers are GPL-3.0 with the GCC Runtime
+// Library Exception.  Only their published algorithms are restated here (no source text is copied); the
+// restatement is what reproduces numpy's tie order, so it follows them step for step.
 // oracle/np_argsort.py is the same restatement in Python, pinned by numpy 1.26.4's own outputs
 // (tests/golden/np_argsort.npz).  Here every range is handled by one wave: the partition's sequential
 // "which side next" walk runs on uniform scalars with the per-group counts held in lane windows, the
