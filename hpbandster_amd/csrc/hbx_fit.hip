@@ -11,6 +11,7 @@
 // 8192-element buffers.  The factor n**(-1/(4+D)) is a host-side glibc pow() per segment, passed in,
 // because the device pow() is not guaranteed to round the same way.
 #include "hbx_common.h"
+#include "hbx_kde_impl.h"
 #include "hbx_npsort.h"
 #include "hbx_sort.h"
 #include <stdlib.h>
@@ -283,6 +284,65 @@ int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, int6
   return HBX_OK;
 }
 
+// One refit of n <= REFIT_SORT_SMALL rows in one workgroup (hbx_kde_refit; bohb.py:211-229): append the
+// n_new staged rows ([n_new][D] then n_new losses) at rows n - n_new .. n - 1, write the split metadata,
+// sort the losses (wave 0: the register network, ties by position), and -- only when two sorted keys are
+// equal -- re-rank the whole segment in numpy 1.26.4's order (hbx_npsort.h, every thread).  The same
+// order as the metadata kernel + counting rank + scatter + tie check + numpy-order launches it replaces.
+__global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(double* __restrict__ X,
+                                                                        double* __restrict__ loss,
+                                                                        const double* __restrict__ staged,
+                                                                        int64_t n_new, RefitMetaArgs a,
+                                                                        RefitMeta* __restrict__ m,
+                                                                        int64_t* __restrict__ order, int32_t* A0) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int n = (int)a.n;
+  const int64_t per = n_new * (int64_t)a.D;
+  for (int64_t e = tid; e < per + n_new; e += NPS_THREADS) {
+    if (e < per) X[(a.n - n_new) * (int64_t)a.D + e] = staged[e];
+    else loss[a.n - n_new + (e - per)] = staged[e];
+  }
+  for (int d = tid; d < a.D; d += NPS_THREADS) m->vt[d] = (a.vt[d >> 5] >> (d & 31)) & 1u;
+  if (tid == 0) {
+    m->seg[0] = 0;
+    m->seg[1] = a.n;
+    m->n_good = a.n_good;
+    m->n_bad = a.n_bad;
+    m->fac_good = a.fac_good;
+    m->fac_bad = a.fac_bad;
+  }
+  __shared__ int tie;
+  if (tid == 0) tie = 0;
+  __syncthreads();  // the appended losses are visible to wave 0
+  if (tid < 64) {
+    uint64_t key[PW_PER_LANE];
+    int32_t pos[PW_PER_LANE];
+    wave_sort_1024<false>(loss, n, lane, key, pos);
+    bool t = false;
+#pragma unroll
+    for (int r = 0; r < PW_PER_LANE; ++r) {
+      const int rank = lane * PW_PER_LANE + r;
+      if (rank < n) order[rank] = pos[r];
+      if (r + 1 < PW_PER_LANE) t |= rank + 1 < n && key[r] == key[r + 1];
+    }
+    const uint64_t nk = __shfl_down(key[0], 1);  // the next lane's first key
+    t |= (lane + 1) * PW_PER_LANE < n && key[PW_PER_LANE - 1] == nk;
+    if (__ballot(t) && lane == 0) tie = 1;
+  }
+  __syncthreads();
+  if (tie)  // (uniform) every position re-ranked in numpy's order
+    nps_order_segment(loss, n, 0, 0.0, A0, A0 + n, A0 + 2 * n, A0 + 3 * n, order, nullptr);
+}
+
+int refit_sort_small(double* X, double* loss, const double* staged, int64_t n_new, const RefitMetaArgs& a,
+                     RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s) {
+  if (a.n < 1 || a.n > REFIT_SORT_SMALL) return hbx_fail(HBX_ERR_ARG, "refit_sort_small: n=%lld", (long long)a.n);
+  hipLaunchKernelGGL(kde_refit_sort_small_kernel, dim3(1), dim3(NPS_THREADS), 0, s, X, loss, staged, n_new, a, m,
+                     order, arrays);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}
+
 // one thread per (segment, set in {good, bad}, dim): bandwidth and observed level count
 __global__ __launch_bounds__(128) void kde_fit_stats_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
@@ -351,7 +411,7 @@ __global__ __launch_bounds__(128) void kde_fit_stats_kernel(
 // block (once: up to FIT_TILE rows stay resident for both passes); thread 0 then adds strictly in row
 // order (np.std's axis-0 reduction order, D > 1), so the result is bit-identical to the
 // thread-per-column kernel.  Level counts come from a block-wide bitmap (order-independent).
-#define FIT_TILE 16384
+#define FIT_TILE FIT_TILE_ROWS
 // numpy's axis-0 order: one dependent add per row.  The LDS reads of the next 32 rows are issued
 // before the adds of the current 32, so the read latency hides behind the add chain (same additions,
 // same order).  SQ: add (v - mean)^2.
@@ -385,12 +445,15 @@ __device__ __forceinline__ double fit_chain(const double* v, int m, double acc, 
   return acc;
 }
 
+// cs_good / cs_bad (a single segment's refit, both sets within one tile; nullable): the preparation's column
+// statistics of each set (kde_colstats_kernel's values, its summation order) from the gathered column --
+// one launch less
 __global__ __launch_bounds__(256) void kde_fit_col_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off,
     const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
     const double* __restrict__ fac_good, const double* __restrict__ fac_bad, const int32_t* __restrict__ vartype,
     double* __restrict__ bw_good, double* __restrict__ bw_bad, int32_t* __restrict__ nlev_good,
-    int32_t* __restrict__ nlev_bad) {
+    int32_t* __restrict__ nlev_bad, ColStats* __restrict__ cs_good, ColStats* __restrict__ cs_bad) {
   __shared__ double v[FIT_TILE];
   __shared__ uint32_t bits[32];
   __shared__ double red;
@@ -435,6 +498,34 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
   for (int64_t c = 0; c < ns; c += FIT_TILE) {
     const int m = (int)((ns - c) < FIT_TILE ? (ns - c) : FIT_TILE);
     gather(c, m, true);
+    if (cs_good && ns <= FIT_TILE) {  // kde_colstats_kernel's statistic of this (set, dim), its order
+      ColStats* cs = good ? cs_good : cs_bad;
+      __shared__ double cred[4];
+      __shared__ int mred[4];
+      if (!cat) {
+        double a = 0.0;
+        for (int j = threadIdx.x; j < m; j += 256) a += v[j];
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        if ((threadIdx.x & 63) == 0) cred[threadIdx.x >> 6] = a;
+      } else {
+        int mx = -1;
+        for (int j = threadIdx.x; j < m; j += 256) {
+          const double x = v[j];
+          mx = max(mx, (!(x >= 0.0 && x < 1024.0) || x != floor(x)) ? 100000 : (int)x);
+        }
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        if ((threadIdx.x & 63) == 0) mred[threadIdx.x >> 6] = mx;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        if (!cat) {
+          cs->mean[d] = ((cred[0] + cred[1]) + (cred[2] + cred[3])) / (double)ns;
+        } else {
+          const int mm = max(max(mred[0], mred[1]), max(mred[2], mred[3]));
+          cs->maxcode[d] = mm >= 100000 ? -1 : mm;
+        }
+      }
+    }
     if (threadIdx.x == 0) acc = fit_chain<false>(v, m, acc, 0.0);
   }
   if (threadIdx.x == 0) red = acc;
@@ -690,12 +781,10 @@ static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_
   if (!loss || !seg_off || !order || (!scratch && N > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort: null");
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
-  const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-segment kernel for every size
-  const char* renv = getenv("HBX_SORT_RANK");     // 0: LDS tiles + merges for every segment > 1024
-  const bool rank_ok = max_seg <= RANK_MAX_SEG && B <= 65535 && !(renv && atoi(renv) == 0);
+  const bool rank_ok = max_seg <= RANK_MAX_SEG && B <= 65535;
   // many short segments: one wave each; a few (a single refit split): the counting rank spreads
-  // each segment over many workgroups
-  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0) && (B >= 64 || !rank_ok)) {
+  // each segment over many workgroups; longer segments or more of them: LDS tiles + merges
+  if (max_seg <= 64 * PW_PER_LANE && (B >= 64 || !rank_ok)) {
     hipLaunchKernelGGL(seg_argsort_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        loss, seg_off, B, order);
     HBX_LAUNCH_CHECK();
@@ -739,8 +828,7 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
   if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
   if (B <= 0) return HBX_OK;
   const int64_t total = B * 2 * D;
-  const char* lenv = getenv("HBX_FIT_LDS");  // 0: the thread-per-column gather kernel for many segments
-  if (D > 1 && total >= 16384 && !(lenv && atoi(lenv) == 0)) {  // many segments: rows read once into LDS
+  if (D > 1 && total >= 16384) {  // many segments: rows read once into LDS
     const int32_t ngroups = (D + FIT_DQ - 1) / FIT_DQ;
     const int64_t per_xcd = (B * ngroups + 7) / 8;
     if (8 * per_xcd > 0x7fffffffLL) return hbx_fail(HBX_ERR_ARG, "hbx_kde_fit: too many segments");
@@ -749,7 +837,8 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
                        nlev_bad, ngroups, per_xcd);
   } else if (D > 1 && total < 16384) {  // few columns: one workgroup each (LDS-staged gathers)
     hipLaunchKernelGGL(kde_fit_col_kernel, dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, X, D, seg_off,
-                       order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad);
+                       order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad,
+                       (ColStats*)nullptr, (ColStats*)nullptr);
   } else {
     hipLaunchKernelGGL(kde_fit_stats_kernel, dim3((unsigned)((total + 127) / 128)), dim3(128), 0,
                        (hipStream_t)stream, X, D, seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype,
@@ -760,3 +849,15 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
 }
 
 }  // extern "C"
+
+// A single refit's fit (B = 1, D > 1, both sets within one LDS tile) that also writes the preparation's column
+// statistics of both sets (the colstats launch saved): hbx_kde_refit's path
+int refit_fit_colstats(const double* X, int32_t D, const int64_t* seg_off, const int64_t* order, const int64_t* n_good,
+                       const int64_t* n_bad, const double* fac_good, const double* fac_bad, const int32_t* vartype,
+                       double* bw_good, double* bw_bad, int32_t* nlev_good, int32_t* nlev_bad, ColStats* cs_good,
+                       ColStats* cs_bad, hipStream_t s) {
+  hipLaunchKernelGGL(kde_fit_col_kernel, dim3((unsigned)(2 * D)), dim3(256), 0, s, X, D, seg_off, order, n_good, n_bad,
+                     fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad, cs_good, cs_bad);
+  HBX_LAUNCH_CHECK();
+  return HBX_OK;
+}

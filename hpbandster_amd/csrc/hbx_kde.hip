@@ -78,7 +78,7 @@ struct PrepSet {
 
 __device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
 
-__device__ __forceinline__ ColStats* col_stats(KdeParams* P) { return (ColStats*)((char*)P + HBX_COLSTATS_OFF); }
+__host__ __device__ __forceinline__ ColStats* col_stats(KdeParams* P) { return (ColStats*)((char*)P + HBX_COLSTATS_OFF); }
 
 // Column statistics of every (KDE, dim), one workgroup each (blocks [k*D, (k+1)*D) belong to KDE k):
 // the mean of a continuous column (the centre of the scaled coordinates: any finite centre is correct
@@ -112,6 +112,12 @@ __global__ __launch_bounds__(256) void kde_colstats_kernel(PrepSet ps) {
       cs->maxcode[d] = mm >= 100000 ? -1 : mm;
     }
   }
+}
+
+// the table launch's block counter of a KDE (in its parameter buffer's staging area, after the info
+// record; zeroed by kde_params_kernel)
+__device__ __forceinline__ int32_t* prep_counter(KdeParams* P) {
+  return (int32_t*)((char*)P + HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 32);
 }
 
 // The parameter block of one KDE (one workgroup): the per-dim transcendentals in parallel, then the
@@ -148,6 +154,7 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    *prep_counter(P) = 0;  // the table launch's block counter (finish by the last block)
     double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
     float sad = 0.f;
     int dc = 0, du = 0, nconst = 0, dc_tot = 0, du_tot = 0;
@@ -511,75 +518,12 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
 // f32-MFMA layout of an hmode KDE whose C_j left the f16 range of the three-piece split
 __device__ __forceinline__ bool table_needs_rebuild(const KdeParams* P) { return P->hmode && !(P->cmax <= H_CMAX); }
 
-// pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
-// block of a KDE that needs none exits at once)
-// The block's 64 observation rows are staged in LDS first (all loads in flight at once, coalesced
-// within each row) when D <= 64; the per-dim walk then reads LDS instead of waiting on one dependent
-// global load per dim.
-#define TABLE_STAGE_D 64
-__global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0, float* table1, int pass) {
-  const bool second = ps.nk > 1 && (int)blockIdx.x >= ps.k[0].nblk_table;
-  const PrepArgs& A = ps.k[second ? 1 : 0];
-  KdeParams* P = A.P;
-  const int j0 = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64;
-  const int j = j0 + threadIdx.x;
-  if (pass != 0 && !table_needs_rebuild(P)) return;
-  // the parameter block is copied to LDS: loads from the global block the kernel also writes (atomics)
-  // would be vector loads, one memory latency each along the per-dim walk
-  __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
-  for (int i = threadIdx.x; i < (int)((sizeof(KdeParams) + 15) / 16); i += 64) pl[i] = ((const uint4*)P)[i];
-  __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
-  __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_MAX];  // h32 rows assembled here
-  const int D = A.D, n = A.n;
-  const KdeParams* Pl = (const KdeParams*)pl;
-  float* tab = second ? table1 : table0;
-  // two inlined copies of the body: rows read from LDS (every load a ds_read) or from global memory
-  // (a generic pointer would make each row read wait for the outstanding table stores as well)
-  auto run = [&](const double* x) {
-    if (pass == 0)
-      kde_table_body(x, Pl, P, tab, j, Pl->hmode, Pl->chunk_floats, &P->cmax, h32s + threadIdx.x * H32_ROW_MAX);
-    else
-      kde_table_body(x, Pl, P, tab, j, 0, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
-                     &P->cmax2, h32s + threadIdx.x * H32_ROW_MAX);
-  };
-  if (D <= TABLE_STAGE_D) {
-    const int DS = D | 1;  // odd row stride: the 64 threads' reads of one dim hit distinct banks
-    __shared__ int64_t rs[64];
-    rs[threadIdx.x] = A.rows[j < n ? j : 0];
-    __syncthreads();
-    // 16 independent loads in flight per thread per batch (coalesced within each row); past the end
-    // the last element is re-read and re-stored (same value, same place)
-    const int tot = 64 * D;
-    for (int e0 = 0; e0 < tot; e0 += 16 * 64) {
-      double t[16];
-      int at[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = min(e0 + q * 64 + (int)threadIdx.x, tot - 1);
-        const int i = e / D, c = e - i * D;
-        at[q] = i * DS + c;
-        t[q] = A.X[rs[i] * (int64_t)D + c];
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) xs[at[q]] = t[q];
-    }
-    __syncthreads();
-    run(xs + threadIdx.x * DS);
-  } else {
-    __syncthreads();  // the parameter copy
-    run(A.X + A.rows[j < n ? j : 0] * (int64_t)D);
-  }
-}
-
 // Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
 // du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6 |
-// (coarse table) << 7 selects the scoring kernel.
-__global__ void kde_prep_finish_kernel(PrepSet ps) {
-  const int k = threadIdx.x;
-  if (k >= ps.nk) return;
-  const PrepArgs& A = k ? ps.k[1] : ps.k[0];
+// (coarse table) << 7 selects the scoring kernel.  rebuild: the table needed its f32 rebuild.
+__device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) {
   KdeParams* P = A.P;
-  if (table_needs_rebuild(P)) {
+  if (rebuild) {
     P->hmode = 0;
     P->chunk_floats = chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0);
     P->cmax = P->cmax2;
@@ -595,6 +539,102 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
   info[5] = P->nconst;
   info[6] = P->dc_pad;
   info[7] = P->du_pad;
+}
+
+// pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
+// block of a KDE that needs none exits at once)
+// The block's 64 observation rows are staged in LDS first (all loads in flight at once, coalesced
+// within each row) when D <= 64; the per-dim walk then reads LDS instead of waiting on one dependent
+// global load per dim.
+// finish (pass 0 only): the KDE's last block to finish -- told by the counter its add returns, after every
+// wave's stores and maxima atomics have been acknowledged -- rebuilds the table in the f32 layout when its
+// C_j left the f16 range (rare: every row, in this block) and writes the final mode and the info record:
+// the rebuild and finish launches saved.
+#define TABLE_STAGE_D 64
+__global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0, float* table1, int pass, int finish) {
+  const bool second = ps.nk > 1 && (int)blockIdx.x >= ps.k[0].nblk_table;
+  const PrepArgs& A = ps.k[second ? 1 : 0];
+  KdeParams* P = A.P;
+  const int j0 = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64;
+  if (pass != 0 && !table_needs_rebuild(P)) return;
+  // the parameter block is copied to LDS: loads from the global block the kernel also writes (atomics)
+  // would be vector loads, one memory latency each along the per-dim walk
+  __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
+  for (int i = threadIdx.x; i < (int)((sizeof(KdeParams) + 15) / 16); i += 64) pl[i] = ((const uint4*)P)[i];
+  __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
+  __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_MAX];  // h32 rows assembled here
+  const int D = A.D, n = A.n;
+  const KdeParams* Pl = (const KdeParams*)pl;
+  float* tab = second ? table1 : table0;
+  // one block's 64 rows [r0, r0 + 64) of pass ps_: two inlined copies of the body, rows read from LDS
+  // (every load a ds_read) or from global memory (a generic pointer would make each row read wait for the
+  // outstanding table stores as well)
+  auto rows64 = [&](int r0, int ps_) {
+    const int j = r0 + threadIdx.x;
+    auto run = [&](const double* x) {
+      if (ps_ == 0)
+        kde_table_body(x, Pl, P, tab, j, Pl->hmode, Pl->chunk_floats, &P->cmax, h32s + threadIdx.x * H32_ROW_MAX);
+      else
+        kde_table_body(x, Pl, P, tab, j, 0, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
+                       &P->cmax2, h32s + threadIdx.x * H32_ROW_MAX);
+    };
+    if (D <= TABLE_STAGE_D) {
+      const int DS = D | 1;  // odd row stride: the 64 threads' reads of one dim hit distinct banks
+      __shared__ int64_t rs[64];
+      __syncthreads();  // the parameter copy; the previous rows' readers done
+      rs[threadIdx.x] = A.rows[j < n ? j : 0];
+      __syncthreads();
+      // 16 independent loads in flight per thread per batch (coalesced within each row); past the end
+      // the last element is re-read and re-stored (same value, same place)
+      const int tot = 64 * D;
+      for (int e0 = 0; e0 < tot; e0 += 16 * 64) {
+        double t[16];
+        int at[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int e = min(e0 + q * 64 + (int)threadIdx.x, tot - 1);
+          const int i = e / D, c = e - i * D;
+          at[q] = i * DS + c;
+          t[q] = A.X[rs[i] * (int64_t)D + c];
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xs[at[q]] = t[q];
+      }
+      __syncthreads();
+      run(xs + threadIdx.x * DS);
+    } else {
+      __syncthreads();  // the parameter copy
+      run(A.X + A.rows[j < n ? j : 0] * (int64_t)D);
+    }
+  };
+  rows64(j0, pass);
+  if (pass != 0 || !finish) return;
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores and maxima atomics are done
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) last = atomicAdd(prep_counter(P), 1) == A.nblk_table - 1;
+  __syncthreads();
+  if (!last) return;
+  // every block's |C_j| maximum is in (atomics at the device level; read past this CU's cache)
+  const float cmax = __hip_atomic_load(&P->cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool rebuild = Pl->hmode && !(cmax <= H_CMAX);
+  if (rebuild) {
+    for (int r0 = 0; r0 < A.nblk_table * 64; r0 += 64) rows64(r0, 1);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (rebuild) P->cmax2 = __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prep_finish_one(A, rebuild);
+  }
+}
+
+// Final mode of each KDE and its info record (the separate launch of hbx_kde_prepare's path)
+__global__ void kde_prep_finish_kernel(PrepSet ps) {
+  const int k = threadIdx.x;
+  if (k >= ps.nk) return;
+  const PrepArgs& A = k ? ps.k[1] : ps.k[0];
+  prep_finish_one(A, table_needs_rebuild(A.P));
 }
 
 static int64_t prep_table_blocks(int64_t n) { return (((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK + 63) / 64; }
@@ -637,21 +677,30 @@ static int prep_args(PrepArgs* A, const double* X, int32_t D, const int64_t* row
   return HBX_OK;
 }
 
-// enqueue the preparation of ps.nk KDEs (no host synchronisation)
-static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s) {
-  hipLaunchKernelGGL(kde_colstats_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
-  HBX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kde_params_kernel, dim3(ps.nk), dim3(256), 0, s, ps);
-  HBX_LAUNCH_CHECK();
-  const unsigned tb = (unsigned)(ps.k[0].nblk_table + (ps.nk > 1 ? ps.k[1].nblk_table : 0));
-  if (tb > 0) {
-    hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 0);
-    HBX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 1);
+// enqueue the preparation of ps.nk KDEs (no host synchronisation).  colstats_done: the fit wrote the column
+// statistics already (refit_fit_colstats).  Every KDE with a table: the table launch's last block per KDE
+// does the rare f32 rebuild and writes the final mode (3 launches; 5 before round 5)
+static int prep_launch(PrepSet& ps, float* table0, float* table1, hipStream_t s, bool colstats_done = false) {
+  if (!colstats_done) {
+    hipLaunchKernelGGL(kde_colstats_kernel, dim3(ps.nk * ps.k[0].D), dim3(256), 0, s, ps);
     HBX_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(kde_prep_finish_kernel, dim3(1), dim3(64), 0, s, ps);
+  hipLaunchKernelGGL(kde_params_kernel, dim3(ps.nk), dim3(256), 0, s, ps);
   HBX_LAUNCH_CHECK();
+  const bool all_tables = ps.k[0].nblk_table > 0 && (ps.nk < 2 || ps.k[1].nblk_table > 0);
+  const unsigned tb = (unsigned)(ps.k[0].nblk_table + (ps.nk > 1 ? ps.k[1].nblk_table : 0));
+  if (tb > 0) {
+    hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 0, all_tables ? 1 : 0);
+    HBX_LAUNCH_CHECK();
+  }
+  if (!all_tables) {  // an exact-only KDE (no table) in the set: the separate passes
+    if (tb > 0) {
+      hipLaunchKernelGGL(kde_table_kernel, dim3(tb), dim3(64), 0, s, ps, table0, table1, 1, 0);
+      HBX_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(kde_prep_finish_kernel, dim3(1), dim3(64), 0, s, ps);
+    HBX_LAUNCH_CHECK();
+  }
   return HBX_OK;
 }
 
@@ -1716,6 +1765,8 @@ struct ScoreFns {
   bool split_ok = false;  // the pair kernel takes observation splits and initialises a single acquisition's
                           // state (the 32x32-tile instances)
   combine_fn combine_rescue = nullptr;  // the combine kernel doing the rescue pass of this instance
+  logpdf_pair_fn pair_ct1 = nullptr;    // the coarse pair instance with one column tile per wave, or nullptr
+  int cands_per_block_ct1 = 0;
 };
 
 // Observation splits of a pair launch with `tiles` candidate tiles per KDE over <= nmax observations: a
@@ -1738,20 +1789,6 @@ static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
   if (sp > nch / 4) sp = nch / 4;
   if (sp > OBS_SPLIT_MAX) sp = OBS_SPLIT_MAX;
   return sp < 1 ? 1 : (int)sp;
-}
-
-// the shortlist done by the exact re-score's blocks for few candidates (HBX_EXACT_SCAN=0: its own launch;
-// read per call)
-static bool exact_scan_enabled() {
-  const char* e = getenv("HBX_EXACT_SCAN");
-  return !(e && atoi(e) == 0);
-}
-
-// the rescue pass done by the combine kernel where it can (HBX_COMBINE_RESCUE=0: its own launch; read per
-// call: tests switch it in-process)
-static bool combine_rescue_enabled() {
-  const char* e = getenv("HBX_COMBINE_RESCUE");
-  return !(e && atoi(e) == 0);
 }
 
 // l and g scored by one launch of the pair kernel when both KDEs run the same hmode instance;
@@ -1810,7 +1847,8 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
             sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true,
-            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>};
+            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>,
+            (co && H32C_CT > 1) ? hbx_pick_h32_pair_ct1(nsc_of(dc_pad), kp) : nullptr, 32 * hw};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1847,7 +1885,7 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
   const bool pair = f0.pair && f0.main == f1.main && f0.rescue_pair && f0.rescue == f1.rescue && pair_enabled();
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
-    const unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
+    unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
     const bool can = f0.split_ok && nsplit_out && nmax > 0;
@@ -1855,6 +1893,13 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
     // blocks -- splitting only the bad KDE's longer walks in two measured 3-5 us slower, like splitting
     // both: each range repeats the block's prologue, and the merge reads twice the estimates.)
     const int ns0 = can ? obs_splits(gm, nmax) : 1, ns1 = ns0;
+    // at most one two-tile block per slot and KDE without splits (config #2: 2 x 196 blocks of 14 and 3 chunks
+    // on 512 slots, busy 46 %): one column tile per wave -- twice the blocks, each half the work
+    logpdf_pair_fn pk = f0.pair;
+    if (ns0 == 1 && f0.pair_ct1 && f0.pair_ct1 == f1.pair_ct1 && 2 * gm <= 512u) {
+      pk = f0.pair_ct1;
+      gm = (unsigned)((Nc + f0.cands_per_block_ct1 - 1) / f0.cands_per_block_ct1);
+    }
     KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns0,
                   rescue_cnt, {}};
     a.tiles = gm;
@@ -1868,15 +1913,14 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
     const bool pinit = f0.split_ok && HBX_PAIR_INIT;
     if (pinit) a.init = init;  // the 32x32 pair kernel's first workgroup sets the acquisition state
     if (ev)  // events stamped by the dispatch itself at the kernel's start and end (rocprof's duration)
-      hipExtLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
+      hipExtLaunchKernelGGL(pk, dim3(grid), dim3(f0.threads), 0, s, ev[0], ev[1], 0, cand, Nc, D, a);
     else
-      hipLaunchKernelGGL(f0.pair, dim3(grid), dim3(f0.threads), 0, s, cand, Nc, D, a);
+      hipLaunchKernelGGL(pk, dim3(grid), dim3(f0.threads), 0, s, cand, Nc, D, a);
     HBX_LAUNCH_CHECK();
     a.nblk0 = gr;
     a.init = pinit ? KdePairArgs::AcqInitPtrs{} : init;  // else set by the rescue pass's first workgroup
     if (inited) *inited = init.U != nullptr;
-    if (rescue_inline && pinit && f0.combine_rescue && rescue_cnt && ns0 == 1 && ns1 == 1 &&
-        combine_rescue_enabled()) {
+    if (rescue_inline && pinit && f0.combine_rescue && rescue_cnt && ns0 == 1 && ns1 == 1) {
       *rescue_inline = true;  // the combine kernel re-scores the marked candidates
       return HBX_OK;
     }
@@ -1995,18 +2039,6 @@ int hbx_kde_prepare(const double* X, int32_t D, const int64_t* rows, int32_t n, 
 // ---- one-call refit (BOHB.new_result, bohb.py:211-251) ------------------------------------------
 // Split metadata hbx_seg_argsort / hbx_kde_fit read from device memory, written by a kernel from its
 // arguments (no host copy).
-struct RefitMeta {
-  int64_t seg[2];
-  int64_t n_good, n_bad;
-  double fac_good, fac_bad;
-  int32_t vt[HBX_MAX_D];
-};
-struct RefitMetaArgs {
-  int64_t n, n_good, n_bad;
-  double fac_good, fac_bad;
-  int32_t D;
-  uint32_t vt[HBX_MAX_D / 32];
-};
 static size_t refit_meta_bytes() { return (sizeof(RefitMeta) + 255) & ~(size_t)255; }
 
 // Append the n_new staged rows ([n_new][D] then n_new losses) at rows n - n_new .. n - 1 of X / loss,
@@ -2103,19 +2135,30 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
   memcpy(ma.vt, ps.k[0].vt, sizeof(ma.vt));
   RefitMeta* m = (RefitMeta*)scratch;
   char* sort_scratch = (char*)scratch + refit_meta_bytes();
-  const int64_t per = n_new * (int64_t)(D + 1);
-  const unsigned gmeta = (unsigned)(per > 0 ? ((per + 255) / 256 < 1024 ? (per + 255) / 256 : 1024) : 1);
-  hipLaunchKernelGGL(kde_refit_meta_kernel, dim3(gmeta), dim3(256), 0, s, X, loss, staged, n_new, ma, m);
-  HBX_LAUNCH_CHECK();
   // numpy's argsort order (bohb.py:229): tied losses -- crashed +inf runs, quantised losses -- give the
   // reference's rows in the reference's order
-  rc = hbx_seg_argsort_ex(loss, m->seg, 1, n, n, order, sort_scratch, hbx_sort_scratch_bytes(n), HBX_ORDER_NUMPY,
-                          stream);
+  if (n <= REFIT_SORT_SMALL) {  // one launch: rows appended, metadata, sort, numpy's tie order
+    rc = refit_sort_small(X, loss, staged, n_new, ma, m, order, (int32_t*)sort_scratch, s);
+    if (rc) return rc;
+  } else {
+    const int64_t per = n_new * (int64_t)(D + 1);
+    const unsigned gmeta = (unsigned)(per > 0 ? ((per + 255) / 256 < 1024 ? (per + 255) / 256 : 1024) : 1);
+    hipLaunchKernelGGL(kde_refit_meta_kernel, dim3(gmeta), dim3(256), 0, s, X, loss, staged, n_new, ma, m);
+    HBX_LAUNCH_CHECK();
+    rc = hbx_seg_argsort_ex(loss, m->seg, 1, n, n, order, sort_scratch, hbx_sort_scratch_bytes(n), HBX_ORDER_NUMPY,
+                            stream);
+    if (rc) return rc;
+  }
+  // both sets within one LDS tile: the fit also writes the preparation's column statistics (one launch less)
+  const bool fused = D > 1 && n_good <= FIT_TILE_ROWS && n_bad <= FIT_TILE_ROWS;
+  if (fused)
+    rc = refit_fit_colstats(X, D, m->seg, order, &m->n_good, &m->n_bad, &m->fac_good, &m->fac_bad, m->vt, bw_g, bw_b,
+                            nl_g, nl_b, col_stats((KdeParams*)params_good), col_stats((KdeParams*)params_bad), s);
+  else
+    rc = hbx_kde_fit(X, D, m->seg, 1, order, &m->n_good, &m->n_bad, &m->fac_good, &m->fac_bad, m->vt, bw_g, bw_b,
+                     nl_g, nl_b, stream);
   if (rc) return rc;
-  rc = hbx_kde_fit(X, D, m->seg, 1, order, &m->n_good, &m->n_bad, &m->fac_good, &m->fac_bad, m->vt, bw_g, bw_b, nl_g,
-                   nl_b, stream);
-  if (rc) return rc;
-  return prep_launch(ps, table_good, table_bad, s);
+  return prep_launch(ps, table_good, table_bad, s, fused);
 }
 
 }  // extern "C"
@@ -2229,7 +2272,7 @@ static int acquire_impl(const char* who, const double* cand, int64_t Nc, int64_t
       HBX_LAUNCH_CHECK();
     }
     // a single acquisition of few candidates: the exact re-score's blocks shortlist for themselves
-    const bool scan = !batch_res && Nc <= EXACT_SCAN_MAX && exact_scan_enabled();
+    const bool scan = !batch_res && Nc <= EXACT_SCAN_MAX;
     if (!scan) {
       hipLaunchKernelGGL(kde_shortlist_kernel, grid, dim3(256), 0, s, lo, Nc, sg, U, flags, list, count,
                          batch_res ? segcnt : (int32_t*)nullptr, first1, (int32_t*)(ws + w.rescue));
@@ -2500,7 +2543,7 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 // Candidates whose bound stays within 0.99 rtol max(1, |ln p|) are written; the rest go to `list` for the
 // fp64 pass.  KDEs with negative categorical factors, structural NaN or single-level dims: all to `list`.
 template <int DC, int DU, int CPT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 32 ? 4 : 2))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 16 ? 4 : DC + DU <= 40 ? 3 : 2))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
                                                            const KdeParams* __restrict__ P,
                                                            const double* __restrict__ X,
                                                            const int64_t* __restrict__ rows, double rtol,
@@ -2628,7 +2671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 
     f2 a0 = f2{0.f, 0.f}, a1 = f2{0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-      const f2 X2 = f2{r[2 * q], r[2 * q + 1]};
+      const f2 X2 = f2{r[2 * q], r[2 * q + 1]};  // (the row is read as whole 16-byte vectors: see rowv)
       const f2 d = xc[c][q] - X2;
       if (q < NB / 2) a0 = __builtin_elementwise_fma(-d, d, a0);
       else a1 = __builtin_elementwise_fma(-d, d, a1);
@@ -2663,7 +2706,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 
   for (int c = 0; c < CPT; ++c) {
     S[c] = 0.0;
     s4[c] = 0.f;
-    if (!(m[c] > -INFINITY)) m[c] = 0.f;  // no finite term in chunk 0 (or NaN): any reference point
+    // an integer reference point (rescales are exact ldexps); no finite term in chunk 0 (or NaN): any
+    m[c] = m[c] > -INFINITY ? ceilf(m[c]) : 0.f;
   }
   for (int cc = 0; cc < nch; ++cc) {
     const int b = cc & 1;
@@ -2675,17 +2719,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 
     for (int j4 = 0; j4 < jg; j4 += 4) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float* r = &xs[b][j4 + q][0];
+        float r[W];  // the staged row, read as 16-byte vectors (ds_read_b128)
+#pragma unroll
+        for (int v = 0; v < W / 4; ++v) {
+          const float4 f = reinterpret_cast<const float4*>(&xs[b][j4 + q][0])[v];
+          r[4 * v] = f.x;
+          r[4 * v + 1] = f.y;
+          r[4 * v + 2] = f.z;
+          r[4 * v + 3] = f.w;
+        }
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
           const float t = term(c, r);
           float e = __builtin_amdgcn_exp2f(t - m[c]);
-          if (!(e < 0x1p100f)) {  // rare: a term far above the reference point (or NaN): move it up to t
+          if (!(e < 0x1p100f)) {  // rare: a term far above the reference point (or NaN): move it up to ceil(t)
             if (t == t) {
-              S[c] = (S[c] + (double)s4[c]) * exp2((double)m[c] - (double)t);
+              const float mn = ceilf(t);  // integer reference points: the rescale is an exact ldexp
+              S[c] = ldexp(S[c] + (double)s4[c], (int)(m[c] - mn));
               s4[c] = 0.f;
-              m[c] = t;
-              e = 1.f;
+              m[c] = mn;
+              e = __builtin_amdgcn_exp2f(t - mn);
             }
           }
           s4[c] += e;
@@ -2734,7 +2787,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 
 typedef void (*logpdf_dd_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*, double,
                              double*, int32_t*, int32_t*);
 // candidates per thread: two share each staged row where both fit the register budget
-constexpr int dd_cpt(int dc, int du) { return dc + du <= 16 ? 2 : 1; }
+constexpr int dd_cpt(int dc, int du) { return 2; }
 
 template <int DC>
 static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt) {
@@ -2788,12 +2841,6 @@ extern "C" {
 
 typedef void (*logpdf_tiled_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*,
                                 double*, const int32_t*, const int32_t*);
-
-// HBX_LOGPDF_TILED=0: the per-point fp64 kernel for every re-evaluated candidate (A/B)
-static bool tiled_enabled() {
-  const char* e = getenv("HBX_LOGPDF_TILED");
-  return !(e && atoi(e) == 0);
-}
 
 template <int DC, bool E64>
 static logpdf_tiled_fn pick_tiled_du(int du_pad) {
@@ -2868,7 +2915,7 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
   const unsigned grid = (unsigned)(Nc < EXACT_GRID ? Nc : EXACT_GRID);
   // the rest in fp64 log space (positive factors): tiled over candidates where the bucket has an instance,
   // else one block per point (its kernel exits for KDEs the tiled one would mis-handle: see below)
-  const logpdf_tiled_fn tf = exact_only || !tiled_enabled() ? nullptr : pick_logpdf_tiled(dc_pad, du_pad, rtol < 1e-5);
+  const logpdf_tiled_fn tf = exact_only ? nullptr : pick_logpdf_tiled(dc_pad, du_pad, rtol < 1e-5);
   if (tf)
     hipLaunchKernelGGL(tf, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params,
                        X, rows, out, list, count);

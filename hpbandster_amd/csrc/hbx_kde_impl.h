@@ -312,6 +312,32 @@ __host__ __device__ inline void obs_split_range(int nchunks, int r, int nsplit, 
   *nch = e - *c0;
 }
 
+// one-call refit (hbx_kde_refit): the split metadata hbx_seg_argsort / hbx_kde_fit read from device memory,
+// written by a kernel from its arguments (no host copy)
+struct RefitMeta {
+  int64_t seg[2];
+  int64_t n_good, n_bad;
+  double fac_good, fac_bad;
+  int32_t vt[HBX_MAX_D];
+};
+struct RefitMetaArgs {
+  int64_t n, n_good, n_bad;
+  double fac_good, fac_bad;
+  int32_t D;
+  uint32_t vt[HBX_MAX_D / 32];
+};
+// hbx_fit.hip: append the staged rows, write the metadata and sort a refit's n <= REFIT_SORT_SMALL losses in
+// numpy's order -- one launch for what the metadata kernel, the counting rank and the tie check did in five
+#define REFIT_SORT_SMALL 1024
+int refit_sort_small(double* X, double* loss, const double* staged, int64_t n_new, const RefitMetaArgs& a,
+                     RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s);
+
+int refit_fit_colstats(const double* X, int32_t D, const int64_t* seg_off, const int64_t* order, const int64_t* n_good,
+                       const int64_t* n_bad, const double* fac_good, const double* fac_bad, const int32_t* vartype,
+                       double* bw_good, double* bw_bad, int32_t* nlev_good, int32_t* nlev_bad, ColStats* cs_good,
+                       ColStats* cs_bad, hipStream_t s);
+#define FIT_TILE_ROWS 16384  // kde_fit_col_kernel's LDS tile (FIT_TILE)
+
 // host-side pickers of the scoring kernel instances (nullptr when the bucket has none)
 logpdf_fn hbx_pick_f32(int dc_pad, int du_pad, bool sg);   // hbx_score_f32.hip
 logpdf_fn hbx_pick_oh(int dc_pad, int kc, bool sg);        // hbx_score_oh.hip
@@ -319,3 +345,4 @@ logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
 logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse = false);  // hbx_score_h32.hip
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse = false);
+logpdf_pair_fn hbx_pick_h32_pair_ct1(int nsc, int kp);  // the coarse pair instance, one column tile per wave

@@ -437,8 +437,7 @@ int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int
   int32_t* gi = (int32_t*)(gk2 + N);
   int32_t* gi2 = gi + N;
   int64_t* ord = order ? order : (int64_t*)(sc + ((2 * (sizeof(uint64_t) + sizeof(int32_t)) * N + 7) & ~(size_t)7));
-  const char* wenv = getenv("HBX_PROMOTE_WAVE");  // 0: the block-per-bracket kernel for every size
-  if (max_seg <= 64 * PW_PER_LANE && !(wenv && atoi(wenv) == 0)) {
+  if (max_seg <= 64 * PW_PER_LANE) {  // one wave per bracket; longer brackets: a block each
     hipLaunchKernelGGL(sh_promote_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, loss, seg_off, B, k,
                        ord, advance, n_advance);
   } else {

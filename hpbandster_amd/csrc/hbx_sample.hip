@@ -171,80 +171,13 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
   return fma(bw_factor * h, flip ? -z : z, m);
 }
 
-// A block draws 64 candidates: lane l of every wave is candidate c0 + l, and wave w draws the pairs of
-// dims w, w + W, ... (W waves), so a wave's dims -- continuous or categorical, their bandwidths and
-// levels -- are uniform and the branches of sample_dim never split a wave.  Counter (candidate, pair of
-// dims, stream) and arithmetic as before: the draws do not depend on the launch shape.  Results go
-// through an LDS tile (row stride S doubles, even) and leave as contiguous 16-byte stores of the block's
-// 64 rows.  The datum draw of each candidate is made once (wave 0) and shared through LDS.
-template <bool TAB>
-__global__ __launch_bounds__(512) void kde_sample_kernel(
-    const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
-    const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
-    double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
-    double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
-  extern __shared__ __align__(16) double tile[];  // [64][S]
-  __shared__ int32_t sdat[64];
-  __shared__ double srh[HBX_MAX_D];  // 1 / bw per dim
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int W = blockDim.x >> 6;
-  const int S = (D + 2) & ~1;
-  const int D2 = (D + 1) >> 1;
-  const int64_t c0 = (int64_t)blockIdx.x * 64;
-  const int nc = (int)(Nc - c0 < 64 ? Nc - c0 : 64);  // candidates of this block
-  const int64_t i = c0 + lane;
-  for (int t = threadIdx.x; t < D; t += blockDim.x) srh[t] = 1.0 / bw[t];
-  if (wave == 0 && lane < nc) {
-    const uint64_t rb = hbx_bits64(draw(seed, counter_base + (uint64_t)i, DATUM_WORD, stream_id), 0);
-    const int32_t idx = (int32_t)__umul64hi(rb, (uint64_t)n);  // floor(u * n), u = rb / 2^64
-    sdat[lane] = idx;
-    if (datum) datum[i] = idx;
-  }
-  __syncthreads();
-  if (lane < nc) {
-    const int32_t idx = sdat[lane];
-    const double* xr = X + rows[idx] * (int64_t)D;
-    bool derr = false;
-    for (int k = wave; k < D2; k += W) {
-      const int d = 2 * k;
-      const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
-      const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
-      if (d + 1 < D) {
-        const double v1 = sample_dim<TAB>(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
-        *(double2*)(tile + lane * S + d) = make_double2(v0, v1);
-      } else {
-        tile[lane * S + d] = v0;
-      }
-    }
-    if (derr && domain_err) domain_err[i] = 1;
-  }
-  __syncthreads();
-  // the block's rows are contiguous in HBM: nc * D doubles from cands + c0 * D
-  double* out = cands + c0 * (int64_t)D;
-  if ((D & 1) == 0) {
-    const int h = D >> 1;  // 16-byte pieces per row
-    const float rh = 1.f / (float)h;
-    for (int j = threadIdx.x; j < nc * h; j += blockDim.x) {
-      const int row = (int)(((float)j + 0.5f) * rh);  // exact: (j + 1/2) / h is >= 1/(2h) from an integer
-      const int col = 2 * (j - row * h);
-      *(double2*)(out + 2 * j) = *(const double2*)(tile + row * S + col);
-    }
-  } else {
-    const float rd = 1.f / (float)D;
-    for (int j = threadIdx.x; j < nc * D; j += blockDim.x) {
-      const int row = (int)(((float)j + 0.5f) * rd);
-      out[j] = tile[row * S + (j - row * D)];
-    }
-  }
-}
-
-// The same draws with one (candidate, pair of dims) per lane: 8 lanes per candidate, lane g of the group
-// takes the pairs g, g + 8, ...  A candidate's datum row and Phi-table row are then read by its 8 lanes
-// as contiguous 16-byte pieces (a wave touches ~6 cache lines per candidate instead of 64: the lane-per-
-// candidate kernel above waits on the 64 distinct lines every one of its gathers touches) and its output
-// row is written as contiguous 16-byte stores, no LDS tile.  Dim types and bandwidths vary across the
-// lanes (loaded per lane; the categorical branch is the cheap one).  Counter (candidate, pair, stream),
-// datum draw and arithmetic are the lane-per-candidate kernel's: the draws are identical.
+// The draws with one (candidate, pair of dims) per lane: 8 lanes per candidate, lane g of the group takes
+// the pairs g, g + 8, ...  A candidate's datum row and Phi-table row are then read by its 8 lanes as
+// contiguous 16-byte pieces (a wave touches ~6 cache lines per candidate instead of the 64 a lane-per-
+// candidate layout waited on -- that kernel, 8-9 % slower with the same draws, was removed in round 5) and
+// its output row is written as contiguous 16-byte stores, no LDS tile.  Dim types and bandwidths vary across
+// the lanes (loaded per lane; the categorical branch is the cheap one).  Counter (candidate, pair of dims,
+// stream): the draws do not depend on the launch shape.
 template <bool TAB>
 __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
@@ -333,25 +266,11 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   hipStream_t s = (hipStream_t)stream;
   if (domain_err) HBX_HIP(hipMemsetAsync(domain_err, 0, (size_t)Nc, s));
   if ((D & 1) == 0 && ((uintptr_t)cands & 15)) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: cands not 16-byte aligned");
-  const int D2 = (D + 1) / 2, W = D2 < 8 ? D2 : 8;  // waves per block: pairs of dims drawn side by side
-  const size_t lds = (size_t)64 * ((D + 2) & ~1) * sizeof(double);
-  const int64_t blocks = (Nc + 63) / 64;
-  if (blocks > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
-  const char* kenv = getenv("HBX_SAMPLE_LANES");  // "candidate": the lane-per-candidate kernel
-  if (!(kenv && !strcmp(kenv, "candidate")) && D <= HBX_MAX_D) {  // one (candidate, pair of dims) per lane
-    const int64_t pb = (Nc + 31) / 32;
-    if (pb > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
-    hipLaunchKernelGGL(tab ? kde_sample_pair_kernel<true> : kde_sample_pair_kernel<false>, dim3((unsigned)pb), dim3(256),
-                       0, s, X, D, rows, n, bw, levels, (const double2*)tab, bw_factor, seed, counter_base, stream_id,
-                       Nc, cands, datum, domain_err);
-    HBX_LAUNCH_CHECK();
-    return HBX_OK;
-  }
-  const void* kfn = tab ? (const void*)kde_sample_kernel<true> : (const void*)kde_sample_kernel<false>;
-  if (lds > 65536)  // D > 126: the tile needs more than the default dynamic LDS limit (<= 132 KB at D = 256)
-    HBX_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(tab ? kde_sample_kernel<true> : kde_sample_kernel<false>, dim3((unsigned)blocks), dim3(64 * W), lds, s, X, D, rows, n, bw, levels,
-                     (const double2*)tab, bw_factor, seed, counter_base, stream_id, Nc, cands, datum, domain_err);
+  const int64_t pb = (Nc + 31) / 32;  // one (candidate, pair of dims) per lane: 32 candidates per block
+  if (pb > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
+  hipLaunchKernelGGL(tab ? kde_sample_pair_kernel<true> : kde_sample_pair_kernel<false>, dim3((unsigned)pb), dim3(256),
+                     0, s, X, D, rows, n, bw, levels, (const double2*)tab, bw_factor, seed, counter_base, stream_id,
+                     Nc, cands, datum, domain_err);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }

@@ -1,9 +1,7 @@
 """Batched KDE refit of many segments (hbx_kde_fit; config #5's per-bracket refit, bohb.py:220-246): the
-LDS-resident kernel (rows read once in storage order, placed by rank) and the per-column gather kernel
-against numpy's own np.std(axis=0) / np.unique on the same split -- bit for bit, ragged segments,
+LDS-resident kernel (rows read once in storage order, placed by rank) and, at D = 1, the per-column gather
+kernel, against numpy's own np.std(axis=0) / np.unique on the same split -- bit for bit, ragged segments,
 long segments (the in-kernel gather path), empty and oversized sets, wide and invalid level codes."""
-import os
-
 import numpy as np
 import pytest
 
@@ -38,7 +36,7 @@ def _case(D, dc, seed):
     return B, lens, seg, X, order, ng, nb
 
 
-def _run(device, D, dc, seed, lds):
+def _run(device, D, dc, seed):
     import torch
     from hpbandster_amd import _native as N
     from hpbandster_amd import kde
@@ -49,18 +47,10 @@ def _run(device, D, dc, seed, lds):
     ins = [torch.from_numpy(a).to(device) for a in (X, seg, order, ng, nb, fg, fb, vt)]
     outs = [torch.empty((B, D), dtype=torch.float64, device=device) for _ in range(2)] + \
            [torch.empty((B, D), dtype=torch.int32, device=device) for _ in range(2)]
-    old = os.environ.get("HBX_FIT_LDS")
-    os.environ["HBX_FIT_LDS"] = "1" if lds else "0"
-    try:
-        Xd, segd, od, ngd, nbd, fgd, fbd, vtd = ins
-        N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(od), N.ptr(ngd), N.ptr(nbd), N.ptr(fgd),
-               N.ptr(fbd), N.ptr(vtd), *[N.ptr(o) for o in outs], N.stream_handle())
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            del os.environ["HBX_FIT_LDS"]
-        else:
-            os.environ["HBX_FIT_LDS"] = old
+    Xd, segd, od, ngd, nbd, fgd, fbd, vtd = ins
+    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(od), N.ptr(ngd), N.ptr(nbd), N.ptr(fgd),
+           N.ptr(fbd), N.ptr(vtd), *[N.ptr(o) for o in outs], N.stream_handle())
+    torch.cuda.synchronize()
     bwg, bwb, nlg, nlb = (o.cpu().numpy() for o in outs)
     for b in range(B):
         n = int(lens[b])
@@ -85,8 +75,10 @@ def _run(device, D, dc, seed, lds):
 
 @pytest.mark.parametrize("D,dc", [(32, 24), (13, 9), (40, 40)])
 def test_batched_fit_lds_kernel_bit_exact(device, D, dc):
-    _run(device, D, dc, 100 + D, lds=True)
+    _run(device, D, dc, 100 + D)
 
 
-def test_batched_fit_gather_kernel_bit_exact(device):
-    _run(device, 32, 24, 7, lds=False)
+@pytest.mark.parametrize("dc", [1, 0])
+def test_batched_fit_gather_kernel_bit_exact(device, dc):
+    """D = 1 (one continuous or one categorical dim): the per-column gather kernel."""
+    _run(device, 1, dc, 7)

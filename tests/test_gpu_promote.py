@@ -199,10 +199,11 @@ def test_config5_full_shape_every_mask(device):
 
 
 @pytest.mark.parametrize("B,n", [(300, 1024), (97, 200), (5, 1), (64, 3)])
-def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
-    """Brackets of <= 1024 configurations run the register-resident wave kernel; HBX_PROMOTE_WAVE=0
-    forces the LDS block kernel.  Same (loss, position) order: order, masks and counts identical,
-    masks equal to the oracle; empty brackets, ties and non-finite losses included."""
+def test_wave_kernel_identical_to_block_kernel(device, B, n):
+    """Launches whose brackets are all <= 1024 configurations run the register-resident wave kernel; one
+    longer bracket in the launch sends every bracket to the LDS block kernel.  Same (loss, position) order:
+    the shared brackets' order, masks and counts identical, masks equal to the oracle; empty brackets, ties
+    and non-finite losses included."""
     from hpbandster_amd import promote
     rs = np.random.RandomState(B + n)
     lens = rs.randint(0, n + 1, size=B)
@@ -212,11 +213,13 @@ def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
     loss[rs.rand(seg[-1]) < 0.03] = np.nan
     loss[rs.rand(seg[-1]) < 0.01] = -np.inf
     k = np.maximum(lens * 0.34, 1.0)
-    monkeypatch.setenv("HBX_PROMOTE_WAVE", "1")
     a1, o1, c1 = (t.cpu().numpy() for t in promote.promote_segments(loss, seg, k, device=device, return_order=True))
-    monkeypatch.setenv("HBX_PROMOTE_WAVE", "0")
-    a0, o0, c0 = (t.cpu().numpy() for t in promote.promote_segments(loss, seg, k, device=device, return_order=True))
-    np.testing.assert_array_equal(a1, a0)
+    long = rs.rand(1100)  # a bracket beyond the wave kernel's 1024
+    loss2 = np.concatenate([loss, long])
+    seg2 = np.concatenate([seg, [seg[-1] + long.size]]).astype(np.int64)
+    a0, o0, c0 = (t.cpu().numpy() for t in promote.promote_segments(loss2, seg2, np.concatenate([k, [300.0]]),
+                                                                      device=device, return_order=True))
+    np.testing.assert_array_equal(a1[:seg[-1]], a0[:seg[-1]])
     np.testing.assert_array_equal(o1[:seg[-1]], o0[:seg[-1]])
     np.testing.assert_array_equal(c1[:B], c0[:B])
     for b in range(B):
@@ -225,10 +228,10 @@ def test_wave_kernel_identical_to_block_kernel(device, B, n, monkeypatch):
 
 
 @pytest.mark.parametrize("B,n", [(200, 1024), (33, 100), (1, 1000), (3, 1500), (1, 10000), (4, 3000)])
-def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
+def test_seg_argsort_is_numpy_stable_argsort(device, B, n):
     """hbx_seg_argsort (the refit's split, bohb.py:220): np.argsort order (-inf < finite < +inf < NaN),
     ties by position, through the wave kernel (segments <= 1024) or the counting-rank kernel
-    (1024 < segments <= 65536), and the block kernel (HBX_PROMOTE_WAVE=0 HBX_SORT_RANK=0)."""
+    (1024 < segments <= 65536), and the block kernel (a segment beyond 65536 in the same launch)."""
     import torch
     from hpbandster_amd import _native as N
     rs = np.random.RandomState(B * 3 + n)
@@ -242,16 +245,17 @@ def test_seg_argsort_is_numpy_stable_argsort(device, B, n, monkeypatch):
     loss[rs.rand(seg[-1]) < 0.03] = -0.0  # equal to 0.0 for numpy's sort: ties by position
     loss[rs.rand(seg[-1]) < 0.03] = 0.0
     L = N.lib()
-    ld = torch.from_numpy(loss).to(device)
-    segd = torch.from_numpy(seg).to(device)
-    sb = int(L.hbx_sort_scratch_bytes(int(seg[-1])))
-    scr = torch.empty(max(sb, 1), dtype=torch.uint8, device=device)
     outs = []
-    for wave in ("1", "0"):
-        monkeypatch.setenv("HBX_PROMOTE_WAVE", wave)
-        monkeypatch.setenv("HBX_SORT_RANK", wave)
-        order = torch.full((max(int(seg[-1]), 1),), -1, dtype=torch.int64, device=device)
-        N.call("hbx_seg_argsort", N.ptr(ld), N.ptr(segd), B, int(lens.max()), int(seg[-1]), N.ptr(order),
+    for extra in (0, 70000):  # 70000: one segment beyond the counting rank's limit -> the block kernel
+        lv = np.concatenate([loss, rs.rand(extra)])
+        sg = np.concatenate([seg, [seg[-1] + extra]]).astype(np.int64) if extra else seg
+        ld = torch.from_numpy(lv).to(device)
+        segd = torch.from_numpy(sg).to(device)
+        nt = int(sg[-1])
+        sb = int(L.hbx_sort_scratch_bytes(nt))
+        scr = torch.empty(max(sb, 1), dtype=torch.uint8, device=device)
+        order = torch.full((max(nt, 1),), -1, dtype=torch.int64, device=device)
+        N.call("hbx_seg_argsort", N.ptr(ld), N.ptr(segd), len(sg) - 1, int(np.diff(sg).max()), nt, N.ptr(order),
                N.ptr(scr), sb, N.stream_handle())
         outs.append(order.cpu().numpy()[:seg[-1]])
     np.testing.assert_array_equal(outs[0], outs[1])

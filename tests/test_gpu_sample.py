@@ -183,19 +183,3 @@ def test_norm_ppf_matches_scipy_ndtri(device):
     assert np.abs(z - ref)[~central].max() < 1e-14
 
 
-@pytest.mark.parametrize("dc,du,table", [(24, 8, True), (24, 8, False), (5, 2, True), (6, 3, False)])
-def test_pair_lanes_kernel_identical_draws(device, dc, du, table, monkeypatch):
-    """The (candidate, pair of dims)-per-lane sampler (default) and the lane-per-candidate kernel
-    (HBX_SAMPLE_LANES=candidate) draw the same values bit for bit -- the same counters and arithmetic --
-    at even and odd D, with and without the Phi table, on a ragged last block."""
-    from hpbandster_amd import kde
-    from hpbandster_amd import synthetic as S
-    X = S.make_observations(600, dc, du, 4, seed=31)
-    pair = kde.fit_pair(X, S.make_losses(600, seed=32), S.var_type_string(dc, du), dc + du + 1, device=device)
-    lv = np.array([0] * dc + [4] * du)
-    a, da, ea = pair.good.sample(lv, 3.0, 3001, seed=11, counter_base=7, table=table)
-    monkeypatch.setenv("HBX_SAMPLE_LANES", "candidate")
-    b, db, eb = pair.good.sample(lv, 3.0, 3001, seed=11, counter_base=7, table=table)
-    assert np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True)
-    assert np.array_equal(da.cpu().numpy(), db.cpu().numpy())
-    assert np.array_equal(ea.cpu().numpy(), eb.cpu().numpy())

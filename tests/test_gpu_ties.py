@@ -40,17 +40,19 @@ def _seg_argsort(device, loss, seg, mode):
 
 
 @pytest.mark.parametrize("path", ["wave", "rank", "block"])
-def test_np_argsort_known_answers(device, path, monkeypatch):
+def test_np_argsort_known_answers(device, path):
     """Every numpy 1.26.4 argsort of np_argsort.npz (sizes 1..10000: +-inf, +-0, NaN, quantised, sorted,
-    periodic) as segments of ONE hbx_seg_argsort_ex(HBX_ORDER_NUMPY) call, behind each stable kernel."""
+    periodic) as segments of ONE hbx_seg_argsort_ex(HBX_ORDER_NUMPY) call, behind each stable kernel (the
+    block kernel: a segment beyond the counting rank's 65536 in the same launch)."""
     from hpbandster_amd import _native as N
-    monkeypatch.setenv("HBX_PROMOTE_WAVE", "0" if path == "block" else "1")
-    monkeypatch.setenv("HBX_SORT_RANK", "0" if path == "block" else "1")
     cases = _np_cases()
     if path == "wave":  # many segments <= 1024: the wave kernel
         cases = [c for c in cases if c[0].size <= 1024]
     elif path == "rank":  # few segments: the counting rank
         cases = [c for c in cases if c[0].size > 200][:40]
+    else:  # + a tie-free 70000-element segment
+        x = np.random.RandomState(5).rand(70000)
+        cases = cases + [(x, np.argsort(x, kind="stable"))]
     loss = np.concatenate([c[0] for c in cases])
     seg = np.concatenate([[0], np.cumsum([c[0].size for c in cases])]).astype(np.int64)
     got = _seg_argsort(device, loss, seg, N.ORDER_NUMPY)

@@ -5,6 +5,7 @@
 #   bash tools/gpu_session.sh TAG bench [BENCH_ARGS...]    -> one bench.py line
 #   bash tools/gpu_session.sh TAG both                     -> the suite, then the default bench line
 #   bash tools/gpu_session.sh TAG py SCRIPT [ARGS...]      -> a tools/ measurement script
+#   bash tools/gpu_session.sh TAG prof SCRIPT [ARGS...]    -> the same under rocprofv3 --kernel-trace --stats
 # Output under gpurun_out/TAG/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -33,5 +34,8 @@ case $MODE in
   bench) run_bench "$@" ;;
   both) run_tests && run_bench ;;
   py) S=$1; shift; timeout -k 10 900 python -u $S "$@" > $OUT/$(basename $S .py).txt 2>&1; rc=$?; tail -40 $OUT/$(basename $S .py).txt; exit $rc ;;
+  prof) S=$1; shift; cd /tmp && export TMPDIR=/tmp && cd $R
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u $S "$@" \
+      > $OUT/$(basename $S .py)_prof.txt 2>&1; rc=$?; tail -20 $OUT/$(basename $S .py)_prof.txt; exit $rc ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac

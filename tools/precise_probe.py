@@ -1,5 +1,4 @@
-"""The ln-pdf contract line of bench.py (precise_logpdf) alone, with the tiled fp64 kernel and the
-per-point one (GPU box): python tools/precise_probe.py"""
+"""The ln-pdf contract line of bench.py (precise_logpdf) alone (GPU box): python tools/precise_probe.py"""
 import json
 import os
 import sys
@@ -15,13 +14,8 @@ def main():
     dev = torch.device("cuda", 0)
     X = S.make_observations(10000, 24, 8, 4)
     pair = kde.fit_pair(X, S.make_losses(10000), S.var_type_string(24, 8), 33, device=dev)
-    C = torch.from_numpy(S.make_candidates(1000000, 24, 8, 4)).to(dev)
-    out = {}
-    for t in ("1", "0"):
-        os.environ["HBX_LOGPDF_TILED"] = t
-        out["tiled" if t == "1" else "per_point"] = bench.precise_line(pair, C if t == "1" else C[:20000].contiguous(),
-                                                                       dev, reps=3 if t == "1" else 1)
-    print(json.dumps(out))
+    C = torch.from_numpy(S.make_candidates_blocked(0, 1000000, 24, 8, 4)).to(dev)
+    print(json.dumps(bench.precise_line(pair, C, dev, reps=5)))
 
 
 if __name__ == "__main__":

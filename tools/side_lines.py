@@ -23,6 +23,17 @@ def main():
                                                                            dims=(4, 2))
         elif name == "config2":
             out["config2"] = bench.config2_line(dev)
+        elif name == "config5":
+            out["config5"] = bench.config5(dev)
+        elif name == "sampler":
+            import numpy as np
+            import torch
+            from hpbandster_amd import kde
+            from hpbandster_amd import synthetic as S
+            X = S.make_observations(10000, 24, 8, 4)
+            pair = kde.fit_pair(X, S.make_losses(10000), S.var_type_string(24, 8), 33, device=dev)
+            ws = torch.empty(pair.workspace_bytes(1_000_000), dtype=torch.uint8, device=dev)
+            out["gpu_sampler"] = bench.sampler_line(pair, dev, 24, 8, 4, 1_000_000, ws)
         print(json.dumps({name: {k: v for k, v in out.items()}}), flush=True)
 
 
