@@ -975,7 +975,7 @@ def kde_result_bytes():
     return kde.RESULT_BYTES
 
 
-PROFILE_SET = "profiles/r04"
+PROFILE_SET = "profiles/r05"
 
 
 def load_traffic(workload):

@@ -15,6 +15,9 @@
 #include "hbx_npsort.h"
 #include "hbx_sort.h"
 #include <stdlib.h>
+#include <string.h>
+#include <stddef.h>
+#include <type_traits>
 
 __device__ double np_pairwise_gather(const double* X, int32_t D, int32_t d, const int64_t* rows, int64_t n,
                                      double mean, bool sq);
@@ -289,18 +292,37 @@ int hbx_np_order_fix(const double* loss, const int64_t* seg_off, int64_t B, int6
 // sort the losses (wave 0: the register network, ties by position), and -- only when two sorted keys are
 // equal -- re-rank the whole segment in numpy 1.26.4's order (hbx_npsort.h, every thread).  The same
 // order as the metadata kernel + counting rank + scatter + tie check + numpy-order launches it replaces.
-__global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(double* __restrict__ X,
-                                                                        double* __restrict__ loss,
-                                                                        const double* __restrict__ staged,
-                                                                        int64_t n_new, RefitMetaArgs a,
-                                                                        RefitMeta* __restrict__ m,
-                                                                        int64_t* __restrict__ order, int32_t* A0) {
+struct RefitSortArgs {
+  double* X;
+  double* loss;
+  const double* staged;  // device rows to append (nullptr: the inline copy below)
+  int64_t n_new;
+  RefitMetaArgs a;
+  RefitMeta* m;
+  int64_t* order;
+  int32_t* A0;
+  double inl[REFIT_INLINE];  // the appended rows then their losses, when they fit (no host-to-device copy)
+};
+
+__global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(RefitSortArgs g) {
   const int tid = threadIdx.x, lane = tid & 63;
+  const RefitMetaArgs& a = g.a;
+  double* __restrict__ X = g.X;
+  double* __restrict__ loss = g.loss;
+  RefitMeta* __restrict__ m = g.m;
+  int64_t* __restrict__ order = g.order;
+  int32_t* A0 = g.A0;
+  const int64_t n_new = g.n_new;
+  // the inline rows read in place from the kernel-argument segment (indexing the by-value argument would copy
+  // it to scratch)
+  const double* inl =
+      (const double*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RefitSortArgs, inl));
   const int n = (int)a.n;
   const int64_t per = n_new * (int64_t)a.D;
   for (int64_t e = tid; e < per + n_new; e += NPS_THREADS) {
-    if (e < per) X[(a.n - n_new) * (int64_t)a.D + e] = staged[e];
-    else loss[a.n - n_new + (e - per)] = staged[e];
+    const double v = g.staged ? g.staged[e] : inl[e];
+    if (e < per) X[(a.n - n_new) * (int64_t)a.D + e] = v;
+    else loss[a.n - n_new + (e - per)] = v;
   }
   for (int d = tid; d < a.D; d += NPS_THREADS) m->vt[d] = (a.vt[d >> 5] >> (d & 31)) & 1u;
   if (tid == 0) {
@@ -334,11 +356,26 @@ __global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(doubl
     nps_order_segment(loss, n, 0, 0.0, A0, A0 + n, A0 + 2 * n, A0 + 3 * n, order, nullptr);
 }
 
-int refit_sort_small(double* X, double* loss, const double* staged, int64_t n_new, const RefitMetaArgs& a,
-                     RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s) {
+int refit_sort_small(double* X, double* loss, const double* staged, const double* staged_inline, int64_t n_new,
+                     const RefitMetaArgs& a, RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s) {
   if (a.n < 1 || a.n > REFIT_SORT_SMALL) return hbx_fail(HBX_ERR_ARG, "refit_sort_small: n=%lld", (long long)a.n);
-  hipLaunchKernelGGL(kde_refit_sort_small_kernel, dim3(1), dim3(NPS_THREADS), 0, s, X, loss, staged, n_new, a, m,
-                     order, arrays);
+  RefitSortArgs g;
+  memset(&g, 0, offsetof(RefitSortArgs, inl));
+  g.X = X;
+  g.loss = loss;
+  g.staged = staged;
+  g.n_new = n_new;
+  g.a = a;
+  g.m = m;
+  g.order = order;
+  g.A0 = arrays;
+  const int64_t nst = n_new * ((int64_t)a.D + 1);
+  if (staged_inline) {
+    if (nst > REFIT_INLINE) return hbx_fail(HBX_ERR_ARG, "refit_sort_small: %lld inline doubles", (long long)nst);
+    g.staged = nullptr;
+    memcpy(g.inl, staged_inline, 8 * (size_t)nst);
+  }
+  hipLaunchKernelGGL(kde_refit_sort_small_kernel, dim3(1), dim3(NPS_THREADS), 0, s, g);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }
@@ -558,181 +595,111 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
   }
 }
 
-// Batched refit of many short segments (config #5: 1e4 brackets x 1e3 configurations at D = 32): one
-// workgroup per (segment, group of FIT_DQ dims).  The segment's rows are read ONCE, in storage order (a
-// group's slice of a row is one 64-byte piece; the segment is one contiguous block), and each slice is
-// written into LDS at its row's rank (the inverse of the argsort).  np.std's two sequential passes --
-// the sum, then the squared deviations, strictly in rank order (axis-0 order, D > 1) -- then read LDS
-// instead of gathering 256-byte rows from HBM twice (random row gathers ran at ~2 TB/s: kde_fit_stats).
-// One wave runs the 2 x FIT_DQ chains ({good, bad} x dims); the CU's other workgroup loads meanwhile.
-// Level counts: one bitmap per (set, dim), filled as the slices land (order-independent).  Segments
-// longer than FIT_LDS_ROWS take the per-column gather path inside the same kernel.
-#define FIT_LDS_ROWS 1024
-#ifndef FIT_DQ
-#define FIT_DQ 4  // dims per workgroup (LDS: FIT_LDS_ROWS x FIT_DQ doubles; 4: four workgroups per CU)
-#endif
-template <bool SQ>
-__device__ __forceinline__ double fit_chain8(const double* v, int m, double mean) {
-  auto val = [&](double x) {
-    if (SQ) {
-      const double q = x - mean;
-      return q * q;
-    }
-    return x;
-  };
-  double acc = 0.0;
-  const int m16 = m & ~15;
-  if (m16 > 0) {  // the next 16 LDS reads in flight during the current 16 dependent adds
-    double r[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r[k] = v[FIT_DQ * k];
-    for (int i = 16; i < m16; i += 16) {
-      double nx[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) nx[k] = v[FIT_DQ * (i + k)];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc = acc + val(r[k]);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) r[k] = nx[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc = acc + val(r[k]);
-  }
-  for (int i = m16; i < m; ++i) acc = acc + val(v[FIT_DQ * i]);
-  return acc;
-}
-
-// One (set, dim) column of a segment by gathering its rows through the order (kde_fit_stats' way): the
-// long-segment path of the LDS kernels.  bm: 33 words of this lane's scratch (level bitmap).
-__device__ void fit_column_gather(const double* Xs, int32_t D, const int64_t* ord, int64_t len, int set, int d,
-                                  int64_t ng, int64_t nb, double fg, double fb, const int32_t* vartype, uint32_t* bm,
-                                  double* bwg, double* bwb, int32_t* nlg, int32_t* nlb) {
-  const int64_t ns = set ? nb : ng;
-  double* bwo = (set ? bwb : bwg) + d;
-  int32_t* nlo = (set ? nlb : nlg) + d;
-  if (ns <= 0 || ns > len) {
-    *bwo = NAN;
-    *nlo = 0;
-    return;
-  }
-  const int64_t* o = ord + (set ? len - ns : 0);
-  const double mean = np_sum_column(Xs, D, d, o, ns, 0.0, false) / (double)ns;
-  const double var = np_sum_column(Xs, D, d, o, ns, mean, true) / (double)ns;
-  int32_t cnt = 0;
-  if (vartype[d] != 0) {
-    for (int w = 0; w < 32; ++w) bm[w] = 0u;
-    for (int64_t i = 0; i < ns && cnt >= 0; ++i) {
-      const double x = Xs[o[i] * (int64_t)D + d];
-      const int v = (int)x;
-      if (!(x >= 0.0 && x < 1024.0) || (double)v != x) {
-        cnt = -1;
-        break;
-      }
-      const uint32_t m = 1u << (v & 31);
-      if (!(bm[v >> 5] & m)) {
-        bm[v >> 5] |= m;
-        ++cnt;
-      }
-    }
-  }
-  *bwo = (1.06 * sqrt(var)) * (set ? fb : fg);
-  *nlo = cnt;
-}
-
-__global__ __launch_bounds__(256) void kde_fit_lds_kernel(
+// Many segments, one LANE per (set, segment, dim) chain, set-major (q = (set B + b) D + d): a wave's lanes are
+// the D dims of one or more segments of the same set, so every step reads whole observation rows (D
+// consecutive doubles: coalesced) and the wave's chains have one length (the set's size).  np.std's
+// axis-0 reduction is one sequential add chain per column (the mean, then the squared deviations); with 64
+// chains per wave instead of the LDS kernel's 8 per workgroup, the chains' add latency hides behind the
+// other waves of the SIMD, and the kernel runs at the rate of its two HBM reads of the rows.  The order is
+// read two batches ahead and the rows one batch ahead of the adds (U loads of each in flight per lane).
+// Level counts: a 128-bit register mask per categorical lane in the mean pass; codes >= 128 (rare) take
+// one more pass per 128-code window.
+#define FIT_WAVE_U 8
+__global__ __launch_bounds__(256) void kde_fit_wave_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
     const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
     const double* __restrict__ fac_good, const double* __restrict__ fac_bad, const int32_t* __restrict__ vartype,
     double* __restrict__ bw_good, double* __restrict__ bw_bad, int32_t* __restrict__ nlev_good,
-    int32_t* __restrict__ nlev_bad, int32_t ngroups, int64_t per_xcd) {
-  __shared__ double vals[FIT_LDS_ROWS * FIT_DQ];  // slot = rank, FIT_DQ dims per slot
-  __shared__ int16_t inv[FIT_LDS_ROWS];            // rank of each row of the segment
-  __shared__ uint32_t bits[2][FIT_DQ][32];         // observed levels per (set, dim)
-  __shared__ int32_t bad_code[2][FIT_DQ];
-  // XCD-aware: workgroup k of XCD x (blockIdx = 8 k + x) takes logical item x per_xcd + k, so the groups
-  // of one segment (neighbouring items, halves of the same 128-byte lines) run on one XCD's L2 together
-  const int64_t item = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (item >= B * ngroups) return;
-  const int64_t b = item / ngroups;
-  const int32_t d0 = (int32_t)(item % ngroups) * FIT_DQ;
-  const int nd = D - d0 < FIT_DQ ? D - d0 : FIT_DQ;
+    int32_t* __restrict__ nlev_bad) {
+  constexpr int U = FIT_WAVE_U;
+  const int64_t per_set = B * (int64_t)D;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= 2 * per_set) return;  // (no barriers below)
+  const int set = q >= per_set ? 1 : 0;
+  const int64_t qq = q - set * per_set;
+  const int64_t b = qq / D;
+  const int32_t d = (int32_t)(qq - b * D);
+  const int64_t ns = set ? n_bad[b] : n_good[b];
   const int64_t s0 = seg_off[b], len = seg_off[b + 1] - s0;
-  const int64_t ng = n_good[b], nb = n_bad[b];
-  const bool okg = ng > 0 && ng <= len, okb = nb > 0 && nb <= len;
-  const int tid = threadIdx.x;
-  const int64_t* ord = order + s0;  // segment-local positions, rank order
-  const double* Xs = X + s0 * (int64_t)D;
-  auto outputs = [&](int set, int j, double bw, int32_t nl) {
-    ((set ? bw_bad : bw_good) + b * D + d0)[j] = bw;
-    ((set ? nlev_bad : nlev_good) + b * D + d0)[j] = nl;
-  };
-  if (len > FIT_LDS_ROWS) {  // long segment: one lane per (set, dim) gathers its column (kde_fit_stats' way)
-    if (tid < 2 * nd)
-      fit_column_gather(Xs, D, ord, len, tid / nd, d0 + tid % nd, ng, nb, fac_good[b], fac_bad[b], vartype,
-                        (uint32_t*)vals + tid * 33, bw_good + b * D, bw_bad + b * D, nlev_good + b * D,
-                        nlev_bad + b * D);
+  double* bwo = (set ? bw_bad : bw_good) + b * D + d;
+  int32_t* nlo = (set ? nlev_bad : nlev_good) + b * D + d;
+  if (ns <= 0 || ns > len) {  // segment not refit (host decided): NaN marker
+    *bwo = NAN;
+    *nlo = 0;
     return;
   }
-  for (int i = tid; i < 2 * FIT_DQ * 32; i += 256) (&bits[0][0][0])[i] = 0u;
-  if (tid < 2 * FIT_DQ) (&bad_code[0][0])[tid] = 0;
-  for (int64_t r = tid; r < len; r += 256) inv[ord[r]] = (int16_t)r;
-  __syncthreads();
-  // the slices: element e = (row e / FIT_DQ, dim e % FIT_DQ), U loads per thread in flight
-  const int64_t total = len * FIT_DQ;
-  const int j = tid % FIT_DQ;  // uniform per thread across e (256 is a multiple of FIT_DQ)
-  const bool catd = j < nd && vartype[d0 + j] != 0;
-  constexpr int U = 16;
-  for (int64_t e0 = 0; e0 < total; e0 += 256 * U) {
-    double v[U];
+  const int64_t* ord = order + s0 + (set ? len - ns : 0);  // rows of the set: head / tail of the argsort
+  const double* Xs = X + s0 * (int64_t)D + d;
+  const bool cat = vartype[d] != 0;
+  uint64_t m0 = 0, m1 = 0;
+  bool badc = false, big = false;
+  // one pass over the set's rows in rank order; SQ: squared deviations from mean, else the plain values
+  // (and the level masks of a categorical column)
+  auto pass = [&](auto sq_tag, double mean) __attribute__((always_inline)) -> double {
+    constexpr bool SQ = decltype(sq_tag)::value;
+    double acc = 0.0;
+    int64_t o1[U], o2[U];
+    double v0[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int64_t e = e0 + k * 256 + tid;
-      v[k] = (e < total && j < nd) ? Xs[(e / FIT_DQ) * D + d0 + j] : 0.0;
-    }
+    for (int k = 0; k < U; ++k) o1[k] = k < ns ? ord[k] : 0;  // (row 0 past the end: read, unused)
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int64_t e = e0 + k * 256 + tid;
-      if (e < total && j < nd) {
-        const int slot = inv[e / FIT_DQ];
-        vals[slot * FIT_DQ + j] = v[k];
-        if (catd) {
-          const double x = v[k];
-          const int iv = (int)x;
-          const bool in_g = okg && slot < ng, in_b = okb && slot >= len - nb;
-          if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) {
-            if (in_g) bad_code[0][j] = 1;
-            if (in_b) bad_code[1][j] = 1;
+    for (int k = 0; k < U; ++k) v0[k] = Xs[o1[k] * (int64_t)D];
+#pragma unroll
+    for (int k = 0; k < U; ++k) o1[k] = U + k < ns ? ord[U + k] : 0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) o2[k] = 2 * U + k < ns ? ord[2 * U + k] : 0;
+    for (int64_t i = 0; i < ns; i += U) {
+      double v1[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v1[k] = Xs[o1[k] * (int64_t)D];  // ranks [i + U, i + 2U)
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        o1[k] = o2[k];
+        o2[k] = i + 3 * U + k < ns ? ord[i + 3 * U + k] : 0;  // ranks [i + 3U, i + 4U)
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (i + k < ns) {
+          const double x = v0[k];
+          if constexpr (SQ) {
+            const double t = x - mean;
+            acc = acc + t * t;
           } else {
-            const uint32_t m = 1u << (iv & 31);
-            if (in_g) atomicOr(&bits[0][j][iv >> 5], m);
-            if (in_b) atomicOr(&bits[1][j][iv >> 5], m);
+            acc = acc + x;
+            if (cat) {
+              const int iv = (int)x;
+              if (!(x >= 0.0 && x < 1024.0) || (double)iv != x) badc = true;
+              else if (iv < 64) m0 |= 1ull << iv;
+              else if (iv < 128) m1 |= 1ull << (iv - 64);
+              else big = true;
+            }
           }
         }
       }
+#pragma unroll
+      for (int k = 0; k < U; ++k) v0[k] = v1[k];
     }
-  }
-  __syncthreads();
-  if (tid < 2 * FIT_DQ) {  // wave 0: the chains
-    const int set = tid / FIT_DQ, jj = tid % FIT_DQ;
-    if (jj < nd) {
-      const int64_t ns = set ? nb : ng;
-      if (!(set ? okb : okg)) {
-        outputs(set, jj, NAN, 0);
-      } else {
-        const double* col = vals + (set ? len - ns : 0) * FIT_DQ + jj;
-        const double mean = fit_chain8<false>(col, (int)ns, 0.0) / (double)ns;
-        const double var = fit_chain8<true>(col, (int)ns, mean) / (double)ns;
-        int32_t cnt = 0;
-        if (vartype[d0 + jj] != 0) {
-          for (int w = 0; w < 32; ++w) cnt += __popc(bits[set][jj][w]);
-          if (bad_code[set][jj]) cnt = -1;
-        }
-        outputs(set, jj, (1.06 * sqrt(var)) * (set ? fac_bad[b] : fac_good[b]), cnt);
+    return acc;
+  };
+  const double mean = pass(std::false_type{}, 0.0) / (double)ns;
+  const double var = pass(std::true_type{}, mean) / (double)ns;
+  *bwo = (1.06 * sqrt(var)) * (set ? fac_bad[b] : fac_good[b]);
+  int32_t cnt = 0;
+  if (cat) {
+    cnt = __popcll(m0) + __popcll(m1);
+    for (int w = 1; big && !badc && w < 8; ++w) {  // codes in [128 w, 128 w + 128): one pass per window
+      uint64_t a = 0, c = 0;
+      for (int64_t i = 0; i < ns; ++i) {
+        const int iv = (int)Xs[ord[i] * (int64_t)D] - 128 * w;
+        if (iv >= 0 && iv < 64) a |= 1ull << iv;
+        else if (iv >= 64 && iv < 128) c |= 1ull << (iv - 64);
       }
+      cnt += __popcll(a) + __popcll(c);
     }
+    if (badc) cnt = -1;
   }
+  *nlo = cnt;
 }
-
 
 extern "C" {
 
@@ -828,13 +795,11 @@ int hbx_kde_fit(const double* X, int32_t D, const int64_t* seg_off, int64_t B, c
   if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_UNSUPPORTED, "D=%d outside [1, %d]", D, HBX_MAX_D);
   if (B <= 0) return HBX_OK;
   const int64_t total = B * 2 * D;
-  if (D > 1 && total >= 16384) {  // many segments: rows read once into LDS
-    const int32_t ngroups = (D + FIT_DQ - 1) / FIT_DQ;
-    const int64_t per_xcd = (B * ngroups + 7) / 8;
-    if (8 * per_xcd > 0x7fffffffLL) return hbx_fail(HBX_ERR_ARG, "hbx_kde_fit: too many segments");
-    hipLaunchKernelGGL(kde_fit_lds_kernel, dim3((unsigned)(8 * per_xcd)), dim3(256), 0, (hipStream_t)stream, X, D,
-                       seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good,
-                       nlev_bad, ngroups, per_xcd);
+  if (D > 1 && total >= 16384) {  // many segments: one lane per column chain
+    if ((total + 255) / 256 > 0x7fffffffLL) return hbx_fail(HBX_ERR_ARG, "hbx_kde_fit: too many segments");
+    hipLaunchKernelGGL(kde_fit_wave_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       X, D, seg_off, B, order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad,
+                       nlev_good, nlev_bad);
   } else if (D > 1 && total < 16384) {  // few columns: one workgroup each (LDS-staged gathers)
     hipLaunchKernelGGL(kde_fit_col_kernel, dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, X, D, seg_off,
                        order, n_good, n_bad, fac_good, fac_bad, vartype, bw_good, bw_bad, nlev_good, nlev_bad,

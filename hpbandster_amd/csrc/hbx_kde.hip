@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stddef.h>
 
 #include <new>
 #include <vector>
@@ -23,6 +24,9 @@
 #include "hbx_common.h"
 #include <hip/hip_ext.h>
 #include "hbx_kde_impl.h"
+#include "hbx_npsort.h"
+#include "hbx_sort.h"
+#include <type_traits>
 
 // ------------------------------------------------------------------------------------------
 // model preparation
@@ -120,48 +124,121 @@ __device__ __forceinline__ int32_t* prep_counter(KdeParams* P) {
   return (int32_t*)((char*)P + HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 32);
 }
 
-// The parameter block of one KDE (one workgroup): the per-dim transcendentals in parallel, then the
-// scales, log-ratios and sums (thread 0, serial in dim order), the one-hot layout and the kernel mode.
-__global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
-  const PrepArgs& A = blockIdx.x ? ps.k[1] : ps.k[0];  // (no dynamic index into the kernel arguments)
-  KdeParams* P = A.P;
-  const ColStats* cs = col_stats(P);
+// LDS of the parameter build
+struct ParamsScratch {
+  double t0[HBX_MAX_D], t1[HBX_MAX_D], h[HBX_MAX_D], mean[HBX_MAX_D];
+  int32_t c[HBX_MAX_D], maxc[HBX_MAX_D], cm[HBX_MAX_D], cd[HBX_MAX_D];
+  int32_t ix[HBX_MAX_D];   // index of dim d within its class (continuous slot k, categorical slot u, constant dim)
+  uint8_t kind[HBX_MAX_D]; // 0 continuous, 1 active categorical, 2 constant (one level, h = 0), 3 unsupported
+  int32_t du, dcp, dup, exo, neg, dc_tot, du_tot, dc, nconst;
+};
+
+// The parameter block P of one KDE (the whole workgroup calls it; P in global memory or in LDS): the per-dim
+// transcendentals and fields in parallel (each dim's slot within its class from one wave's ballots), the
+// sums by thread 0 in dim order, the one-hot layout and the kernel mode.
+__device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P, const ColStats* cs, ParamsScratch& S) {
   const int D = A.D, n = A.n;
+  const int tid = threadIdx.x;
   uint32_t* pz = (uint32_t*)P;
-  for (int i = threadIdx.x; i < (int)(sizeof(KdeParams) / 4); i += blockDim.x) pz[i] = 0u;
-  // per dim: continuous -> ln h and the scale; categorical -> log2 of the match / mismatch factors
-  // (inputs staged in LDS too: thread 0's serial walk below stores to P, and global loads behind
-  // global stores it may not reorder would each wait a full memory latency)
-  __shared__ double s_t0[HBX_MAX_D], s_t1[HBX_MAX_D], s_h[HBX_MAX_D], s_mean[HBX_MAX_D];
-  __shared__ int32_t s_c[HBX_MAX_D], s_maxc[HBX_MAX_D], s_cm[HBX_MAX_D], s_cd[HBX_MAX_D];
-  __shared__ int32_t s_du, s_dcp, s_dup, s_exo, s_neg;
+  for (int i = tid; i < (int)(sizeof(KdeParams) / 4); i += blockDim.x) pz[i] = 0u;
+  if (tid == 0) S.neg = 0;
+  // per dim: continuous -> ln h and the scale; categorical -> log2 of the match / mismatch factors, and its class
   const double LOG2E = 1.4426950408889634;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+  for (int d = tid; d < D; d += blockDim.x) {
     const double h = A.bw[d];
     const int c = A.nlev[d];
-    s_h[d] = h;
-    s_c[d] = c;
-    s_mean[d] = cs->mean[d];
-    s_maxc[d] = cs->maxcode[d];
+    S.h[d] = h;
+    S.c[d] = c;
+    S.mean[d] = cs->mean[d];
+    S.maxc[d] = cs->maxcode[d];
     if (!prep_cat(A, d)) {
-      s_t0[d] = (h > 0.0) ? log(h) : 0.0;
-      s_t1[d] = (h > 0.0) ? sqrt(LOG2E / 2.0) / h : 0.0;
+      S.kind[d] = 0;
+      S.t0[d] = (h > 0.0) ? log(h) : 0.0;
+      S.t1[d] = (h > 0.0) ? sqrt(LOG2E / 2.0) / h : 0.0;
     } else {
+      // single observed level: match -> 1, mismatch -> 0/0 = NaN (a constant dim); c < 2 otherwise, h <= 0 or
+      // NaN (c == -1: codes not integers in [0, 1024)): not modelled
+      S.kind[d] = (c == 1 && h == 0.0) ? 2 : ((c < 2 || !(h > 0.0) || h != h) ? 3 : 1);
       const double a = 1.0 - h, b = h / (double)(c - 1);
-      s_t0[d] = log2(b);
-      s_t1[d] = (a == 0.0) ? -INFINITY : log2(fabs(a));
+      S.t0[d] = log2(b);
+      S.t1[d] = (a == 0.0) ? -INFINITY : log2(fabs(a));
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    *prep_counter(P) = 0;  // the table launch's block counter (finish by the last block)
+  if (tid < 64) {  // each dim's slot within its class: ballots over 64-dim groups, in dim order
+    const uint64_t below = (1ull << tid) - 1ull;
+    int bc = 0, bu = 0, bk = 0, nu = 0;
+    for (int g = 0; g < D; g += 64) {
+      const int d = g + tid;
+      const int kd = d < D ? S.kind[d] : -1;
+      const uint64_t mc = __ballot(kd == 0), mu = __ballot(kd == 1), mk = __ballot(kd == 2), ma = __ballot(kd >= 1);
+      if (d < D) S.ix[d] = kd == 0 ? bc + __popcll(mc & below) : kd == 1 ? bu + __popcll(mu & below)
+                                                                         : bk + __popcll(mk & below);
+      bc += __popcll(mc);
+      bu += __popcll(mu);
+      bk += __popcll(mk);
+      nu += __popcll(ma);
+    }
+    if (tid == 0) {
+      S.dc_tot = bc;  // every continuous dim has a slot
+      S.du_tot = nu;  // every categorical dim, active or not
+      S.du = bu;
+      S.nconst = bk;
+    }
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += blockDim.x) {
+    const double h = S.h[d];
+    const int kd = S.kind[d], ix = S.ix[d];
+    P->vartype[d] = kd != 0 ? 1 : 0;
+    P->nlev[d] = S.c[d];
+    P->bw[d] = h;
+    if (kd == 0) {
+      P->cont_dim[ix] = d;
+      const double m = S.mean[d];
+      P->center[ix] = (m == m && m - m == 0.0) ? m : 0.0;
+      if (!(h > 0.0)) {
+        P->nan_all = 1;  // exp(-0/0) * ... / 0 -> NaN for every candidate
+        P->cont_scale[ix] = 0.0;
+      } else {
+        P->cont_scale[ix] = S.t1[d];
+      }
+    } else if (kd == 2) {
+      P->const_dim[ix] = d;
+    } else if (kd == 3) {
+      P->unsupported = 1;
+    } else {
+      const double a = 1.0 - h;
+      P->cat_dim[ix] = d;
+      P->cat_maxcode[ix] = S.maxc[d];
+      S.cm[ix] = S.maxc[d];
+      S.cd[ix] = d;
+      P->cat_delta[ix] = (a == 0.0) ? -1e30f : (float)(S.t1[d] - S.t0[d]);
+      P->cat_negf[ix] = (a < 0.0) ? 1.f : 0.f;
+      if (a < 0.0) {
+        P->has_neg = 1;
+        S.neg = 1;
+      }
+    }
+  }
+  if (tid == 0) {  // the sums in dim order (np.prod(bw[iscontinuous]) sequential: the reference's order)
     double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
     float sad = 0.f;
-    int dc = 0, du = 0, nconst = 0, dc_tot = 0, du_tot = 0;
-    s_neg = 0;
-    for (int d = 0; d < D; ++d) (prep_cat(A, d) ? du_tot : dc_tot)++;
+    for (int d = 0; d < D; ++d) {
+      const int kd = S.kind[d];
+      if (kd == 0) {
+        const double h = S.h[d];
+        prod_bw_c *= h;
+        if (h > 0.0) sum_ln_h += S.t0[d];
+      } else if (kd == 1) {
+        const double lb = S.t0[d], la = S.t1[d];
+        m0 += (la > lb) ? la : lb;
+        lb_sum += lb;
+        if (1.0 - S.h[d] != 0.0) sad += fabsf((float)(la - lb));
+      }
+    }
     int dcp, dup;
-    bucket_dims(dc_tot, du_tot, &dcp, &dup);
+    bucket_dims(S.dc_tot, S.du_tot, &dcp, &dup);
     P->n = n;
     P->D = D;
     P->dc_pad = dcp;
@@ -169,63 +246,13 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     const int exo = (dcp < 0 || dup < 0) ? 1 : 0;
     P->exact_only = exo;
     P->stride = exo ? 0 : table_stride(dcp, dup);
-    for (int d = 0; d < D; ++d) {
-      const double h = s_h[d];
-      const bool cat = prep_cat(A, d);
-      P->vartype[d] = cat ? 1 : 0;
-      P->nlev[d] = s_c[d];
-      P->bw[d] = h;
-      if (!cat) {
-        const int k = dc++;
-        P->cont_dim[k] = d;
-        const double m = s_mean[d];
-        P->center[k] = (m == m && m - m == 0.0) ? m : 0.0;
-        prod_bw_c *= h;  // np.prod(bw[iscontinuous]), sequential in dim order
-        if (!(h > 0.0)) {
-          P->nan_all = 1;  // exp(-0/0) * ... / 0 -> NaN for every candidate
-          P->cont_scale[k] = 0.0;
-        } else {
-          P->cont_scale[k] = s_t1[d];
-          sum_ln_h += s_t0[d];
-        }
-      } else {
-        const int c = s_c[d];
-        if (c == 1 && h == 0.0) {  // single observed level: match -> 1, mismatch -> 0/0 = NaN
-          P->const_dim[nconst++] = d;
-          continue;
-        }
-        if (c < 2 || !(h > 0.0) || h != h) {  // includes c == -1: codes not integers in [0, 1024)
-          P->unsupported = 1;
-          continue;
-        }
-        const double a = 1.0 - h;
-        const double lb = s_t0[d], la = s_t1[d];
-        const int u = du++;
-        P->cat_dim[u] = d;
-        P->cat_maxcode[u] = s_maxc[d];
-        s_cm[u] = s_maxc[d];
-        s_cd[u] = d;
-        m0 += (la > lb) ? la : lb;
-        lb_sum += lb;
-        if (a == 0.0) {
-          P->cat_delta[u] = -1e30f;
-        } else {
-          const float dl = (float)(la - lb);
-          P->cat_delta[u] = dl;
-          sad += fabsf(dl);
-        }
-        P->cat_negf[u] = (a < 0.0) ? 1.f : 0.f;
-        if (a < 0.0) P->has_neg = 1;
-        if (a < 0.0) s_neg = 1;
-      }
-    }
+    const int dc = S.dc_tot;
     P->dc = dc;
-    P->du = du;
-    s_du = du;
-    s_dcp = dcp;
-    s_dup = dup;
-    s_exo = exo;
-    P->nconst = nconst;
+    P->du = S.du;
+    S.dcp = dcp;
+    S.dup = dup;
+    S.exo = exo;
+    P->nconst = S.nconst;
     P->m0_log2 = m0;
     P->lb_sum = lb_sum;
     P->prod_bw_c = prod_bw_c;
@@ -234,6 +261,7 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     P->X = A.X;
     P->rows = A.rows;
   }
+  __syncthreads();  // (S.neg and the slot arrays from every thread)
   if (threadIdx.x != 0) return;
   for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
     P->oh_col[t] = 0;
@@ -244,8 +272,8 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   // One-hot positions: every dim's block starts at an even position (a padding position, level -1,
   // never matches) -- the sparse matrix-core kernel relies on adjacent pairs never spanning dims.
   // (read back from LDS, not from the P just written: see above)
-  const int du = s_du, dcp = s_dcp, dup = s_dup, has_neg = s_neg;
-  if (s_exo) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
+  const int du = S.du, dcp = S.dcp, dup = S.dup, has_neg = S.neg;
+  if (S.exo) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
     P->hmode = 0;
     P->nsc = 0;
     P->chunk_floats = 0;
@@ -256,8 +284,8 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
     int tot = 0;
     bool ok = true;
     for (int u = 0; u < du; ++u) {
-      if (s_cm[u] < 0) ok = false;
-      else tot = ((tot + 1) & ~1) + s_cm[u] + 1;
+      if (S.cm[u] < 0) ok = false;
+      else tot = ((tot + 1) & ~1) + S.cm[u] + 1;
     }
     if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
       kc = (2 * tot + 31) / 32;
@@ -270,10 +298,10 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
           P->oh_level[t] = -1;
           ++t;
         }
-        for (int l = 0; l <= s_cm[u]; ++l) {
+        for (int l = 0; l <= S.cm[u]; ++l) {
           P->oh_dim[t] = u;
           P->oh_level[t] = l;
-          P->oh_col[t] = s_cd[u];
+          P->oh_col[t] = S.cd[u];
           P->oh_val[t] = (double)l;
           ++t;
         }
@@ -295,6 +323,13 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   const bool co = hmode == 2 && !has_neg && A.co_allowed;
   P->coarse_chunk_floats = co ? h32c_chunk_floats(nsc_of(dcp), h32_kp(kc)) : 0;
   P->coarse_off = co ? (int32_t)(n_chunks_dev(n) * P->chunk_floats) : 0;
+}
+
+__global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
+  const PrepArgs& A = blockIdx.x ? ps.k[1] : ps.k[0];  // (no dynamic index into the kernel arguments)
+  __shared__ ParamsScratch S;
+  if (threadIdx.x == 0) *prep_counter(A.P) = 0;  // the table launch's block counter (finish by the last block)
+  kde_params_body(A, A.P, col_stats(A.P), S);
 }
 
 // Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
@@ -521,15 +556,13 @@ __device__ __forceinline__ bool table_needs_rebuild(const KdeParams* P) { return
 // Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
 // du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6 |
 // (coarse table) << 7 selects the scoring kernel.  rebuild: the table needed its f32 rebuild.
-__device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) {
-  KdeParams* P = A.P;
+__device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool rebuild) {
   if (rebuild) {
     P->hmode = 0;
     P->chunk_floats = chunk_floats(P->dc_pad, P->du_pad, P->kc, P->kc ? P->has_neg : 0);
     P->cmax = P->cmax2;
     P->coarse_off = 0;
   }
-  int32_t* info = A.info;
   info[0] = P->has_neg | (P->kc << 1) | ((P->hmode != 0) << 4) | (P->exact_only << 5) | ((P->hmode == 2) << 6) |
             ((P->hmode == 2 && P->coarse_off > 0) << 7);
   info[1] = P->nan_all;
@@ -540,6 +573,7 @@ __device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild)
   info[6] = P->dc_pad;
   info[7] = P->du_pad;
 }
+__device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) { prep_finish_p(A.P, A.info, rebuild); }
 
 // pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
 // block of a KDE that needs none exits at once)
@@ -1765,8 +1799,6 @@ struct ScoreFns {
   bool split_ok = false;  // the pair kernel takes observation splits and initialises a single acquisition's
                           // state (the 32x32-tile instances)
   combine_fn combine_rescue = nullptr;  // the combine kernel doing the rescue pass of this instance
-  logpdf_pair_fn pair_ct1 = nullptr;    // the coarse pair instance with one column tile per wave, or nullptr
-  int cands_per_block_ct1 = 0;
 };
 
 // Observation splits of a pair launch with `tiles` candidate tiles per KDE over <= nmax observations: a
@@ -1847,8 +1879,7 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
             hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
             sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true,
-            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>,
-            (co && H32C_CT > 1) ? hbx_pick_h32_pair_ct1(nsc_of(dc_pad), kp) : nullptr, 32 * hw};
+            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>};
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1893,13 +1924,7 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
     // blocks -- splitting only the bad KDE's longer walks in two measured 3-5 us slower, like splitting
     // both: each range repeats the block's prologue, and the merge reads twice the estimates.)
     const int ns0 = can ? obs_splits(gm, nmax) : 1, ns1 = ns0;
-    // at most one two-tile block per slot and KDE without splits (config #2: 2 x 196 blocks of 14 and 3 chunks
-    // on 512 slots, busy 46 %): one column tile per wave -- twice the blocks, each half the work
     logpdf_pair_fn pk = f0.pair;
-    if (ns0 == 1 && f0.pair_ct1 && f0.pair_ct1 == f1.pair_ct1 && 2 * gm <= 512u) {
-      pk = f0.pair_ct1;
-      gm = (unsigned)((Nc + f0.cands_per_block_ct1 - 1) / f0.cands_per_block_ct1);
-    }
     KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns0,
                   rescue_cnt, {}};
     a.tiles = gm;
@@ -2086,8 +2111,19 @@ extern "C" {
 
 int64_t hbx_kde_refit_out_bytes(int64_t n, int32_t D) { return (int64_t)refit_out_layout(n, D).total; }
 int64_t hbx_kde_refit_scratch_bytes(int64_t n, int32_t D) {
-  return (int64_t)refit_meta_bytes() + hbx_sort_scratch_bytes(n);
+  // metadata | sort scratch | host rows staged to the device (hbx_kde_refit_host_rows, beyond the inline copy)
+  return (int64_t)refit_meta_bytes() + ((hbx_sort_scratch_bytes(n) + 15) & ~(int64_t)15) + 8 * n * ((int64_t)D + 1);
 }
+
+}  // extern "C"
+
+static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
+                      bool staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad,
+                      void* params_good, float* table_good, int64_t table_good_floats, void* params_bad,
+                      float* table_bad, int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes,
+                      void* stream);
+
+extern "C" {
 
 // The whole refit of one budget in one call, enqueued without host synchronisation: append the staged
 // rows, stable argsort of the losses, normal-reference bandwidths and level counts of the good (head
@@ -2097,6 +2133,32 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
                   int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad, void* params_good,
                   float* table_good, int64_t table_good_floats, void* params_bad, float* table_bad,
                   int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream) {
+  return refit_impl(X, loss, n, D, vartype, staged, false, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
+                    table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
+                    stream);
+}
+
+// The same with the appended rows in HOST memory (rows then losses, n_new (D + 1) doubles): up to 256 doubles
+// ride in the kernel arguments of the one-launch refit (no copy at all); more are copied into the scratch.
+int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
+                            const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
+                            double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
+                            void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
+                            int64_t scratch_bytes, void* stream) {
+  return refit_impl(X, loss, n, D, vartype, staged_host, true, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
+                    table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
+                    stream);
+}
+
+}  // extern "C"
+
+
+// hbx_kde_refit / hbx_kde_refit_host_rows (staged_host: the appended rows are in host memory)
+static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
+                      bool staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad,
+                      void* params_good, float* table_good, int64_t table_good_floats, void* params_bad,
+                      float* table_bad, int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes,
+                      void* stream) {
   if (!X || !loss || !vartype || !params_good || !table_good || !params_bad || !table_bad || !out || !scratch ||
       (n_new > 0 && !staged))
     return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit: null pointer");
@@ -2135,10 +2197,19 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
   memcpy(ma.vt, ps.k[0].vt, sizeof(ma.vt));
   RefitMeta* m = (RefitMeta*)scratch;
   char* sort_scratch = (char*)scratch + refit_meta_bytes();
+  double* stage_dev = (double*)(sort_scratch + ((hbx_sort_scratch_bytes(n) + 15) & ~(int64_t)15));
+  const int64_t nst = n_new * ((int64_t)D + 1);  // staged doubles: the rows, then their losses
+  // host rows: carried in the sort launch's arguments when they fit (no copy), else copied through the scratch
+  const bool inl = staged_host && n <= REFIT_SORT_SMALL && nst <= REFIT_INLINE;
+  if (staged_host && !inl && nst > 0) {
+    HBX_HIP(hipMemcpyAsync(stage_dev, staged, 8 * (size_t)nst, hipMemcpyHostToDevice, s));
+    staged = stage_dev;
+  }
   // numpy's argsort order (bohb.py:229): tied losses -- crashed +inf runs, quantised losses -- give the
   // reference's rows in the reference's order
   if (n <= REFIT_SORT_SMALL) {  // one launch: rows appended, metadata, sort, numpy's tie order
-    rc = refit_sort_small(X, loss, staged, n_new, ma, m, order, (int32_t*)sort_scratch, s);
+    rc = refit_sort_small(X, loss, inl ? nullptr : staged, inl ? staged : nullptr, n_new, ma, m, order,
+                          (int32_t*)sort_scratch, s);
     if (rc) return rc;
   } else {
     const int64_t per = n_new * (int64_t)(D + 1);
@@ -2161,7 +2232,7 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
   return prep_launch(ps, table_good, table_bad, s, fused);
 }
 
-}  // extern "C"
+
 
 extern "C" {
 

@@ -329,8 +329,10 @@ struct RefitMetaArgs {
 // hbx_fit.hip: append the staged rows, write the metadata and sort a refit's n <= REFIT_SORT_SMALL losses in
 // numpy's order -- one launch for what the metadata kernel, the counting rank and the tie check did in five
 #define REFIT_SORT_SMALL 1024
-int refit_sort_small(double* X, double* loss, const double* staged, int64_t n_new, const RefitMetaArgs& a,
-                     RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s);
+#define REFIT_INLINE 256  // appended doubles (rows, then losses) carried in that launch's kernel arguments
+// staged: device rows to append, or (staged_inline non-null) host rows copied into the kernel arguments
+int refit_sort_small(double* X, double* loss, const double* staged, const double* staged_inline, int64_t n_new,
+                     const RefitMetaArgs& a, RefitMeta* m, int64_t* order, int32_t* arrays, hipStream_t s);
 
 int refit_fit_colstats(const double* X, int32_t D, const int64_t* seg_off, const int64_t* order, const int64_t* n_good,
                        const int64_t* n_bad, const double* fac_good, const double* fac_bad, const int32_t* vartype,
@@ -345,4 +347,3 @@ logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
 logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse = false);  // hbx_score_h32.hip
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse = false);
-logpdf_pair_fn hbx_pick_h32_pair_ct1(int nsc, int kp);  // the coarse pair instance, one column tile per wave

@@ -7,16 +7,17 @@
 //   categorical (levels[d] = t): keep m with probability 1 - bw, else U{0..t-1} (bohb.py:143-146).
 // The truncated normal is drawn by inversion, z = Phi^-1(p), p = Phi(a) + u (Phi(b) - Phi(a)) (Phi at
 // the bounds in fp64; a > 0 is mirrored), Phi^-1 on the smaller tail min(p, 1 - p) in fp32
-// (-sqrt(2) erfcinv(2 min(p, 1 - p)): ~1e-7 relative in z, far below what a distributional test can see).
-// Random numbers: Philox4x32-10 keyed by the seed; counter = (candidate index, pair of dims, stream),
-// 32-bit words (dim 2k: words 0, 1; dim 2k + 1: words 2, 3 -- the uniform, then the categorical level
-// draw) -- the reference draws from numpy's global RNG, so parity is distributional
-// (tests/test_gpu_sample.py).
+// (-sqrt(2) erfcinv(2 min(p, 1 - p)): ~1e-7 relative in z, far below what a distributional test can see;
+// a branch-free fp32 erfinv polynomial measured 3 % slower in round 5).
+// Random numbers: Philox4x32-10 keyed by the seed; counter = (candidate index, word, stream): word w of lane
+// g's blocks (w = g + 8 i) gives the uniforms u of the lane's pairs g + 16 i and g + 8 + 16 i (32-bit words,
+// u = (w + 1/2) 2^-32).  A categorical dim keeps m when
+// u < 1 - h and otherwise takes level floor(t (u - (1 - h)) / h) -- the conditional uniform of the same draw
+// (h >= 1: always resampled, level floor(t u)) -- the reference draws from numpy's global RNG, so parity is
+// distributional (tests/test_gpu_sample.py).
 //
-// One Philox block per (candidate, pair of dims); a wave draws one pair of dims for 64 candidates (the
-// dim's branch and parameters uniform), the block's 64 rows leave through an LDS tile as contiguous
-// 16-byte stores.  Phi at the bounds comes from a per-model table when many candidates are drawn
-// (hbx_kde_sample_table).
+// One lane per (candidate, pair of dims), 8 lanes per candidate (kde_sample_pair_kernel).  Phi at the
+// bounds comes from a per-model table when many candidates are drawn (hbx_kde_sample_table).
 // hbx_norm_ppf keeps the fp64 inverse normal CDF (Wichura's AS 241) as a library function.
 #include <math.h>
 
@@ -139,19 +140,25 @@ __device__ __forceinline__ double tn_invert_f32(double plo, double phi, double l
   return fmin(fmax(z, lo), hi);
 }
 
-// One draw of dim d of a candidate whose datum row is xr: w0 the uniform, w1 the categorical level draw.
+// One draw of dim d of a candidate whose datum row is xr from the 32-bit uniform word w0.
 // TAB: the Phi table is given (one instance each way: the table instance carries no inlined normcdf)
 template <bool TAB>
 __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int d, int32_t idx, int32_t D,
                                              const double* __restrict__ bw, const double* __restrict__ rbw,
                                              const int32_t* __restrict__ levels,
                                              const double2* __restrict__ tab, double bw_factor, uint32_t w0,
-                                             uint32_t w1, bool* derr) {
+                                             bool* derr) {
   const double m = xr[d];
   const double h = bw[d];
   const int t = levels[d];
   const double u = ((double)w0 + 0.5) * 0x1p-32;  // open (0, 1)
-  if (t != 0) return (u < 1.0 - h) ? m : (double)(uint32_t)(((uint64_t)w1 * (uint64_t)t) >> 32);
+  if (t != 0) {  // keep m with probability 1 - h, else a uniform level: both from the one uniform
+    const double thr = 1.0 - h;
+    if (u < thr) return m;
+    const double v = thr > 0.0 ? (u - thr) * rbw[d] : u;  // ~uniform on [0, 1) given the resample (1 / h: LDS)
+    const int lv = (int)(v * (double)t);
+    return (double)(lv < t ? lv : t - 1);
+  }
   double lo, hi;
   bool flip;
   if (!tn_bounds(m, rbw[d], &lo, &hi, &flip)) {  // scipy's argcheck fails: the reference call raises
@@ -173,11 +180,13 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
 
 // The draws with one (candidate, pair of dims) per lane: 8 lanes per candidate, lane g of the group takes
 // the pairs g, g + 8, ...  A candidate's datum row and Phi-table row are then read by its 8 lanes as
-// contiguous 16-byte pieces (a wave touches ~6 cache lines per candidate instead of the 64 a lane-per-
-// candidate layout waited on -- that kernel, 8-9 % slower with the same draws, was removed in round 5) and
-// its output row is written as contiguous 16-byte stores, no LDS tile.  Dim types and bandwidths vary across
-// the lanes (loaded per lane; the categorical branch is the cheap one).  Counter (candidate, pair of dims,
-// stream): the draws do not depend on the launch shape.
+// contiguous 16-byte pieces and its output row is written as contiguous 16-byte stores (a lane-per-
+// candidate layout, 8-9 % slower with the same draws, was removed in round 5).  One Philox block per lane and
+// two pairs (word g + 8 i for pairs g + 16 i and g + 8 + 16 i): the block's four words are the four dims'
+// uniforms -- a categorical dim takes both its keep-or-resample decision and its level from its uniform --
+// so a candidate costs D / 4 blocks (D before round 5: two words per dim, the generator half the work).
+// Dim types and bandwidths vary across the lanes (loaded per lane; the categorical branch is the cheap
+// one).  Counter (candidate, word, stream): the draws do not depend on the launch shape.
 template <bool TAB>
 __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
@@ -205,12 +214,15 @@ __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
   double* out = cands + i * (int64_t)D;
   const int D2 = (D + 1) >> 1;
   bool derr = false;
+  HbxU32x4 r;
   for (int k = g; k < D2; k += 8) {
+    const int q = (k - g) >> 3;  // this lane's q-th pair: a new block every second pair
+    if ((q & 1) == 0) r = draw(seed, counter_base + (uint64_t)i, (uint32_t)(g + 8 * (q >> 1)), stream_id);
+    const uint32_t w0 = (q & 1) ? r.x[2] : r.x[0], w1 = (q & 1) ? r.x[3] : r.x[1];
     const int d = 2 * k;
-    const HbxU32x4 r = draw(seed, counter_base + (uint64_t)i, (uint32_t)k, stream_id);
-    const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, r.x[0], r.x[1], &derr);
+    const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, w0, &derr);
     if (d + 1 < D) {
-      const double v1 = sample_dim<TAB>(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, r.x[2], r.x[3], &derr);
+      const double v1 = sample_dim<TAB>(xr, d + 1, idx, D, bw, srh, levels, tab, bw_factor, w1, &derr);
       if ((D & 1) == 0) {
         *(double2*)(out + d) = make_double2(v0, v1);
       } else {

@@ -519,10 +519,8 @@ __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((
   kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, P, table, out, blockIdx.x);
 }
 
-// both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel).  CT: candidate column tiles per
-// wave of the coarse instance (H32C_CT; 1 -- half the candidates per block, twice the blocks -- for launches of
-// few tiles, where two-tile blocks would leave most block slots idle behind the long KDE's walks)
-template <int NSC, int KP, bool FAST, bool CO, int CT = (CO ? H32C_CT : 1)>
+// both KDEs of an acquisition in one grid (see kde_logpdf_h_pair_kernel)
+template <int NSC, int KP, bool FAST, bool CO>
 __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((amdgpu_waves_per_eu(CO ? H32C_EU : 4))) void kde_logpdf_h32_pair_kernel(
     const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
 #if HBX_PAIR_INIT
@@ -534,8 +532,8 @@ __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((
   const int ns = second ? a.nsplit1 : a.nsplit0;
   const unsigned tile = ns > 1 ? loc % a.tiles : loc;  // blocks of one chunk range are consecutive
   const int split = ns > 1 ? (int)(loc / a.tiles) : 0;
-  kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CT>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
-                                                   second ? a.out1 : a.out0, tile, a.rescue, split, ns);
+  kde_logpdf_h32_body<NSC, KP, false, FAST, CO, CO ? H32C_CT : 1>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                                second ? a.out1 : a.out0, tile, a.rescue, split, ns);
 }
 
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
@@ -611,25 +609,4 @@ logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse) {
 
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse) {
   return sg ? pick32<true, true>(nsc, kp, fast, false) : pick32<false, true>(nsc, kp, fast, coarse);
-}
-
-// the coarse pair instance with one candidate column tile per wave (launches of few tiles)
-template <int NSC>
-static logpdf_pair_fn pick32_ct1_kp(int kp) {
-  switch (kp) {
-    case 0: if constexpr (h32_ok(NSC, 0, false)) return kde_logpdf_h32_pair_kernel<NSC, 0, false, true, 1>; break;
-    case 1: if constexpr (h32_ok(NSC, 1, false)) return kde_logpdf_h32_pair_kernel<NSC, 1, false, true, 1>; break;
-    case 2: if constexpr (h32_ok(NSC, 2, false)) return kde_logpdf_h32_pair_kernel<NSC, 2, false, true, 1>; break;
-  }
-  return nullptr;
-}
-
-logpdf_pair_fn hbx_pick_h32_pair_ct1(int nsc, int kp) {
-  switch (nsc) {
-    case 1: return pick32_ct1_kp<1>(kp);
-    case 2: return pick32_ct1_kp<2>(kp);
-    case 3: return pick32_ct1_kp<3>(kp);
-    case 4: return pick32_ct1_kp<4>(kp);
-  }
-  return nullptr;
 }

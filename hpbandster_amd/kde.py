@@ -746,30 +746,32 @@ class ObservationStore(object):
         self._reserve(n)
         cur = stream if stream is not None else torch.cuda.current_stream(self.device)
         sh = cur.cuda_stream
+        # the new rows then their losses, from host memory: the native call carries up to 256 doubles in the
+        # refit launch's arguments (no copy), more through its scratch
         staged = None
-        if n_new:  # the new rows then their losses, one pinned copy
-            m = n_new * (D + 1)
-            st = self._pinned("_stage_h", 8 * m)
-            sv = st[:8 * m].numpy().view(np.float64)
-            sv[:n_new * D] = X_host[self.n:].reshape(-1)
-            sv[n_new * D:] = losses[self.n:]
-            staged = torch.empty(m, dtype=torch.float64, device=self.device)
-            staged.view(torch.uint8).copy_(st[:8 * m], non_blocking=True)
+        if n_new:
+            staged = np.empty(n_new * (D + 1), dtype=np.float64)
+            staged[:n_new * D] = X_host[self.n:].reshape(-1)
+            staged[n_new * D:] = losses[self.n:]
+        # every device block of the refit in ONE allocation (views: out, scratch, parameter blocks, tables)
         ob = int(L.hbx_kde_refit_out_bytes(n, D))
-        out = torch.empty(ob, dtype=torch.uint8, device=self.device)
         sb = int(L.hbx_kde_refit_scratch_bytes(n, D))
-        scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
         pb = int(L.hbx_kde_param_bytes())
-        pg = torch.empty(pb, dtype=torch.uint8, device=self.device)
-        pbad = torch.empty(pb, dtype=torch.uint8, device=self.device)
-        tg = torch.empty(int(L.hbx_kde_table_floats(n_good, self.dc_pad, self.du_pad)), dtype=torch.float32,
-                         device=self.device)
-        tb = torch.empty(int(L.hbx_kde_table_floats(n_bad, self.dc_pad, self.du_pad)), dtype=torch.float32,
-                         device=self.device)
-        N.check(L.hbx_kde_refit(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt), N.ptr(staged), n_new,
-                                n_good, n_bad, bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D),
-                                N.ptr(pg), N.ptr(tg), tg.numel(), N.ptr(pbad), N.ptr(tb), tb.numel(),
-                                N.ptr(out), N.ptr(scratch), sb, sh))
+        tgf = int(L.hbx_kde_table_floats(n_good, self.dc_pad, self.du_pad))
+        tbf = int(L.hbx_kde_table_floats(n_bad, self.dc_pad, self.du_pad))
+        sizes_b = (ob, sb, pb, pb, 4 * tgf, 4 * tbf)
+        offs = [0]
+        for b in sizes_b:
+            offs.append(offs[-1] + ((b + 255) & ~255))
+        blk = torch.empty(offs[-1], dtype=torch.uint8, device=self.device)
+        out, scratch, pg, pbad = (blk[offs[i]:offs[i] + sizes_b[i]] for i in range(4))
+        tg = blk[offs[4]:offs[4] + 4 * tgf].view(torch.float32)
+        tb = blk[offs[5]:offs[5] + 4 * tbf].view(torch.float32)
+        N.check(L.hbx_kde_refit_host_rows(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt),
+                                          staged.ctypes.data if staged is not None else None, n_new, n_good, n_bad,
+                                          bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D), N.ptr(pg),
+                                          N.ptr(tg), tgf, N.ptr(pbad), N.ptr(tb), tbf, N.ptr(out), N.ptr(scratch),
+                                          sb, sh))
         oh = self._pinned("_out_h", ob)
         oh[:ob].copy_(out, non_blocking=True)
         cur.synchronize()

@@ -1,7 +1,8 @@
 """Batched KDE refit of many segments (hbx_kde_fit; config #5's per-bracket refit, bohb.py:220-246): the
-LDS-resident kernel (rows read once in storage order, placed by rank) and, at D = 1, the per-column gather
-kernel, against numpy's own np.std(axis=0) / np.unique on the same split -- bit for bit, ragged segments,
-long segments (the in-kernel gather path), empty and oversized sets, wide and invalid level codes."""
+lane-per-column kernel (64 add chains per wave, codes of up to 1000 levels through its window passes) and, at
+D = 1, the per-column gather kernel, against numpy's own np.std(axis=0) / np.unique on the same split -- bit
+for bit, ragged segments, segments longer than 1024 rows, empty and oversized sets, wide and invalid level
+codes."""
 import numpy as np
 import pytest
 
@@ -73,8 +74,8 @@ def _run(device, D, dc, seed):
                 assert nl[d] == want, (b, d, nl[d], want)
 
 
-@pytest.mark.parametrize("D,dc", [(32, 24), (13, 9), (40, 40)])
-def test_batched_fit_lds_kernel_bit_exact(device, D, dc):
+@pytest.mark.parametrize("D,dc", [(32, 24), (13, 9), (40, 40), (2, 1)])
+def test_batched_fit_many_segments_bit_exact(device, D, dc):
     _run(device, D, dc, 100 + D)
 
 

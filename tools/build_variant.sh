@@ -6,7 +6,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 OBJ=$R/hpbandster_amd/_lib/obj
 OUT=$R/tools/_abl
 mkdir -p $OUT $R/ab
-FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/hpbandster_amd/csrc -I $R/include -Wno-unused-result -munsafe-fp-atomics -ffp-contract=off -fno-slp-vectorize"
+FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/hpbandster_amd/csrc -I $R/include -Wno-unused-result -munsafe-fp-atomics -ffp-contract=off"
 objs=$(ls $OBJ/*.o)
 vobjs=""
 for SRC in ${2//,/ }; do

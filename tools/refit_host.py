@@ -29,7 +29,7 @@ def main():
     torch.cuda.synchronize()
     L = N.lib()
     native = []
-    orig = L.hbx_kde_refit
+    orig = L.hbx_kde_refit_host_rows
 
     def timed(*a):
         t0 = time.perf_counter()
@@ -37,7 +37,7 @@ def main():
         native.append(time.perf_counter() - t0)
         return rc
 
-    L.hbx_kde_refit = timed
+    L.hbx_kde_refit_host_rows = timed
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     wall, stream = [], []
     for r in range(reps):
@@ -49,7 +49,7 @@ def main():
         e1.synchronize()
         wall.append(time.perf_counter() - t0)
         stream.append(e0.elapsed_time(e1) * 1e-3)
-    L.hbx_kde_refit = orig
+    L.hbx_kde_refit_host_rows = orig
     print(json.dumps({"wall_us": float(np.median(wall)) * 1e6, "native_call_us": float(np.median(native)) * 1e6,
                       "stream_us": float(np.median(stream)) * 1e6}))
 
