@@ -333,26 +333,53 @@ __global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(Refit
     m->fac_good = a.fac_good;
     m->fac_bad = a.fac_bad;
   }
-  __shared__ int tie;
-  if (tid == 0) tie = 0;
-  __syncthreads();  // the appended losses are visible to wave 0
-  if (tid < 64) {
-    uint64_t key[PW_PER_LANE];
-    int32_t pos[PW_PER_LANE];
-    wave_sort_1024<false>(loss, n, lane, key, pos);
-    bool t = false;
+  __shared__ uint64_t rk[REFIT_SORT_SMALL];  // the four waves' sorted runs, then the keys by rank
+  __shared__ int32_t rp[REFIT_SORT_SMALL];
+  __syncthreads();  // the appended losses are visible to every wave
+  // each wave sorts its run of 256 losses in registers (a quarter of one wave's 1024-network), the runs are
+  // merged by rank: an element's rank is its place in its run plus, in each other run, the count of (key,
+  // position) pairs below it (binary searches in LDS); positions are distinct, so the ranks are a permutation
+  constexpr int PW = REFIT_SORT_SMALL / NPS_THREADS;
+  const int w = tid >> 6;
+  uint64_t key[PW];
+  int32_t pos[PW];
+  wave_sort_run<false, PW>(loss, 64 * PW * w, n, lane, key, pos);
 #pragma unroll
-    for (int r = 0; r < PW_PER_LANE; ++r) {
-      const int rank = lane * PW_PER_LANE + r;
-      if (rank < n) order[rank] = pos[r];
-      if (r + 1 < PW_PER_LANE) t |= rank + 1 < n && key[r] == key[r + 1];
-    }
-    const uint64_t nk = __shfl_down(key[0], 1);  // the next lane's first key
-    t |= (lane + 1) * PW_PER_LANE < n && key[PW_PER_LANE - 1] == nk;
-    if (__ballot(t) && lane == 0) tie = 1;
+  for (int r = 0; r < PW; ++r) {
+    rk[64 * PW * w + PW * lane + r] = key[r];
+    rp[64 * PW * w + PW * lane + r] = pos[r];
   }
   __syncthreads();
-  if (tie)  // (uniform) every position re-ranked in numpy's order
+  int rank[PW];
+#pragma unroll
+  for (int r = 0; r < PW; ++r) rank[r] = PW * lane + r;
+  for (int v = 0; v < NPS_THREADS / 64; ++v) {
+    if (v == w) continue;
+    const uint64_t* kv = rk + 64 * PW * v;
+    const int32_t* pv = rp + 64 * PW * v;
+#pragma unroll
+    for (int r = 0; r < PW; ++r) {
+      int lo = 0, hi = 64 * PW;  // first entry of run v not below (key, pos)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (kv_less(kv[mid], pv[mid], key[r], pos[r])) lo = mid + 1;
+        else hi = mid;
+      }
+      rank[r] += lo;
+    }
+  }
+  __syncthreads();  // every run read
+#pragma unroll
+  for (int r = 0; r < PW; ++r) {
+    if (pos[r] != 0x7fffffff) {  // a real element: rank < n
+      rk[rank[r]] = key[r];
+      order[rank[r]] = pos[r];
+    }
+  }
+  __syncthreads();
+  int t = 0;
+  for (int i = tid; i + 1 < n; i += NPS_THREADS) t |= rk[i] == rk[i + 1];
+  if (__syncthreads_or(t))  // tied losses: every position re-ranked in numpy's order
     nps_order_segment(loss, n, 0, 0.0, A0, A0 + n, A0 + 2 * n, A0 + 3 * n, order, nullptr);
 }
 

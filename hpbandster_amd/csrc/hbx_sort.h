@@ -183,3 +183,55 @@ __device__ __forceinline__ void wave_sort_1024(const double* __restrict__ loss, 
     }
   }
 }
+
+// The same network over 64 PW elements starting at position base of loss (register r of lane `lane` =
+// element base + PW lane + r; padding past n: key ~0, position 0x7fffffff): one wave's run of a
+// multi-wave sort (kde_refit_sort_small_kernel: four runs of 256, merged by rank).
+template <bool PROMOTE, int PW>
+__device__ __forceinline__ void wave_sort_run(const double* __restrict__ loss, int base, int n, int lane,
+                                              uint64_t (&key)[PW], int32_t (&pos)[PW]) {
+#pragma unroll
+  for (int r = 0; r < PW; ++r) {
+    const int i = base + lane * PW + r;
+    key[r] = i < n ? (PROMOTE ? key_promote(loss[i]) : key_argsort(loss[i])) : ~0ull;
+    pos[r] = i < n ? i : 0x7fffffff;
+  }
+#pragma unroll
+  for (int size = 2; size <= 64 * PW; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= PW) {
+        const int lm = stride / PW;
+        const bool lower = (lane & lm) == 0;
+#pragma unroll
+        for (int r = 0; r < PW; ++r) {
+          const uint64_t ok = __shfl_xor(key[r], lm);
+          const int32_t op = __shfl_xor(pos[r], lm);
+          const bool up = ((lane * PW + r) & size) == 0;
+          const bool other_less = kv_less(ok, op, key[r], pos[r]);
+          const bool take = (lower == up) ? other_less : !other_less;
+          if (take) {
+            key[r] = ok;
+            pos[r] = op;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < PW; ++r) {
+          if (r & stride) continue;
+          const int q = r | stride;
+          const bool up = ((lane * PW + r) & size) == 0;
+          const bool gt = kv_less(key[q], pos[q], key[r], pos[r]);
+          if (gt == up) {
+            const uint64_t tk = key[r];
+            key[r] = key[q];
+            key[q] = tk;
+            const int32_t tp = pos[r];
+            pos[r] = pos[q];
+            pos[q] = tp;
+          }
+        }
+      }
+    }
+  }
+}

@@ -141,8 +141,6 @@ class DeviceKDE(object):
         """Prepare a KDE for scoring with ``hbx_kde_prepare`` -- or, with ``prepared`` = (params, table,
         info) from ``hbx_kde_refit``, wrap an already prepared one.  ``data_host``: the observation rows
         (n x D), or a pair (host rows, row indices) gathered on first use of ``.data``."""
-        torch = _torch()
-        L = N.lib()
         self.var_type = var_type
         self.k_vars = len(var_type)
         self.bw = np.asarray(bw, dtype=np.float64)
@@ -153,8 +151,10 @@ class DeviceKDE(object):
         self.rows_dev = rows_dev
         self.device = X_dev.device
         D = self.k_vars
-        vt = var_type_codes(var_type)
         if prepared is None:
+            torch = _torch()
+            L = N.lib()
+            vt = var_type_codes(var_type)
             dcp, dup = scoring_bucket(vt)
             with N.on_device(self.device, stream):
                 self.params = torch.empty(int(L.hbx_kde_param_bytes()), dtype=torch.uint8, device=self.device)
@@ -169,7 +169,7 @@ class DeviceKDE(object):
         else:
             self.params, self.table, info = prepared
         self.variant, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
-            [int(v) for v in info]
+            info.tolist()
         self.has_neg, self.kc = self.variant & 1, (self.variant >> 1) & 7
         self.exact_only = bool((self.variant >> 5) & 1)
         if unsupported:
@@ -759,14 +759,11 @@ class ObservationStore(object):
         pb = int(L.hbx_kde_param_bytes())
         tgf = int(L.hbx_kde_table_floats(n_good, self.dc_pad, self.du_pad))
         tbf = int(L.hbx_kde_table_floats(n_bad, self.dc_pad, self.du_pad))
-        sizes_b = (ob, sb, pb, pb, 4 * tgf, 4 * tbf)
-        offs = [0]
-        for b in sizes_b:
-            offs.append(offs[-1] + ((b + 255) & ~255))
-        blk = torch.empty(offs[-1], dtype=torch.uint8, device=self.device)
-        out, scratch, pg, pbad = (blk[offs[i]:offs[i] + sizes_b[i]] for i in range(4))
-        tg = blk[offs[4]:offs[4] + 4 * tgf].view(torch.float32)
-        tb = blk[offs[5]:offs[5] + 4 * tbf].view(torch.float32)
+        sizes_b = [(b + 255) & ~255 for b in (ob, sb, pb, pb, 4 * tgf, 4 * tbf)]  # 256-byte aligned pieces
+        blk = torch.empty(sum(sizes_b), dtype=torch.uint8, device=self.device)
+        out, scratch, pg, pbad, tg, tb = torch.split(blk, sizes_b)
+        out = out[:ob]  # (the read-back's exact size)
+        tg, tb = tg.view(torch.float32), tb.view(torch.float32)
         N.check(L.hbx_kde_refit_host_rows(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt),
                                           staged.ctypes.data if staged is not None else None, n_new, n_good, n_bad,
                                           bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D), N.ptr(pg),
