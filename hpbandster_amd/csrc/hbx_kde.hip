@@ -124,6 +124,17 @@ __device__ __forceinline__ int32_t* prep_counter(KdeParams* P) {
   return (int32_t*)((char*)P + HBX_PARAM_STAGE + 8 * HBX_MAX_D + 4 * HBX_MAX_D + 32);
 }
 
+// PREP_STAMPS (diagnostic builds only): s_memtime at the phase boundaries of the parameter build (block 0) and of
+// the table launch (block 1's and the finishing block's thread 0) into a buffer of their own, read back by
+// hbx_debug_prep_stamps; no stamp executes in the product build
+#ifdef PREP_STAMPS
+__device__ unsigned long long prep_stamps[32];
+#define PSTAMP(i) \
+  if (threadIdx.x == 0) prep_stamps[i] = __builtin_amdgcn_s_memtime()
+#else
+#define PSTAMP(i)
+#endif
+
 // LDS of the parameter build
 struct ParamsScratch {
   double t0[HBX_MAX_D], t1[HBX_MAX_D], h[HBX_MAX_D], mean[HBX_MAX_D];
@@ -144,6 +155,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   if (tid == 0) S.neg = 0;
   // per dim: continuous -> ln h and the scale; categorical -> log2 of the match / mismatch factors, and its class
   const double LOG2E = 1.4426950408889634;
+  if (blockIdx.x == 0) PSTAMP(0);
   for (int d = tid; d < D; d += blockDim.x) {
     const double h = A.bw[d];
     const int c = A.nlev[d];
@@ -165,6 +177,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
     }
   }
   __syncthreads();
+  if (blockIdx.x == 0) PSTAMP(1);
   if (tid < 64) {  // each dim's slot within its class: ballots over 64-dim groups, in dim order
     const uint64_t below = (1ull << tid) - 1ull;
     int bc = 0, bu = 0, bk = 0, nu = 0;
@@ -262,6 +275,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
     P->rows = A.rows;
   }
   __syncthreads();  // (S.neg and the slot arrays from every thread)
+  if (blockIdx.x == 0) PSTAMP(2);
   if (threadIdx.x != 0) return;
   for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
     P->oh_col[t] = 0;
@@ -323,6 +337,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   const bool co = hmode == 2 && !has_neg && A.co_allowed;
   P->coarse_chunk_floats = co ? h32c_chunk_floats(nsc_of(dcp), h32_kp(kc)) : 0;
   P->coarse_off = co ? (int32_t)(n_chunks_dev(n) * P->chunk_floats) : 0;
+  if (blockIdx.x == 0) PSTAMP(3);
 }
 
 __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
@@ -396,6 +411,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     const uint32_t a = wave_reduce_dpp(__float_as_uint(fabsf(v)), OpMax());
     if ((threadIdx.x & 63) == 0 && k < dc) atomicMax((unsigned int*)&Pw->xmax[k], a);
   }
+  if (blockIdx.x == 1) PSTAMP(14);
   const h8 z8 = {};
   if (hm == 1 && slot) {  // dc_pad is a multiple of 8: the dims filled whole groups
     for (int k = 4 * dcp; k < 32 * P->nsc; k += 8) *(h8*)(hrow + k) = z8;
@@ -500,6 +516,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     if (hm == 1 && P->has_neg)
       for (int k = W; k < h_kpp(P->kc); k += 8) *(h8*)(par + k) = z8;
   }
+  if (blockIdx.x == 1) PSTAMP(15);
   C += P->lb_sum - P->m0_log2;
   const float Cf = ok ? (float)C : -1e30f;
   if (slot) {
@@ -544,6 +561,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
         for (int k = 0; k < KP; ++k) ch[k * KROW + OBS_CHUNK + jj] = 0.f;
     }
   }
+  if (blockIdx.x == 1) PSTAMP(16);
   const uint32_t a = wave_reduce_dpp(__float_as_uint(ok ? fabsf(Cf) : 0.f), OpMax());
   if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)cmax_acc, a);
   if (j == 0)
@@ -591,6 +609,7 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
   KdeParams* P = A.P;
   const int j0 = (int)(blockIdx.x - (second ? ps.k[0].nblk_table : 0)) * 64;
   if (pass != 0 && !table_needs_rebuild(P)) return;
+  if (blockIdx.x == 1) PSTAMP(8);
   // the parameter block is copied to LDS: loads from the global block the kernel also writes (atomics)
   // would be vector loads, one memory latency each along the per-dim walk
   __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
@@ -635,7 +654,9 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
         for (int q = 0; q < 16; ++q) xs[at[q]] = t[q];
       }
       __syncthreads();
+      if (blockIdx.x == 1 && ps_ == 0) PSTAMP(9);
       run(xs + threadIdx.x * DS);
+      if (blockIdx.x == 1 && ps_ == 0) PSTAMP(10);
     } else {
       __syncthreads();  // the parameter copy
       run(A.X + A.rows[j < n ? j : 0] * (int64_t)D);
@@ -645,10 +666,12 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
   if (pass != 0 || !finish) return;
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores and maxima atomics are done
   __syncthreads();
+  if (blockIdx.x == 1) PSTAMP(11);
   __shared__ int last;
   if (threadIdx.x == 0) last = atomicAdd(prep_counter(P), 1) == A.nblk_table - 1;
   __syncthreads();
   if (!last) return;
+  PSTAMP(12);
   // every block's |C_j| maximum is in (atomics at the device level; read past this CU's cache)
   const float cmax = __hip_atomic_load(&P->cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool rebuild = Pl->hmode && !(cmax <= H_CMAX);
@@ -661,6 +684,7 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     if (rebuild) P->cmax2 = __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prep_finish_one(A, rebuild);
   }
+  PSTAMP(13);
 }
 
 // Final mode of each KDE and its info record (the separate launch of hbx_kde_prepare's path)
@@ -2613,8 +2637,11 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 //   exp2: v_exp_f32 within 2 ulp (2^-22 relative); sums: 3 x 2^-24 (fp32 groups of 4) + n 2^-52 (fp64).
 // Candidates whose bound stays within 0.99 rtol max(1, |ln p|) are written; the rest go to `list` for the
 // fp64 pass.  KDEs with negative categorical factors, structural NaN or single-level dims: all to `list`.
+#ifndef DD_WPE
+#define DD_WPE(w) ((w) <= 16 ? 4 : (w) <= 40 ? 3 : 2)  // waves per SIMD the register budget is sized for
+#endif
 template <int DC, int DU, int CPT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 16 ? 4 : DC + DU <= 40 ? 3 : 2))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC + DU)))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
                                                            const KdeParams* __restrict__ P,
                                                            const double* __restrict__ X,
                                                            const int64_t* __restrict__ rows, double rtol,
@@ -2858,7 +2885,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DC + DU <= 
 typedef void (*logpdf_dd_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*, double,
                              double*, int32_t*, int32_t*);
 // candidates per thread: two share each staged row where both fit the register budget
-constexpr int dd_cpt(int dc, int du) { return 2; }
+#ifndef DD_CPT
+#define DD_CPT 2
+#endif
+constexpr int dd_cpt(int dc, int du) { return DD_CPT; }
 
 template <int DC>
 static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt) {
@@ -3206,3 +3236,10 @@ int hbx_kde_ws_offsets(int64_t Nc, int64_t seg, int64_t nmax, int64_t* out) {
 }
 
 }  // extern "C"
+
+#ifdef PREP_STAMPS
+extern "C" int hbx_debug_prep_stamps(unsigned long long* out) {
+  HBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(prep_stamps), sizeof(prep_stamps)));
+  return HBX_OK;
+}
+#endif
