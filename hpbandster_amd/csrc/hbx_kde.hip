@@ -141,7 +141,8 @@ struct ParamsScratch {
   int32_t c[HBX_MAX_D], maxc[HBX_MAX_D], cm[HBX_MAX_D], cd[HBX_MAX_D];
   int32_t ix[HBX_MAX_D];   // index of dim d within its class (continuous slot k, categorical slot u, constant dim)
   uint8_t kind[HBX_MAX_D]; // 0 continuous, 1 active categorical, 2 constant (one level, h = 0), 3 unsupported
-  int32_t du, dcp, dup, exo, neg, dc_tot, du_tot, dc, nconst;
+  int32_t ohs[HBX_MAX_D];  // first one-hot position of each active categorical dim's block
+  int32_t du, dcp, dup, exo, neg, dc_tot, du_tot, dc, nconst, kc, tot;
 };
 
 // The parameter block P of one KDE (the whole workgroup calls it; P in global memory or in LDS): the per-dim
@@ -237,18 +238,17 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   if (tid == 0) {  // the sums in dim order (np.prod(bw[iscontinuous]) sequential: the reference's order)
     double sum_ln_h = 0.0, m0 = 0.0, lb_sum = 0.0, prod_bw_c = 1.0;
     float sad = 0.f;
+    // branch-free (a factor 1 or a term +0.0 where a dim does not count: exact), so the loads of several dims
+    // are in flight at once
+#pragma unroll 4
     for (int d = 0; d < D; ++d) {
       const int kd = S.kind[d];
-      if (kd == 0) {
-        const double h = S.h[d];
-        prod_bw_c *= h;
-        if (h > 0.0) sum_ln_h += S.t0[d];
-      } else if (kd == 1) {
-        const double lb = S.t0[d], la = S.t1[d];
-        m0 += (la > lb) ? la : lb;
-        lb_sum += lb;
-        if (1.0 - S.h[d] != 0.0) sad += fabsf((float)(la - lb));
-      }
+      const double h = S.h[d], lb = S.t0[d], la = S.t1[d];
+      prod_bw_c *= (kd == 0) ? h : 1.0;
+      sum_ln_h += (kd == 0 && h > 0.0) ? lb : 0.0;
+      m0 += (kd == 1) ? ((la > lb) ? la : lb) : 0.0;
+      lb_sum += (kd == 1) ? lb : 0.0;
+      sad += (kd == 1 && 1.0 - h != 0.0) ? fabsf((float)(la - lb)) : 0.f;
     }
     int dcp, dup;
     bucket_dims(S.dc_tot, S.du_tot, &dcp, &dup);
@@ -276,8 +276,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   }
   __syncthreads();  // (S.neg and the slot arrays from every thread)
   if (blockIdx.x == 0) PSTAMP(2);
-  if (threadIdx.x != 0) return;
-  for (int t = 0; t < 64; ++t) {  // padding read branch-free by the scoring prologue: never a match
+  for (int t = tid; t < 64; t += blockDim.x) {  // padding read branch-free by the scoring prologue: never a match
     P->oh_col[t] = 0;
     P->oh_val[t] = NAN;
   }
@@ -285,42 +284,51 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   // [0, 1024) and the one-hot width sum(max code + 1) fits OH_MAX_KC K-steps; else VALU matching.
   // One-hot positions: every dim's block starts at an even position (a padding position, level -1,
   // never matches) -- the sparse matrix-core kernel relies on adjacent pairs never spanning dims.
+  // Thread 0 places the blocks (each dim's first level position), then one thread per dim fills its block.
+  const int du = S.du;
+  if (tid == 0) {
+    int tot = 0;
+    bool ok = true;
+    for (int u = 0; u < du; ++u) {
+      if (S.cm[u] < 0) {
+        ok = false;
+      } else {
+        S.ohs[u] = (tot + 1) & ~1;
+        tot = S.ohs[u] + S.cm[u] + 1;
+      }
+    }
+    S.kc = (!S.exo && du > 0 && ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) ? (2 * tot + 31) / 32 : 0;
+    S.tot = tot;
+  }
+  __syncthreads();
+  const int kc = S.kc;
+  if (kc > 0) {
+    for (int u = tid; u < du; u += blockDim.x) {
+      int t = S.ohs[u];
+      if (t > 0 && (u == 0 || t != S.ohs[u - 1] + S.cm[u - 1] + 1)) {  // the padding position before the block
+        P->oh_dim[t - 1] = u;
+        P->oh_level[t - 1] = -1;
+      }
+      for (int l = 0; l <= S.cm[u]; ++l, ++t) {
+        P->oh_dim[t] = u;
+        P->oh_level[t] = l;
+        P->oh_col[t] = S.cd[u];
+        P->oh_val[t] = (double)l;
+      }
+    }
+  }
+  if (threadIdx.x != 0) return;
   // (read back from LDS, not from the P just written: see above)
-  const int du = S.du, dcp = S.dcp, dup = S.dup, has_neg = S.neg;
+  const int dcp = S.dcp, dup = S.dup, has_neg = S.neg;
   if (S.exo) {  // no table, no fp32 scoring: the acquisition re-scores every candidate
     P->hmode = 0;
     P->nsc = 0;
     P->chunk_floats = 0;
     return;
   }
-  int kc = 0;
-  if (du > 0) {
-    int tot = 0;
-    bool ok = true;
-    for (int u = 0; u < du; ++u) {
-      if (S.cm[u] < 0) ok = false;
-      else tot = ((tot + 1) & ~1) + S.cm[u] + 1;
-    }
-    if (ok && 2 * tot <= 32 * OH_MAX_KC && tot <= 64) {
-      kc = (2 * tot + 31) / 32;
-      P->kc = kc;
-      P->oh_total = tot;
-      int t = 0;
-      for (int u = 0; u < du; ++u) {
-        if (t & 1) {
-          P->oh_dim[t] = u;
-          P->oh_level[t] = -1;
-          ++t;
-        }
-        for (int l = 0; l <= S.cm[u]; ++l) {
-          P->oh_dim[t] = u;
-          P->oh_level[t] = l;
-          P->oh_col[t] = S.cd[u];
-          P->oh_val[t] = (double)l;
-          ++t;
-        }
-      }
-    }
+  if (kc > 0) {
+    P->kc = kc;
+    P->oh_total = S.tot;
   }
   // continuous product on the f16 matrix cores (hi/lo split) when it has >= 8 dims (one full
   // 32-wide K-step; the C_j pieces ride in dims 0-2) and the categorical part is one-hot (or absent);
