@@ -71,6 +71,7 @@ struct KdeParams {
   int32_t oh_level[64]; // one-hot slot -> code level
   int32_t oh_col[64];   // one-hot slot -> candidate column (cat_dim[oh_dim[t]])
   double oh_val[64];    // one-hot slot -> code level as the fp64 value a matching column holds
+  int32_t oh_start[64]; // active categorical dim u -> one-hot slot of its level 0 (one-hot mode only)
   int32_t cat_maxcode[HBX_MAX_D]; // per active categorical dim: max observed code (-1: not an integer code)
   int32_t cont_dim[HBX_MAX_D];
   double cont_scale[HBX_MAX_D];     // s_c = sqrt(log2(e) / 2) / h_c

@@ -75,9 +75,22 @@ struct PrepArgs {
   int32_t nblk_table;   // blocks of this KDE in the table launches
   uint32_t vt[HBX_MAX_D / 32];  // bit d: dim d categorical ('u')
 };
+// The refit's output block published to device-mapped host memory by the preparation's finishing blocks
+// (hbx_kde_refit_sync): the split's rows (KDE 0's block), each KDE's bandwidths, level counts and info record,
+// then a completion word per KDE; dst == nullptr: nothing published
+struct PrepPub {
+  uint32_t* dst;        // mapped host copy of the output block (same word offsets as src)
+  const uint32_t* src;  // the device output block
+  int32_t* done;        // completion words, one per KDE
+  int32_t seq;
+  int32_t order_words;  // 2 n
+  int32_t bw_off[2], nl_off[2], info_off[2];  // word offsets of KDE k's pieces
+  int32_t D;
+};
 struct PrepSet {
   PrepArgs k[2];
   int32_t nk;
+  PrepPub pub;
 };
 
 __device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
@@ -305,6 +318,7 @@ __device__ __forceinline__ void kde_params_body(const PrepArgs& A, KdeParams* P,
   if (kc > 0) {
     for (int u = tid; u < du; u += blockDim.x) {
       int t = S.ohs[u];
+      P->oh_start[u] = t;
       if (t > 0 && (u == 0 || t != S.ohs[u - 1] + S.cm[u - 1] + 1)) {  // the padding position before the block
         P->oh_dim[t - 1] = u;
         P->oh_level[t - 1] = -1;
@@ -359,6 +373,22 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
 // C_j = -sum_c X'_jc^2 + lb_sum - M0 (log2 units).  One thread per observation row (a serial walk over
 // its dims), 64-thread blocks so a 1e4-row table spreads over ~150 CUs.  `hm` / `chunk_f` select the
 // layout; |C_j| and |X'| maxima go to *cmax_acc / P->xmax.
+// The one-hot positions observation row x matches, as a bit mask: position oh_start[u] + l for each active
+// categorical dim u whose code is the integer l in [0, max code] -- exactly the positions t where
+// x[oh_col[t]] == oh_val[t] (padding positions hold NaN: never), found with du loads instead of oh_total.
+__device__ __forceinline__ uint64_t onehot_hits(const double* x, const KdeParams* P, bool ok) {
+  uint64_t hit = 0;
+  if (!ok) return hit;
+  for (int u = 0; u < P->du; ++u) {
+    const double v = x[P->cat_dim[u]];
+    if (v >= 0.0 && v <= (double)P->cat_maxcode[u]) {
+      const int l = (int)v;
+      if (v == (double)l) hit |= 1ull << (P->oh_start[u] + l);
+    }
+  }
+  return hit;
+}
+
 __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, const KdeParams* __restrict__ P,
                                                KdeParams* __restrict__ Pw, float* __restrict__ table, int j,
                                                int hm, int chunk_f, float* cmax_acc, _Float16* hst) {
@@ -443,6 +473,7 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     _Float16* cz = hrow + 16 * nd32;
     _Float16* cp = hrow + h32_par(P->nsc, kp);  // parity block (signed KDEs)
     const int ksp = h32_ksp(kp);
+    const uint64_t hit = onehot_hits(x, P, ok);
     uint32_t iw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     for (int s = 0; s < kp; ++s) {
       h8 vh[2] = {{}, {}}, vl[2] = {{}, {}}, pv[2] = {{}, {}};
@@ -452,9 +483,9 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
           const int t0 = 32 * s + 4 * g + 2 * pr;
-          bool m0 = false, m1 = false;
-          if (ok && t0 < P->oh_total) m0 = x[P->oh_col[t0]] == P->oh_val[t0];
-          if (ok && t0 + 1 < P->oh_total) m1 = x[P->oh_col[t0 + 1]] == P->oh_val[t0 + 1];
+          // (oh_total <= 64: a position at or past it never matches)
+          const bool m0 = t0 < P->oh_total && ((hit >> t0) & 1u);
+          const bool m1 = t0 + 1 < P->oh_total && ((hit >> (t0 + 1)) & 1u);
           if (m0 || m1) {
             const int u = P->oh_dim[m1 ? t0 + 1 : t0];
             const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
@@ -500,14 +531,15 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
       oh = (_Float16*)(ch + KP * KROW) + jj * W;
       par = (_Float16*)(ch + KP * KROW) + OBS_CHUNK * W + jj * W;
     }
+    const uint64_t hit = onehot_hits(x, P, ok);
     h8 og = {}, pg = {};
 #pragma unroll 8
     for (int k = 0; k < W; ++k) {
       const int t = k >> 1, p = k & 1;
       float v = 0.f, pv = 0.f;
-      if (ok && t < P->oh_total) {
+      if (t < P->oh_total) {
         const int u = P->oh_dim[t];
-        if (x[P->oh_col[t]] == P->oh_val[t]) {  // oh_col = cat_dim[oh_dim], oh_val = the level
+        if ((hit >> t) & 1u) {
           const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
           const float hi = (float)(_Float16)dl;
           v = (p == 0) ? hi : (fabsf(dl) < 60000.f ? dl - hi : 0.f);
@@ -601,6 +633,17 @@ __device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool 
 }
 __device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) { prep_finish_p(A.P, A.info, rebuild); }
 
+// KDE k's words of the published output block, thread t of nt (order, bandwidths and level counts come
+// from earlier launches; the info record is thread 0's own stores of prep_finish_one, read back by it)
+__device__ __forceinline__ void prep_publish_words(const PrepPub& q, const PrepArgs& A, int k, int t, int nt) {
+  if (k == 0)
+    for (int i = t; i < q.order_words; i += nt) hbx_publish_store(q.dst + i, q.src[i]);
+  for (int i = t; i < 2 * q.D; i += nt) hbx_publish_store(q.dst + q.bw_off[k] + i, q.src[q.bw_off[k] + i]);
+  for (int i = t; i < q.D; i += nt) hbx_publish_store(q.dst + q.nl_off[k] + i, q.src[q.nl_off[k] + i]);
+  if (t == 0)
+    for (int i = 0; i < 8; ++i) hbx_publish_store(q.dst + q.info_off[k] + i, (uint32_t)A.info[i]);
+}
+
 // pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
 // block of a KDE that needs none exits at once)
 // The block's 64 observation rows are staged in LDS first (all loads in flight at once, coalesced
@@ -620,8 +663,19 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
   if (blockIdx.x == 1) PSTAMP(8);
   // the parameter block is copied to LDS: loads from the global block the kernel also writes (atomics)
   // would be vector loads, one memory latency each along the per-dim walk
-  __shared__ uint4 pl[(sizeof(KdeParams) + 15) / 16];
-  for (int i = threadIdx.x; i < (int)((sizeof(KdeParams) + 15) / 16); i += 64) pl[i] = ((const uint4*)P)[i];
+  // (every load issued before the first store: one memory latency for the whole block, not one per 1 KiB)
+  constexpr int NPL = (int)((sizeof(KdeParams) + 15) / 16);
+  __shared__ uint4 pl[NPL];
+  for (int i0 = 0; i0 < NPL; i0 += 8 * 64) {
+    uint4 t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = min(i0 + (int)threadIdx.x + 64 * q, NPL - 1);  // past the end: the last entry again
+      t[q] = ((const uint4*)P)[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pl[min(i0 + (int)threadIdx.x + 64 * q, NPL - 1)] = t[q];
+  }
   __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
   __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_MAX];  // h32 rows assembled here
   const int D = A.D, n = A.n;
@@ -692,6 +746,11 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     if (rebuild) P->cmax2 = __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prep_finish_one(A, rebuild);
   }
+  if (ps.pub.dst) {  // the refit's output block to the host (hbx_kde_refit_sync)
+    prep_publish_words(ps.pub, A, second ? 1 : 0, threadIdx.x, 64);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words acknowledged (one wave)
+    if (threadIdx.x == 0) hbx_publish_done(ps.pub.done + (second ? 1 : 0), ps.pub.seq);
+  }
   PSTAMP(13);
 }
 
@@ -701,6 +760,10 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
   if (k >= ps.nk) return;
   const PrepArgs& A = k ? ps.k[1] : ps.k[0];
   prep_finish_one(A, table_needs_rebuild(A.P));
+  if (ps.pub.dst) {
+    prep_publish_words(ps.pub, A, k, 0, 1);
+    hbx_publish_done(ps.pub.done + k, ps.pub.seq);
+  }
 }
 
 static int64_t prep_table_blocks(int64_t n) { return (((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK + 63) / 64; }
@@ -2153,7 +2216,7 @@ static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32
                       bool staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad,
                       void* params_good, float* table_good, int64_t table_good_floats, void* params_bad,
                       float* table_bad, int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes,
-                      void* stream);
+                      void* stream, const PrepPub* pub = nullptr);
 
 extern "C" {
 
@@ -2184,13 +2247,81 @@ int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const
 
 }  // extern "C"
 
+// this thread's device-mapped coherent host buffer for refit output blocks (grown on demand, kept for the
+// thread's lifetime): `cap` bytes of data, then two completion words
+static int wait_done(int32_t* done, int32_t seq, hipStream_t s, const char* who);
+thread_local char* t_refit_mapped = nullptr;
+thread_local int64_t t_refit_cap = 0;
+thread_local int32_t t_refit_seq = 0;
+static int refit_mapped_buffer(int64_t bytes, char** out) {
+  if (bytes > t_refit_cap) {
+    int64_t cap = t_refit_cap > 0 ? t_refit_cap : 16384;
+    while (cap < bytes) cap *= 2;
+    void* p = nullptr;
+    HBX_HIP(hipHostMalloc(&p, (size_t)cap + 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    void* dp = nullptr;
+    HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
+    if (dp != p) {
+      (void)hipHostFree(p);
+      return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+    }
+    if (t_refit_mapped) {  // (a call that failed after its launches may still have words in flight)
+      HBX_HIP(hipDeviceSynchronize());
+      (void)hipHostFree(t_refit_mapped);
+    }
+    t_refit_mapped = (char*)p;
+    t_refit_cap = cap;
+    ((volatile int32_t*)(t_refit_mapped + cap))[0] = 0;
+    ((volatile int32_t*)(t_refit_mapped + cap))[1] = 0;
+  }
+  *out = t_refit_mapped;
+  return HBX_OK;
+}
+
+extern "C" {
+
+// hbx_kde_refit_host_rows, then the output block in host memory (out_host, hbx_kde_refit_out_bytes) when the
+// call returns: the preparation's finishing blocks publish it to a device-mapped host buffer with a
+// completion word per KDE, and the call spins on those words -- no copy launch, no blocking stream
+// synchronisation (bounded: then the stream is synchronised and the words checked)
+int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
+                       const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
+                       double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
+                       void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
+                       int64_t scratch_bytes, void* stream, void* out_host) {
+  if (!out_host) return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit_sync: null host output");
+  const int64_t bytes = (int64_t)refit_out_layout(n, D).total;
+  char* mapped = nullptr;
+  int rc = refit_mapped_buffer(bytes, &mapped);
+  if (rc) return rc;
+  int32_t* done = (int32_t*)(mapped + t_refit_cap);
+  const int32_t seq = t_refit_seq = t_refit_seq == INT32_MAX ? 1 : t_refit_seq + 1;
+  PrepPub pub;
+  memset(&pub, 0, sizeof(pub));
+  pub.dst = (uint32_t*)mapped;
+  pub.done = done;
+  pub.seq = seq;
+  rc = refit_impl(X, loss, n, D, vartype, staged_host, true, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
+                  table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
+                  stream, &pub);
+  if (rc) return rc;
+  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_refit_sync");
+  if (rc) return rc;
+  rc = wait_done(done + 1, seq, (hipStream_t)stream, "hbx_kde_refit_sync");
+  if (rc) return rc;
+  memcpy(out_host, mapped, (size_t)bytes);
+  return HBX_OK;
+}
+
+}  // extern "C"
+
 
 // hbx_kde_refit / hbx_kde_refit_host_rows (staged_host: the appended rows are in host memory)
 static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
                       bool staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad,
                       void* params_good, float* table_good, int64_t table_good_floats, void* params_bad,
                       float* table_bad, int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes,
-                      void* stream) {
+                      void* stream, const PrepPub* pub) {
   if (!X || !loss || !vartype || !params_good || !table_good || !params_bad || !table_bad || !out || !scratch ||
       (n_new > 0 && !staged))
     return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit: null pointer");
@@ -2218,6 +2349,18 @@ static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32
   rc = prep_args(&ps.k[1], X, D, order + (n - n_bad), (int32_t)n_bad, vartype, bw_b, nl_b, params_bad,
                  (int32_t*)(ob + o.info_bad), table_bad_floats);
   if (rc) return rc;
+  if (pub) {  // the finishing blocks publish the output block (word offsets of the layout above)
+    ps.pub = *pub;
+    ps.pub.src = (const uint32_t*)out;
+    ps.pub.order_words = (int32_t)(2 * n);
+    ps.pub.bw_off[0] = (int32_t)(o.bw_good / 4);
+    ps.pub.bw_off[1] = (int32_t)(o.bw_bad / 4);
+    ps.pub.nl_off[0] = (int32_t)(o.nlev_good / 4);
+    ps.pub.nl_off[1] = (int32_t)(o.nlev_bad / 4);
+    ps.pub.info_off[0] = (int32_t)(o.info_good / 4);
+    ps.pub.info_off[1] = (int32_t)(o.info_bad / 4);
+    ps.pub.D = D;
+  }
   RefitMetaArgs ma;
   memset(&ma, 0, sizeof(ma));
   ma.n = n;

@@ -645,6 +645,30 @@ def split_sizes(n, D, min_points, top_n_percent=15, split_rule="bohb"):
     return min(n_good, n), min(n_bad, n)
 
 
+class _DevSlice(object):
+    """A piece of a device allocation by address (a refit's parameter blocks and tables): what the engine
+    reads of them is the address (``data_ptr``) and the size (``numel``); ``base`` keeps the allocation."""
+    __slots__ = ("base", "_ptr", "_numel")
+
+    def __init__(self, base, ptr, numel):
+        self.base, self._ptr, self._numel = base, ptr, numel
+
+    def data_ptr(self):
+        return self._ptr
+
+    def numel(self):
+        return self._numel
+
+
+def _raw_stream(device):
+    """The device's current HIP stream handle (torch's raw accessor where it exists)."""
+    torch = _torch()
+    f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if f is not None:
+        return f(device.index if device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 class ObservationStore(object):
     """One budget's observations (``get_array()`` rows and losses) resident in HBM, appended to as
     results arrive (bohb.py:211-213), so a refit moves only the new rows to the device: one pinned
@@ -666,8 +690,6 @@ class ObservationStore(object):
         self._Xh = self._lh = None
         self._cap = 0
         self.X_dev = self.loss_dev = None
-        self._stage_h = None
-        self._out_h = None
         self._init_cap = int(capacity)
         self.dc_pad, self.du_pad = scoring_bucket(self.vt)
 
@@ -684,14 +706,6 @@ class ObservationStore(object):
             X[:self.n].copy_(self.X_dev[:self.n])
             L[:self.n].copy_(self.loss_dev[:self.n])
         self.X_dev, self.loss_dev, self._cap = X, L, cap
-
-    def _pinned(self, attr, nbytes):
-        torch = _torch()
-        buf = getattr(self, attr)
-        if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
-            setattr(self, attr, buf)
-        return buf
 
     def add(self, rows, losses):
         """Append observations on the host side (O(rows x D)); the next refit moves them."""
@@ -744,8 +758,7 @@ class ObservationStore(object):
         n_good, n_bad = sizes
         n_new = n - self.n
         self._reserve(n)
-        cur = stream if stream is not None else torch.cuda.current_stream(self.device)
-        sh = cur.cuda_stream
+        sh = stream.cuda_stream if stream is not None else _raw_stream(self.device)
         # the new rows then their losses, from host memory: the native call carries up to 256 doubles in the
         # refit launch's arguments (no copy), more through its scratch
         staged = None
@@ -759,39 +772,41 @@ class ObservationStore(object):
         pb = int(L.hbx_kde_param_bytes())
         tgf = int(L.hbx_kde_table_floats(n_good, self.dc_pad, self.du_pad))
         tbf = int(L.hbx_kde_table_floats(n_bad, self.dc_pad, self.du_pad))
-        sizes_b = [(b + 255) & ~255 for b in (ob, sb, pb, pb, 4 * tgf, 4 * tbf)]  # 256-byte aligned pieces
-        blk = torch.empty(sum(sizes_b), dtype=torch.uint8, device=self.device)
-        out, scratch, pg, pbad, tg, tb = torch.split(blk, sizes_b)
-        out = out[:ob]  # (the read-back's exact size)
-        tg, tb = tg.view(torch.float32), tb.view(torch.float32)
-        N.check(L.hbx_kde_refit_host_rows(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt),
-                                          staged.ctypes.data if staged is not None else None, n_new, n_good, n_bad,
-                                          bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D), N.ptr(pg),
-                                          N.ptr(tg), tgf, N.ptr(pbad), N.ptr(tb), tbf, N.ptr(out), N.ptr(scratch),
-                                          sb, sh))
-        oh = self._pinned("_out_h", ob)
-        oh[:ob].copy_(out, non_blocking=True)
-        cur.synchronize()
-        ah = oh[:ob].numpy()
-        order_h = ah[:8 * n].view(np.int64).copy()
+        a_ob, a_sb, a_pb, a_tg = (ob + 255) & ~255, (sb + 255) & ~255, (pb + 255) & ~255, (4 * tgf + 255) & ~255
+        blk = torch.empty(a_ob + a_sb + 2 * a_pb + a_tg + 4 * tbf, dtype=torch.uint8, device=self.device)
+        # 256-byte aligned pieces: out | scratch | params good | params bad | table good | table bad
+        p0 = blk.data_ptr()
+        p_scr = p0 + a_ob
+        pg = _DevSlice(blk, p_scr + a_sb, pb)
+        pbad = _DevSlice(blk, pg._ptr + a_pb, pb)
+        tg = _DevSlice(blk, pbad._ptr + a_pb, tgf)
+        tb = _DevSlice(blk, tg._ptr + a_tg, tbf)
+        # the output block lands in a fresh host array when the call returns (published by the preparation's
+        # last workgroups through mapped host memory): its pieces are views, no copies
+        ah = np.empty(ob, dtype=np.uint8)
+        N.check(L.hbx_kde_refit_sync(N.ptr(self.X_dev), N.ptr(self.loss_dev), n, D, N.ptr(self.vt),
+                                     staged.ctypes.data if staged is not None else None, n_new, n_good, n_bad,
+                                     bandwidth_factor(n_good, D), bandwidth_factor(n_bad, D), pg._ptr,
+                                     tg._ptr, tgf, pbad._ptr, tb._ptr, tbf, p0, p_scr, sb, sh, ah.ctypes.data))
+        order_h = ah[:8 * n].view(np.int64)
         o = 8 * n
-        bw_gh = ah[o:o + 8 * D].view(np.float64).copy()
-        bw_bh = ah[o + 8 * D:o + 16 * D].view(np.float64).copy()
-        nl_gh = ah[o + 16 * D:o + 20 * D].view(np.int32).copy()
-        nl_bh = ah[o + 20 * D:o + 24 * D].view(np.int32).copy()
-        info_g = ah[o + 24 * D:o + 24 * D + 32].view(np.int32).copy()
-        info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32).copy()
+        bw_gh = ah[o:o + 8 * D].view(np.float64)
+        bw_bh = ah[o + 8 * D:o + 16 * D].view(np.float64)
+        nl_gh = ah[o + 16 * D:o + 20 * D].view(np.int32)
+        nl_bh = ah[o + 20 * D:o + 24 * D].view(np.int32)
+        info_g = ah[o + 24 * D:o + 24 * D + 32].view(np.int32)
+        info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32)
         if (nl_gh < 0).any() or (nl_bh < 0).any():
             raise N.HbxError("categorical codes must be integers in [0, 1024)")
         self.n = n  # the rows count as resident only once the refit has completed and validated
-        order = out[:8 * n].view(torch.int64)
+        order = blk[:8 * n].view(torch.int64)
         X_dev = self.X_dev
         good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, (X_host, order_h[:n_good]),
                          prepared=(pg, tg, info_g))
         bad = DeviceKDE(X_dev, order[n - n_bad:], self.var_type, bw_bh, nl_bh, (X_host, order_h[n - n_bad:]),
                         prepared=(pbad, tb, info_b))
         pair = KDEPair(good, bad)
-        pair._keep = (out,)  # the rows tensors are views of the refit's output block
+        pair._keep = (blk,)  # the rows tensors are views of the refit's block
         return pair
 
 

@@ -16,6 +16,7 @@
  *                                      np.argsort + sm.nonparametric.KDEMultivariate(..,'normal_reference'))
  *   hbx_kde_refit                   <- bohb.py:211-251 (the same refit plus both KDEs' preparation, one call)
  *   hbx_kde_refit_host_rows         <- bohb.py:211-251 (the same, new rows from host memory: no copy for one row)
+ *   hbx_kde_refit_sync              <- bohb.py:211-251 (the same, the output block on the host when it returns)
  *   hbx_kde_prepare                 <- KDEMultivariate.__init__ model state (statsmodels 0.12.2
  *                                      kernel_density.py:101-115)
  *   hbx_kde_acquire                 <- bohb.py:124-169 (the num_samples loop: pdf of l and g per
@@ -107,13 +108,22 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
                   int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream);
 /* The same with `staged_host` in HOST memory (rows, then losses: n_new*(D+1) doubles).  Up to 256 staged
  * doubles of a budget of at most 1024 rows ride in the kernel arguments of the refit's first launch (no
- * host-to-device copy); more go through `scratch`.  The drop-in's ObservationStore.refit calls this one
- * (bohb.py:211-251, one new_result per call). */
+ * host-to-device copy); more go through `scratch`. */
 int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
                             const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
                             double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
                             void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
                             int64_t scratch_bytes, void* stream);
+/* hbx_kde_refit_host_rows, synchronous: when the call returns, `out_host` (host memory,
+ * hbx_kde_refit_out_bytes) holds the output block.  The preparation's finishing workgroups publish it to a
+ * device-mapped host buffer with a completion word per KDE and the call spins on those words (no copy
+ * launch, no blocking stream synchronisation).  The drop-in's ObservationStore.refit calls this one
+ * (bohb.py:211-251, one new_result per call). */
+int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
+                       const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
+                       double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
+                       void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
+                       int64_t scratch_bytes, void* stream, void* out_host);
 
 /* ---- KDE model preparation ----------------------------------------------------------------- */
 /* Template bucket of the scoring kernel for dc continuous / du categorical dims

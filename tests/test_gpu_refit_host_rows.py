@@ -112,3 +112,56 @@ def test_device_staged_rows_equal_host_rows(device):
         np.testing.assert_array_equal(x, y)
     np.testing.assert_array_equal(a[3], X)
     np.testing.assert_array_equal(a[4], L)
+
+
+@pytest.mark.parametrize("dc,du,lev,n,n_new", [(24, 8, 4, 400, 1), (8, 0, 0, 1000, 2), (24, 8, 4, 3000, 1),
+                                               (70, 0, 0, 300, 1), (4, 40, 3, 200, 1)])
+def test_sync_refit_publishes_the_output_block(device, dc, du, lev, n, n_new):
+    """hbx_kde_refit_sync's host copy of the output block (published by the finishing workgroups through mapped
+    host memory -- the table launch's last blocks, or the separate finish launch when a KDE is exact-only) equals
+    the device block and the block of hbx_kde_refit_host_rows; three calls in a row (the completion words'
+    sequence), a block larger than the first mapped buffer (it grows)."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    D = dc + du
+    X = S.make_observations(n, dc, du, lev, seed=91 + n)
+    L = S.make_losses(n, seed=92 + n)
+    vt = np.array([0] * dc + [1] * du, dtype=np.int32)
+    ng, nb = kde.bohb_split_sizes(n, D + 1)
+    Lb = N.lib()
+    ob, sb, pb = (int(Lb.hbx_kde_refit_out_bytes(n, D)), int(Lb.hbx_kde_refit_scratch_bytes(n, D)),
+                  int(Lb.hbx_kde_param_bytes()))
+    dcp, dup = kde.scoring_bucket(vt)
+    tgf, tbf = int(Lb.hbx_kde_table_floats(ng, dcp, dup)), int(Lb.hbx_kde_table_floats(nb, dcp, dup))
+    fg, fb = kde.bandwidth_factor(ng, D), kde.bandwidth_factor(nb, D)
+    st = np.concatenate([X[n - n_new:].reshape(-1), L[n - n_new:]])
+    blocks = []
+    for call in ("hbx_kde_refit_host_rows", "hbx_kde_refit_sync", "hbx_kde_refit_sync", "hbx_kde_refit_sync"):
+        Xd = torch.zeros((n, D), dtype=torch.float64, device=device)
+        Ld = torch.zeros(n, dtype=torch.float64, device=device)
+        Xd[:n - n_new] = torch.from_numpy(X[:n - n_new]).to(device)
+        Ld[:n - n_new] = torch.from_numpy(L[:n - n_new]).to(device)
+        out = torch.zeros(ob, dtype=torch.uint8, device=device)
+        scr = torch.zeros(sb, dtype=torch.uint8, device=device)
+        pg, pbd = (torch.zeros(pb, dtype=torch.uint8, device=device) for _ in range(2))
+        tg = torch.zeros(max(tgf, 1), dtype=torch.float32, device=device)
+        tb = torch.zeros(max(tbf, 1), dtype=torch.float32, device=device)
+        args = [N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, st.ctypes.data, n_new, ng, nb, fg, fb, N.ptr(pg),
+                N.ptr(tg), tgf, N.ptr(pbd), N.ptr(tb), tbf, N.ptr(out), N.ptr(scr), sb, N.stream_handle()]
+        host = np.full(ob, 0xAB, dtype=np.uint8)
+        if call == "hbx_kde_refit_sync":
+            N.call(call, *args, host.ctypes.data)
+        else:
+            N.call(call, *args)
+        torch.cuda.synchronize()
+        dev_block = out.cpu().numpy()
+        if call == "hbx_kde_refit_sync":
+            np.testing.assert_array_equal(host, dev_block)
+        blocks.append(dev_block)
+    for b in blocks[1:]:
+        np.testing.assert_array_equal(b, blocks[0])
+    info = blocks[0][8 * n + 24 * D:].view(np.int32)
+    if dc > 64:
+        assert (info[0] >> 5) & 1 and (info[8] >> 5) & 1  # exact-only KDEs: the finish launch published

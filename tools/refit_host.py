@@ -1,6 +1,6 @@
 """Host-side pieces of one BOHB refit (ObservationStore.refit at config #3's 1e4 x 32, or n x 32), GPU box:
     python tools/refit_host.py [n]
-Wall time per refit, the native hbx_kde_refit call's own host time, and the stream time (events)."""
+Wall time per refit, the native hbx_kde_refit_sync call's own host time, and the stream time (events)."""
 import json
 import os
 import sys
@@ -29,7 +29,7 @@ def main():
     torch.cuda.synchronize()
     L = N.lib()
     native = []
-    orig = L.hbx_kde_refit_host_rows
+    orig = L.hbx_kde_refit_sync
 
     def timed(*a):
         t0 = time.perf_counter()
@@ -37,7 +37,7 @@ def main():
         native.append(time.perf_counter() - t0)
         return rc
 
-    L.hbx_kde_refit_host_rows = timed
+    L.hbx_kde_refit_sync = timed
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     wall, stream = [], []
     for r in range(reps):
@@ -49,7 +49,7 @@ def main():
         e1.synchronize()
         wall.append(time.perf_counter() - t0)
         stream.append(e0.elapsed_time(e1) * 1e-3)
-    L.hbx_kde_refit_host_rows = orig
+    L.hbx_kde_refit_sync = orig
     print(json.dumps({"wall_us": float(np.median(wall)) * 1e6, "native_call_us": float(np.median(native)) * 1e6,
                       "stream_us": float(np.median(stream)) * 1e6}))
 
