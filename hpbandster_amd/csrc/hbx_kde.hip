@@ -93,6 +93,30 @@ struct PrepSet {
   PrepPub pub;
 };
 
+// The split's rows (KDE 0) and KDE k's bandwidths and level counts -- written by the launches before the
+// parameter launch -- published by the parameter launch's block k (thread t of nt), 8-byte words: the rows
+// of a 400-observation refit are ~2 stores per thread, not 14 dependent load/store pairs of one wave
+__device__ __forceinline__ void prep_publish_rows(const PrepPub& q, int k, int t, int nt) {
+  auto seg = [&](int off, int words) {  // (even offsets and counts: 8-byte pieces of the layout)
+    const uint64_t* src = (const uint64_t*)(q.src + off);
+    uint64_t* dst = (uint64_t*)(q.dst + off);
+    for (int i = t; i < words / 2; i += nt)
+      __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
+  if (k == 0) seg(0, q.order_words);
+  seg(q.bw_off[k], 2 * q.D);
+  if ((q.nl_off[k] | q.D) & 1) {
+    for (int i = t; i < q.D; i += nt) hbx_publish_store(q.dst + q.nl_off[k] + i, q.src[q.nl_off[k] + i]);
+  } else {
+    seg(q.nl_off[k], q.D);
+  }
+}
+// KDE k's info record (thread 0's own stores of prep_finish_one, read back by it), then its completion word
+__device__ __forceinline__ void prep_publish_info(const PrepPub& q, const PrepArgs& A, int k) {
+  for (int i = 0; i < 8; ++i) hbx_publish_store(q.dst + q.info_off[k] + i, (uint32_t)A.info[i]);
+  hbx_publish_done(q.done + k, q.seq);  // (waits for every store of this wave first)
+}
+
 __device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
 
 __host__ __device__ __forceinline__ ColStats* col_stats(KdeParams* P) { return (ColStats*)((char*)P + HBX_COLSTATS_OFF); }
@@ -366,7 +390,10 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   const PrepArgs& A = blockIdx.x ? ps.k[1] : ps.k[0];  // (no dynamic index into the kernel arguments)
   __shared__ ParamsScratch S;
   if (threadIdx.x == 0) *prep_counter(A.P) = 0;  // the table launch's block counter (finish by the last block)
+  if (ps.pub.dst) prep_publish_rows(ps.pub, blockIdx.x ? 1 : 0, threadIdx.x, blockDim.x);
   kde_params_body(A, A.P, col_stats(A.P), S);
+  // the published words acknowledged before the launch ends: the finishing block's completion word follows them
+  if (ps.pub.dst) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Fill the chunked observation table (layout in hbx_kde_impl.h).  X'_jc = s_c * (X_jc - mu_c),
@@ -416,22 +443,48 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   h8 grp = {};
   const int nd32 = h32_nd(P->nsc);
-  if (hm == 2)
+  if (hm == 2) {
     for (int q = 0; q < 2 * nd32; ++q) *(h8*)(hst + 8 * q) = h8{};
+    // eight dims at a time with no branch between them: their loads in flight together, then the stores and
+    // the eight |X'| maxima (independent reductions); C accumulates in dim order as below
+    for (int k0 = 0; k0 < dcp; k0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + i;
+        const bool live = ok && k < dc;
+        const double xv = x[live ? P->cont_dim[k] : 0];
+        v[i] = live ? (float)(P->cont_scale[k] * (xv - P->center[k])) : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + i;
+        C -= (double)v[i] * (double)v[i];
+        if (slot && k < dcp) {  // slots 6 + 3k: Xh, Xl, Xh
+          const float vc = fminf(fmaxf(v[i], -60000.f), 60000.f);
+          const _Float16 h = (_Float16)vc;
+          const _Float16 l = (_Float16)(vc - (float)h);
+          hst[6 + 3 * k] = h;
+          hst[7 + 3 * k] = l;
+          hst[8 + 3 * k] = h;
+        }
+      }
+      uint32_t a[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = wave_reduce_dpp(__float_as_uint(fabsf(v[i])), OpMax());
+      if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (k0 + i < dc) atomicMax((unsigned int*)&Pw->xmax[k0 + i], a[i]);
+    }
+  }
 #pragma unroll 8
-  for (int k = 0; k < (hm ? dcp : KP - 2); ++k) {
+  for (int k = 0; k < (hm == 2 ? 0 : hm ? dcp : KP - 2); ++k) {
     float v = 0.f;
     if (ok && k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
     C -= (double)v * (double)v;
     if (slot) {
-      if (hm == 2) {  // slots 6 + 3k: Xh, Xl, Xh
-        const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
-        const _Float16 h = (_Float16)vc;
-        const _Float16 l = (_Float16)(vc - (float)h);
-        hst[6 + 3 * k] = h;
-        hst[7 + 3 * k] = l;
-        hst[8 + 3 * k] = h;
-      } else if (hm) {
+      if (hm) {
         const float vc = fminf(fmaxf(v, -60000.f), 60000.f);
         const _Float16 h = (_Float16)vc;
         const _Float16 l = (_Float16)(vc - (float)h);
@@ -472,44 +525,59 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     const int kp = h32_kp(P->kc);
     _Float16* cz = hrow + 16 * nd32;
     _Float16* cp = hrow + h32_par(P->nsc, kp);  // parity block (signed KDEs)
+    _Float16* cc = crow ? crow + 16 * h32c_nd(P->nsc) : nullptr;
     const int ksp = h32_ksp(kp);
-    const uint64_t hit = onehot_hits(x, P, ok);
-    uint32_t iw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    for (int s = 0; s < kp; ++s) {
-      h8 vh[2] = {{}, {}}, vl[2] = {{}, {}}, pv[2] = {{}, {}};
+    if (blockIdx.x == 1) PSTAMP(17);
+    // the matched position t of dim u (at most one per dim, never two in one pair: every dim's block starts at
+    // an even position) puts delta_u's hi / lo (and the parity 1/2) at half t >> 1 of its part; every other
+    // half is 0: zero-filled first, then one scattered half per matched dim (this thread's own row, in order)
+    for (int q = 0; q < 2 * kp; ++q) {
+      *(h8*)(cz + 8 * q) = z8;
+      *(h8*)(cz + 16 * kp + 8 * q) = z8;
+      if (cc) *(h8*)(cc + 8 * q) = z8;
+      if (P->has_neg) *(h8*)(cp + 8 * q) = z8;
+    }
+    if (blockIdx.x == 1) PSTAMP(18);
+    // eight dims at a time, every load of the eight issued before the first use (the positions matched are
+    // those of onehot_hits: x[oh_col[t]] == oh_val[t])
+    uint64_t hit = 0;
+    for (int u0 = 0; u0 < (ok ? du : 0); u0 += 8) {
+      int cd[8], cm[8], os[8];
+      float dlt[8], ngf[8];
+      double v[8];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        uint32_t nib = 0u;
+      for (int i = 0; i < 8; ++i) {  // (indices < du + 8 <= 72: inside the HBX_MAX_D arrays)
+        cd[i] = P->cat_dim[u0 + i];
+        cm[i] = u0 + i < du ? P->cat_maxcode[u0 + i] : -1;
+        os[i] = P->oh_start[u0 + i];
+        dlt[i] = P->cat_delta[u0 + i];
+        ngf[i] = P->cat_negf[u0 + i];
+      }
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          const int t0 = 32 * s + 4 * g + 2 * pr;
-          // (oh_total <= 64: a position at or past it never matches)
-          const bool m0 = t0 < P->oh_total && ((hit >> t0) & 1u);
-          const bool m1 = t0 + 1 < P->oh_total && ((hit >> (t0 + 1)) & 1u);
-          if (m0 || m1) {
-            const int u = P->oh_dim[m1 ? t0 + 1 : t0];
-            const float dl = fminf(fmaxf(P->cat_delta[u], -60000.f), 60000.f);
-            const float hi = (float)(_Float16)dl;
-            vh[g >> 2][2 * (g & 3) + pr] = (_Float16)hi;
-            vl[g >> 2][2 * (g & 3) + pr] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
-            if (P->cat_negf[u] != 0.f) pv[g >> 2][2 * (g & 3) + pr] = (_Float16)0.5f;
-          }
-          nib |= (uint32_t)(2 * pr + (m1 ? 1 : 0)) << (2 * pr);
-        }
-        iw[ksp * (g >> 2) + s] |= nib << (4 * (g & 3));
+      for (int i = 0; i < 8; ++i) v[i] = x[u0 + i < du ? cd[i] : 0];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (!(v[i] >= 0.0 && v[i] <= (double)cm[i]) || v[i] != (double)(int)v[i]) continue;
+        const int t = os[i] + (int)v[i], h = t >> 1;
+        hit |= 1ull << t;
+        const float dl = fminf(fmaxf(dlt[i], -60000.f), 60000.f);
+        const float hi = (float)(_Float16)dl;
+        cz[h] = (_Float16)hi;
+        cz[16 * kp + h] = (_Float16)(fabsf(dl) < 60000.f ? dl - hi : 0.f);
+        if (cc) cc[h] = (_Float16)hi;
+        if (P->has_neg && ngf[i] != 0.f) cp[h] = (_Float16)0.5f;
       }
-      *(h8*)(cz + 16 * s) = vh[0];
-      *(h8*)(cz + 16 * s + 8) = vh[1];
-      *(h8*)(cz + 16 * kp + 16 * s) = vl[0];
-      *(h8*)(cz + 16 * kp + 16 * s + 8) = vl[1];
-      if (crow) {  // the coarse row: the hi parts only
-        *(h8*)(crow + 16 * h32c_nd(P->nsc) + 16 * s) = vh[0];
-        *(h8*)(crow + 16 * h32c_nd(P->nsc) + 16 * s + 8) = vh[1];
-      }
-      if (P->has_neg) {
-        *(h8*)(cp + 16 * s) = pv[0];
-        *(h8*)(cp + 16 * s + 8) = pv[1];
-      }
+    }
+    if (blockIdx.x == 1) PSTAMP(19);
+    if (blockIdx.x == 1) PSTAMP(20);
+    // index nibble of group g (positions t0 = 32 s + 4 g .. t0 + 3): i0 | i1 << 2 with i0 = 0 or 1, i1 = 2 or 3
+    // (1 / 3 where the odd position of the pair matched); dword ksp h + s holds groups 4h..4h+3 of step s
+    uint32_t iw[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int hh = q / ksp, st = q - hh * ksp, sh = 32 * st + 16 * hh;
+      const uint32_t win = (st < kp && hh < 2 && sh < 64) ? (uint32_t)(hit >> sh) & 0xFFFFu : 0u;
+      iw[q] = (st < kp && hh < 2) ? 0x8888u | ((win & 0xAAAAu) >> 1) : 0u;
     }
     for (int w = 0; w < (crow ? 2 : 1); ++w) {  // index words of the precise row, then of the coarse row
       uint32_t* ix = w == 0 ? (uint32_t*)(hrow + 16 * nd32 + 32 * kp) : (uint32_t*)(crow + 16 * h32c_nd(P->nsc) + 16 * kp);
@@ -633,17 +701,6 @@ __device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool 
 }
 __device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) { prep_finish_p(A.P, A.info, rebuild); }
 
-// KDE k's words of the published output block, thread t of nt (order, bandwidths and level counts come
-// from earlier launches; the info record is thread 0's own stores of prep_finish_one, read back by it)
-__device__ __forceinline__ void prep_publish_words(const PrepPub& q, const PrepArgs& A, int k, int t, int nt) {
-  if (k == 0)
-    for (int i = t; i < q.order_words; i += nt) hbx_publish_store(q.dst + i, q.src[i]);
-  for (int i = t; i < 2 * q.D; i += nt) hbx_publish_store(q.dst + q.bw_off[k] + i, q.src[q.bw_off[k] + i]);
-  for (int i = t; i < q.D; i += nt) hbx_publish_store(q.dst + q.nl_off[k] + i, q.src[q.nl_off[k] + i]);
-  if (t == 0)
-    for (int i = 0; i < 8; ++i) hbx_publish_store(q.dst + q.info_off[k] + i, (uint32_t)A.info[i]);
-}
-
 // pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
 // block of a KDE that needs none exits at once)
 // The block's 64 observation rows are staged in LDS first (all loads in flight at once, coalesced
@@ -654,6 +711,12 @@ __device__ __forceinline__ void prep_publish_words(const PrepPub& q, const PrepA
 // C_j left the f16 range (rare: every row, in this block) and writes the final mode and the info record:
 // the rebuild and finish launches saved.
 #define TABLE_STAGE_D 64
+// LDS row stride (halves) of the table launch's h32 rows: a 16-byte multiple >= H32_ROW_MAX whose dword count
+// is not a multiple of 8 (112 halves = 56 dwords put lanes i and i + 8 on one bank: 8-way conflicts on the
+// per-dim half stores; 120 = 60 dwords: 4-way)
+#ifndef H32_ROW_STRIDE
+#define H32_ROW_STRIDE 120
+#endif
 __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0, float* table1, int pass, int finish) {
   const bool second = ps.nk > 1 && (int)blockIdx.x >= ps.k[0].nblk_table;
   const PrepArgs& A = ps.k[second ? 1 : 0];
@@ -677,7 +740,7 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     for (int q = 0; q < 8; ++q) pl[min(i0 + (int)threadIdx.x + 64 * q, NPL - 1)] = t[q];
   }
   __shared__ double xs[64 * (TABLE_STAGE_D + 1)];
-  __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_MAX];  // h32 rows assembled here
+  __shared__ __align__(16) _Float16 h32s[64 * H32_ROW_STRIDE];  // h32 rows assembled here
   const int D = A.D, n = A.n;
   const KdeParams* Pl = (const KdeParams*)pl;
   float* tab = second ? table1 : table0;
@@ -688,10 +751,10 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     const int j = r0 + threadIdx.x;
     auto run = [&](const double* x) {
       if (ps_ == 0)
-        kde_table_body(x, Pl, P, tab, j, Pl->hmode, Pl->chunk_floats, &P->cmax, h32s + threadIdx.x * H32_ROW_MAX);
+        kde_table_body(x, Pl, P, tab, j, Pl->hmode, Pl->chunk_floats, &P->cmax, h32s + threadIdx.x * H32_ROW_STRIDE);
       else
         kde_table_body(x, Pl, P, tab, j, 0, chunk_floats(Pl->dc_pad, Pl->du_pad, Pl->kc, Pl->kc ? Pl->has_neg : 0),
-                       &P->cmax2, h32s + threadIdx.x * H32_ROW_MAX);
+                       &P->cmax2, h32s + threadIdx.x * H32_ROW_STRIDE);
     };
     if (D <= TABLE_STAGE_D) {
       const int DS = D | 1;  // odd row stride: the 64 threads' reads of one dim hit distinct banks
@@ -746,11 +809,8 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     if (rebuild) P->cmax2 = __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prep_finish_one(A, rebuild);
   }
-  if (ps.pub.dst) {  // the refit's output block to the host (hbx_kde_refit_sync)
-    prep_publish_words(ps.pub, A, second ? 1 : 0, threadIdx.x, 64);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words acknowledged (one wave)
-    if (threadIdx.x == 0) hbx_publish_done(ps.pub.done + (second ? 1 : 0), ps.pub.seq);
-  }
+  // the refit's output block to the host (hbx_kde_refit_sync): the rest went out with the parameter launch
+  if (ps.pub.dst && threadIdx.x == 0) prep_publish_info(ps.pub, A, second ? 1 : 0);
   PSTAMP(13);
 }
 
@@ -760,10 +820,7 @@ __global__ void kde_prep_finish_kernel(PrepSet ps) {
   if (k >= ps.nk) return;
   const PrepArgs& A = k ? ps.k[1] : ps.k[0];
   prep_finish_one(A, table_needs_rebuild(A.P));
-  if (ps.pub.dst) {
-    prep_publish_words(ps.pub, A, k, 0, 1);
-    hbx_publish_done(ps.pub.done + k, ps.pub.seq);
-  }
+  if (ps.pub.dst) prep_publish_info(ps.pub, A, k);
 }
 
 static int64_t prep_table_blocks(int64_t n) { return (((n + OBS_CHUNK - 1) / OBS_CHUNK) * OBS_CHUNK + 63) / 64; }

@@ -30,7 +30,9 @@ def main():
     spans = {"params parallel part": (0, 1), "params slots+fields+sums": (1, 2), "params one-hot+mode": (2, 3),
              "table block1 prologue (P copy, rows, stage)": (8, 9), "table body: dims": (9, 14),
              "table body: one-hot": (14, 15), "table body: C, row stores": (15, 16), "table body: cmax": (16, 10),
-             "table block1 drain": (10, 11), "table finish (last block)": (12, 13)}
+             "table block1 drain": (10, 11), "table finish (last block)": (12, 13),
+             "one-hot: padding": (14, 17), "one-hot: zero fill": (17, 18), "one-hot: hits + scatter": (18, 19),
+             "one-hot: index words": (20, 15)}
     rows = []
     for r in range(20):
         store.add(X[n0 + r], losses[n0 + r])
