@@ -304,7 +304,23 @@ struct RefitSortArgs {
   double inl[REFIT_INLINE];  // the appended rows then their losses, when they fit (no host-to-device copy)
 };
 
+// SORT_STAMPS (diagnostic builds only): s_memtime at the phase boundaries of the one-launch refit sort (thread 0)
+#ifdef SORT_STAMPS
+__device__ unsigned long long sort_stamps[16];
+#define SSTAMP(i) \
+  if (threadIdx.x == 0) sort_stamps[i] = __builtin_amdgcn_s_memtime()
+extern "C" int hbx_debug_sort_stamps(unsigned long long* out) {
+  HBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(sort_stamps), sizeof(sort_stamps)));
+  return HBX_OK;
+}
+#else
+#define SSTAMP(i)
+#endif
+
+// PW losses per lane (runs of 64 PW): 2 while n <= 512 (the shorter network and searches), else 4
+template <int PW>
 __global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(RefitSortArgs g) {
+  SSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const RefitMetaArgs& a = g.a;
   double* __restrict__ X = g.X;
@@ -334,40 +350,58 @@ __global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(Refit
     m->fac_bad = a.fac_bad;
   }
   __shared__ uint64_t rk[REFIT_SORT_SMALL];  // the four waves' sorted runs, then the keys by rank
-  __shared__ int32_t rp[REFIT_SORT_SMALL];
+  SSTAMP(1);
   __syncthreads();  // the appended losses are visible to every wave
+  SSTAMP(2);
   // each wave sorts its run of 256 losses in registers (a quarter of one wave's 1024-network), the runs are
   // merged by rank: an element's rank is its place in its run plus, in each other run, the count of (key,
   // position) pairs below it (binary searches in LDS); positions are distinct, so the ranks are a permutation
-  constexpr int PW = REFIT_SORT_SMALL / NPS_THREADS;
+  static_assert(PW * NPS_THREADS <= REFIT_SORT_SMALL, "runs beyond the LDS arrays");
   const int w = tid >> 6;
   uint64_t key[PW];
   int32_t pos[PW];
   wave_sort_run<false, PW>(loss, 64 * PW * w, n, lane, key, pos);
+  SSTAMP(3);
 #pragma unroll
   for (int r = 0; r < PW; ++r) {
     rk[64 * PW * w + PW * lane + r] = key[r];
-    rp[64 * PW * w + PW * lane + r] = pos[r];
   }
   __syncthreads();
-  int rank[PW];
+  // count of entries of each other run below (key, pos).  Run v holds positions [RUN v, RUN v + RUN), so against
+  // an earlier run (v < w) that is the count of keys <= key, against a later one the count of keys < key: the
+  // keys alone decide.  A fixed-step search over the run's real entries (b = 256, 128, .., 1: step b adds b when
+  // entry c + b - 1 counts), every (run, register) chain advanced together -- one LDS round trip per step for
+  // all of them, not a dependent loop per element
+  constexpr int NR = NPS_THREADS / 64, RUN = 64 * PW;
+  int cnt[NR][PW];
 #pragma unroll
-  for (int r = 0; r < PW; ++r) rank[r] = PW * lane + r;
-  for (int v = 0; v < NPS_THREADS / 64; ++v) {
-    if (v == w) continue;
-    const uint64_t* kv = rk + 64 * PW * v;
-    const int32_t* pv = rp + 64 * PW * v;
+  for (int v = 0; v < NR; ++v)
 #pragma unroll
-    for (int r = 0; r < PW; ++r) {
-      int lo = 0, hi = 64 * PW;  // first entry of run v not below (key, pos)
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (kv_less(kv[mid], pv[mid], key[r], pos[r])) lo = mid + 1;
-        else hi = mid;
+    for (int r = 0; r < PW; ++r) cnt[v][r] = 0;
+#pragma unroll
+  for (int b = RUN; b > 0; b >>= 1) {
+#pragma unroll
+    for (int v = 0; v < NR - 1; ++v) {
+      const int vr = v < w ? v : v + 1;  // the other runs
+      const int len = min(max(n - RUN * vr, 0), RUN);
+#pragma unroll
+      for (int r = 0; r < PW; ++r) {
+        const int c = cnt[v][r] + b - 1;
+        if (c < len) {
+          const uint64_t e = rk[RUN * vr + c];
+          if (vr < w ? e <= key[r] : e < key[r]) cnt[v][r] += b;
+        }
       }
-      rank[r] += lo;
     }
   }
+  int rank[PW];
+#pragma unroll
+  for (int r = 0; r < PW; ++r) {
+    rank[r] = PW * lane + r;
+#pragma unroll
+    for (int v = 0; v < NR - 1; ++v) rank[r] += cnt[v][r];
+  }
+  SSTAMP(4);
   __syncthreads();  // every run read
 #pragma unroll
   for (int r = 0; r < PW; ++r) {
@@ -376,11 +410,13 @@ __global__ __launch_bounds__(NPS_THREADS) void kde_refit_sort_small_kernel(Refit
       order[rank[r]] = pos[r];
     }
   }
+  SSTAMP(5);
   __syncthreads();
   int t = 0;
   for (int i = tid; i + 1 < n; i += NPS_THREADS) t |= rk[i] == rk[i + 1];
   if (__syncthreads_or(t))  // tied losses: every position re-ranked in numpy's order
     nps_order_segment(loss, n, 0, 0.0, A0, A0 + n, A0 + 2 * n, A0 + 3 * n, order, nullptr);
+  SSTAMP(6);
 }
 
 int refit_sort_small(double* X, double* loss, const double* staged, const double* staged_inline, int64_t n_new,
@@ -402,7 +438,10 @@ int refit_sort_small(double* X, double* loss, const double* staged, const double
     g.staged = nullptr;
     memcpy(g.inl, staged_inline, 8 * (size_t)nst);
   }
-  hipLaunchKernelGGL(kde_refit_sort_small_kernel, dim3(1), dim3(NPS_THREADS), 0, s, g);
+  if (a.n <= 2 * NPS_THREADS)
+    hipLaunchKernelGGL(kde_refit_sort_small_kernel<2>, dim3(1), dim3(NPS_THREADS), 0, s, g);
+  else
+    hipLaunchKernelGGL(kde_refit_sort_small_kernel<REFIT_SORT_SMALL / NPS_THREADS>, dim3(1), dim3(NPS_THREADS), 0, s, g);
   HBX_LAUNCH_CHECK();
   return HBX_OK;
 }

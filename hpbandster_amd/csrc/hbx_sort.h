@@ -21,6 +21,27 @@ __device__ __forceinline__ bool kv_less(uint64_t ka, int32_t ia, uint64_t kb, in
   return ka < kb || (ka == kb && ia < ib);
 }
 
+// The value of lane `lane ^ lm` (lm a power of two known after unrolling) without the LDS crossbar where the
+// pattern allows: xor 1 / 2 by a quad permutation, xor 4 / 8 by row rotations (row_ror:n gives lane i the
+// value of lane i - n within its 16-lane row), xor 16 by ds_swizzle's bit mode; xor 32 by ds_bpermute
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v, int lm, int lane) {
+  switch (lm) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    case 4: {
+      const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4  (i - 4)
+      const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12c, 0xf, 0xf, false);  // row_ror:12 (i + 4)
+      return (lane & 4) ? a : b;
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401f);  // and 0x1f, xor 0x10
+    default: return (uint32_t)__shfl_xor((int)v, lm);
+  }
+}
+__device__ __forceinline__ uint64_t lane_xor_u64(uint64_t v, int lm, int lane) {
+  return (uint64_t)lane_xor_u32((uint32_t)v, lm, lane) | ((uint64_t)lane_xor_u32((uint32_t)(v >> 32), lm, lane) << 32);
+}
+
 // Bitonic sort of P (power of two) pairs in LDS, whole block participates.
 __device__ void block_bitonic(uint64_t* k, int32_t* ix, int P) {
   for (int size = 2; size <= P; size <<= 1) {
@@ -152,8 +173,8 @@ __device__ __forceinline__ void wave_sort_1024(const double* __restrict__ loss, 
         const bool lower = (lane & lm) == 0;
 #pragma unroll
         for (int r = 0; r < PW_PER_LANE; ++r) {
-          const uint64_t ok = __shfl_xor(key[r], lm);
-          const int32_t op = __shfl_xor(pos[r], lm);
+          const uint64_t ok = lane_xor_u64(key[r], lm, lane);
+          const int32_t op = (int32_t)lane_xor_u32((uint32_t)pos[r], lm, lane);
           const bool up = ((lane * PW_PER_LANE + r) & size) == 0;
           const bool other_less = kv_less(ok, op, key[r], pos[r]);
           // ascending run: the lower index keeps the smaller element; descending: the larger
@@ -205,8 +226,8 @@ __device__ __forceinline__ void wave_sort_run(const double* __restrict__ loss, i
         const bool lower = (lane & lm) == 0;
 #pragma unroll
         for (int r = 0; r < PW; ++r) {
-          const uint64_t ok = __shfl_xor(key[r], lm);
-          const int32_t op = __shfl_xor(pos[r], lm);
+          const uint64_t ok = lane_xor_u64(key[r], lm, lane);
+          const int32_t op = (int32_t)lane_xor_u32((uint32_t)pos[r], lm, lane);
           const bool up = ((lane * PW + r) & size) == 0;
           const bool other_less = kv_less(ok, op, key[r], pos[r]);
           const bool take = (lower == up) ? other_less : !other_less;
