@@ -2367,6 +2367,10 @@ int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int3
   rc = wait_done(done + 1, seq, (hipStream_t)stream, "hbx_kde_refit_sync");
   if (rc) return rc;
   memcpy(out_host, mapped, (size_t)bytes);
+  const RefitOut o = refit_out_layout(n, D);
+  const int32_t* nl = (const int32_t*)((const char*)out_host + o.nlev_good);  // good then bad
+  for (int32_t d = 0; d < 2 * D; ++d)
+    if (nl[d] < 0) return hbx_fail(HBX_ERR_ARG, "categorical codes must be integers in [0, 1024)");
   return HBX_OK;
 }
 

@@ -317,6 +317,18 @@ def _levels_on_device(key, lv, device):
     return t
 
 
+_FAST_FNS = None
+
+
+def _torch_fast_fns():
+    """torch's raw current-device and current-stream accessors (None where this torch lacks them)."""
+    global _FAST_FNS
+    if _FAST_FNS is None:
+        torch = _torch()
+        _FAST_FNS = (getattr(torch._C, "_cuda_getDevice", None), getattr(torch._C, "_cuda_getCurrentRawStream", None))
+    return _FAST_FNS
+
+
 class KDEPair(object):
     """The (good, bad) KDE pair of one budget -- BOHB's ``kde_models[budget]`` entry.
 
@@ -339,15 +351,14 @@ class KDEPair(object):
         self._wsb = {}
         self._roff = None
         # the synchronous fast path's constants (acquire: a call on the model's own device)
-        torch = _torch()
-        self._dev_index = torch.device(good.device).index
-        self._cur_dev = getattr(torch._C, "_cuda_getDevice", None)
-        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-        self._host_fn = N.lib().hbx_kde_acquire_host
+        dev = good.device
+        self._dev_index = dev.index if dev.index is not None else _torch().cuda.current_device()
+        self._cur_dev, self._raw_stream = _torch_fast_fns()
+        L = N.lib()
+        self._host_fn = L.hbx_kde_acquire_host
         self._ws_cache = {}  # (thread, Nc) -> workspace of synchronous calls made without one
         # the fixed arguments bound once on the native side: the synchronous call converts 8 arguments
         # instead of 22 (hbx_kde_acquire_bound)
-        L = N.lib()
         self._bound = None
         if N.DIAGNOSTIC_BUILD and not hasattr(L, "hbx_kde_pair_bind"):
             return  # an older diagnostic build (A/B runs): the unbound call
@@ -748,6 +759,9 @@ class ObservationStore(object):
         sizes = split_sizes(n, self.D, min_points, top_n_percent, split_rule)
         if sizes is None:
             return None
+        cur, _ = _torch_fast_fns()
+        if stream is None and cur is not None and self.device.index is not None and cur() == self.device.index:
+            return self._refit(self._Xh[:n], self._lh[:n], n, sizes, stream)  # (already current: no context)
         with N.on_device(self.device, stream):
             return self._refit(self._Xh[:n], self._lh[:n], n, sizes, stream)
 
@@ -795,9 +809,7 @@ class ObservationStore(object):
         nl_gh = ah[o + 16 * D:o + 20 * D].view(np.int32)
         nl_bh = ah[o + 20 * D:o + 24 * D].view(np.int32)
         info_g = ah[o + 24 * D:o + 24 * D + 32].view(np.int32)
-        info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32)
-        if (nl_gh < 0).any() or (nl_bh < 0).any():
-            raise N.HbxError("categorical codes must be integers in [0, 1024)")
+        info_b = ah[o + 24 * D + 32:o + 24 * D + 64].view(np.int32)  # (level counts < 0: the call failed)
         self.n = n  # the rows count as resident only once the refit has completed and validated
         order = blk[:8 * n].view(torch.int64)
         X_dev = self.X_dev
