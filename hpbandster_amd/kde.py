@@ -345,9 +345,10 @@ class KDEPair(object):
         # per-call constants of acquire(): the prepared KDEs' device pointers and variant codes, the
         # workspace size per candidate count, the result record's offset (host overhead of a
         # get_config at the reference's 64 candidates is of the order of the GPU work)
-        self._kde_args = (N.ptr(good.params), N.ptr(good.table), N.ptr(good.X_dev), N.ptr(good.rows_dev),
-                          good.variant, N.ptr(bad.params), N.ptr(bad.table), N.ptr(bad.X_dev),
-                          N.ptr(bad.rows_dev), bad.variant, good.dc_pad, good.du_pad, self.nmax)
+        self._kde_args = (good.params.data_ptr(), good.table.data_ptr(), good.X_dev.data_ptr(),
+                          good.rows_dev.data_ptr(), good.variant, bad.params.data_ptr(), bad.table.data_ptr(),
+                          bad.X_dev.data_ptr(), bad.rows_dev.data_ptr(), bad.variant, good.dc_pad, good.du_pad,
+                          self.nmax)
         self._wsb = {}
         self._roff = None
         # the synchronous fast path's constants (acquire: a call on the model's own device)
