@@ -131,11 +131,44 @@ __global__ __launch_bounds__(SAMPLE_BLOCK) void kde_sample_table_kernel(
 }
 
 // z = Phi^-1(p) on the smaller tail in fp32, p = Phi(lo) + u (Phi(hi) - Phi(lo)) in fp64, clamped to [lo, hi]
+// erfcinv(t), t in (0, 1], in single precision without the library's branches: M. Giles' single-precision erfinv
+// polynomials ("Approximating the erfinv function", GPU Computing Gems Jade, 2011; relative error ~4e-7) at
+// x = 1 - t, with w = -ln((1 - x)(1 + x)) formed from t itself (t (2 - t): exact in the tail where 1 - t rounds)
+__device__ __forceinline__ float fast_erfcinvf(float t) {
+  float w = -__logf(t * (2.0f - t));
+  float p;
+  if (w < 5.0f) {
+    w = w - 2.5f;
+    p = 2.81022636e-08f;
+    p = fmaf(p, w, 3.43273939e-07f);
+    p = fmaf(p, w, -3.5233877e-06f);
+    p = fmaf(p, w, -4.39150654e-06f);
+    p = fmaf(p, w, 0.00021858087f);
+    p = fmaf(p, w, -0.00125372503f);
+    p = fmaf(p, w, -0.00417768164f);
+    p = fmaf(p, w, 0.246640727f);
+    p = fmaf(p, w, 1.50140941f);
+  } else {
+    w = sqrtf(w) - 3.0f;
+    p = -0.000200214257f;
+    p = fmaf(p, w, 0.000100950558f);
+    p = fmaf(p, w, 0.00134934322f);
+    p = fmaf(p, w, -0.00367342844f);
+    p = fmaf(p, w, 0.00573950773f);
+    p = fmaf(p, w, -0.0076224613f);
+    p = fmaf(p, w, 0.00943887047f);
+    p = fmaf(p, w, 1.00167406f);
+    p = fmaf(p, w, 2.83297682f);
+  }
+  return p * (1.0f - t);
+}
+
 __device__ __forceinline__ double tn_invert_f32(double plo, double phi, double lo, double hi, double u) {
   const double p = fma(u, phi - plo, plo);
   const bool up = p > 0.5;
   const float t = (float)(2.0 * (up ? 1.0 - p : p));        // in (0, 1]
-  const float zt = -1.41421356237309505f * erfcinvf(t);    // Phi^-1(min(p, 1 - p)) <= 0
+  const float zt = -1.41421356237309505f * fast_erfcinvf(t);  // Phi^-1(min(p, 1 - p)) <= 0
+  // (the library's erfcinvf: the same draws in distribution, 0.126 instead of 0.113 ms per 1e6 x 32 launch)
   const double z = (double)(up ? -zt : zt);
   return fmin(fmax(z, lo), hi);
 }
