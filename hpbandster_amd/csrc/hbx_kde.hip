@@ -77,11 +77,11 @@ struct PrepArgs {
 };
 // The refit's output block published to device-mapped host memory by the preparation's finishing blocks
 // (hbx_kde_refit_sync): the split's rows (KDE 0's block), each KDE's bandwidths, level counts and info record,
-// then a completion word per KDE; dst == nullptr: nothing published
+// then the info records as flagged words; dst == nullptr: nothing published
 struct PrepPub {
   uint32_t* dst;        // mapped host copy of the output block (same word offsets as src)
   const uint32_t* src;  // the device output block
-  int32_t* done;        // completion words, one per KDE
+  uint64_t* ll;         // the two info records as 16 flagged words: seq << 32 | word (no completion word)
   int32_t seq;
   int32_t order_words;  // 2 n
   int32_t bw_off[2], nl_off[2], info_off[2];  // word offsets of KDE k's pieces
@@ -111,10 +111,15 @@ __device__ __forceinline__ void prep_publish_rows(const PrepPub& q, int k, int t
     seg(q.nl_off[k], q.D);
   }
 }
-// KDE k's info record (thread 0's own stores of prep_finish_one, read back by it), then its completion word
+// KDE k's info record (thread 0's own stores of prep_finish_one, read back by it) as flagged 8-byte words:
+// each carries the call's sequence number beside its value, so the host knows every word from the word itself
+// and no store has to wait for the others' acknowledgement (a completion word after an acknowledged record
+// cost ~12k cycles of round trip to host memory).  The parameter launch's words were acknowledged before
+// that launch ended, so they are in place too.
 __device__ __forceinline__ void prep_publish_info(const PrepPub& q, const PrepArgs& A, int k) {
-  for (int i = 0; i < 8; ++i) hbx_publish_store(q.dst + q.info_off[k] + i, (uint32_t)A.info[i]);
-  hbx_publish_done(q.done + k, q.seq);  // (waits for every store of this wave first)
+  for (int i = 0; i < 8; ++i)
+    __hip_atomic_store(q.ll + 8 * k + i, ((uint64_t)(uint32_t)q.seq << 32) | (uint32_t)A.info[i], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ bool prep_cat(const PrepArgs& A, int d) { return (A.vt[d >> 5] >> (d & 31)) & 1u; }
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(256) void kde_params_kernel(PrepSet ps) {
   if (threadIdx.x == 0) *prep_counter(A.P) = 0;  // the table launch's block counter (finish by the last block)
   if (ps.pub.dst) prep_publish_rows(ps.pub, blockIdx.x ? 1 : 0, threadIdx.x, blockDim.x);
   kde_params_body(A, A.P, col_stats(A.P), S);
-  // the published words acknowledged before the launch ends: the finishing block's completion word follows them
+  // the published words acknowledged before the launch ends: the finishing blocks' flagged info words follow them
   if (ps.pub.dst) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -2315,7 +2320,7 @@ static int refit_mapped_buffer(int64_t bytes, char** out) {
     int64_t cap = t_refit_cap > 0 ? t_refit_cap : 16384;
     while (cap < bytes) cap *= 2;
     void* p = nullptr;
-    HBX_HIP(hipHostMalloc(&p, (size_t)cap + 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    HBX_HIP(hipHostMalloc(&p, (size_t)cap + 256, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
     void* dp = nullptr;
     HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
     if (dp != p) {
@@ -2328,8 +2333,7 @@ static int refit_mapped_buffer(int64_t bytes, char** out) {
     }
     t_refit_mapped = (char*)p;
     t_refit_cap = cap;
-    ((volatile int32_t*)(t_refit_mapped + cap))[0] = 0;
-    ((volatile int32_t*)(t_refit_mapped + cap))[1] = 0;
+    for (int i = 0; i < 16; ++i) ((volatile uint64_t*)(t_refit_mapped + cap))[i] = 0;  // flagged info words
   }
   *out = t_refit_mapped;
   return HBX_OK;
@@ -2339,7 +2343,7 @@ extern "C" {
 
 // hbx_kde_refit_host_rows, then the output block in host memory (out_host, hbx_kde_refit_out_bytes) when the
 // call returns: the preparation's finishing blocks publish it to a device-mapped host buffer with a
-// completion word per KDE, and the call spins on those words -- no copy launch, no blocking stream
+// the info records as flagged words, and the call spins on those flags -- no copy launch, no blocking stream
 // synchronisation (bounded: then the stream is synchronised and the words checked)
 int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
                        const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
@@ -2351,23 +2355,35 @@ int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int3
   char* mapped = nullptr;
   int rc = refit_mapped_buffer(bytes, &mapped);
   if (rc) return rc;
-  int32_t* done = (int32_t*)(mapped + t_refit_cap);
+  uint64_t* ll = (uint64_t*)(mapped + t_refit_cap);
   const int32_t seq = t_refit_seq = t_refit_seq == INT32_MAX ? 1 : t_refit_seq + 1;
   PrepPub pub;
   memset(&pub, 0, sizeof(pub));
   pub.dst = (uint32_t*)mapped;
-  pub.done = done;
+  pub.ll = ll;
   pub.seq = seq;
   rc = refit_impl(X, loss, n, D, vartype, staged_host, true, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
                   table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
                   stream, &pub);
   if (rc) return rc;
-  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_refit_sync");
-  if (rc) return rc;
-  rc = wait_done(done + 1, seq, (hipStream_t)stream, "hbx_kde_refit_sync");
-  if (rc) return rc;
+  // spin until all 16 flagged info words carry this call's sequence number (bounded: ~0.1 s, then the stream
+  // is synchronised and the words checked once more)
+  auto all_in = [&]() {
+    for (int i = 0; i < 16; ++i)
+      if ((int32_t)(__atomic_load_n(ll + i, __ATOMIC_ACQUIRE) >> 32) != seq) return false;
+    return true;
+  };
+  bool seen = false;
+  for (int64_t i = 0; i < 5000000 && !seen; ++i) seen = all_in();
+  if (!seen) {
+    HBX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (!all_in()) return hbx_fail(HBX_ERR_HIP, "hbx_kde_refit_sync: the device did not publish its info records");
+  }
   memcpy(out_host, mapped, (size_t)bytes);
   const RefitOut o = refit_out_layout(n, D);
+  for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < 8; ++i)
+      ((int32_t*)((char*)out_host + (k ? o.info_bad : o.info_good)))[i] = (int32_t)(uint32_t)ll[8 * k + i];
   const int32_t* nl = (const int32_t*)((const char*)out_host + o.nlev_good);  // good then bad
   for (int32_t d = 0; d < 2 * D; ++d)
     if (nl[d] < 0) return hbx_fail(HBX_ERR_ARG, "categorical codes must be integers in [0, 1024)");

@@ -116,7 +116,8 @@ int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const
                             int64_t scratch_bytes, void* stream);
 /* hbx_kde_refit_host_rows, synchronous: when the call returns, `out_host` (host memory,
  * hbx_kde_refit_out_bytes) holds the output block.  The preparation's finishing workgroups publish it to a
- * device-mapped host buffer with a completion word per KDE and the call spins on those words (no copy
+ * device-mapped host buffer, the info records as words flagged with the call's sequence number, and the call
+ * spins on those flags (no copy
  * launch, no blocking stream synchronisation).  The drop-in's ObservationStore.refit calls this one
  * (bohb.py:211-251, one new_result per call). */
 int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
