@@ -2342,8 +2342,9 @@ static int refit_mapped_buffer(int64_t bytes, char** out) {
 extern "C" {
 
 // hbx_kde_refit_host_rows, then the output block in host memory (out_host, hbx_kde_refit_out_bytes) when the
-// call returns: the preparation's finishing blocks publish it to a device-mapped host buffer with a
-// the info records as flagged words, and the call spins on those flags -- no copy launch, no blocking stream
+// call returns: the preparation's launches publish it to a device-mapped host buffer (the parameter launch the
+// rows, bandwidths and level counts, the finishing blocks the info records as flagged words), and the call
+// spins on those flags -- no copy launch, no blocking stream
 // synchronisation (bounded: then the stream is synchronised and the words checked)
 int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
                        const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
