@@ -16,7 +16,7 @@
 // (h >= 1: always resampled, level floor(t u)) -- the reference draws from numpy's global RNG, so parity is
 // distributional (tests/test_gpu_sample.py).
 //
-// One lane per (candidate, pair of dims), 8 lanes per candidate (kde_sample_pair_kernel).  Phi at the
+// One lane per (candidate, pair of dims), 4 lanes per candidate (kde_sample_pair_kernel).  Phi at the
 // bounds comes from a per-model table when many candidates are drawn (hbx_kde_sample_table).
 // hbx_norm_ppf keeps the fp64 inverse normal CDF (Wichura's AS 241) as a library function.
 #include <math.h>
@@ -211,25 +211,31 @@ __device__ __forceinline__ double sample_dim(const double* __restrict__ xr, int 
   return fma(bw_factor * h, flip ? -z : z, m);
 }
 
-// The draws with one (candidate, pair of dims) per lane: 8 lanes per candidate, lane g of the group takes
-// the pairs g, g + 8, ...  A candidate's datum row and Phi-table row are then read by its 8 lanes as
-// contiguous 16-byte pieces and its output row is written as contiguous 16-byte stores (a lane-per-
+// The draws with one (candidate, pair of dims) per lane: L = SAMPLE_LPC lanes per candidate, lane g of the
+// group takes the pairs g, g + L, ...  A candidate's datum row and Phi-table row are then read by its L lanes
+// as contiguous 16-byte pieces and its output row is written as contiguous 16-byte stores (a lane-per-
 // candidate layout, 8-9 % slower with the same draws, was removed in round 5).  One Philox block per lane and
-// two pairs (word g + 8 i for pairs g + 16 i and g + 8 + 16 i): the block's four words are the four dims'
+// two pairs (word g + L i for pairs g + 2 L i and g + L + 2 L i): the block's four words are the four dims'
 // uniforms -- a categorical dim takes both its keep-or-resample decision and its level from its uniform --
 // so a candidate costs D / 4 blocks (D before round 5: two words per dim, the generator half the work).
 // Dim types and bandwidths vary across the lanes (loaded per lane; the categorical branch is the cheap
-// one).  Counter (candidate, word, stream): the draws do not depend on the launch shape.
+// one): with 4 lanes a 24c + 8u candidate's 16 pairs take three all-continuous steps and one all-categorical
+// step, where 8 lanes ran a mixed step through both branches.  Counter (candidate, word, stream): the draws
+// do not depend on the launch shape.
+#ifndef SAMPLE_LPC
+#define SAMPLE_LPC 4  // lanes per candidate (8: 0.130 ms, 2: 0.196 ms per 1e6 x 32 launch against 0.119 ms; lib_ab)
+#endif
 template <bool TAB>
 __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ rows, int64_t n,
     const double* __restrict__ bw, const int32_t* __restrict__ levels, const double2* __restrict__ tab,
     double bw_factor, uint64_t seed, uint64_t counter_base, uint32_t stream_id, int64_t Nc,
     double* __restrict__ cands, int64_t* __restrict__ datum, uint8_t* __restrict__ domain_err) {
-  __shared__ int32_t sdat[32];
+  constexpr int CPB = 256 / SAMPLE_LPC;  // candidates per block
+  __shared__ int32_t sdat[CPB];
   __shared__ double srh[HBX_MAX_D];  // 1 / bw per dim
-  const int64_t c0 = (int64_t)blockIdx.x * 32;  // 32 candidates per block: 8 lanes each
-  const int nc = (int)(Nc - c0 < 32 ? Nc - c0 : 32);
+  const int64_t c0 = (int64_t)blockIdx.x * CPB;
+  const int nc = (int)(Nc - c0 < CPB ? Nc - c0 : CPB);
   for (int t = threadIdx.x; t < D; t += 256) srh[t] = 1.0 / bw[t];
   if (threadIdx.x < nc) {
     const int64_t i = c0 + threadIdx.x;
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
     if (datum) datum[i] = idx;
   }
   __syncthreads();
-  const int cl = threadIdx.x >> 3, g = threadIdx.x & 7;
+  const int cl = threadIdx.x / SAMPLE_LPC, g = threadIdx.x % SAMPLE_LPC;
   if (cl >= nc) return;
   const int64_t i = c0 + cl;
   const int32_t idx = sdat[cl];
@@ -248,9 +254,9 @@ __global__ __launch_bounds__(256) void kde_sample_pair_kernel(
   const int D2 = (D + 1) >> 1;
   bool derr = false;
   HbxU32x4 r;
-  for (int k = g; k < D2; k += 8) {
-    const int q = (k - g) >> 3;  // this lane's q-th pair: a new block every second pair
-    if ((q & 1) == 0) r = draw(seed, counter_base + (uint64_t)i, (uint32_t)(g + 8 * (q >> 1)), stream_id);
+  for (int k = g; k < D2; k += SAMPLE_LPC) {
+    const int q = (k - g) / SAMPLE_LPC;  // this lane's q-th pair: a new block every second pair
+    if ((q & 1) == 0) r = draw(seed, counter_base + (uint64_t)i, (uint32_t)(g + SAMPLE_LPC * (q >> 1)), stream_id);
     const uint32_t w0 = (q & 1) ? r.x[2] : r.x[0], w1 = (q & 1) ? r.x[3] : r.x[1];
     const int d = 2 * k;
     const double v0 = sample_dim<TAB>(xr, d, idx, D, bw, srh, levels, tab, bw_factor, w0, &derr);
@@ -311,7 +317,8 @@ int hbx_kde_sample(const double* X, int32_t D, const int64_t* rows, int64_t n, c
   hipStream_t s = (hipStream_t)stream;
   if (domain_err) HBX_HIP(hipMemsetAsync(domain_err, 0, (size_t)Nc, s));
   if ((D & 1) == 0 && ((uintptr_t)cands & 15)) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: cands not 16-byte aligned");
-  const int64_t pb = (Nc + 31) / 32;  // one (candidate, pair of dims) per lane: 32 candidates per block
+  constexpr int CPB = 256 / SAMPLE_LPC;
+  const int64_t pb = (Nc + CPB - 1) / CPB;  // one (candidate, pair of dims) per lane
   if (pb > INT32_MAX) return hbx_fail(HBX_ERR_ARG, "hbx_kde_sample: Nc=%lld", (long long)Nc);
   hipLaunchKernelGGL(tab ? kde_sample_pair_kernel<true> : kde_sample_pair_kernel<false>, dim3((unsigned)pb), dim3(256),
                      0, s, X, D, rows, n, bw, levels, (const double2*)tab, bw_factor, seed, counter_base, stream_id,
