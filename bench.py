@@ -852,8 +852,8 @@ def config2_line(device, reps=50):
 def refit_line(X, losses, var_type, device, reps=20):
     """Side measurement: one BOHB refit at config #3's observation set as
     new_result runs it (bohb.py:211-251): one new observation appended to the budget's rows resident in
-    HBM, then ``hbx_kde_refit`` (split, bandwidths, level counts, both KDEs prepared for scoring) and
-    one read-back -- beside the same arithmetic in host numpy (argsort, row gathers,
+    HBM, then ``hbx_kde_refit_sync`` (split, bandwidths, level counts, both KDEs prepared for scoring; the
+    output block published to mapped host memory) -- beside the same arithmetic in host numpy (argsort, row gathers,
     1.06 std n^(-1/(4+D)), unique level counts), and the refit from host arrays (all rows uploaded)."""
     import torch
     from hpbandster_amd import kde
@@ -894,7 +894,7 @@ def refit_line(X, losses, var_type, device, reps=20):
             "stream_ms_median": float(np.median(gpu_ms)),
             "stream_ms_note": "events bracketing store.refit on its stream: the kernels plus the host's enqueue gaps "
                               "(wall clock ms_per_refit adds add(), allocation and the read-back)",
-            "note": "wall clock per new_result refit: one row appended in HBM, one hbx_kde_refit, one read-back; "
+            "note": "wall clock per new_result refit: one row appended in HBM, one hbx_kde_refit_sync (its output block published to mapped host memory); "
                     "host_arrays = every row uploaded"}
 
 
