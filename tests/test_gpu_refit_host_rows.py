@@ -165,3 +165,46 @@ def test_sync_refit_publishes_the_output_block(device, dc, du, lev, n, n_new):
     info = blocks[0][8 * n + 24 * D:].view(np.int32)
     if dc > 64:
         assert (info[0] >> 5) & 1 and (info[8] >> 5) & 1  # exact-only KDEs: the finish launch published
+
+
+def test_sync_refit_rejects_bad_codes_then_recovers(device):
+    """A categorical code that is not an integer in [0, 1024) makes hbx_kde_refit_sync fail with the drop-in's
+    message (its level-count check on the host block); the thread's next call on valid rows succeeds."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lev, n = 6, 2, 3, 120
+    D = dc + du
+    vt = np.array([0] * dc + [1] * du, dtype=np.int32)
+    ng, nb = kde.bohb_split_sizes(n, D + 1)
+    Lb = N.lib()
+    ob, sb, pb = (int(Lb.hbx_kde_refit_out_bytes(n, D)), int(Lb.hbx_kde_refit_scratch_bytes(n, D)),
+                  int(Lb.hbx_kde_param_bytes()))
+    dcp, dup = kde.scoring_bucket(vt)
+    tgf, tbf = int(Lb.hbx_kde_table_floats(ng, dcp, dup)), int(Lb.hbx_kde_table_floats(nb, dcp, dup))
+    for bad in (True, False):
+        X = S.make_observations(n, dc, du, lev, seed=7)
+        if bad:
+            X[:, dc] = 0.5  # every row: not an integer code, in both sets
+        L = S.make_losses(n, seed=8)
+        Xd = torch.from_numpy(X).to(device)
+        Ld = torch.from_numpy(L).to(device)
+        out = torch.zeros(ob, dtype=torch.uint8, device=device)
+        scr = torch.zeros(sb, dtype=torch.uint8, device=device)
+        pg, pbd = (torch.zeros(pb, dtype=torch.uint8, device=device) for _ in range(2))
+        tg = torch.zeros(tgf, dtype=torch.float32, device=device)
+        tb = torch.zeros(tbf, dtype=torch.float32, device=device)
+        host = np.zeros(ob, dtype=np.uint8)
+        args = [N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, None, 0, ng, nb, kde.bandwidth_factor(ng, D),
+                kde.bandwidth_factor(nb, D), N.ptr(pg), N.ptr(tg), tgf, N.ptr(pbd), N.ptr(tb), tbf, N.ptr(out),
+                N.ptr(scr), sb, N.stream_handle(), host.ctypes.data]
+        if bad:
+            with pytest.raises(N.HbxError, match="categorical codes"):
+                N.call("hbx_kde_refit_sync", *args)
+        else:
+            N.call("hbx_kde_refit_sync", *args)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(host, out.cpu().numpy())
+            g_idx, _ = O.bohb_split(X, L, D + 1)
+            np.testing.assert_array_equal(host[:8 * n].view(np.int64)[:ng], g_idx)
