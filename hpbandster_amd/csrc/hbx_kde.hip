@@ -111,6 +111,12 @@ __device__ __forceinline__ void prep_publish_rows(const PrepPub& q, int k, int t
     seg(q.nl_off[k], q.D);
   }
 }
+// KDE k's info record (from registers) as flagged 8-byte words: (prep_publish_info below reads it back)
+__device__ __forceinline__ void prep_publish_vals(const PrepPub& q, const int32_t (&vals)[8], int k) {
+  for (int i = 0; i < 8; ++i)
+    __hip_atomic_store(q.ll + 8 * k + i, ((uint64_t)(uint32_t)q.seq << 32) | (uint32_t)vals[i], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // KDE k's info record (thread 0's own stores of prep_finish_one, read back by it) as flagged 8-byte words:
 // each carries the call's sequence number beside its value, so the host knows every word from the word itself
 // and no store has to wait for the others' acknowledgement (a completion word after an acknowledged record
@@ -474,13 +480,24 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
           hst[8 + 3 * k] = h;
         }
       }
-      uint32_t a[8];
+      // the eight |X'| maxima over the wave's 64 rows at once: every lane writes its eight, then lane (i, p)
+      // takes dim i's rows 8p..8p+7 and the 8 lanes of dim i combine by lane exchanges (eight serial wave
+      // reductions cost ~5k cycles per block); non-negative floats order as their bit patterns
+      __shared__ __align__(16) uint32_t vab[8][64];
+      const int ln = threadIdx.x & 63;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = wave_reduce_dpp(__float_as_uint(fabsf(v[i])), OpMax());
-      if ((threadIdx.x & 63) == 0)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (k0 + i < dc) atomicMax((unsigned int*)&Pw->xmax[k0 + i], a[i]);
+      for (int i = 0; i < 8; ++i) vab[i][ln] = __float_as_uint(fabsf(v[i]));
+      __syncthreads();
+      {
+        const int i = ln >> 3, p8 = ln & 7;
+        const uint4 q0 = *(const uint4*)&vab[i][8 * p8], q1 = *(const uint4*)&vab[i][8 * p8 + 4];
+        uint32_t mx = max(max(max(q0.x, q0.y), max(q0.z, q0.w)), max(max(q1.x, q1.y), max(q1.z, q1.w)));
+        mx = max(mx, lane_xor_u32(mx, 1, ln));
+        mx = max(mx, lane_xor_u32(mx, 2, ln));
+        mx = max(mx, lane_xor_u32(mx, 4, ln));
+        if (p8 == 0 && k0 + i < dc) atomicMax((unsigned int*)&Pw->xmax[k0 + i], mx);
+      }
+      __syncthreads();  // (vab is rewritten by the next eight dims)
     }
   }
 #pragma unroll 8
@@ -705,6 +722,33 @@ __device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool 
   info[7] = P->du_pad;
 }
 __device__ __forceinline__ void prep_finish_one(const PrepArgs& A, bool rebuild) { prep_finish_p(A.P, A.info, rebuild); }
+// The same from R, the table launch's LDS copy of the block (every field read here is final before that
+// launch), the rebuild's changes written to W, the record kept in vals: no global reads on the finishing
+// block's path (cmax2: the rebuild's maximum, read by the caller)
+__device__ __forceinline__ void prep_finish_lds(const KdeParams* R, KdeParams* W, int32_t* info, bool rebuild,
+                                                float cmax2, int32_t (&vals)[8]) {
+  int hmode = R->hmode, coarse = R->coarse_off;
+  if (rebuild) {
+    hmode = 0;
+    coarse = 0;
+    W->hmode = 0;
+    W->chunk_floats = chunk_floats(R->dc_pad, R->du_pad, R->kc, R->kc ? R->has_neg : 0);
+    W->cmax2 = cmax2;
+    W->cmax = cmax2;
+    W->coarse_off = 0;
+  }
+  vals[0] = R->has_neg | (R->kc << 1) | ((hmode != 0) << 4) | (R->exact_only << 5) | ((hmode == 2) << 6) |
+            ((hmode == 2 && coarse > 0) << 7);
+  vals[1] = R->nan_all;
+  vals[2] = R->unsupported;
+  vals[3] = R->dc;
+  vals[4] = R->du;
+  vals[5] = R->nconst;
+  vals[6] = R->dc_pad;
+  vals[7] = R->du_pad;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) info[i] = vals[i];
+}
 
 // pass 0: the layout the parameter kernel chose; pass 1: the f32 rebuild where it is needed (every
 // block of a KDE that needs none exits at once)
@@ -811,11 +855,12 @@ __global__ __launch_bounds__(64) void kde_table_kernel(PrepSet ps, float* table0
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (rebuild) P->cmax2 = __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prep_finish_one(A, rebuild);
+    const float cm2 = rebuild ? __hip_atomic_load(&P->cmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    int32_t vals[8];
+    prep_finish_lds(Pl, P, A.info, rebuild, cm2, vals);
+    // the refit's output block to the host (hbx_kde_refit_sync): the rest went out with the parameter launch
+    if (ps.pub.dst) prep_publish_vals(ps.pub, vals, second ? 1 : 0);
   }
-  // the refit's output block to the host (hbx_kde_refit_sync): the rest went out with the parameter launch
-  if (ps.pub.dst && threadIdx.x == 0) prep_publish_info(ps.pub, A, second ? 1 : 0);
   PSTAMP(13);
 }
 
