@@ -363,9 +363,10 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
                  for d in range(dc, D))
     bw_ok = bool(np.array_equal(bwg[b].cpu().numpy(), 1.06 * np.std(good_b, axis=0) * ng ** (-1. / (4 + D))) and
                  np.array_equal(bwb[b].cpu().numpy(), 1.06 * np.std(bad_b, axis=0) * nb ** (-1. / (4 + D))) and lev_ok)
-    # algorithmic HBM bytes: losses read (8) and the order written and read (16) per config, each KDE's rows
-    # read twice (mean pass, deviation pass) through the order: 2 (ng + nb) D 8 per bracket
-    fit_bytes = Bl * (24 * n + 2 * (ng + nb) * D * 8)
+    # algorithmic HBM bytes: losses read (8) and the order written and read (16) per config, each set's rows
+    # read ONCE: (ng + nb) D 8 per bracket (the deviation pass is a re-read a kernel holding the rows on chip
+    # would not make; the wave kernel makes it, profiles/r06/side/)
+    fit_bytes = Bl * (24 * n + (ng + nb) * D * 8)
     fit_gbs = fit_bytes / (ms_fit * 1e-3) / 1e9
     del X
     torch.cuda.empty_cache()
@@ -389,7 +390,7 @@ def config5(device, B=10_000, n=1_000, reps=10, rank=0, world=1, dist=None):
            "refit_bandwidths_spot_check": bw_ok,
            "refit_roofline": {"bound": "hbm", "achieved": fit_gbs, "peak": 8000.0, "unit": "GB/s",
                               "frac": fit_gbs / 8000.0, "bytes": fit_bytes,
-                              "basis": "losses 8 + order 16 per config, + 2 (n_good + n_bad) D 8 per bracket"},
+                              "basis": "losses 8 + order 16 per config, + (n_good + n_bad) D 8 per bracket: every row read once"},
            "cpu_reference_rule": {"s_for_all_brackets": cpu_s, "cores": 1,
                                   "sample": "%d brackets of numpy argsort(argsort) < k, x %d" % (nb_cpu, B)}}
     return out

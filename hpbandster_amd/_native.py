@@ -44,6 +44,7 @@ SIGNATURES = {
     "hbx_kde_refit_sync": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_double,
                                    ctypes.c_double, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                    c_vp, c_vp]),
+    "hbx_stream_order": (c_i32, [c_vp, c_vp]),
     "hbx_kde_logpdf": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "hbx_kde_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "hbx_kde_acquire": (c_i32, [c_vp, c_i64, c_i32, c_i64,

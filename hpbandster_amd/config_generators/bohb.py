@@ -169,12 +169,112 @@ def _draw_rvs(kde_good, levels, bw_factor, num_samples, R):
     return cands
 
 
+class _TruncnormTerms(object):
+    """The uniform-independent terms of scipy's ``truncnorm._ppf`` for one KDE's observation rows, filled
+    row by row as draws first pick them (a model serves every call until the next refit, and BOHB's datum is
+    one of its good rows: after a call or two every row is in).  Per (row, continuous dim), with a = -m/bw,
+    b = (1 - m)/bw (scipy 1.15 ``_continuous_distns.py``, ``truncnorm_gen._ppf`` / ``_log_gauss_mass``):
+    ``lp`` = log_ndtr(a) where a < 0 (``ppf_left``), log_ndtr(-b) otherwise (``ppf_right``); ``mass`` =
+    log1p(-ndtr(a) - ndtr(-b)), the central case of ``_log_gauss_mass``; ``ok`` False where that case does not
+    apply (b <= 0: a datum at the upper bound, a > 0, non-finite bounds) -- those elements take scipy's own
+    ``_ppf``."""
+
+    def __init__(self, data, bw):
+        self.data, self.bw = data, bw
+        n, D = data.shape
+        self.lp = np.empty((n, D))
+        self.mass = np.empty((n, D))
+        self.left = np.zeros((n, D), dtype=np.bool_)
+        self.ok = np.zeros((n, D), dtype=np.bool_)
+        self.have = np.zeros(n, dtype=np.bool_)
+
+    def fill(self, rows, cont):
+        import scipy.special as sc
+        r = np.unique(rows[~self.have[rows]])
+        if r.size:
+            m = self.data[np.ix_(r, cont)]
+            h = self.bw[cont]
+            with np.errstate(all="ignore"):  # (a zero bandwidth: no inversion is asked for that dim)
+                a, b = -m / h, (1 - m) / h
+                left = a < 0
+                self.lp[np.ix_(r, cont)] = sc.log_ndtr(np.where(left, a, -b))
+                self.mass[np.ix_(r, cont)] = sc.log1p(-sc.ndtr(a) - sc.ndtr(-b))
+            self.left[np.ix_(r, cont)] = left
+            self.ok[np.ix_(r, cont)] = (b > 0) & (a <= 0) & np.isfinite(a) & np.isfinite(b)
+            self.have[r] = True
+
+
+_LOG2 = [None]
+
+
+def _ppf_from_terms(q, lp, mass, left):
+    """scipy's truncnorm._ppf at uniforms q from the terms above, the same numpy / scipy.special ufuncs in the
+    same order: log_Phi_x = logsumexp([lp, log(q) + mass]) (log1p(-q) on the right), scipy 1.15's
+    ``_logsumexp`` for two real rows (the larger one taken out of the sum: (log1p(exp(lo - hi)) + log(m)) + hi,
+    m the number of rows equal to the larger), then ndtri_exp (negated on the right).  Elementwise, so a subset
+    gives the values the whole array would.  Non-finite log_Phi_x inputs come back as None positions
+    (``bad``) for scipy's own _ppf."""
+    import scipy.special as sc
+    if _LOG2[0] is None:
+        _LOG2[0] = np.log(np.array([1.0, 2.0]))
+    with np.errstate(all="ignore"):
+        x = np.where(left, np.log(q), np.log1p(-q)) + mass
+        hi = np.maximum(lp, x)
+        e0, e1 = lp == hi, x == hi
+        both = e0 & e1
+        lo = np.where(e0, x, lp)
+        s = np.where(both, 0.0, np.exp(lo - hi))
+        out = np.log1p(s) + np.where(both, _LOG2[0][1], _LOG2[0][0]) + hi
+        y = sc.ndtri_exp(out)
+    y = np.where(left, y, -y)
+    return y, ~np.isfinite(hi)
+
+
+_PPF = [None]
+
+
+def ppf_terms_ok():
+    """Once per process: _ppf_from_terms equals scipy's own truncnorm._ppf bit for bit over BOHB's range and its
+    edges (uniforms 0, tiny, near 1; a datum at 0 (a = -0: the right case), at 1 (b = 0: scipy's path), near the
+    bounds; narrow and wide bandwidths).  False (never raising) otherwise: the draws then invert through scipy's
+    _ppf, as before."""
+    if _PPF[0] is None:
+        ok = False
+        try:
+            rs = np.random.RandomState(17)
+            nr, nd = 200, 20
+            m = rs.rand(nr, nd)
+            m[:4] = 0.0
+            m[4:6] = 1.0
+            m[6:10] = rs.choice([1e-12, 1 - 1e-12, 1e-300, 0.5], (4, nd))
+            h = np.exp(rs.uniform(np.log(1e-4), np.log(5.0), nd))
+            q = rs.rand(nr, nd)
+            q[10:12] = 0.0
+            q[12:16] = rs.choice([1e-300, 1e-17, 1 - 2 ** -53, 0.5], (4, nd))
+            t = _TruncnormTerms(m, h)
+            t.fill(np.arange(nr), np.arange(nd))
+            with np.errstate(all="ignore"):
+                ref = sps.truncnorm._ppf(q, -m / h, (1 - m) / h)
+            y, bad = _ppf_from_terms(q, t.lp, t.mass, t.left)
+            use = t.ok & ~bad
+            ok = bool(use.sum() > nr * nd - 3 * nd) and np.array_equal(y[use].view(np.uint64),
+                                                                       ref[use].view(np.uint64))
+        except Exception:
+            ok = False
+        _PPF[0] = bool(ok)
+        if not ok:
+            logging.getLogger('hpbandster').warning(
+                "the truncnorm inversion terms disagree with scipy's truncnorm._ppf here: BOHB inverts through scipy")
+    return _PPF[0]
+
+
 def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt):
     """The same draws in one native call on R's own MT19937 state (hbx_bohb_draw, the reference's
-    consumption order), then ONE vectorised ``truncnorm._ppf`` over the call's uniforms and rvs's
-    ``* scale + loc`` -- the arithmetic rvs applies to each uniform, elementwise, so the values are the
-    per-element path's bit for bit (checked by host_draw_ok and tests/test_host_draw.py).  A domain error
-    raises ValueError with R left where scipy's raise leaves it."""
+    consumption order), then the truncnorm inversion of the call's uniforms and rvs's ``* scale + loc`` --
+    the arithmetic rvs applies to each uniform, elementwise, so the values are the per-element path's bit for
+    bit (checked by host_draw_ok and tests/test_host_draw.py).  The inversion reuses the model's per-row terms
+    (``_TruncnormTerms``; scipy's own ``truncnorm._ppf`` when ppf_terms_ok() fails and for the elements the
+    terms do not cover).  A domain error raises ValueError with R left where scipy's raise leaves it."""
     data = kde_good.data
     if not (isinstance(data, np.ndarray) and data.dtype == np.float64 and data.flags.c_contiguous):
         data = np.ascontiguousarray(data, dtype=np.float64)
@@ -184,21 +284,39 @@ def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt):
     vals = np.empty((num_samples, D))
     uni = np.empty((num_samples, D))
     need = np.empty((num_samples, D), dtype=np.uint8)
+    datum = np.empty(num_samples, dtype=np.int64)
     stop = ctypes.c_int64(-1)
     with mt.lock:
         rc = _native.lib().hbx_bohb_draw(mt.addr, data.ctypes.data, n, D, bws.ctypes.data, lv.ctypes.data,
                                          float(bw_factor), num_samples, vals.ctypes.data, uni.ctypes.data,
-                                         need.ctypes.data, None, ctypes.addressof(stop))
+                                         need.ctypes.data, datum.ctypes.data, ctypes.addressof(stop))
     if rc == 1:
         raise ValueError("Domain error in arguments (truncnorm bounds of candidate %d, dim %d; bohb.py:141)"
                          % divmod(stop.value, D))
     _native.check(rc)
     m = need.view(np.bool_)
-    if m.any():
-        h = np.broadcast_to(bws, (num_samples, D))[m]
-        loc = vals[m]
+    if not m.any():
+        return vals
+    h = np.broadcast_to(bws, (num_samples, D))[m]
+    loc = vals[m]
+    if ppf_terms_ok():
+        t = getattr(kde_good, "_tn_terms", None)
+        if t is None or t.data is not data or t.bw is not bws or t.lp.shape != (n, D):
+            t = _TruncnormTerms(data, bws)
+            try:
+                kde_good._tn_terms = t
+            except AttributeError:  # (an object that takes no attributes: terms for this call only)
+                pass
+        t.fill(datum, np.flatnonzero(lv == 0))
+        ri, di = np.nonzero(m)
+        rr = datum[ri]
+        y, bad = _ppf_from_terms(uni[m], t.lp[rr, di], t.mass[rr, di], t.left[rr, di])
+        rest = bad | ~t.ok[rr, di]
+        if rest.any():
+            y[rest] = sps.truncnorm._ppf(uni[m][rest], -loc[rest] / h[rest], (1 - loc[rest]) / h[rest])
+    else:
         y = sps.truncnorm._ppf(uni[m], -loc / h, (1 - loc) / h)
-        vals[m] = y * (bw_factor * h) + loc
+    vals[m] = y * (bw_factor * h) + loc
     return vals
 
 
@@ -390,10 +508,14 @@ class BOHB(base_config_generator):
         if host_draw_ok():
             mt = _global_mt() if rng is None else getattr(self, "_rng_mt", (None, None))[1]
             if mt is None or mt.rs is not R:
-                mt = _MT(R)
-                if rng is not None:
+                try:
+                    mt = _MT(R)
+                except (TypeError, AttributeError):  # a legacy RandomState over another bit generator (PCG64 ...)
+                    mt = None
+                if rng is not None and mt is not None:
                     self._rng_mt = (R, mt)
-            return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt)
+            if mt is not None:
+                return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt)
         return _draw_rvs(kde_good, self.vartypes, self.bw_factor, num_samples, R)
 
     def draw_candidates(self, pair, num_samples):
@@ -527,6 +649,8 @@ class BOHB(base_config_generator):
         lvd = _levels_on_device(lvb, self._lv_np, g.device)
         cands, datum, err, ws = keep
         sh = pair._raw_stream(pair._dev_index)
+        if sh != pair._home:
+            pair._order(sh)
         _native.check(L.hbx_kde_sample(g.X_dev.data_ptr(), g.k_vars, g.rows_dev.data_ptr(), g.nobs,
                                        g.params.data_ptr() + self._bw_off, lvd.data_ptr(), None, float(self.bw_factor),
                                        int(self.sampler_seed) & (2 ** 64 - 1), int(counter) & (2 ** 64 - 1), 0, n,

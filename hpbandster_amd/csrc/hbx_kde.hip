@@ -18,6 +18,7 @@
 #include <string.h>
 #include <stddef.h>
 
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -75,16 +76,19 @@ struct PrepArgs {
   int32_t nblk_table;   // blocks of this KDE in the table launches
   uint32_t vt[HBX_MAX_D / 32];  // bit d: dim d categorical ('u')
 };
-// The refit's output block published to device-mapped host memory by the preparation's finishing blocks
-// (hbx_kde_refit_sync): the split's rows (KDE 0's block), each KDE's bandwidths, level counts and info record,
-// then the info records as flagged words; dst == nullptr: nothing published
+// The refit's output block published to device-mapped host memory (hbx_kde_refit_sync), every 32-bit word of it
+// as one flagged 8-byte word (seq << 32 | word): the split's rows (n words: indices < 2^31), each KDE's
+// bandwidths (2 D words: the doubles' low then high halves) and level counts (D words) by the parameter
+// launch, then the two info records (16 words, `ll`) by the finishing blocks.  The host accepts a word only when
+// it carries the call's sequence number, so it needs no ordering between the launches' stores and the host
+// (dst == nullptr: nothing published)
 struct PrepPub {
-  uint32_t* dst;        // mapped host copy of the output block (same word offsets as src)
+  uint64_t* dst;        // mapped flagged words: order [0, n), bw KDE k [n + 2 D k, + 2 D), nlev KDE k [n + 4 D + D k, + D)
   const uint32_t* src;  // the device output block
-  uint64_t* ll;         // the two info records as 16 flagged words: seq << 32 | word (no completion word)
+  uint64_t* ll;         // the two info records as 16 flagged words
   int32_t seq;
-  int32_t order_words;  // 2 n
-  int32_t bw_off[2], nl_off[2], info_off[2];  // word offsets of KDE k's pieces
+  int32_t n;            // rows of the split
+  int32_t bw_off[2], nl_off[2], info_off[2];  // word offsets of KDE k's pieces in src
   int32_t D;
 };
 struct PrepSet {
@@ -94,22 +98,20 @@ struct PrepSet {
 };
 
 // The split's rows (KDE 0) and KDE k's bandwidths and level counts -- written by the launches before the
-// parameter launch -- published by the parameter launch's block k (thread t of nt), 8-byte words: the rows
+// parameter launch -- published by the parameter launch's block k (thread t of nt) as flagged words: the rows
 // of a 400-observation refit are ~2 stores per thread, not 14 dependent load/store pairs of one wave
 __device__ __forceinline__ void prep_publish_rows(const PrepPub& q, int k, int t, int nt) {
-  auto seg = [&](int off, int words) {  // (even offsets and counts: 8-byte pieces of the layout)
-    const uint64_t* src = (const uint64_t*)(q.src + off);
-    uint64_t* dst = (uint64_t*)(q.dst + off);
-    for (int i = t; i < words / 2; i += nt)
-      __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t tag = (uint64_t)(uint32_t)q.seq << 32;
+  auto put = [&](int64_t i, uint32_t w) {
+    __hip_atomic_store(q.dst + i, tag | w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   };
-  if (k == 0) seg(0, q.order_words);
-  seg(q.bw_off[k], 2 * q.D);
-  if ((q.nl_off[k] | q.D) & 1) {
-    for (int i = t; i < q.D; i += nt) hbx_publish_store(q.dst + q.nl_off[k] + i, q.src[q.nl_off[k] + i]);
-  } else {
-    seg(q.nl_off[k], q.D);
+  if (k == 0) {
+    const int64_t* order = (const int64_t*)q.src;  // (the order sits at word 0 of the block)
+    for (int i = t; i < q.n; i += nt) put(i, (uint32_t)order[i]);
   }
+  const int64_t bw0 = (int64_t)q.n + 2 * (int64_t)q.D * k, nl0 = (int64_t)q.n + 4 * (int64_t)q.D + (int64_t)q.D * k;
+  for (int i = t; i < 2 * q.D; i += nt) put(bw0 + i, q.src[q.bw_off[k] + i]);
+  for (int i = t; i < q.D; i += nt) put(nl0 + i, q.src[q.nl_off[k] + i]);
 }
 // KDE k's info record (from registers) as flagged 8-byte words: (prep_publish_info below reads it back)
 __device__ __forceinline__ void prep_publish_vals(const PrepPub& q, const int32_t (&vals)[8], int k) {
@@ -120,8 +122,9 @@ __device__ __forceinline__ void prep_publish_vals(const PrepPub& q, const int32_
 // KDE k's info record (thread 0's own stores of prep_finish_one, read back by it) as flagged 8-byte words:
 // each carries the call's sequence number beside its value, so the host knows every word from the word itself
 // and no store has to wait for the others' acknowledgement (a completion word after an acknowledged record
-// cost ~12k cycles of round trip to host memory).  The parameter launch's words were acknowledged before
-// that launch ended, so they are in place too.
+// cost ~12k cycles of round trip to host memory).  The host reads the block only once the flags match AND
+// the stream has completed (hbx_kde_refit_sync), so the parameter launch's unflagged words come from launches
+// that have ended.
 __device__ __forceinline__ void prep_publish_info(const PrepPub& q, const PrepArgs& A, int k) {
   for (int i = 0; i < 8; ++i)
     __hip_atomic_store(q.ll + 8 * k + i, ((uint64_t)(uint32_t)q.seq << 32) | (uint32_t)A.info[i], __ATOMIC_RELAXED,
@@ -2354,85 +2357,143 @@ int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const
 
 }  // extern "C"
 
-// this thread's device-mapped coherent host buffer for refit output blocks (grown on demand, kept for the
-// thread's lifetime): `cap` bytes of data, then two completion words
-static int wait_done(int32_t* done, int32_t seq, hipStream_t s, const char* who);
-thread_local char* t_refit_mapped = nullptr;
-thread_local int64_t t_refit_cap = 0;
-thread_local int32_t t_refit_seq = 0;
-static int refit_mapped_buffer(int64_t bytes, char** out) {
-  if (bytes > t_refit_cap) {
-    int64_t cap = t_refit_cap > 0 ? t_refit_cap : 16384;
-    while (cap < bytes) cap *= 2;
-    void* p = nullptr;
-    HBX_HIP(hipHostMalloc(&p, (size_t)cap + 256, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
-    void* dp = nullptr;
-    HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
-    if (dp != p) {
-      (void)hipHostFree(p);
-      return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
-    }
-    if (t_refit_mapped) {  // (a call that failed after its launches may still have words in flight)
-      HBX_HIP(hipDeviceSynchronize());
-      (void)hipHostFree(t_refit_mapped);
-    }
-    t_refit_mapped = (char*)p;
-    t_refit_cap = cap;
-    for (int i = 0; i < 16; ++i) ((volatile uint64_t*)(t_refit_mapped + cap))[i] = 0;  // flagged info words
+// Device-mapped coherent host buffers for refit output blocks: `cap` bytes of data, then the 16 flagged info
+// words.  A thread holds one while it refits (grown on demand); when the thread ends, its buffer goes back to a
+// process-wide pool for the next thread (no HIP call from a thread-exit destructor, no pinned memory lost per
+// short-lived result thread).  The sequence number travels with the buffer, so a pooled buffer's old flags
+// never match a new owner's next call.
+struct RefitMapped {
+  char* p = nullptr;
+  int64_t cap = 0;
+  int32_t seq = 0;
+  bool pending = false;  // a call failed with its launches possibly still writing into the buffer
+};
+static std::mutex* refit_pool_mu = new std::mutex;                       // never destroyed: thread exits at
+static std::vector<RefitMapped>* refit_pool = new std::vector<RefitMapped>;  // process end may still return buffers
+struct RefitMappedHolder {
+  RefitMapped b;
+  ~RefitMappedHolder() {
+    if (b.p && !b.pending) {
+      std::lock_guard<std::mutex> g(*refit_pool_mu);
+      refit_pool->push_back(b);
+    }  // (a pending buffer is left to the process: its words may still be in flight)
   }
-  *out = t_refit_mapped;
+};
+thread_local RefitMappedHolder t_refit;
+static int refit_mapped_buffer(int64_t bytes, RefitMapped** out) {
+  RefitMapped& b = t_refit.b;
+  if (b.pending) {  // the last call failed after its launches: let them land before the buffer is reused
+    HBX_HIP(hipDeviceSynchronize());
+    b.pending = false;
+  }
+  if (bytes > b.cap) {
+    RefitMapped nb;
+    {
+      std::lock_guard<std::mutex> g(*refit_pool_mu);
+      for (size_t i = 0; i < refit_pool->size(); ++i)
+        if ((*refit_pool)[i].cap >= bytes) {
+          nb = (*refit_pool)[i];
+          refit_pool->erase(refit_pool->begin() + i);
+          break;
+        }
+    }
+    if (!nb.p) {
+      int64_t cap = b.cap > 0 ? b.cap : 16384;
+      while (cap < bytes) cap *= 2;
+      void* p = nullptr;
+      HBX_HIP(hipHostMalloc(&p, (size_t)cap + 256, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+      void* dp = nullptr;
+      HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
+      if (dp != p) {
+        (void)hipHostFree(p);
+        return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+      }
+      nb.p = (char*)p;
+      nb.cap = cap;
+      for (int i = 0; i < 16; ++i) ((volatile uint64_t*)(nb.p + cap))[i] = 0;  // flagged info words
+    }
+    if (b.p) {  // the smaller buffer (every call on it completed) back to the pool
+      std::lock_guard<std::mutex> g(*refit_pool_mu);
+      refit_pool->push_back(b);
+    }
+    b = nb;
+  }
+  *out = &b;
   return HBX_OK;
 }
 
 extern "C" {
 
 // hbx_kde_refit_host_rows, then the output block in host memory (out_host, hbx_kde_refit_out_bytes) when the
-// call returns: the preparation's launches publish it to a device-mapped host buffer (the parameter launch the
-// rows, bandwidths and level counts, the finishing blocks the info records as flagged words), and the call
-// spins on those flags -- no copy launch, no blocking stream
-// synchronisation (bounded: then the stream is synchronised and the words checked)
+// call returns: the preparation's launches publish it to a device-mapped host buffer, every 32-bit word as a
+// flagged word carrying the call's sequence number (the parameter launch the rows, bandwidths and level counts,
+// the finishing blocks the info records; PrepPub), and the call spins until every word carries it -- no copy
+// launch, no stream synchronisation, and no reliance on the order in which the launches' stores reach the host
+// (bounded spin: then the stream is synchronised and the words checked once more).  The prepared parameter
+// blocks and tables are complete for work on the refit's stream; another stream orders itself after the refit
+// with hbx_stream_order (KDEPair does it when the calling stream is not the refit's)
 int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
                        const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
                        double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
                        void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
                        int64_t scratch_bytes, void* stream, void* out_host) {
   if (!out_host) return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit_sync: null host output");
-  const int64_t bytes = (int64_t)refit_out_layout(n, D).total;
-  char* mapped = nullptr;
-  int rc = refit_mapped_buffer(bytes, &mapped);
+  if (n < 1 || n > INT32_MAX || D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_refit_sync: n, D");
+  const int64_t words = n + 6 * (int64_t)D;  // flagged words before the info records
+  RefitMapped* mb = nullptr;
+  int rc = refit_mapped_buffer(8 * words, &mb);
   if (rc) return rc;
-  uint64_t* ll = (uint64_t*)(mapped + t_refit_cap);
-  const int32_t seq = t_refit_seq = t_refit_seq == INT32_MAX ? 1 : t_refit_seq + 1;
+  uint64_t* w = (uint64_t*)mb->p;
+  uint64_t* ll = (uint64_t*)(mb->p + mb->cap);
+  const int32_t seq = mb->seq = mb->seq == INT32_MAX ? 1 : mb->seq + 1;
   PrepPub pub;
   memset(&pub, 0, sizeof(pub));
-  pub.dst = (uint32_t*)mapped;
+  pub.dst = w;
   pub.ll = ll;
   pub.seq = seq;
+  mb->pending = true;
   rc = refit_impl(X, loss, n, D, vartype, staged_host, true, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
                   table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
                   stream, &pub);
   if (rc) return rc;
-  // spin until all 16 flagged info words carry this call's sequence number (bounded: ~0.1 s, then the stream
-  // is synchronised and the words checked once more)
-  auto all_in = [&]() {
-    for (int i = 0; i < 16; ++i)
-      if ((int32_t)(__atomic_load_n(ll + i, __ATOMIC_ACQUIRE) >> 32) != seq) return false;
+  auto tagged = [&](const uint64_t* p, int64_t cnt) {
+    for (int64_t i = 0; i < cnt; ++i)
+      if ((int32_t)(__atomic_load_n(p + i, __ATOMIC_ACQUIRE) >> 32) != seq) return false;
     return true;
   };
+  // the info records come last: spin on them, then every other word (bounded: ~0.1 s, then the stream is
+  // synchronised and every word checked once more)
   bool seen = false;
-  for (int64_t i = 0; i < 5000000 && !seen; ++i) seen = all_in();
+  for (int64_t i = 0; i < 5000000 && !seen; ++i) seen = tagged(ll, 16) && tagged(w, words);
   if (!seen) {
     HBX_HIP(hipStreamSynchronize((hipStream_t)stream));
-    if (!all_in()) return hbx_fail(HBX_ERR_HIP, "hbx_kde_refit_sync: the device did not publish its info records");
+    if (!tagged(ll, 16) || !tagged(w, words))
+      return hbx_fail(HBX_ERR_HIP, "hbx_kde_refit_sync: the device did not publish the output block");
   }
-  memcpy(out_host, mapped, (size_t)bytes);
+  mb->pending = false;
   const RefitOut o = refit_out_layout(n, D);
+  int64_t* order = (int64_t*)out_host;
+  for (int64_t i = 0; i < n; ++i) order[i] = (int64_t)(uint32_t)w[i];
+  uint32_t* rest = (uint32_t*)((char*)out_host + o.bw_good);  // bw good | bw bad | nlev good | nlev bad
+  for (int64_t j = 0; j < 6 * (int64_t)D; ++j) rest[j] = (uint32_t)w[n + j];
   for (int k = 0; k < 2; ++k)
     for (int i = 0; i < 8; ++i)
       ((int32_t*)((char*)out_host + (k ? o.info_bad : o.info_good)))[i] = (int32_t)(uint32_t)ll[8 * k + i];
   const int32_t* nl = (const int32_t*)((const char*)out_host + o.nlev_good);  // good then bad
   for (int32_t d = 0; d < 2 * D; ++d)
     if (nl[d] < 0) return hbx_fail(HBX_ERR_ARG, "categorical codes must be integers in [0, 1024)");
+  return HBX_OK;
+}
+
+// Order stream `waiter` after everything enqueued on stream `signaller` so far (an event recorded on the
+// signaller, waited for by the waiter; no host wait): a model refit or prepared on one stream and used from
+// another (KDEPair / DeviceKDE call it when the calling stream is not the model's)
+int hbx_stream_order(void* waiter, void* signaller) {
+  if (waiter == signaller) return HBX_OK;
+  thread_local hipEvent_t ev = nullptr;
+  if (!ev) HBX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HBX_HIP(hipEventRecord(ev, (hipStream_t)signaller));
+  HBX_HIP(hipStreamWaitEvent((hipStream_t)waiter, ev, 0));
   return HBX_OK;
 }
 
@@ -2475,7 +2536,7 @@ static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32
   if (pub) {  // the finishing blocks publish the output block (word offsets of the layout above)
     ps.pub = *pub;
     ps.pub.src = (const uint32_t*)out;
-    ps.pub.order_words = (int32_t)(2 * n);
+    ps.pub.n = (int32_t)n;
     ps.pub.bw_off[0] = (int32_t)(o.bw_good / 4);
     ps.pub.bw_off[1] = (int32_t)(o.bw_bad / 4);
     ps.pub.nl_off[0] = (int32_t)(o.nlev_good / 4);
@@ -3074,12 +3135,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
   }
   double S[CPT];
   float s4[CPT];
+  bool ref0[CPT];  // chunk 0 had a finite term: the bound's reference point (S' >= 1/2) holds
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     S[c] = 0.0;
     s4[c] = 0.f;
-    // an integer reference point (rescales are exact ldexps); no finite term in chunk 0 (or NaN): any
-    m[c] = m[c] > -INFINITY ? ceilf(m[c]) : 0.f;
+    // an integer reference point (rescales are exact ldexps); no finite term in chunk 0 (or NaN): m = 0, and
+    // the candidate goes to the fp64 pass (the bound assumes a term at or above m - 1)
+    ref0[c] = m[c] > -INFINITY;
+    m[c] = ref0[c] ? ceilf(m[c]) : 0.f;
   }
   for (int cc = 0; cc < nch; ++cc) {
     const int b = cc & 1;
@@ -3150,7 +3214,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     const double lnS = log(S[c]) + (double)m[c] * 0.69314718055994531;
     const double lp = lnS + log_c * 0.69314718055994531 + P->log_norm;
     const double bound = rel / (1.0 - rel) + 0x1p-50 * fabs(lp);
-    const bool ok = valid[c] && S[c] > 0.0 && lp - lp == 0.0 && rel < 0.5 && bound <= 0.99 * rtol * fmax(1.0, fabs(lp));
+    const bool ok = valid[c] && ref0[c] && S[c] > 0.0 && lp - lp == 0.0 && rel < 0.5 && bound <= 0.99 * rtol * fmax(1.0, fabs(lp));
     if (ok) out[cid[c]] = lp;
     to_list(valid[c] && !ok, cid[c]);
   }

@@ -137,10 +137,11 @@ class DeviceKDE(object):
     reads ``.data``, ``.bw`` and ``.pdf``); ``pdf`` evaluates the exact fp64 density on the GPU.
     """
 
-    def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None, prepared=None):
+    def __init__(self, X_dev, rows_dev, var_type, bw, nlev, data_host, stream=None, prepared=None, home=None):
         """Prepare a KDE for scoring with ``hbx_kde_prepare`` -- or, with ``prepared`` = (params, table,
-        info) from ``hbx_kde_refit``, wrap an already prepared one.  ``data_host``: the observation rows
-        (n x D), or a pair (host rows, row indices) gathered on first use of ``.data``."""
+        info) from ``hbx_kde_refit``, wrap an already prepared one (``home``: the stream it was prepared on).
+        ``data_host``: the observation rows (n x D), or a pair (host rows, row indices) gathered on first use of
+        ``.data``.  Work on another stream is ordered after the preparation first (``_order``)."""
         self.var_type = var_type
         self.k_vars = len(var_type)
         self.bw = np.asarray(bw, dtype=np.float64)
@@ -163,11 +164,14 @@ class DeviceKDE(object):
                 info = np.zeros(8, dtype=np.int32)
                 bw_c = np.ascontiguousarray(self.bw)
                 nlev_c = np.ascontiguousarray(self.nlev)
+                home = N.stream_handle(stream, self.device)
                 N.check(L.hbx_kde_prepare(N.ptr(X_dev), D, N.ptr(rows_dev), self.nobs, N.ptr(vt), N.ptr(bw_c),
                                           N.ptr(nlev_c), N.ptr(self.params), N.ptr(self.table), self.table.numel(),
-                                          N.ptr(info), N.stream_handle(stream, self.device)))
+                                          N.ptr(info), home))
         else:
             self.params, self.table, info = prepared
+        self._home = home        # the stream the parameter block and table were written on
+        self._ordered = set()    # other streams already ordered after that
         self.variant, self.nan_all, unsupported, self.dc, self.du, self.nconst, self.dc_pad, self.du_pad = \
             info.tolist()
         self.has_neg, self.kc = self.variant & 1, (self.variant >> 1) & 7
@@ -182,6 +186,15 @@ class DeviceKDE(object):
             src, idx = self._data
             self._data = src[idx]
         return self._data
+
+    def _order(self, sh):
+        """Order stream ``sh`` after this model's preparation when it is not the stream that prepared it (once per
+        stream: hbx_stream_order, no host wait)."""
+        h = self._home
+        if h is None or sh == h or sh in self._ordered:
+            return
+        N.check(N.lib().hbx_stream_order(sh, h))
+        self._ordered.add(sh)
 
     def pdf(self, data_predict=None, stream=None):
         """Exact fp64 pdf on the GPU (KDEMultivariate.pdf semantics, np.squeeze'd)."""
@@ -199,9 +212,11 @@ class DeviceKDE(object):
             out = torch.empty(pts.shape[0], dtype=torch.float64, device=self.device)
             sb = int(L.hbx_kde_pdf_scratch_bytes(self.nobs))
             scratch = torch.empty(sb, dtype=torch.uint8, device=self.device)
+            sh = N.stream_handle(stream, self.device)
+            self._order(sh)
             N.check(L.hbx_kde_pdf_exact(N.ptr(p_dev), pts.shape[0], self.k_vars, N.ptr(self.params),
                                         N.ptr(self.X_dev), N.ptr(self.rows_dev), self.nobs, N.ptr(out), N.ptr(scratch),
-                                        sb, N.stream_handle(stream, self.device)))
+                                        sb, sh))
             return np.squeeze(out.cpu().numpy())
 
     def sample(self, levels, bw_factor, Nc, seed, counter_base, stream_id=0, stream=None, table=None, out=None):
@@ -218,6 +233,7 @@ class DeviceKDE(object):
         L = N.lib()
         D = self.k_vars
         sh = N.stream_handle(stream, self.device)
+        self._order(sh)
         # the bandwidths the sampler reads: the prepared parameter block's own fp64 bw[D] (bit-identical
         # to self.bw, which was read back from it) -- no upload per refit
         bw_ptr = N.ptr(self.params) + int(L.hbx_kde_param_bw_offset())
@@ -270,10 +286,11 @@ class DeviceKDE(object):
             out = torch.empty(Nc, dtype=torch.float64, device=self.device)
             sb = int(L.hbx_kde_logpdf_rtol_scratch_bytes(Nc))
             scr = torch.empty(sb, dtype=torch.uint8, device=self.device)
+            sh = N.stream_handle(stream, self.device)
+            self._order(sh)
             N.check(L.hbx_kde_logpdf_rtol(N.ptr(c_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
                                           N.ptr(self.X_dev), N.ptr(self.rows_dev), self.dc_pad, self.du_pad,
-                                          self.variant, float(rtol), N.ptr(out), N.ptr(scr), sb,
-                                          N.stream_handle(stream, self.device)))
+                                          self.variant, float(rtol), N.ptr(out), N.ptr(scr), sb, sh))
             return out.cpu().numpy()
 
     def _logpdf_exact(self, C, stream):
@@ -285,9 +302,10 @@ class DeviceKDE(object):
             with N.on_device(self.device, stream):
                 p_dev = torch.from_numpy(np.ascontiguousarray(C)).to(self.device)
                 o = torch.empty(C.shape[0], dtype=torch.float64, device=self.device)
+                sh = N.stream_handle(stream, self.device)
+                self._order(sh)
                 N.check(L.hbx_kde_logpdf_exact(N.ptr(p_dev), C.shape[0], self.k_vars, N.ptr(self.params),
-                                               N.ptr(self.X_dev), N.ptr(self.rows_dev), N.ptr(o),
-                                               N.stream_handle(stream, self.device)))
+                                               N.ptr(self.X_dev), N.ptr(self.rows_dev), N.ptr(o), sh))
                 return o.cpu().numpy()
         exact = np.atleast_1d(self.pdf(C, stream=stream))
         with np.errstate(divide="ignore", invalid="ignore"):
@@ -300,9 +318,10 @@ class DeviceKDE(object):
         Nc = int(cand_dev.shape[0])
         with N.on_device(self.device, stream):
             est = torch.empty((Nc, 4), dtype=torch.float32, device=self.device)
+            sh = N.stream_handle(stream, self.device)
+            self._order(sh)
             N.check(L.hbx_kde_logpdf(N.ptr(cand_dev), Nc, self.k_vars, N.ptr(self.params), N.ptr(self.table),
-                                     self.dc_pad, self.du_pad, self.variant, N.ptr(est),
-                                     N.stream_handle(stream, self.device)))
+                                     self.dc_pad, self.du_pad, self.variant, N.ptr(est), sh))
             e = est.cpu().numpy()
         return e[:, 0], e[:, 1], e[:, 2]
 
@@ -351,6 +370,7 @@ class KDEPair(object):
                           self.nmax)
         self._wsb = {}
         self._roff = None
+        self._home = good._home if good._home == bad._home else None  # (None: each KDE checks for itself)
         # the synchronous fast path's constants (acquire: a call on the model's own device)
         dev = good.device
         self._dev_index = dev.index if dev.index is not None else _torch().cuda.current_device()
@@ -383,6 +403,12 @@ class KDEPair(object):
 
     def keys(self):
         return ["good", "bad"]
+
+    def _order(self, sh):
+        """Order stream ``sh`` after both KDEs' preparation (DeviceKDE._order) unless it is their stream."""
+        if sh != self._home:
+            self.good._order(sh)
+            self.bad._order(sh)
 
     def result_offset(self):
         """Byte offset of the AcqResult record inside an acquisition workspace."""
@@ -448,13 +474,15 @@ class KDEPair(object):
         if n < wsb:
             raise N.HbxError("workspace too small")
         rec = _record_buffer()
+        sh = self._raw_stream(self._dev_index)
+        if sh != self._home:
+            self._order(sh)
         if events is None and self._bound:
-            N.check(self._bound_fn(self._bound, cands.data_ptr(), Nc, int(index_base), workspace.data_ptr(), n,
-                                   self._raw_stream(self._dev_index), rec))
+            N.check(self._bound_fn(self._bound, cands.data_ptr(), Nc, int(index_base), workspace.data_ptr(), n, sh,
+                                   rec))
         else:
             N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
-                                  events.address if events is not None else None,
-                                  self._raw_stream(self._dev_index), rec))
+                                  events.address if events is not None else None, sh, rec))
         return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):
@@ -478,18 +506,19 @@ class KDEPair(object):
         logl = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         logg = torch.empty(Nc, dtype=torch.float32, device=dev) if logs else None
         wsp = ws.data_ptr()
+        sh = N.stream_handle(stream, dev)
+        self._order(sh)
         if sync and not logs:  # one native call: the acquisition and its record on the host
             rec = _record_buffer()
             N.check(L.hbx_kde_acquire_host(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args, wsp,
-                                           ws.numel(), events.address if events is not None else None,
-                                           N.stream_handle(stream, dev), rec))
+                                           ws.numel(), events.address if events is not None else None, sh, rec))
             res = AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
             if ties == "process" and res.flags & ACQ_NEAR_TIE:
                 self._resolve(res, ws, Nc, Nc, cands if isinstance(cands, np.ndarray) else c_dev, int(index_base))
             return res
         N.check(L.hbx_kde_acquire(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args,
                                   N.ptr(logl), N.ptr(logg), wsp, ws.numel(),
-                                  events.address if events is not None else None, N.stream_handle(stream, dev)))
+                                  events.address if events is not None else None, sh))
         if self._roff is None:
             self._roff = int(L.hbx_kde_result_ptr(wsp)) - wsp
         off = self._roff
@@ -545,10 +574,11 @@ class KDEPair(object):
         if not self._bound:
             raise N.HbxError("acquire_ahead needs the bound pair entry")
         with N.on_device(self.good.device):
+            sh = N.stream_handle(None, self.good.device)
+            self._order(sh)
             N.check(N.lib().hbx_kde_acquire_ahead(self._bound, cands.data_ptr(), int(cands.shape[0]),
                                                   workspace.data_ptr(), workspace.numel(),
-                                                  err.data_ptr() if err is not None else None, out, int(seq),
-                                                  N.stream_handle(None, self.good.device)))
+                                                  err.data_ptr() if err is not None else None, out, int(seq), sh))
 
     def batch_workspace_bytes(self, Nc, seg):
         return int(N.lib().hbx_kde_batch_workspace_bytes(int(Nc), int(seg), self.nmax))
@@ -587,11 +617,13 @@ class KDEPair(object):
         if out.numel() < B * RESULT_BYTES:
             raise N.HbxError("result buffer too small")
         g, b = self.good, self.bad
+        sh = N.stream_handle(stream, dev)
+        self._order(sh)
         N.check(L.hbx_kde_acquire_batch(N.ptr(c_dev), Nc, seg, D, 0,
                                         N.ptr(g.params), N.ptr(g.table), N.ptr(g.X_dev), N.ptr(g.rows_dev), g.variant,
                                         N.ptr(b.params), N.ptr(b.table), N.ptr(b.X_dev), N.ptr(b.rows_dev), b.variant,
                                         g.dc_pad, g.du_pad, self.nmax, None, None, N.ptr(out), N.ptr(ws), ws.numel(),
-                                        N.stream_handle(stream, dev)))
+                                        sh))
         if not sync:
             return out[:B * RESULT_BYTES]
         raw = fetch_bytes(out[:B * RESULT_BYTES], stream)
@@ -815,9 +847,9 @@ class ObservationStore(object):
         order = blk[:8 * n].view(torch.int64)
         X_dev = self.X_dev
         good = DeviceKDE(X_dev, order[:n_good], self.var_type, bw_gh, nl_gh, (X_host, order_h[:n_good]),
-                         prepared=(pg, tg, info_g))
+                         prepared=(pg, tg, info_g), home=sh)
         bad = DeviceKDE(X_dev, order[n - n_bad:], self.var_type, bw_bh, nl_bh, (X_host, order_h[n - n_bad:]),
-                        prepared=(pbad, tb, info_b))
+                        prepared=(pbad, tb, info_b), home=sh)
         pair = KDEPair(good, bad)
         pair._keep = (blk,)  # the rows tensors are views of the refit's block
         return pair

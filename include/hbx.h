@@ -115,16 +115,20 @@ int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const
                             void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
                             int64_t scratch_bytes, void* stream);
 /* hbx_kde_refit_host_rows, synchronous: when the call returns, `out_host` (host memory,
- * hbx_kde_refit_out_bytes) holds the output block.  The preparation's finishing workgroups publish it to a
- * device-mapped host buffer, the info records as words flagged with the call's sequence number, and the call
- * spins on those flags (no copy
- * launch, no blocking stream synchronisation).  The drop-in's ObservationStore.refit calls this one
+ * hbx_kde_refit_out_bytes) holds the output block.  The preparation's launches publish it to a device-mapped
+ * host buffer, every 32-bit word as an 8-byte word flagged with the call's sequence number, and the call spins
+ * until every word carries it (no copy launch, no blocking stream synchronisation).  The prepared models are
+ * complete for work enqueued on `stream` afterwards; work on ANOTHER stream must first be ordered after the
+ * refit (hbx_stream_order(other, stream)).  The drop-in's ObservationStore.refit calls this one
  * (bohb.py:211-251, one new_result per call). */
 int hbx_kde_refit_sync(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
                        const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
                        double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
                        void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
                        int64_t scratch_bytes, void* stream, void* out_host);
+/* Order stream `waiter` after all work enqueued on `signaller` so far (event record + stream wait, no host
+ * wait): a model refit / prepared on one stream, used from another. */
+int hbx_stream_order(void* waiter, void* signaller);
 
 /* ---- KDE model preparation ----------------------------------------------------------------- */
 /* Template bucket of the scoring kernel for dc continuous / du categorical dims

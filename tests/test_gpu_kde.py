@@ -635,6 +635,37 @@ def test_capi_logpdf_rtol_contract(device, case, rtol):
         assert err.max() <= max(rtol, 2e-12), (case, err.max())
 
 
+def test_dd_pass_no_finite_term_in_first_chunk(device):
+    """A categorical bandwidth of exactly 1 (the Aitchison-Aitken match factor 1 - h is 0) with the first 64
+    observations all matching the candidates in that dim: chunk 0 of the direct-difference pass has no finite
+    term, so its reference point is not a term of the sum and the bound does not hold; those candidates take the
+    fp64 pass, and every ln pdf meets the contract."""
+    from hpbandster_amd import kde
+    rs = np.random.RandomState(31)
+    n, dc = 400, 8
+    vt = "c" * dc + "uu"
+    X = np.empty((n, dc + 2))
+    X[:, :dc] = rs.rand(n, dc)
+    X[:64, dc] = 1.0                             # chunk 0: every row matches the candidates' code 1 ...
+    X[64:, dc] = 2.0 * rs.randint(0, 2, n - 64)  # ... and no later row does
+    X[:, dc + 1] = rs.randint(0, 3, n)
+    C = rs.rand(96, dc + 2)
+    C[:, dc] = 1.0
+    C[:, dc + 1] = rs.randint(0, 3, 96)
+    rows = np.arange(n)
+    bw = np.r_[np.full(dc, 0.2), 1.0, 0.3]
+    nlev = np.r_[np.zeros(dc, dtype=np.int32), 3, 3].astype(np.int32)
+    pair = kde.fit_pair_from_rows(X, rows, rows, vt, bw, bw, nlev, nlev, device=device)
+    k = pair.good
+    lref = O.log_pdf_many(X, bw, vt, C, nlev)
+    for rtol in (1e-5, 1e-7):
+        got = _capi_logpdf_rtol(k, C, rtol=rtol)
+        fin = np.isfinite(lref)
+        assert fin.all()
+        err = np.abs(got - lref) / np.maximum(1.0, np.abs(lref))
+        assert err.max() <= max(rtol, 2e-12), (rtol, err.max())
+
+
 @pytest.mark.parametrize("dc,du,lev", [(24, 8, 4), (8, 0, 2), (16, 4, 3), (32, 4, 2)])
 def test_coarse_prescreen_matches_fast_and_oracle(device, dc, du, lev, monkeypatch):
     """The acquisition's coarse pre-screen (one f16 product per continuous dim, the dropped products in

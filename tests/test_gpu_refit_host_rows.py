@@ -208,3 +208,52 @@ def test_sync_refit_rejects_bad_codes_then_recovers(device):
             np.testing.assert_array_equal(host, out.cpu().numpy())
             g_idx, _ = O.bohb_split(X, L, D + 1)
             np.testing.assert_array_equal(host[:8 * n].view(np.int64)[:ng], g_idx)
+
+
+def test_sync_refit_every_published_word_over_many_calls(device):
+    """300 back-to-back refits through the drop-in's store (hbx_kde_refit_sync), one row more each time, the
+    store's device arrays growing on the way: the host block each call returned (the models' bw / nlev / rows
+    views) equals the device output block word for word."""
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lev, n0, calls = 24, 8, 4, 200, 300
+    D = dc + du
+    X = S.make_observations(n0 + calls, dc, du, lev, seed=123)
+    L = S.make_losses(n0 + calls, seed=124)
+    store = kde.ObservationStore(D, S.var_type_string(dc, du), device=device, capacity=64)
+    store.add(X[:n0], L[:n0])
+    for i in range(calls):
+        store.add(X[n0 + i], L[n0 + i])
+        pair = store.refit(D + 1)
+        host = pair.good.bw
+        while host.base is not None:
+            host = host.base
+        ob = int(N.lib().hbx_kde_refit_out_bytes(n0 + i + 1, D))
+        assert host.nbytes == ob
+        np.testing.assert_array_equal(host.view(np.uint8), pair._keep[0][:ob].cpu().numpy())
+
+
+def test_refit_then_acquire_on_another_stream(device):
+    """A model refit on the current stream and used at once from another stream (a side stream of another
+    thread's work): hbx_kde_refit_sync returns with the refit's launches complete, so the acquisition there sees
+    the finished parameter blocks and tables -- its record equals the same acquisition on the refit's stream."""
+    import torch
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lev, n0 = 24, 8, 4, 400
+    D = dc + du
+    X = S.make_observations(n0 + 20, dc, du, lev, seed=125)
+    L = S.make_losses(n0 + 20, seed=126)
+    C = torch.from_numpy(S.make_candidates(4096, dc, du, lev, seed=127)).to(device)
+    store = kde.ObservationStore(D, S.var_type_string(dc, du), device=device)
+    store.add(X[:n0], L[:n0])
+    side = torch.cuda.Stream(device)
+    for i in range(20):
+        store.add(X[n0 + i], L[n0 + i])
+        pair = store.refit(D + 1)
+        with torch.cuda.stream(side):
+            r = pair.acquire(C, stream=side)
+        torch.cuda.synchronize()
+        ref = pair.acquire(C)
+        assert (r.index, r.score, r.pdf_l, r.pdf_g) == (ref.index, ref.score, ref.pdf_l, ref.pdf_g)

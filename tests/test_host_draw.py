@@ -124,3 +124,46 @@ def test_sample_candidates_uses_the_global_rng_like_the_reference():
     r1, r2 = np.random.RandomState(44), np.random.RandomState(44)
     assert np.array_equal(cg.sample_candidates(kde, 10, rng=r1), B._draw_rvs(kde, cg.vartypes, 3, 10, r2))
     assert B._MT(r1).snap() == B._MT(r2).snap()
+    # a legacy RandomState over another bit generator: no raw MT19937 state, the per-element path
+    r3, r4 = np.random.RandomState(np.random.PCG64(5)), np.random.RandomState(np.random.PCG64(5))
+    assert np.array_equal(cg.sample_candidates(kde, 10, rng=r3), B._draw_rvs(kde, cg.vartypes, 3, 10, r4))
+    assert r3.random_sample() == r4.random_sample()
+
+
+def test_truncnorm_terms_equal_scipy_ppf():
+    """The cached inversion terms (B._TruncnormTerms + B._ppf_from_terms) against scipy's own truncnorm._ppf on
+    200k elements of BOHB's range (datum in [0, 1], bandwidths 1e-6 .. 10) and its edges: bit for bit wherever the
+    terms apply; where they do not (a datum exactly at 1, i.e. b = 0) _draw_fast hands the element to scipy."""
+    rs = np.random.RandomState(3)
+    nr, nd = 5000, 40
+    m = rs.rand(nr, nd)
+    m[rs.rand(nr, nd) < 0.01] = 0.0
+    m[rs.rand(nr, nd) < 0.005] = 1.0
+    m[:50] = rs.choice([1e-15, 1 - 1e-15, 5e-324, 2 ** -30, 0.5], (50, nd))
+    h = np.exp(rs.uniform(np.log(1e-6), np.log(10.0), nd))
+    q = rs.rand(nr, nd)
+    q[50:60] = 0.0
+    q[60:100] = rs.choice([5e-324, 1e-200, 1e-16, 1 - 2 ** -53, 1 - 1e-12], (40, nd))
+    t = B._TruncnormTerms(m, h)
+    t.fill(rs.permutation(nr), np.arange(nd))
+    assert t.have.all()
+    with np.errstate(all="ignore"):
+        ref = B.sps.truncnorm._ppf(q, -m / h, (1 - m) / h)
+    y, bad = B._ppf_from_terms(q, t.lp, t.mass, t.left)
+    use = t.ok & ~bad
+    assert not t.ok[m == 1.0].any() and t.ok[m < 1.0].all()
+    assert np.array_equal(y[use].view(np.uint64), ref[use].view(np.uint64))
+
+
+def test_draws_reuse_the_models_terms():
+    """Calls on one model fill its per-row terms once (rows picked by earlier calls are not recomputed) and stay
+    bit-identical to the per-element path, a datum at the upper bound included."""
+    rs = np.random.RandomState(8)
+    kde, lv = _model(rs, 40, 6, 2, [3, 4])
+    kde.data[3, 2] = 1.0
+    kde.data[7, 0] = 0.0
+    for k in range(6):
+        fa, fb, ea, eb, same = _both(kde, lv, 64, 300 + k)
+        assert ea is None and eb is None and same
+        assert np.array_equal(fa, fb)
+    assert kde._tn_terms.have.sum() > 30

@@ -21,6 +21,18 @@ def main():
             out["sh_stage_interleaved_host_sampler"] = bench.sh_stage_line(dev, n_obs=100, stage=27, reps=3,
                                                                            interleaved=True, sampler="host",
                                                                            dims=(4, 2))
+        elif name == "getconfig":
+            out["get_config_default"] = bench.get_config_line(dev)
+        elif name == "refit":
+            from hpbandster_amd import synthetic as S
+            X = S.make_observations(10000, 24, 8, 4)
+            out["refit"] = bench.refit_line(X, S.make_losses(10000), S.var_type_string(24, 8), dev)
+        elif name == "precise":
+            from hpbandster_amd import kde
+            from hpbandster_amd import synthetic as S
+            X = S.make_observations(10000, 24, 8, 4)
+            pair = kde.fit_pair(X, S.make_losses(10000), S.var_type_string(24, 8), 33, device=dev)
+            out["precise_logpdf"] = bench.precise_line(pair, bench.blocked_candidates(0, 1_000_000, 24, 8, 4, dev), dev)
         elif name == "config2":
             out["config2"] = bench.config2_line(dev)
         elif name == "config5":
