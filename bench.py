@@ -168,6 +168,32 @@ def host_info():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_max": quota, "cgroup_cpus": qcpus}
 
 
+_CPU_PDFS = [None]     # (pdf_l, pdf_g) of cpu_baseline's candidate sample (C oracle, fp64)
+_PRECISE_OUT = [None]  # (ln l, ln g) of precise_line over every candidate (hbx_kde_logpdf_rtol)
+
+
+def logpdf_oracle_check(rtol=1e-5):
+    """precise_logpdf at full size against the C oracle: the GPU's ln l(x), ln g(x) of the candidates whose pdfs
+    cpu_baseline computed anyway (its bounded sample: the first n candidates), relative error
+    |ln p_gpu - ln p_oracle| / max(1, |ln p_oracle|) -- the north-star contract (1e-5)."""
+    if _CPU_PDFS[0] is None or _PRECISE_OUT[0] is None:
+        return None
+    res = {}
+    worst = 0.0
+    for name, ref, got in (("l", _CPU_PDFS[0][0], _PRECISE_OUT[0][0]), ("g", _CPU_PDFS[0][1], _PRECISE_OUT[0][1])):
+        n = ref.shape[0]
+        with np.errstate(divide="ignore"):
+            lr = np.log(ref)
+        fin = np.isfinite(lr)
+        err = np.abs(got[:n][fin] - lr[fin]) / np.maximum(1.0, np.abs(lr[fin]))
+        res[name] = {"candidates": int(fin.sum()), "max_rel_err": float(err.max()) if err.size else None,
+                     "not_finite_in_oracle": int((~fin).sum())}
+        worst = max(worst, float(err.max()) if err.size else 0.0)
+    res.update(max_rel_err=worst, rtol=rtol, ok=bool(worst <= rtol),
+               checker="oracle/kde_oracle.c (fp64, the reference's arithmetic with libm exp), cpu_baseline's sample")
+    return res
+
+
 def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     """CPU baselines on the host cores, bounded samples of the same workload:
     * value: the C oracle (oracle/kde_oracle.c, fp64, the reference's arithmetic, OpenMP over
@@ -190,12 +216,13 @@ def cpu_baseline(X, good_rows, bad_rows, pair, var_type, cands, target_s):
     n = max(threads, 16)
     while True:
         t0 = time.perf_counter()
-        c_oracle.kde_pdf(*args_g, cands[:n], nthreads=threads)
-        c_oracle.kde_pdf(*args_b, cands[:n], nthreads=threads)
+        pl = c_oracle.kde_pdf(*args_g, cands[:n], nthreads=threads)
+        pg = c_oracle.kde_pdf(*args_b, cands[:n], nthreads=threads)
         dt = time.perf_counter() - t0
         if dt >= target_s * 0.5 or n >= cands.shape[0]:
             break
         n = int(min(cands.shape[0], max(2 * n, n * (target_s / max(dt, 1e-3)))))
+    _CPU_PDFS[0] = (pl, pg)  # the sample's oracle pdfs: precise_logpdf's full-size check (main)
     nobs = Xg.shape[0] + Xb.shape[0]
     out = {"value": n * nobs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
            "sample": "%d of the %d candidates x %d observations (D=%d), fp64 C oracle (reference arithmetic), "
@@ -701,6 +728,56 @@ def sh_stage_line(device, n_obs=400, stage=81, reps=5, interleaved=False, sample
                      "the first call computed ahead" % stage)}
 
 
+def threaded_run_line(device, n_iterations=16, workers=8, reps=3, dims=(24, 8)):
+    """Side line: the drop-in HpBandSter.run with BOHB (GPU sampler) and `workers` in-process
+    zero-cost workers (dispatch.ThreadedDispatcher: results reach job_callback -> new_result on the dispatcher
+    thread while the master loop requests runs, HB_master.py:170-177,192-208), job_queue_sizes=(-1, 0) with the
+    queue sized to the workers (the reference's BOHB optimizer settings): wall time of the whole run for
+    speculative='never', 'auto' (the default: speculative batches + the next call computed ahead) and 'auto' with
+    the compute-ahead off, alternated, best of `reps` each.  Thread timing makes the proposals differ run to run;
+    the line reports how many picks a computed-ahead acquisition served."""
+    from hpbandster_amd.config_generators import BOHB
+    from hpbandster_amd.dispatch import ThreadedDispatcher
+    from hpbandster_amd.HB_master import HpBandSter
+    CS, space, _ = _space_and_jobs(dims)
+
+    def compute(config, budget, working_directory):
+        return {"loss": float(sum(v for v in config.values() if isinstance(v, float))) / budget, "info": None}
+
+    def run(variant):
+        np.random.seed(7)
+        space.seed(8)
+        cg = BOHB(space, device=device, sampler="gpu", sampler_seed=5,
+                  speculative="never" if variant == "never" else "auto", min_points_in_model=40)
+        if variant == "auto_no_ahead":
+            cg._ahead_enabled = lambda: False
+        disp = ThreadedDispatcher(compute, n_workers=workers)
+        m = HpBandSter("bench", cg, eta=3, min_budget=1, max_budget=27, job_queue_sizes=(-1, 0),
+                       dynamic_queue_size=True, dispatcher=disp)
+        m.adjust_queue_size(workers)
+        t0 = time.perf_counter()
+        res = m.run(n_iterations)
+        el = time.perf_counter() - t0
+        m.shutdown()
+        return el, len(res.get_all_runs()), dict(cg._ahead_stats), cg._calls
+
+    res = {}
+    variants = ("never", "auto", "auto_no_ahead")
+    for r in range(reps):
+        for v in variants[r % 3:] + variants[:r % 3]:
+            el, runs, st, calls = run(v)
+            if v not in res or el < res[v][0]:
+                res[v] = (el, runs, st, calls)
+    return {"workload": "hpbandster_run_%d_iterations_%d_threaded_workers_d%d" % (n_iterations, workers, sum(dims)),
+            "ms_never": res["never"][0] * 1e3, "ms_auto": res["auto"][0] * 1e3,
+            "ms_auto_no_ahead": res["auto_no_ahead"][0] * 1e3,
+            "speedup_auto_vs_never": res["never"][0] / res["auto"][0],
+            "speedup_ahead": res["auto_no_ahead"][0] / res["auto"][0], "runs": res["auto"][1],
+            "get_config_calls_auto": res["auto"][3], "ahead_stats_auto": res["auto"][2],
+            "note": "BOHB(sampler='gpu'), zero-cost compute, results on the dispatcher thread; speedup_ahead = "
+                    "auto with the compute-ahead off / auto"}
+
+
 def _space_and_jobs(dims, levels=4):
     from hpbandster_amd import configspace as CS
 
@@ -781,6 +858,7 @@ def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
     out = torch.empty(Nc, dtype=torch.float64, device=device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {}
+    keep = []
     for name, k in (("l", pair.good), ("g", pair.bad)):
         def call():
             N.check(L.hbx_kde_logpdf_rtol(N.ptr(c_dev), Nc, k.k_vars, N.ptr(k.params), N.ptr(k.table), N.ptr(k.X_dev),
@@ -798,6 +876,8 @@ def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
         refined = int(scr[:4].view(torch.int32).item())
         res[name] = {"ms_per_call": float(np.median(ms)), "observations": k.nobs, "fp64_reevaluated": refined,
                      "fp64_fraction": refined / Nc, "finite": bool(torch.isfinite(out).all().item())}
+        keep.append(out.cpu().numpy())
+    _PRECISE_OUT[0] = tuple(keep)
     t = res["l"]["ms_per_call"] + res["g"]["ms_per_call"]
     pairs = Nc * (pair.good.nobs + pair.bad.nobs)
     rate = pairs / (t * 1e-3)
@@ -1298,6 +1378,11 @@ def main():
             out["cpu_baseline"]["reference_loop"] = reference_loop_baseline(device)
         except Exception as e:
             out["cpu_baseline"]["reference_loop"] = {"error": repr(e)}
+        if isinstance(out.get("precise_logpdf"), dict) and "error" not in out["precise_logpdf"]:
+            try:
+                out["precise_logpdf"]["oracle_check"] = logpdf_oracle_check()
+            except Exception as e:
+                out["precise_logpdf"]["oracle_check"] = {"error": repr(e)}
     if world > 1:
         out["cpu_baseline_note"] = ("the CPU baseline is measured on rank 0 at N=1 only (bench contract): see that "
                                     "line's cpu_baseline")

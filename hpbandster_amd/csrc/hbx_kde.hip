@@ -703,10 +703,18 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
 
 // f32-MFMA layout of an hmode KDE whose C_j left the f16 range of the three-piece split
 __device__ __forceinline__ bool table_needs_rebuild(const KdeParams* P) { return P->hmode && !(P->cmax <= H_CMAX); }
+// variant bit 8: at most 8 categorical slots and every active categorical dim's codes in [0, 3] -- the
+// direct-difference ln-pdf pass then matches codes through two-bit fields and 256-entry tables (DD_LUT)
+__device__ __forceinline__ int small_codes(const KdeParams* P) {
+  if (P->du_pad != 4 && P->du_pad != 8) return 0;
+  for (int u = 0; u < P->du; ++u)
+    if (P->cat_maxcode[u] < 0 || P->cat_maxcode[u] > 3) return 0;
+  return 1;
+}
 
 // Final mode of each KDE and its info record {variant, nan_all, unsupported, dc, du, nconst, dc_pad,
 // du_pad}; variant = has_neg | kc << 1 | (hmode != 0) << 4 | exact_only << 5 | (hmode == 2) << 6 |
-// (coarse table) << 7 selects the scoring kernel.  rebuild: the table needed its f32 rebuild.
+// (coarse table) << 7 | small_codes << 8 selects the scoring kernel.  rebuild: the table needed its f32 rebuild.
 __device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool rebuild) {
   if (rebuild) {
     P->hmode = 0;
@@ -715,7 +723,7 @@ __device__ __forceinline__ void prep_finish_p(KdeParams* P, int32_t* info, bool 
     P->coarse_off = 0;
   }
   info[0] = P->has_neg | (P->kc << 1) | ((P->hmode != 0) << 4) | (P->exact_only << 5) | ((P->hmode == 2) << 6) |
-            ((P->hmode == 2 && P->coarse_off > 0) << 7);
+            ((P->hmode == 2 && P->coarse_off > 0) << 7) | (small_codes(P) << 8);
   info[1] = P->nan_all;
   info[2] = P->unsupported;
   info[3] = P->dc;
@@ -741,7 +749,7 @@ __device__ __forceinline__ void prep_finish_lds(const KdeParams* R, KdeParams* W
     W->coarse_off = 0;
   }
   vals[0] = R->has_neg | (R->kc << 1) | ((hmode != 0) << 4) | (R->exact_only << 5) | ((hmode == 2) << 6) |
-            ((hmode == 2 && coarse > 0) << 7);
+            ((hmode == 2 && coarse > 0) << 7) | (small_codes(R) << 8);
   vals[1] = R->nan_all;
   vals[2] = R->unsupported;
   vals[3] = R->dc;
@@ -2972,10 +2980,15 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 //   exp2: v_exp_f32 within 2 ulp (2^-22 relative); sums: 3 x 2^-24 (fp32 groups of 4) + n 2^-52 (fp64).
 // Candidates whose bound stays within 0.99 rtol max(1, |ln p|) are written; the rest go to `list` for the
 // fp64 pass.  KDEs with negative categorical factors, structural NaN or single-level dims: all to `list`.
+// LUT (variant bit 8: <= 8 categorical slots, codes in [0, 3]): the categorical part of a pair is two table
+// reads instead of 1.5 packed instructions per dim -- the candidate's and the observation's codes packed as
+// two-bit fields (dims 0-3 at bits 2..9, dims 4-7 at bits 12..19), their xor's two 8-bit field groups index
+// 256-entry LDS tables whose entry is sum_u delta_u [field u == 0] (summed in fp64, rounded once: within
+// 2^-24 sum|delta|, the bound's delta term); a candidate whose code is not an integer in [0, 3] goes to `list`.
 #ifndef DD_WPE
 #define DD_WPE(w) ((w) <= 16 ? 4 : (w) <= 40 ? 3 : 2)  // waves per SIMD the register budget is sized for
 #endif
-template <int DC, int DU, int CPT>
+template <int DC, int DU, int CPT, bool LUT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC + DU)))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
                                                            const KdeParams* __restrict__ P,
                                                            const double* __restrict__ X,
@@ -2984,13 +2997,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
                                                            int32_t* __restrict__ count) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int OB = 64;      // observations per staged chunk
-  constexpr int W = DC + DU;  // floats per staged row: DC scaled coordinates, DU codes
+  // floats per staged row: DC scaled coordinates, then DU codes (LUT: the packed code word and 3 pad slots)
+  constexpr int W = LUT ? DC + 4 : DC + DU;
+  constexpr int WC = LUT ? DC : W;  // staged elements per row written by the element loop
   constexpr int NB = DC / 2, NU = DU / 2;  // packed pairs
   static_assert(DC % 4 == 0 && DU % 4 == 0, "pairs of pairs");
+  static_assert(!LUT || DU == 4 || DU == 8, "LUT: 4 or 8 categorical slots");
   __shared__ __align__(16) float xs[2][OB][W];
   __shared__ double s_scale[DC > 0 ? DC : 1], s_mu[DC > 0 ? DC : 1];
-  __shared__ int32_t s_col[W > 0 ? W : 1];
+  __shared__ int32_t s_col[DC + DU > 0 ? DC + DU : 1];
   __shared__ float s_dl[DU > 0 ? DU : 1];
+  __shared__ float s_lut[LUT ? 512 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int n = P->n, dc = P->dc, du = P->du;
   const int64_t i0 = (int64_t)blockIdx.x * 256 * CPT;
@@ -3016,7 +3033,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     for (int c = 0; c < CPT; ++c) to_list(valid[c], cid[c]);
     return;
   }
-  for (int k = tid; k < W; k += 256) {
+  for (int k = tid; k < DC + DU; k += 256) {
     if (k < DC) {
       const bool act = k < dc;
       s_scale[k] = act ? P->cont_scale[k] : 0.0;
@@ -3030,8 +3047,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     }
   }
   __syncthreads();
+  if constexpr (LUT) {  // table k, entry i: the deltas of the dims 4k..4k+3 whose two-bit field of i is 0
+#pragma unroll
+    for (int k = 0; k < DU / 4; ++k) {
+      double v = 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (((tid >> (2 * u)) & 3) == 0) v += (double)s_dl[4 * k + u];
+      s_lut[256 * k + tid] = (float)v;
+    }
+  }
   // the candidates: scaled continuous coordinates and codes in registers, pairs of dims packed
-  f2 xc[CPT][NB > 0 ? NB : 1], xu[CPT][NU > 0 ? NU : 1];
+  f2 xc[CPT][NB > 0 ? NB : 1], xu[CPT][(NU > 0 && !LUT) ? NU : 1];
+  uint32_t cw[CPT];  // LUT: the candidate's packed codes
+  bool cbad[CPT];    // LUT: a code outside [0, 3] (or not an integer): the candidate goes to the fp64 pass
   float nx2[CPT];  // sum_k (|x'_k| + xmax_k)^2
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
@@ -3049,34 +3078,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
       }
       xc[c][q] = f2{v[0], v[1]};
     }
+    cw[c] = 0u;
+    cbad[c] = false;
+    if constexpr (LUT) {
 #pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      float v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = DC + 2 * q + h;
-        v[h] = s_col[k] >= 0 ? cand_code(x[s_col[k]]) : 0.f;
+      for (int u = 0; u < DU; ++u) {
+        const int k = DC + u;
+        const double v = s_col[k] >= 0 ? x[s_col[k]] : 0.0;
+        const bool ok = v == rint(v) && v >= 0.0 && v <= 3.0;
+        cbad[c] = cbad[c] || !ok;
+        cw[c] |= (ok ? (uint32_t)v : 0u) << (u < 4 ? 2 + 2 * u : 12 + 2 * (u - 4));
       }
-      xu[c][q] = f2{v[0], v[1]};
+    } else {
+#pragma unroll
+      for (int q = 0; q < NU; ++q) {
+        float v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = DC + 2 * q + h;
+          v[h] = s_col[k] >= 0 ? cand_code(x[s_col[k]]) : 0.f;
+        }
+        xu[c][q] = f2{v[0], v[1]};
+      }
     }
     nx2[c] = acc;
   }
-  f2 dl2[NU > 0 ? NU : 1];
+  f2 dl2[(NU > 0 && !LUT) ? NU : 1];
+  if constexpr (!LUT) {
 #pragma unroll
-  for (int q = 0; q < NU; ++q) dl2[q] = f2{s_dl[2 * q], s_dl[2 * q + 1]};
+    for (int q = 0; q < NU; ++q) dl2[q] = f2{s_dl[2 * q], s_dl[2 * q + 1]};
+  }
   // stage chunk cc into buffer b (padding dims 0 -- codes 0 against the candidate's 0: a match of delta 0;
   // an observation past n: first coordinate +inf, its term 2^-inf = 0)
   // the loads of a chunk are issued into registers before the previous chunk's math and stored after it
-  constexpr int PER = (OB * W + 255) / 256;
+  constexpr int PER = (OB * WC + 255) / 256;
   double pre[PER];
+  uint32_t prc[LUT ? DU : 1];  // LUT, threads < OB: row tid's codes (the high words of the f64 values)
   auto fetch = [&](int cc) __attribute__((always_inline)) {
     const int j0 = cc * OB;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = tid + 256 * q;
-      const int jj = e / W, k = e - jj * W;
+      const int jj = e / WC, k = e - jj * WC;
       const int j = j0 + jj;
-      pre[q] = (e < OB * W && j < n && s_col[k] >= 0) ? X[rows[j] * (int64_t)D + s_col[k]] : 0.0;
+      pre[q] = (e < OB * WC && j < n && s_col[k] >= 0) ? X[rows[j] * (int64_t)D + s_col[k]] : 0.0;
+    }
+    if constexpr (LUT) {
+      const int j = j0 + tid;
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const int k = DC + u;
+        prc[u] = (tid < OB && j < n && s_col[k] >= 0)
+                     ? reinterpret_cast<const uint32_t*>(X + rows[j] * (int64_t)D + s_col[k])[1] : 0u;
+      }
     }
   };
   auto store = [&](int cc, int b) __attribute__((always_inline)) {
@@ -3084,8 +3138,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = tid + 256 * q;
-      if (e >= OB * W) break;
-      const int jj = e / W, k = e - jj * W;
+      if (e >= OB * WC) break;
+      const int jj = e / WC, k = e - jj * WC;
       float v = 0.f;
       if (j0 + jj < n) {
         if (s_col[k] >= 0) v = k < DC ? (float)(s_scale[k] * (pre[q] - s_mu[k])) : cand_code(pre[q]);
@@ -3093,6 +3147,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
         v = __builtin_inf();
       }
       xs[b][jj][k] = v;
+    }
+    if constexpr (LUT) {
+      if (tid < OB) {  // the codes are integers in [0, 3] (variant bit 8): exact from the f64 high word
+        uint32_t w = 0u;
+#pragma unroll
+        for (int u = 0; u < DU; ++u)
+          w |= (uint32_t)__hiloint2double((int)prc[u], 0) << (u < 4 ? 2 + 2 * u : 12 + 2 * (u - 4));
+        xs[b][tid][DC] = __uint_as_float(w);
+        xs[b][tid][DC + 1] = xs[b][tid][DC + 2] = xs[b][tid][DC + 3] = 0.f;
+      }
     }
   };
   auto stage = [&](int cc, int b) __attribute__((always_inline)) {
@@ -3102,6 +3166,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
   // exponent t' of the pair (candidate c, staged row r): two packed accumulators (four fma chains)
   auto term = [&](int c, const float* r) __attribute__((always_inline)) -> float {
     f2 a0 = f2{0.f, 0.f}, a1 = f2{0.f, 0.f};
+    if constexpr (LUT) {  // the categorical part: two table reads of the codes' xor
+      const uint32_t x = cw[c] ^ __float_as_uint(r[DC]);
+      const float l0 = *(const float*)((const char*)s_lut + (x & 0x3FFu));
+      const float l1 = DU > 4 ? *(const float*)((const char*)s_lut + 1024 + ((x >> 10) & 0x3FFu)) : 0.f;
+      a0 = f2{l0, l1};
+    }
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const f2 X2 = f2{r[2 * q], r[2 * q + 1]};  // (the row is read as whole 16-byte vectors: see rowv)
@@ -3110,7 +3180,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
       else a1 = __builtin_elementwise_fma(-d, d, a1);
     }
 #pragma unroll
-    for (int q = 0; q < NU; ++q) {
+    for (int q = 0; q < (LUT ? 0 : NU); ++q) {
       const f2 E2 = f2{r[DC + 2 * q], r[DC + 2 * q + 1]};
       const f2 e = xu[c][q] - E2;
       f2 m;  // [x_u == X_u] = clamp(1 - e^2) for integer code differences e
@@ -3152,32 +3222,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     // terms summed in fp32 in groups of 4, the groups into the fp64 sums (a chunk's last group: rows past jn
     // are the padding rows, whose first coordinate is +inf: exact zeros)
     const int jg = (jn + 3) & ~3;
+    auto row = [&](int jr, float (&r)[W]) __attribute__((always_inline)) {  // 16-byte vectors (ds_read_b128)
+#pragma unroll
+      for (int v = 0; v < W / 4; ++v) {
+        const float4 f = reinterpret_cast<const float4*>(&xs[b][jr][0])[v];
+        r[4 * v] = f.x;
+        r[4 * v + 1] = f.y;
+        r[4 * v + 2] = f.z;
+        r[4 * v + 3] = f.w;
+      }
+    };
     for (int j4 = 0; j4 < jg; j4 += 4) {
+      float tmx[CPT];  // the group's largest exponent per candidate
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) tmx[c] = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float r[W];  // the staged row, read as 16-byte vectors (ds_read_b128)
-#pragma unroll
-        for (int v = 0; v < W / 4; ++v) {
-          const float4 f = reinterpret_cast<const float4*>(&xs[b][j4 + q][0])[v];
-          r[4 * v] = f.x;
-          r[4 * v + 1] = f.y;
-          r[4 * v + 2] = f.z;
-          r[4 * v + 3] = f.w;
-        }
+        float r[W];
+        row(j4 + q, r);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
           const float t = term(c, r);
-          float e = __builtin_amdgcn_exp2f(t - m[c]);
-          if (!(e < 0x1p100f)) {  // rare: a term far above the reference point (or NaN): move it up to ceil(t)
-            if (t == t) {
-              const float mn = ceilf(t);  // integer reference points: the rescale is an exact ldexp
-              S[c] = ldexp(S[c] + (double)s4[c], (int)(m[c] - mn));
-              s4[c] = 0.f;
-              m[c] = mn;
-              e = __builtin_amdgcn_exp2f(t - mn);
-            }
+          tmx[c] = fmaxf(tmx[c], t);
+          s4[c] += __builtin_amdgcn_exp2f(t - m[c]);
+        }
+      }
+      // rare: a term far above the reference point, or NaN (one test per candidate and group of 4): the reference
+      // point moves up to ceil of the group's largest exponent (an integer: the rescale is an exact ldexp) and the
+      // group is summed again (a wave-uniform branch; the lanes that need it)
+      bool redo[CPT];
+      bool any = false;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        redo[c] = !(s4[c] < 0x1p100f);
+        any = any || redo[c];
+      }
+      if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+          const float mn = ceilf(tmx[c]);
+          if (redo[c] && mn > m[c]) {
+            S[c] = ldexp(S[c], (int)(m[c] - mn));
+            m[c] = mn;
           }
-          s4[c] += e;
+          if (redo[c]) s4[c] = 0.f;
+        }
+        for (int q = 0; q < 4; ++q) {
+          float r[W];
+          row(j4 + q, r);
+#pragma unroll
+          for (int c = 0; c < CPT; ++c) {
+            const float e = __builtin_amdgcn_exp2f(term(c, r) - m[c]);
+            if (redo[c]) s4[c] += e;
+          }
         }
       }
 #pragma unroll
@@ -3214,7 +3311,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     const double lnS = log(S[c]) + (double)m[c] * 0.69314718055994531;
     const double lp = lnS + log_c * 0.69314718055994531 + P->log_norm;
     const double bound = rel / (1.0 - rel) + 0x1p-50 * fabs(lp);
-    const bool ok = valid[c] && ref0[c] && S[c] > 0.0 && lp - lp == 0.0 && rel < 0.5 && bound <= 0.99 * rtol * fmax(1.0, fabs(lp));
+    const bool ok = valid[c] && ref0[c] && !cbad[c] && S[c] > 0.0 && lp - lp == 0.0 && rel < 0.5 && bound <= 0.99 * rtol * fmax(1.0, fabs(lp));
     if (ok) out[cid[c]] = lp;
     to_list(valid[c] && !ok, cid[c]);
   }
@@ -3227,9 +3324,20 @@ typedef void (*logpdf_dd_fn)(const double*, int64_t, int32_t, const KdeParams*, 
 #define DD_CPT 2
 #endif
 constexpr int dd_cpt(int dc, int du) { return DD_CPT; }
+#ifndef DD_CPT_LUT
+#define DD_CPT_LUT 2
+#endif
 
 template <int DC>
-static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt) {
+static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt, bool lut) {
+  if (lut && du_pad == 4) {
+    *cpt = DD_CPT_LUT;
+    return kde_logpdf_dd_kernel<DC, 4, DD_CPT_LUT, true>;
+  }
+  if (lut && du_pad == 8) {
+    *cpt = DD_CPT_LUT;
+    return kde_logpdf_dd_kernel<DC, 8, DD_CPT_LUT, true>;
+  }
   switch (du_pad) {
     case 0: *cpt = dd_cpt(DC, 0); return kde_logpdf_dd_kernel<DC, 0, dd_cpt(DC, 0)>;
     case 4: *cpt = dd_cpt(DC, 4); return kde_logpdf_dd_kernel<DC, 4, dd_cpt(DC, 4)>;
@@ -3241,14 +3349,14 @@ static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt) {
 }
 
 // the direct-difference fp32 kernel of a bucket (continuous slots rounded up to a multiple of 4)
-static logpdf_dd_fn pick_logpdf_dd(int dc_pad, int du_pad, int* cpt) {
+static logpdf_dd_fn pick_logpdf_dd(int dc_pad, int du_pad, int* cpt, bool lut) {
   switch (dc_pad) {
     case 0:
-    case 4: return pick_dd_du<4>(du_pad, cpt);
-    case 8: return pick_dd_du<8>(du_pad, cpt);
-    case 16: return pick_dd_du<16>(du_pad, cpt);
-    case 24: return pick_dd_du<24>(du_pad, cpt);
-    case 32: return pick_dd_du<32>(du_pad, cpt);
+    case 4: return pick_dd_du<4>(du_pad, cpt, lut);
+    case 8: return pick_dd_du<8>(du_pad, cpt, lut);
+    case 16: return pick_dd_du<16>(du_pad, cpt, lut);
+    case 24: return pick_dd_du<24>(du_pad, cpt, lut);
+    case 32: return pick_dd_du<32>(du_pad, cpt, lut);
   }
   return nullptr;  // 64 continuous slots: the estimate + fp64 path
 }
@@ -3333,7 +3441,9 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
   // unsigned KDEs of a bucket with <= 32 continuous slots: the direct-difference fp32 pass writes every
   // candidate its bound accepts and lists the rest (its kernel lists all of a KDE it does not model)
   int cpt = 1;
-  const logpdf_dd_fn dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt) : nullptr;
+  const char* lut_env = getenv("HBX_DD_LUT");  // 0: the packed-match categorical path everywhere (tests)
+  const bool lut = ((variant >> 8) & 1) && !(lut_env && atoi(lut_env) == 0);
+  const logpdf_dd_fn dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt, lut) : nullptr;
   HBX_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), s));
   if (dd) {
     hipLaunchKernelGGL(dd, dim3((unsigned)((Nc + 256 * cpt - 1) / (256 * cpt))), dim3(256), 0, s, cand, Nc, D,

@@ -21,6 +21,8 @@ def main():
             out["sh_stage_interleaved_host_sampler"] = bench.sh_stage_line(dev, n_obs=100, stage=27, reps=3,
                                                                            interleaved=True, sampler="host",
                                                                            dims=(4, 2))
+        elif name == "threaded":
+            out["threaded_run"] = bench.threaded_run_line(dev)
         elif name == "getconfig":
             out["get_config_default"] = bench.get_config_line(dev)
         elif name == "refit":
