@@ -38,9 +38,6 @@ SIGNATURES = {
     "hbx_kde_refit_scratch_bytes": (c_i64, [c_i64, c_i32]),
     "hbx_kde_refit": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_double,
                               ctypes.c_double, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
-    "hbx_kde_refit_host_rows": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_double,
-                                        ctypes.c_double, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
-                                        c_vp]),
     "hbx_kde_refit_sync": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_double,
                                    ctypes.c_double, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                    c_vp, c_vp]),
@@ -51,16 +48,10 @@ SIGNATURES = {
                                 c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
                                 c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
-    "hbx_kde_acquire_host": (c_i32, [c_vp, c_i64, c_i32, c_i64,
-                                     c_vp, c_vp, c_vp, c_vp, c_i32,
-                                     c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
-                                     c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "hbx_kde_pair_bind": (c_vp, [c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
                                  c_i64]),
-    "hbx_kde_acquire_bound": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "hbx_kde_acquire_bound": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hbx_kde_pair_free": (None, [c_vp]),
-    "hbx_kde_acquire_ahead": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp]),
-    "hbx_wait_word": (c_i32, [c_vp, c_i32, c_vp]),
     "hbx_kde_batch_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "hbx_kde_acquire_batch": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i64,
                                       c_vp, c_vp, c_vp, c_vp, c_i32,

@@ -18,14 +18,13 @@ reference's order), so a seeded run proposes the same configurations.  What move
 import ctypes
 import logging
 import threading
-import time
 import traceback
 
 import numpy as np
 import scipy.stats as sps
 
 from .. import _native
-from ..kde import AcqResult, ObservationStore, RESULT_BYTES
+from ..kde import ACQ_DOMAIN_ERR, ObservationStore
 from .base import base_config_generator
 from ._cs import ConfigSpace
 
@@ -363,59 +362,6 @@ class SpeculativeBatch(object):
         return j == len(self.entries) and self._valid_at(j) and self.mt.snap() == self.states[j]
 
 
-# layout of a pick published by hbx_kde_acquire_ahead (include/hbx.h HBX_PICK_*)
-PICK_ERR, PICK_DONE, PICK_ROW = 48, 52, 64
-
-
-class _PickBuffers(object):
-    """Device-mapped host buffers for published picks, shared by every BOHB of the process: hipHostMalloc
-    is slow (and a generator's buffers would otherwise be freed -- after a device synchronisation -- when
-    it is collected, at whatever moment the garbage collector picks).  A buffer the device may still
-    write (a dropped pick) waits in `pending` until its completion word shows its sequence number."""
-
-    def __init__(self):
-        self.lock = threading.Lock()
-        self.free = {}     # bytes -> [buffer]
-        self.pending = []  # (buffer, seq, bytes)
-
-    def get(self, nbytes):
-        with self.lock:
-            still = []
-            for buf, seq, nb in self.pending:
-                if ctypes.c_int32.from_address(buf + PICK_DONE).value == seq:
-                    self.free.setdefault(nb, []).append(buf)
-                else:
-                    still.append((buf, seq, nb))
-            self.pending = still
-            lst = self.free.get(nbytes)
-            if lst:
-                return lst.pop()
-        p = ctypes.c_void_p()
-        _native.check(_native.lib().hbx_host_alloc(nbytes, ctypes.addressof(p)))
-        return p.value
-
-    def put(self, buf, nbytes, seq=None):
-        with self.lock:
-            if seq is None:
-                self.free.setdefault(nbytes, []).append(buf)
-            else:
-                self.pending.append((buf, seq, nbytes))
-
-
-_PICKS = _PickBuffers()
-
-
-class _Ahead(object):
-    """One get_config call's acquisition enqueued before the call (BOHB._launch_ahead): the model it was
-    drawn from, the sampler counter it starts at, the model version, the completion word's value, the
-    device tensors it uses, its mapped output buffer and what launched it ('get_config' / 'new_result')."""
-    __slots__ = ("pair", "counter", "version", "seq", "keep", "buf", "source", "calls")
-
-    def __init__(self, pair, counter, version, seq, keep, buf, source, calls):
-        self.pair, self.counter, self.version, self.seq = pair, counter, version, seq
-        self.keep, self.buf, self.source, self.calls = keep, buf, source, calls
-
-
 class BOHB(base_config_generator):
     def __init__(self, configspace, min_points_in_model=None, top_n_percent=15, num_samples=64,
                  random_fraction=1 / 3, bandwidth_factor=3, device=None, sampler="host", sampler_seed=None,
@@ -475,26 +421,8 @@ class BOHB(base_config_generator):
         self.kde_models = dict()
         self._stores = dict()  # budget -> ObservationStore: the budget's rows resident in HBM
         self._model_version = 0  # bumped whenever kde_models changes (speculative batches check it)
-        # the next get_config's acquisition computed ahead (GPU sampler: its candidates depend only on the
-        # model and the sampler's counter, not on the global RNG) -- launched after a refit or a served
-        # call, served when the call finds the same model and counter.  A source whose last one went unused
-        # (a result arrived first, a batch took over, a burst of results) pauses until the pattern it serves
-        # shows up again: a call right after a call (no refit between) for 'get_config', a call after a
-        # result for 'new_result'
-        self._ahead = None
-        self._ahead_lock = threading.Lock()
-        self._ahead_on = {"get_config": True, "new_result": True}
-        self._last_call_version = None
-        # a refit's launch pays only when the caller leaves time before the next call to hide the device
-        # work in (HB_master: the dispatcher thread's callback, then a hand-off to the master loop): the
-        # gap from a new_result's end to the next call, smoothed; below AHEAD_MIN_GAP_S refits launch nothing
-        self._result_end = None
-        self._gap = None
-        self._ahead_stats = {"launched": 0, "served": 0, "dropped": 0}
         self._calls = 0  # get_config calls so far
-        self._pick_free = []     # mapped output buffers ready for reuse
-        self._pick_pending = []  # (buffer, seq, tensors, pair) of dropped ones the device may still use
-        self._pick_seq = 0
+        self._pick_tls = threading.local()  # GPU sampler: this thread's draw / pick buffers (_pick)
 
     # -- candidates ---------------------------------------------------------------------------
     def sample_candidates(self, kde_good, num_samples, rng=None):
@@ -518,27 +446,10 @@ class BOHB(base_config_generator):
                 return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt)
         return _draw_rvs(kde_good, self.vartypes, self.bw_factor, num_samples, R)
 
-    def draw_candidates(self, pair, num_samples):
-        """Candidates of one get_config call (or of several back to back): host numpy array, or with
-        the GPU sampler a device tensor plus its per-candidate domain-error flags."""
-        if self.sampler == "host":
-            return self.sample_candidates(pair['good'], num_samples), None
-        cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, num_samples, self.sampler_seed,
-                                            self._sample_counter)
-        self._sample_counter += num_samples
-        return cands, err
-
     def get_config(self, budget):
         sample = None
         info_dict = {}
         self._calls += 1
-        if self._last_call_version is not None:  # the pattern since the previous call re-enables its source
-            self._ahead_on["get_config" if self._last_call_version == self._model_version else "new_result"] = True
-        t_end = self._result_end
-        if t_end is not None:  # a result came before this call: how long after it
-            self._result_end = None
-            gap = time.perf_counter() - t_end
-            self._gap = gap if self._gap is None else 0.75 * self._gap + 0.25 * gap
         if len(self.kde_models.keys()) == 0 or np.random.rand() < self.random_fraction:
             sample = self.configspace.sample_configuration().get_dictionary()
             info_dict['model_based_pick'] = False
@@ -547,37 +458,23 @@ class BOHB(base_config_generator):
             try:
                 budget = max(self.kde_models.keys())  # always the largest-budget model (bohb.py:124)
                 pair = self.kde_models[budget]        # immutable snapshot (new_result swaps entries)
-                a = self._take_ahead(pair) if self._ahead is not None else None
-                if a is not None:  # this call's draws and acquisition, computed ahead on the same counter
-                    res, bad, best_vector = self._serve_ahead(a)
+                if self.sampler == "gpu":
+                    # one wait: the draws, the acquisition, the domain-error flag and the winning row come back
+                    # together (no separate device reduction and row copy)
+                    res, best_vector = self._pick(pair, self._sample_counter)
                     self._sample_counter += self.num_samples
-                    if bad:
-                        raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
-                elif self.sampler == "gpu" and getattr(pair, "_bound", None):
-                    # on the spot, one wait: the draws, the acquisition, the error flag and the winning row
-                    # published together (no separate device reduction and row copy)
-                    with self._ahead_lock:
-                        a = self._enqueue_pick(pair, self._sample_counter, self._model_version, None)
-                    res, bad, best_vector = self._serve_ahead(a)
-                    self._sample_counter += self.num_samples
-                    if bad:
+                    if res.flags & ACQ_DOMAIN_ERR:
                         raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
                 else:
-                    cands, err = self.draw_candidates(pair, self.num_samples)
+                    cands = self.sample_candidates(pair['good'], self.num_samples)
                     res = pair.acquire(cands)
-                    if err is not None and bool(err.any()):
-                        raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
-                    best_vector = None
+                    best_vector = cands[res.index] if res.index >= 0 else None
                 if res.index < 0:
                     self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
                                       % self.num_samples)
                     sample = self.configspace.sample_configuration().get_dictionary()
                     info_dict['model_based_pick'] = False
                 else:
-                    if best_vector is None:
-                        best_vector = cands[res.index]
-                        if err is not None:
-                            best_vector = best_vector.cpu().numpy()
                     if self.logger.isEnabledFor(logging.DEBUG):  # (formatting the vector costs ~0.1 ms)
                         self.logger.debug('best_vector: {}, {}'.format(best_vector, res.score))
                     sample = ConfigSpace.Configuration(self.configspace, vector=best_vector).get_dictionary()
@@ -589,166 +486,50 @@ class BOHB(base_config_generator):
                                     % (self.num_samples, traceback.format_exc()))
                 sample = self.configspace.sample_configuration().get_dictionary()
                 info_dict['model_based_pick'] = False
-        self._last_call_version = self._model_version
-        self._launch_ahead("get_config")
         return sample, info_dict
 
-    # -- the next call computed ahead (GPU sampler) ----------------------------------------------
-    AHEAD_MIN_GAP_S = 40e-6  # ~ the device time of a 64-candidate draw + acquisition
-    def _ahead_enabled(self):
-        return self.sampler == "gpu" and self.speculative != "never"
-
-    def _launch_ahead(self, source):
-        """Enqueue the next get_config call's draws and acquisition (hbx_kde_acquire_ahead, no wait) on the
-        current model and sampler counter, unless that one is in flight already."""
-        if not self._ahead_enabled() or not self.kde_models or not self._ahead_on[source]:
-            return
-        if self.random_fraction > 0 and self._next_call_is_random():
-            return
-        with self._ahead_lock:
-            if not self._ahead_on[source]:
-                return
-            pair = self.kde_models[max(self.kde_models.keys())]
-            counter, version = self._sample_counter, self._model_version
-            a = self._ahead
-            if a is not None:
-                if a.pair is pair and a.counter == counter and a.version == version:
-                    return
-                self._drop_ahead(a)
-            if not getattr(pair, "_bound", None):
-                return
-            self._ahead = self._enqueue_pick(pair, counter, version, source)
-            self._ahead_stats["launched"] += 1
-
-    def _enqueue_pick(self, pair, counter, version, source):  # under the lock
-        """One call's draws on `counter` and its acquisition, published to a pooled mapped buffer."""
-        buf, keep = self._pick_buffer(pair)
-        self._pick_seq = self._pick_seq % 0x7FFFFFFF + 1
-        if not self._enqueue_pick_direct(pair, counter, keep, buf):
-            cands, _, err = pair['good'].sample(self.vartypes, self.bw_factor, self.num_samples, self.sampler_seed,
-                                                counter, out=keep[:3])
-            pair.acquire_ahead(cands, err, keep[3], buf, self._pick_seq)
-        return _Ahead(pair, counter, version, self._pick_seq, keep, buf, source, self._calls)
-
-    def _enqueue_pick_direct(self, pair, counter, keep, buf):
-        """The same two native calls (hbx_kde_sample, hbx_kde_acquire_ahead) without the wrappers' device
-        switch and argument checks, when they are not needed: the calling thread's current device is the
-        model's and the draw needs no Phi table.  False: take the wrapped path."""
-        g = pair.good
-        n = self.num_samples
-        if (pair._cur_dev is None or pair._raw_stream is None or pair._cur_dev() != pair._dev_index
-                or n >= 4 * g.nobs or not pair._bound):
-            return False
-        from ..kde import _levels_on_device
-        L = _native.lib()
-        lvb = getattr(self, "_lv_bytes", None)
-        if lvb is None:
-            self._lv_np = np.ascontiguousarray(self.vartypes, dtype=np.int32)
-            lvb = self._lv_bytes = self._lv_np.tobytes()
-            self._bw_off = int(L.hbx_kde_param_bw_offset())
-        lvd = _levels_on_device(lvb, self._lv_np, g.device)
-        cands, datum, err, ws = keep
-        sh = pair._raw_stream(pair._dev_index)
-        if sh != pair._home:
-            pair._order(sh)
-        _native.check(L.hbx_kde_sample(g.X_dev.data_ptr(), g.k_vars, g.rows_dev.data_ptr(), g.nobs,
-                                       g.params.data_ptr() + self._bw_off, lvd.data_ptr(), None, float(self.bw_factor),
-                                       int(self.sampler_seed) & (2 ** 64 - 1), int(counter) & (2 ** 64 - 1), 0, n,
-                                       cands.data_ptr(), datum.data_ptr(), err.data_ptr(), sh))
-        _native.check(L.hbx_kde_acquire_ahead(pair._bound, cands.data_ptr(), n, ws.data_ptr(), ws.numel(),
-                                              err.data_ptr(), buf, self._pick_seq, sh))
-        return True
-
-    def _next_call_is_random(self):
-        """A hint only: the next get_config's first draw (bohb.py:124, np.random.rand() < random_fraction)
-        read from a private copy of the global RNG as it stands -- a random pick would not use an
-        acquisition computed ahead.  Another draw before that call makes the hint wrong, never a result."""
-        g = _global_mt()
-        if g is None:
-            return False
-        pm = getattr(self, "_peek_mt", None)
-        if pm is None:
-            pm = self._peek_mt = _MT(np.random.RandomState())
-        pm.load(g.snap())
-        return pm.rs.rand() < self.random_fraction
-
-    def _drop_ahead(self, a):  # under the lock
-        """An unused one: wasted if nothing could have served it -- launched by a call (the next was a batch
-        or followed a result), or by a refit with no call since (a burst of results); a refit's that met
-        only random picks (bohb.py:124's random_fraction) was just not needed."""
-        self._ahead = None
-        # the pair stays referenced too: the dropped launch may still read its parameters, tables and rows
-        # (allocated on another thread's stream) until its completion word lands
-        self._pick_pending.append((a.buf, a.seq, a.keep, a.pair))
-        if a.source == "get_config" or self._calls == a.calls:
-            self._ahead_on[a.source] = False
-        self._ahead_stats["dropped"] += 1
-
-    def _pick_buffer(self, pair):  # under the lock
-        """A mapped output buffer and device tensors (candidates, datum, error flags, workspace) for one
-        computed-ahead call: reused once the device is done with them (a served call, or a dropped one whose
-        completion word has landed) -- no allocation per call."""
+    # -- one GPU-sampler call: draws and acquisition, one wait ----------------------------------------
+    def _pick(self, pair, counter):
+        """The call's num_samples draws on the Philox `counter` (hbx_kde_sample) and their acquisition with the
+        pick on the host (hbx_kde_acquire_bound with the draws' error flags and the winning row): (AcqResult,
+        winning row or None).  The draw buffers are kept per thread and reused; the native calls go straight
+        through when the thread's current device is the model's and the draw needs no Phi table."""
         import torch
-        still = []
-        for buf, seq, keep, pr in self._pick_pending:  # the device has finished with a dropped one
-            if ctypes.c_int32.from_address(buf + PICK_DONE).value == seq:
-                self._pick_free.append((buf, keep))
-            else:
-                still.append((buf, seq, keep, pr))
-        self._pick_pending = still
-        wsb = pair.workspace_bytes(self.num_samples)
-        dev = pair.good.device
-        if self._pick_free:
-            buf, keep = self._pick_free.pop()
+        g = pair.good
+        n, D = self.num_samples, len(self.vartypes)
+        t = self._pick_tls
+        keep = getattr(t, "keep", None)
+        wsb = pair.workspace_bytes(n)
+        if keep is None or keep[3].numel() < wsb or keep[0].device != g.device:
+            keep = t.keep = (torch.empty((n, D), dtype=torch.float64, device=g.device),
+                             torch.empty(n, dtype=torch.int64, device=g.device),
+                             torch.empty(n, dtype=torch.uint8, device=g.device),
+                             torch.empty(wsb, dtype=torch.uint8, device=g.device), np.empty(D))
+        cands, datum, err, ws, row = keep
+        if (pair._cur_dev is not None and pair._raw_stream is not None and pair._cur_dev() == pair._dev_index
+                and n < 4 * g.nobs):
+            from ..kde import _levels_on_device
+            L = _native.lib()
+            lvb = getattr(self, "_lv_bytes", None)
+            if lvb is None:
+                self._lv_np = np.ascontiguousarray(self.vartypes, dtype=np.int32)
+                lvb = self._lv_bytes = self._lv_np.tobytes()
+                self._bw_off = int(L.hbx_kde_param_bw_offset())
+            lvd = _levels_on_device(lvb, self._lv_np, g.device)
+            sh = pair._raw_stream(pair._dev_index)
+            if sh != pair._home:
+                pair._order(sh)
+            _native.check(L.hbx_kde_sample(g.X_dev.data_ptr(), g.k_vars, g.rows_dev.data_ptr(), g.nobs,
+                                           g.params.data_ptr() + self._bw_off, lvd.data_ptr(), None,
+                                           float(self.bw_factor), int(self.sampler_seed) & (2 ** 64 - 1),
+                                           int(counter) & (2 ** 64 - 1), 0, n, cands.data_ptr(), datum.data_ptr(),
+                                           err.data_ptr(), sh))
+            res = pair.acquire_pick(cands, err, ws, row, sh)
         else:
-            buf, keep = _PICKS.get(PICK_ROW + 8 * len(self.vartypes)), None
-        if keep is None or keep[3].numel() < wsb or keep[0].device != torch.device(dev):
-            n, D = self.num_samples, len(self.vartypes)
-            keep = (torch.empty((n, D), dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
-                    torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(wsb, dtype=torch.uint8, device=dev))
-        ctypes.c_int32.from_address(buf + PICK_DONE).value = 0
-        return buf, keep
-
-    def _take_ahead(self, pair):
-        """The computed-ahead acquisition when it is exactly this call's (same model, version and counter)."""
-        with self._ahead_lock:
-            a = self._ahead
-            if a is None:
-                return None
-            if a.pair is pair and a.counter == self._sample_counter and a.version == self._model_version:
-                self._ahead = None
-                return a
-            self._drop_ahead(a)
-            return None
-
-    def _serve_ahead(self, a):
-        """(record, any domain error, winning row) of a computed-ahead acquisition, once the device is done."""
-        L = _native.lib()
-        _native.check(L.hbx_wait_word(a.buf + PICK_DONE, a.seq, _native.stream_handle(None, a.pair.good.device)))
-        res = AcqResult.from_bytes(ctypes.string_at(a.buf, RESULT_BYTES))
-        bad = ctypes.c_int32.from_address(a.buf + PICK_ERR).value != 0
-        row = None
-        if res.index >= 0:
-            row = np.frombuffer(ctypes.string_at(a.buf + PICK_ROW, 8 * len(self.vartypes)), dtype=np.float64).copy()
-        with self._ahead_lock:
-            self._pick_free.append((a.buf, a.keep))
-            if a.source is not None:  # computed ahead (None: the call's own)
-                self._ahead_on[a.source] = True
-                self._ahead_stats["served"] += 1
-        return res, bad, row
-
-    def __del__(self):  # the mapped buffers back to the process-wide pool (no synchronisation)
-        try:
-            nb = PICK_ROW + 8 * len(self.vartypes)
-            for b, _ in getattr(self, "_pick_free", []):
-                _PICKS.put(b, nb)
-            for b, seq, _, _ in getattr(self, "_pick_pending", []):
-                _PICKS.put(b, nb, seq)
-            a = getattr(self, "_ahead", None)
-            if a is not None:
-                _PICKS.put(a.buf, nb, a.seq)
-        except Exception:
-            pass
+            with _native.on_device(g.device):
+                g.sample(self.vartypes, self.bw_factor, n, self.sampler_seed, counter, out=keep[:3])
+                res = pair.acquire_pick(cands, err, ws, row)
+        return res, (row.copy() if res.index >= 0 else None)
 
     # -- several get_config calls in one GPU pass (SURVEY 8f row 1) ----------------------------
     def speculation_enabled(self):
@@ -913,9 +694,6 @@ class BOHB(base_config_generator):
             return
         self.kde_models[budget] = pair  # atomic swap: a concurrent get_config keeps its snapshot
         self._model_version += 1
-        if self._gap is None or self._gap >= self.AHEAD_MIN_GAP_S:
-            self._launch_ahead("new_result")
-        self._result_end = time.perf_counter()
         if self.logger.isEnabledFor(logging.DEBUG):
             self.logger.debug('done building a new model for budget %f based on %i/%i split\nBest loss for this '
                               'budget:%f\n\n\n\n\n' % (budget, pair.good.nobs, pair.bad.nobs,

@@ -1707,8 +1707,12 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
   return s < INFINITY && s <= best * (1.0 + 1.0001 * (rp + rb));
 }
 
-// A get_config pick published to device-mapped host memory by the final argmin (hbx_kde_acquire_ahead):
-// the record, whether any of the call's candidates hit a sampler domain error, the winning row
+// A get_config pick published to device-mapped host memory by the final argmin (hbx_kde_acquire_bound with err /
+// row_out): the record, whether any of the call's candidates hit a sampler domain error, the winning row,
+// then the completion word (byte offsets below)
+#define HBX_PICK_ERR 48
+#define HBX_PICK_DONE 52
+#define HBX_PICK_ROW 64
 struct PickOut {
   const double* cand;
   const uint8_t* err;  // nullable
@@ -1847,7 +1851,7 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     __syncthreads();
     uint32_t* out = pick.out ? (uint32_t*)pick.out : (uint32_t*)host_res;
     if (threadIdx.x < (int)(sizeof(AcqResult) / 4)) hbx_publish_store(out + threadIdx.x, ((const uint32_t*)&rec_sh)[threadIdx.x]);
-    if (pick.out) {  // hbx_kde_acquire_ahead: + the domain-error flag and the winning row
+    if (pick.out) {  // a pick: + the domain-error flag and the winning row
       if (threadIdx.x == 0) hbx_publish_store(out + HBX_PICK_ERR / 4, err_any ? 1u : 0u);
       const int64_t idx = rec_sh.index - index_base;
       if (rec_sh.index >= 0 && idx < pick.Nc)
@@ -2324,7 +2328,7 @@ extern "C" {
 
 int64_t hbx_kde_refit_out_bytes(int64_t n, int32_t D) { return (int64_t)refit_out_layout(n, D).total; }
 int64_t hbx_kde_refit_scratch_bytes(int64_t n, int32_t D) {
-  // metadata | sort scratch | host rows staged to the device (hbx_kde_refit_host_rows, beyond the inline copy)
+  // metadata | sort scratch | host rows staged to the device (hbx_kde_refit_sync, beyond the inline copy)
   return (int64_t)refit_meta_bytes() + ((hbx_sort_scratch_bytes(n) + 15) & ~(int64_t)15) + 8 * n * ((int64_t)D + 1);
 }
 
@@ -2347,18 +2351,6 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
                   float* table_good, int64_t table_good_floats, void* params_bad, float* table_bad,
                   int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream) {
   return refit_impl(X, loss, n, D, vartype, staged, false, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
-                    table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
-                    stream);
-}
-
-// The same with the appended rows in HOST memory (rows then losses, n_new (D + 1) doubles): up to 256 doubles
-// ride in the kernel arguments of the one-launch refit (no copy at all); more are copied into the scratch.
-int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
-                            const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
-                            double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
-                            void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
-                            int64_t scratch_bytes, void* stream) {
-  return refit_impl(X, loss, n, D, vartype, staged_host, true, n_new, n_good, n_bad, fac_good, fac_bad, params_good,
                     table_good, table_good_floats, params_bad, table_bad, table_bad_floats, out, scratch, scratch_bytes,
                     stream);
 }
@@ -2432,7 +2424,9 @@ static int refit_mapped_buffer(int64_t bytes, RefitMapped** out) {
 
 extern "C" {
 
-// hbx_kde_refit_host_rows, then the output block in host memory (out_host, hbx_kde_refit_out_bytes) when the
+// hbx_kde_refit with the appended rows in HOST memory (rows then losses, n_new (D + 1) doubles: up to 256
+// doubles ride in the first launch's kernel arguments, no copy; more go through the scratch), then the output
+// block in host memory (out_host, hbx_kde_refit_out_bytes) when the
 // call returns: the preparation's launches publish it to a device-mapped host buffer, every 32-bit word as a
 // flagged word carrying the call's sequence number (the parameter launch the rows, bandwidths and level counts,
 // the finishing blocks the info records; PrepPub), and the call spins until every word carries it -- no copy
@@ -2508,7 +2502,7 @@ int hbx_stream_order(void* waiter, void* signaller) {
 }  // extern "C"
 
 
-// hbx_kde_refit / hbx_kde_refit_host_rows (staged_host: the appended rows are in host memory)
+// hbx_kde_refit / hbx_kde_refit_sync (staged_host: the appended rows are in host memory)
 static int refit_impl(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype, const double* staged,
                       bool staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad,
                       void* params_good, float* table_good, int64_t table_good_floats, void* params_bad,
@@ -3570,33 +3564,6 @@ int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) 
   return HBX_OK;
 }
 
-// hbx_kde_acquire whose final kernel also stores the record (48 bytes) into this thread's mapped host buffer
-// and a completion word last; the call spins on that word and copies the record to rec_out (host memory):
-// the acquisition and the record on the host in one call, no copy kernel, no blocking synchronisation.
-int hbx_kde_acquire_host(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
-                         const void* params_good, const float* table_good, const double* X_good,
-                         const int64_t* rows_good, int32_t variant_good,
-                         const void* params_bad, const float* table_bad, const double* X_bad,
-                         const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
-                         int64_t nmax, void* workspace, int64_t ws_bytes, void* events, void* stream,
-                         void* rec_out) {
-  if (!rec_out) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_host: null record");
-  char* mapped = nullptr;
-  int rc = mapped_buffer(&mapped);
-  if (rc) return rc;
-  int32_t* done = (int32_t*)(mapped + FETCH_MAPPED_BYTES);
-  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
-  rc = acquire_impl("hbx_kde_acquire_host", cand, Nc, Nc > 0 ? Nc : 1, D, index_base, params_good, table_good,
-                    X_good, rows_good, variant_good, params_bad, table_bad, X_bad, rows_bad, variant_bad, dc_pad,
-                    du_pad, nmax, nullptr, nullptr, nullptr, workspace, ws_bytes, events, stream, (AcqResult*)mapped,
-                    done, seq);
-  if (rc) return rc;
-  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_acquire_host");
-  if (rc) return rc;
-  memcpy(rec_out, mapped, sizeof(AcqResult));
-  return HBX_OK;
-}
-
 struct KdePairBinding {
   int32_t D;
   const void* params_good;
@@ -3627,32 +3594,40 @@ void* hbx_kde_pair_bind(int32_t D, const void* params_good, const float* table_g
   return b;
 }
 
+// The drop-in's synchronous acquisition on a bound pair: the final kernel stores the 48-byte record into this
+// thread's mapped host buffer and a completion word last; the call spins on that word and copies the record to
+// rec_out -- the acquisition and its pick on the host in one call, no copy kernel, no blocking synchronisation.
+// err (nullable, device u8[Nc]: the GPU sampler's domain-error flags) sets HBX_ACQ_DOMAIN_ERR in the record
+// when any is set; row_out (nullable, host f64[D]) receives the winning candidate's row -- both published by
+// the same final kernel with the record (one wait for the draws' check, the pick and its row).
 int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int64_t index_base, void* workspace,
-                          int64_t ws_bytes, void* stream, void* rec_out) {
-  if (!pair) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_bound: null pair");
+                          int64_t ws_bytes, const uint8_t* err, void* events, void* stream, void* rec_out,
+                          double* row_out) {
+  if (!pair || !rec_out || Nc < 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_bound: bad arguments");
   const KdePairBinding& b = *(const KdePairBinding*)pair;
-  return hbx_kde_acquire_host(cand, Nc, b.D, index_base, b.params_good, b.table_good, b.X_good, b.rows_good,
-                              b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad, b.variant_bad, b.dc_pad,
-                              b.du_pad, b.nmax, workspace, ws_bytes, nullptr, stream, rec_out);
+  char* mapped = nullptr;
+  int rc = mapped_buffer(&mapped);
+  if (rc) return rc;
+  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
+  const bool pick = err || row_out;  // (HBX_PICK_ROW + 8 D <= FETCH_MAPPED_BYTES for D <= HBX_MAX_D)
+  int32_t* done = pick ? (int32_t*)(mapped + HBX_PICK_DONE) : (int32_t*)(mapped + FETCH_MAPPED_BYTES);
+  rc = acquire_impl("hbx_kde_acquire_bound", cand, Nc, Nc > 0 ? Nc : 1, b.D, index_base, b.params_good, b.table_good,
+                    b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad, b.variant_bad,
+                    b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes, events, stream,
+                    pick ? nullptr : (AcqResult*)mapped, pick ? nullptr : done, seq,
+                    pick ? PickOut{cand, err, Nc, b.D, mapped} : PickOut{});
+  if (rc) return rc;
+  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_acquire_bound");
+  if (rc) return rc;
+  AcqResult r;
+  memcpy(&r, mapped, sizeof(AcqResult));
+  if (pick && *(const int32_t*)(mapped + HBX_PICK_ERR)) r.flags |= HBX_ACQ_DOMAIN_ERR;
+  memcpy(rec_out, &r, sizeof(AcqResult));
+  if (row_out && r.index >= 0) memcpy(row_out, mapped + HBX_PICK_ROW, 8 * (size_t)b.D);
+  return HBX_OK;
 }
 
 void hbx_kde_pair_free(void* pair) { delete (KdePairBinding*)pair; }
-
-int hbx_kde_acquire_ahead(const void* pair, const double* cand, int64_t Nc, void* workspace, int64_t ws_bytes,
-                          const uint8_t* err, void* out, int32_t seq, void* stream) {
-  if (!pair || !out || Nc < 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_ahead: bad arguments");
-  const KdePairBinding& b = *(const KdePairBinding*)pair;
-  // the final argmin publishes the pick itself (record, error flag, winning row, completion word)
-  return acquire_impl("hbx_kde_acquire_ahead", cand, Nc, Nc > 0 ? Nc : 1, b.D, 0, b.params_good, b.table_good,
-                      b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad,
-                      b.variant_bad, b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes,
-                      nullptr, stream, nullptr, nullptr, seq, PickOut{cand, err, Nc, b.D, (char*)out});
-}
-
-int hbx_wait_word(const void* word, int32_t seq, void* stream) {
-  if (!word) return hbx_fail(HBX_ERR_ARG, "hbx_wait_word: null word");
-  return wait_done((int32_t*)word, seq, (hipStream_t)stream, "hbx_wait_word");
-}
 
 // numpy's float64 exp (hbx_npexp.h) element-wise: the known-answer check of the exact re-score's exp
 __global__ void np_exp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {

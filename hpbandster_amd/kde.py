@@ -23,7 +23,7 @@ from . import _native as N
 
 RESULT_FMT = "<qdfiiidd"  # AcqResult: index, score, rel, flags, shortlist, near, pdf_l, pdf_g
 RESULT_BYTES = struct.calcsize(RESULT_FMT)
-ACQ_OVERFLOW, ACQ_NEAR_TIE, ACQ_RESOLVED = 1, 2, 4  # include/hbx.h HBX_ACQ_*
+ACQ_OVERFLOW, ACQ_NEAR_TIE, ACQ_RESOLVED, ACQ_DOMAIN_ERR = 1, 2, 4, 8  # include/hbx.h HBX_ACQ_*
 
 
 def _torch():
@@ -69,7 +69,7 @@ _pinned_tls = threading.local()
 
 
 def _record_buffer():
-    """This thread's host buffer for one result record (hbx_kde_acquire_host writes it)."""
+    """This thread's host buffer for one result record (hbx_kde_acquire_bound writes it)."""
     import ctypes
     b = getattr(_pinned_tls, "rec", None)
     if b is None:
@@ -376,13 +376,10 @@ class KDEPair(object):
         self._dev_index = dev.index if dev.index is not None else _torch().cuda.current_device()
         self._cur_dev, self._raw_stream = _torch_fast_fns()
         L = N.lib()
-        self._host_fn = L.hbx_kde_acquire_host
         self._ws_cache = {}  # (thread, Nc) -> workspace of synchronous calls made without one
-        # the fixed arguments bound once on the native side: the synchronous call converts 8 arguments
-        # instead of 22 (hbx_kde_acquire_bound)
+        # the fixed arguments bound once on the native side: the synchronous call converts 11 arguments
+        # instead of 25 (hbx_kde_acquire_bound)
         self._bound = None
-        if N.DIAGNOSTIC_BUILD and not hasattr(L, "hbx_kde_pair_bind"):
-            return  # an older diagnostic build (A/B runs): the unbound call
         self._bound_fn = L.hbx_kde_acquire_bound
         self._free_fn = L.hbx_kde_pair_free
         self._bound = L.hbx_kde_pair_bind(good.k_vars, *self._kde_args)
@@ -451,7 +448,7 @@ class KDEPair(object):
     def _acquire_sync(self, cands, index_base, workspace, events):
         """The drop-in's common call -- synchronous, the winner only, on the model's device and its current
         stream, which is this thread's current device (no device switch): one native call
-        (hbx_kde_acquire_host) with the fewest host steps around it; a workspace is kept per thread and
+        (hbx_kde_acquire_bound) with the fewest host steps around it; a workspace is kept per thread and
         candidate count when none is given.  None when the candidates need staging (host arrays, other
         dtypes): the general path then runs."""
         torch = _torch()
@@ -477,12 +474,8 @@ class KDEPair(object):
         sh = self._raw_stream(self._dev_index)
         if sh != self._home:
             self._order(sh)
-        if events is None and self._bound:
-            N.check(self._bound_fn(self._bound, cands.data_ptr(), Nc, int(index_base), workspace.data_ptr(), n, sh,
-                                   rec))
-        else:
-            N.check(self._host_fn(cands.data_ptr(), Nc, D, int(index_base), *self._kde_args, workspace.data_ptr(), n,
-                                  events.address if events is not None else None, sh, rec))
+        N.check(self._bound_fn(self._bound, cands.data_ptr(), Nc, int(index_base), workspace.data_ptr(), n, None,
+                               events.address if events is not None else None, sh, rec, None))
         return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def _acquire(self, cands, index_base, logs, stream, workspace, sync, events, ties):
@@ -510,8 +503,8 @@ class KDEPair(object):
         self._order(sh)
         if sync and not logs:  # one native call: the acquisition and its record on the host
             rec = _record_buffer()
-            N.check(L.hbx_kde_acquire_host(c_dev.data_ptr(), Nc, D, int(index_base), *self._kde_args, wsp,
-                                           ws.numel(), events.address if events is not None else None, sh, rec))
+            N.check(self._bound_fn(self._bound, c_dev.data_ptr(), Nc, int(index_base), wsp, ws.numel(), None,
+                                   events.address if events is not None else None, sh, rec, None))
             res = AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
             if ties == "process" and res.flags & ACQ_NEAR_TIE:
                 self._resolve(res, ws, Nc, Nc, cands if isinstance(cands, np.ndarray) else c_dev, int(index_base))
@@ -565,20 +558,21 @@ class KDEPair(object):
                 r.index, r.score, r.pdf_l, r.pdf_g = pick[0] - b * seg, pick[1], pick[2], pick[3]
             r.flags |= ACQ_RESOLVED
 
-    def acquire_ahead(self, cands, err, workspace, out, seq):
-        """Enqueue the acquisition of ``cands`` (a device [Nc, D] f64 tensor) without waiting: the device
-        stores into ``out`` (device-mapped host memory, hbx_host_alloc) the record, the domain-error flag
-        of ``err`` (the sampler's per-candidate flags, or None) and the winning row, then the completion
-        word ``seq`` (include/hbx.h hbx_kde_acquire_ahead).  The tensors and ``out`` stay in use until the
-        word is seen."""
-        if not self._bound:
-            raise N.HbxError("acquire_ahead needs the bound pair entry")
-        with N.on_device(self.good.device):
+    def acquire_pick(self, cands, err, workspace, row, sh=None):
+        """One synchronous acquisition of ``cands`` (a device [Nc, D] f64 tensor on the model's device) with its
+        whole pick on the host after ONE wait (hbx_kde_acquire_bound with err and row_out): the record, whether
+        any ``err`` flag (the GPU sampler's per-candidate domain errors, a device u8 tensor or None) is set
+        (ACQ_DOMAIN_ERR in ``flags``), and the winning row written into ``row`` (a host f64 array of D).
+        ``sh``: the stream handle (default: the device's current stream).  Returns the AcqResult."""
+        if sh is None:
             sh = N.stream_handle(None, self.good.device)
+        if sh != self._home:
             self._order(sh)
-            N.check(N.lib().hbx_kde_acquire_ahead(self._bound, cands.data_ptr(), int(cands.shape[0]),
-                                                  workspace.data_ptr(), workspace.numel(),
-                                                  err.data_ptr() if err is not None else None, out, int(seq), sh))
+        rec = _record_buffer()
+        N.check(self._bound_fn(self._bound, cands.data_ptr(), int(cands.shape[0]), 0, workspace.data_ptr(),
+                               workspace.numel(), err.data_ptr() if err is not None else None, None, sh, rec,
+                               row.ctypes.data))
+        return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def batch_workspace_bytes(self, Nc, seg):
         return int(N.lib().hbx_kde_batch_workspace_bytes(int(Nc), int(seg), self.nmax))

@@ -15,7 +15,6 @@
  *   hbx_seg_argsort(_ex) + hbx_kde_fit <- bohb.py:220-246 (BOHB.new_result refit:
  *                                      np.argsort + sm.nonparametric.KDEMultivariate(..,'normal_reference'))
  *   hbx_kde_refit                   <- bohb.py:211-251 (the same refit plus both KDEs' preparation, one call)
- *   hbx_kde_refit_host_rows         <- bohb.py:211-251 (the same, new rows from host memory: no copy for one row)
  *   hbx_kde_refit_sync              <- bohb.py:211-251 (the same, the output block on the host when it returns)
  *   hbx_kde_prepare                 <- KDEMultivariate.__init__ model state (statsmodels 0.12.2
  *                                      kernel_density.py:101-115)
@@ -106,15 +105,9 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
                   int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good, double fac_bad, void* params_good,
                   float* table_good, int64_t table_good_floats, void* params_bad, float* table_bad,
                   int64_t table_bad_floats, void* out, void* scratch, int64_t scratch_bytes, void* stream);
-/* The same with `staged_host` in HOST memory (rows, then losses: n_new*(D+1) doubles).  Up to 256 staged
- * doubles of a budget of at most 1024 rows ride in the kernel arguments of the refit's first launch (no
- * host-to-device copy); more go through `scratch`. */
-int hbx_kde_refit_host_rows(double* X, double* loss, int64_t n, int32_t D, const int32_t* vartype,
-                            const double* staged_host, int64_t n_new, int64_t n_good, int64_t n_bad, double fac_good,
-                            double fac_bad, void* params_good, float* table_good, int64_t table_good_floats,
-                            void* params_bad, float* table_bad, int64_t table_bad_floats, void* out, void* scratch,
-                            int64_t scratch_bytes, void* stream);
-/* hbx_kde_refit_host_rows, synchronous: when the call returns, `out_host` (host memory,
+/* hbx_kde_refit with `staged_host` in HOST memory (rows, then losses: n_new*(D+1) doubles; up to 256 staged
+ * doubles of a budget of at most 1024 rows ride in the kernel arguments of the refit's first launch, no
+ * host-to-device copy; more go through `scratch`), synchronous: when the call returns, `out_host` (host memory,
  * hbx_kde_refit_out_bytes) holds the output block.  The preparation's launches publish it to a device-mapped
  * host buffer, every 32-bit word as an 8-byte word flagged with the call's sequence number, and the call spins
  * until every word carries it (no copy launch, no blocking stream synchronisation).  The prepared models are
@@ -175,49 +168,27 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
                     int64_t nmax, float* logl_out, float* logg_out, void* workspace, int64_t ws_bytes,
                     void* events, void* stream);
 
-/* hbx_kde_acquire with the record delivered to the host in the same call (bohb.py:124-169 returns the pick
- * to get_config's caller): the final kernel also stores the 48-byte record into this thread's
- * device-mapped host buffer and a completion word last; the call spins on that word (bounded, then it
- * synchronises `stream`) and copies the record to rec_out (host memory, 48 bytes).  No ln-pdf outputs (the
- * fast scoring instances).  The record also stays in the workspace (hbx_kde_result_ptr). */
-int hbx_kde_acquire_host(const double* cand, int64_t Nc, int32_t D, int64_t index_base,
-                         const void* params_good, const float* table_good, const double* X_good,
-                         const int64_t* rows_good, int32_t variant_good,
-                         const void* params_bad, const float* table_bad, const double* X_bad,
-                         const int64_t* rows_bad, int32_t variant_bad, int32_t dc_pad, int32_t du_pad,
-                         int64_t nmax, void* workspace, int64_t ws_bytes, void* events, void* stream,
-                         void* rec_out);
-
-/* hbx_kde_acquire_host with the KDE pair's fixed arguments (params_good .. nmax, and D) bound once: the
- * drop-in binds each model it fits (bohb.py:248-251 replaces the pair on every refit) and its get_config
- * passes only what changes per call -- 8 arguments for the FFI to convert instead of 22 (about 2 us of host
- * time per acquisition, on the critical path of every call).  The handle holds the pointers only: the caller
- * keeps the KDEs' device buffers alive while it is in use, and frees it with hbx_kde_pair_free.  NULL on
- * bad arguments (hbx_last_error). */
+/* The synchronous acquisition (bohb.py:124-169 returns the pick to get_config's caller) on a KDE pair whose
+ * fixed arguments (D, params_good .. nmax) are bound once: the drop-in binds each model it fits
+ * (bohb.py:248-251 replaces the pair on every refit), and a call passes only what changes -- about 2 us less
+ * host time per acquisition than converting all of them.  The handle holds the pointers only: the caller keeps
+ * the KDEs' device buffers alive while it is in use, and frees it with hbx_kde_pair_free.  NULL on bad
+ * arguments (hbx_last_error).
+ * hbx_kde_acquire_bound: hbx_kde_acquire (fast scoring instances, no ln-pdf outputs) whose final kernel also
+ * stores the 48-byte record into this thread's device-mapped host buffer and a completion word last; the call
+ * spins on that word (bounded, then it synchronises `stream`) and copies the record to rec_out (host, 48 bytes;
+ * it also stays in the workspace, hbx_kde_result_ptr).  err (nullable, device u8[Nc], the GPU sampler's
+ * domain-error flags): HBX_ACQ_DOMAIN_ERR is set in the record when any flag is set.  row_out (nullable, host
+ * f64[D]): the winning candidate's row.  Both come with the record from the same final kernel: one wait for
+ * the whole pick.  events: NULL or hipEvent_t[3] (hbx_kde_acquire). */
 void* hbx_kde_pair_bind(int32_t D, const void* params_good, const float* table_good, const double* X_good,
                         const int64_t* rows_good, int32_t variant_good, const void* params_bad,
                         const float* table_bad, const double* X_bad, const int64_t* rows_bad, int32_t variant_bad,
                         int32_t dc_pad, int32_t du_pad, int64_t nmax);
 int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int64_t index_base, void* workspace,
-                          int64_t ws_bytes, void* stream, void* rec_out);
+                          int64_t ws_bytes, const uint8_t* err, void* events, void* stream, void* rec_out,
+                          double* row_out);
 void hbx_kde_pair_free(void* pair);
-
-/* One get_config's acquisition enqueued AHEAD of the call (bohb.py:124-169 computed before it is asked for:
- * BOHB launches the next call's acquisition right after a refit or a served call, and serves it only if the
- * model and the sampler's counter are unchanged when the call comes).  Returns once enqueued on `stream`;
- * the device then stores into `out` (device-mapped host memory, hbx_host_alloc, >= HBX_PICK_ROW + 8 D
- * bytes): the 48-byte record (index relative to the candidate set), at HBX_PICK_ERR an int32 = 1 when any
- * err[0 .. Nc) byte is set (err nullable: the GPU sampler's domain-error flags), the winning row's D
- * doubles at HBX_PICK_ROW, and last the completion word `seq` at HBX_PICK_DONE.  The workspace, the
- * candidates and `out` stay in use until that word is seen (hbx_wait_word). */
-#define HBX_PICK_ERR 48
-#define HBX_PICK_DONE 52
-#define HBX_PICK_ROW 64
-int hbx_kde_acquire_ahead(const void* pair, const double* cand, int64_t Nc, void* workspace, int64_t ws_bytes,
-                          const uint8_t* err, void* out, int32_t seq, void* stream);
-/* Spin until the int32 at `word` (device-mapped host memory) equals seq; bounded, then `stream` is
- * synchronised and the word checked once more (error if it still differs). */
-int hbx_wait_word(const void* word, int32_t seq, void* stream);
 
 /* Batched acquisition: B = ceil(Nc / seg) independent get_config calls against the same model in one
  * pass (replaces B sequential runs of the bohb.py:124-169 loop, as an SH stage issues
@@ -260,6 +231,7 @@ int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
 #define HBX_ACQ_OVERFLOW 1
 #define HBX_ACQ_NEAR_TIE 2
 #define HBX_ACQ_RESOLVED 4
+#define HBX_ACQ_DOMAIN_ERR 8  /* hbx_kde_acquire_bound with err: a candidate's draw hit a domain error */
 void* hbx_kde_result_ptr(void* workspace);
 /* Byte offsets of [shortlist count (i32), shortlist (i32 candidate indices), near list, exact l (f64),
  * exact g (f64)] inside the workspace of an acquisition over (Nc, seg, nmax) candidates (seg = Nc for

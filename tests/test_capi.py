@@ -86,5 +86,5 @@ def test_pair_binding_host_side():
     assert b"hbx_kde_pair_bind" in L.hbx_last_error()
     assert not L.hbx_kde_pair_bind(32, None, 2, 3, 4, 0, 5, 6, 7, 8, 0, 24, 8, 10000)
     rec = ctypes.create_string_buffer(64)
-    assert L.hbx_kde_acquire_bound(None, None, 0, 0, None, 0, None, rec) != 0
+    assert L.hbx_kde_acquire_bound(None, None, 0, 0, None, 0, None, None, None, rec, None) != 0
     L.hbx_kde_pair_free(None)

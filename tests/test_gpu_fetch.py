@@ -1,4 +1,4 @@
-"""hbx_fetch (include/hbx.h) and hbx_kde_acquire_host: device bytes to the host without a blocking
+"""hbx_fetch (include/hbx.h) and hbx_kde_acquire_bound: device bytes to the host without a blocking
 synchronisation -- through the thread's mapped buffer (<= 4096 aligned bytes, a completion word) or a
 copy plus stream polling (larger / unaligned) -- and the acquisition whose final kernel stores its record
 into mapped memory: the same bytes as the workspace's record."""
@@ -55,7 +55,7 @@ def test_acquire_host_record_equals_workspace_record(device):
     pair = kde.fit_pair(X, S.make_losses(800, seed=6), S.var_type_string(6, 2), 9, device=device)
     C = torch.from_numpy(S.make_candidates(3000, 6, 2, 3, seed=7)).to(device)
     ws = torch.empty(pair.workspace_bytes(3000), dtype=torch.uint8, device=device)
-    r_host = pair.acquire(C, workspace=ws, index_base=11)  # hbx_kde_acquire_host
+    r_host = pair.acquire(C, workspace=ws, index_base=11)  # hbx_kde_acquire_bound
     off = pair.result_offset()
     r_ws = kde.AcqResult.from_bytes(ws[off:off + kde.RESULT_BYTES].cpu().numpy().tobytes())
     r_async = kde.AcqResult.from_bytes(kde.fetch_bytes(pair.acquire(C, workspace=ws, index_base=11, sync=False)))
@@ -66,10 +66,12 @@ def test_acquire_host_record_equals_workspace_record(device):
     assert empty.index == -1
 
 
-def test_bound_pair_record_equals_unbound(device):
-    """hbx_kde_acquire_bound (the drop-in's synchronous call: the pair's fixed arguments bound once) stores
-    the same 48 bytes as hbx_kde_acquire_host with every argument passed, and the record published to mapped
-    memory equals the workspace's -- over many back-to-back calls (the completion word per call)."""
+def test_bound_pair_record_equals_the_async_record(device):
+    """hbx_kde_acquire_bound (the drop-in's synchronous call: the pair's fixed arguments bound once) stores the
+    same 48 bytes as hbx_kde_acquire with every argument passed (fetched from its workspace), and the record
+    published to mapped memory equals the workspace's -- over many back-to-back calls (the completion word per
+    call); with err and row_out (one wait for the whole pick) the record is the same, the row is the winner's,
+    and a set error flag comes back as HBX_ACQ_DOMAIN_ERR."""
     import torch
     from hpbandster_amd import _native as N
     from hpbandster_amd import kde
@@ -81,13 +83,25 @@ def test_bound_pair_record_equals_unbound(device):
     L = N.lib()
     sh = N.stream_handle(None, device)
     off = pair.result_offset()
+    err = torch.zeros(20000, dtype=torch.uint8, device=device)
     for base in (0, 5, 1 << 33):
-        a, b = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
-        N.check(L.hbx_kde_acquire_bound(pair._bound, C.data_ptr(), 20000, base, ws.data_ptr(), ws.numel(), sh, a))
+        a, c = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
+        N.check(L.hbx_kde_acquire_bound(pair._bound, C.data_ptr(), 20000, base, ws.data_ptr(), ws.numel(), None,
+                                        None, sh, a, None))
         w = ws[off:off + kde.RESULT_BYTES].cpu().numpy().tobytes()
-        N.check(L.hbx_kde_acquire_host(C.data_ptr(), 20000, 32, base, *pair._kde_args, ws.data_ptr(), ws.numel(),
-                                       None, sh, b))
-        assert a.raw[:kde.RESULT_BYTES] == b.raw[:kde.RESULT_BYTES] == w
-        assert kde.AcqResult.from_bytes(a.raw[:kde.RESULT_BYTES]).index >= base
+        N.check(L.hbx_kde_acquire(C.data_ptr(), 20000, 32, base, *pair._kde_args, None, None, ws.data_ptr(),
+                                  ws.numel(), None, sh))
+        b = kde.fetch_bytes(ws[off:off + kde.RESULT_BYTES])
+        assert a.raw[:kde.RESULT_BYTES] == b == w
+        r = kde.AcqResult.from_bytes(a.raw[:kde.RESULT_BYTES])
+        assert r.index >= base
+        row = np.full(32, np.nan)
+        N.check(L.hbx_kde_acquire_bound(pair._bound, C.data_ptr(), 20000, base, ws.data_ptr(), ws.numel(),
+                                        err.data_ptr(), None, sh, c, row.ctypes.data))
+        assert c.raw[:kde.RESULT_BYTES] == a.raw[:kde.RESULT_BYTES]
+        np.testing.assert_array_equal(row, C[r.index - base].cpu().numpy())
+    err[17] = 1
+    rec = pair.acquire_pick(C, err, ws, row)
+    assert rec.flags & kde.ACQ_DOMAIN_ERR and rec.index == r.index - (1 << 33)
     seen = {pair.acquire(C[i * 1000:(i + 1) * 1000]).index for i in range(20)}
     assert len(seen) > 1 and min(seen) >= 0

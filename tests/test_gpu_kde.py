@@ -577,16 +577,20 @@ def _capi_logpdf_rtol(k, C, rtol=1e-5):
     return out.cpu().numpy()
 
 
+@pytest.mark.parametrize("lut", ["1", "0"])
 @pytest.mark.parametrize("rtol", [1e-5, 1e-9])
 @pytest.mark.parametrize("case", ["outlier", "d46", "signed", "d32m", "far24c8u", "cat_only"])
-def test_capi_logpdf_rtol_contract(device, case, rtol):
+def test_capi_logpdf_rtol_contract(device, case, rtol, lut, monkeypatch):
     """The north-star ln-pdf contract at the C-ABI (not through DeviceKDE): within rtol * max(1, |ln p|)
     of the reference's ln pdf for every candidate where that is finite, NaN where it is NaN -- next to an
     outlying observation, at D = 46, on a KDE with negative categorical factors, and at config #3's shape.
     rtol 1e-5 (the north star's): the fp32 direct-difference pass writes the candidates its bound accepts;
-    rtol 1e-9: its bound accepts none, and every candidate takes the fp64 pass (tiled kernel, fp64 exp2)."""
+    rtol 1e-9: its bound accepts none, and every candidate takes the fp64 pass (tiled kernel, fp64 exp2).
+    lut: the direct-difference pass matches categorical codes through its LDS tables (HBX_DD_LUT=1, KDEs whose
+    codes fit two bits) or through the packed compare (0)."""
     from hpbandster_amd import kde
     from hpbandster_amd import synthetic as S
+    monkeypatch.setenv("HBX_DD_LUT", lut)
     rs = np.random.RandomState(11)
     if case == "outlier":
         n, D = 8500, 16
@@ -633,6 +637,40 @@ def test_capi_logpdf_rtol_contract(device, case, rtol):
         err = np.abs(got[fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
         # the oracle's log-space restatement is itself ~1e-13 from the reference's fp64 value
         assert err.max() <= max(rtol, 2e-12), (case, err.max())
+
+
+@pytest.mark.parametrize("lut", ["1", "0"])
+@pytest.mark.parametrize("du", [0, 4, 8])
+def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, monkeypatch):
+    """Candidates that sit on an observation of a later chunk while every observation of chunk 0 is thousands of
+    log2 units away: the group holding that observation overflows the first chunk's reference point, which moves
+    up and the group is summed again; candidates with codes outside [0, 3] take the fp64 pass under the tables.
+    Every ln pdf within the contract of the oracle's."""
+    from hpbandster_amd import kde
+    monkeypatch.setenv("HBX_DD_LUT", lut)
+    rs = np.random.RandomState(41)
+    n, dc = 700, 24
+    vt = "c" * dc + "u" * du
+    X = np.empty((n, dc + du))
+    X[:, :dc] = rs.rand(n, dc)
+    X[:64, :dc] = 0.95 + 0.01 * rs.rand(64, dc)  # chunk 0: one far cluster
+    X[:, dc:] = rs.randint(0, 4, (n, du))
+    C = X[rs.choice(np.arange(64, n), 96, replace=False)].copy()
+    C[:8, :dc] += 1e-3 * rs.rand(8, dc)
+    if du:
+        C[8, dc] = 5.0  # a code no observation has (outside the tables' two bits)
+    rows = np.arange(n)
+    bw = np.r_[np.full(dc, 0.05), np.full(du, 0.3)]
+    nlev = np.r_[np.zeros(dc), np.full(du, 4)].astype(np.int32)
+    pair = kde.fit_pair_from_rows(X, rows, rows, vt, bw, bw, nlev, nlev, device=device)
+    k = pair.good
+    if du:
+        assert (k.variant >> 8) & 1
+    lref = O.log_pdf_many(X, bw, vt, C, nlev)
+    got = _capi_logpdf_rtol(k, C)
+    assert np.isfinite(lref).all()
+    err = np.abs(got - lref) / np.maximum(1.0, np.abs(lref))
+    assert err.max() <= 1e-5, err.max()
 
 
 def test_dd_pass_no_finite_term_in_first_chunk(device):

@@ -1,4 +1,4 @@
-"""The drop-in's refit (ObservationStore.refit -> hbx_kde_refit_host_rows: the appended rows carried in the
+"""The drop-in's refit (ObservationStore.refit -> hbx_kde_refit_sync: the appended rows carried in the
 sort launch's kernel arguments when they fit, else copied through the scratch; the column statistics written
 by the fit launch; the table launch's last block finishing each KDE) against the separate preparation of the
 same split (hbx_kde_prepare through fit_pair_from_rows) -- the same kernel instance, the same acquisition
@@ -64,8 +64,8 @@ def test_one_launch_refit_equals_prepare(device, dc, du, lev, n, n_new):
 
 
 def test_device_staged_rows_equal_host_rows(device):
-    """hbx_kde_refit (rows staged in device memory) and hbx_kde_refit_host_rows give the same output block,
-    parameter blocks and tables."""
+    """hbx_kde_refit (rows staged in device memory) and hbx_kde_refit_sync (rows from host memory) give the same
+    output block, parameter blocks and tables."""
     import torch
     from hpbandster_amd import _native as N
     from hpbandster_amd import kde
@@ -95,9 +95,10 @@ def test_device_staged_rows_equal_host_rows(device):
         tb = torch.zeros(tbf, dtype=torch.float32, device=device)
         fg, fb = kde.bandwidth_factor(ng, D), kde.bandwidth_factor(nb, D)
         if host:
-            N.call("hbx_kde_refit_host_rows", N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, st.ctypes.data, n_new, ng, nb,
+            hb = np.empty(ob, dtype=np.uint8)
+            N.call("hbx_kde_refit_sync", N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, st.ctypes.data, n_new, ng, nb,
                    fg, fb, N.ptr(pg), N.ptr(tg), tgf, N.ptr(pbd), N.ptr(tb), tbf, N.ptr(out), N.ptr(scr), sb,
-                   N.stream_handle())
+                   N.stream_handle(), hb.ctypes.data)
         else:
             sd = torch.from_numpy(st).to(device)
             N.call("hbx_kde_refit", N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, N.ptr(sd), n_new, ng, nb, fg, fb,
@@ -119,7 +120,7 @@ def test_device_staged_rows_equal_host_rows(device):
 def test_sync_refit_publishes_the_output_block(device, dc, du, lev, n, n_new):
     """hbx_kde_refit_sync's host copy of the output block (published by the finishing workgroups through mapped
     host memory -- the table launch's last blocks, or the separate finish launch when a KDE is exact-only) equals
-    the device block and the block of hbx_kde_refit_host_rows; three calls in a row (the completion words'
+    the device block and the block of hbx_kde_refit (rows staged in device memory); three calls in a row (the
     sequence), a block larger than the first mapped buffer (it grows)."""
     import torch
     from hpbandster_amd import _native as N
@@ -138,7 +139,7 @@ def test_sync_refit_publishes_the_output_block(device, dc, du, lev, n, n_new):
     fg, fb = kde.bandwidth_factor(ng, D), kde.bandwidth_factor(nb, D)
     st = np.concatenate([X[n - n_new:].reshape(-1), L[n - n_new:]])
     blocks = []
-    for call in ("hbx_kde_refit_host_rows", "hbx_kde_refit_sync", "hbx_kde_refit_sync", "hbx_kde_refit_sync"):
+    for call in ("hbx_kde_refit", "hbx_kde_refit_sync", "hbx_kde_refit_sync", "hbx_kde_refit_sync"):
         Xd = torch.zeros((n, D), dtype=torch.float64, device=device)
         Ld = torch.zeros(n, dtype=torch.float64, device=device)
         Xd[:n - n_new] = torch.from_numpy(X[:n - n_new]).to(device)
@@ -148,8 +149,10 @@ def test_sync_refit_publishes_the_output_block(device, dc, du, lev, n, n_new):
         pg, pbd = (torch.zeros(pb, dtype=torch.uint8, device=device) for _ in range(2))
         tg = torch.zeros(max(tgf, 1), dtype=torch.float32, device=device)
         tb = torch.zeros(max(tbf, 1), dtype=torch.float32, device=device)
-        args = [N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, st.ctypes.data, n_new, ng, nb, fg, fb, N.ptr(pg),
-                N.ptr(tg), tgf, N.ptr(pbd), N.ptr(tb), tbf, N.ptr(out), N.ptr(scr), sb, N.stream_handle()]
+        sd = torch.from_numpy(st).to(device)  # (hbx_kde_refit: the staged rows in device memory)
+        args = [N.ptr(Xd), N.ptr(Ld), n, D, vt.ctypes.data, st.ctypes.data if call == "hbx_kde_refit_sync" else
+                N.ptr(sd), n_new, ng, nb, fg, fb, N.ptr(pg), N.ptr(tg), tgf, N.ptr(pbd), N.ptr(tb), tbf, N.ptr(out),
+                N.ptr(scr), sb, N.stream_handle()]
         host = np.full(ob, 0xAB, dtype=np.uint8)
         if call == "hbx_kde_refit_sync":
             N.call(call, *args, host.ctypes.data)

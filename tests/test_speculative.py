@@ -119,19 +119,3 @@ def test_concurrent_draws_are_never_duplicated():
         t.join()
     assert len(vals) > 50
     assert len(set(vals)) == len(vals)
-
-
-def test_next_call_random_hint_reads_without_drawing():
-    """BOHB._next_call_is_random (the hint that skips computing ahead a call that will be a random pick)
-    predicts the next np.random.rand() < random_fraction from a private copy: the global stream is left
-    untouched, and the prediction equals the draw the call then makes."""
-    class _G(object):
-        random_fraction = 1 / 3
-    gen = _G()
-    hint = B.BOHB._next_call_is_random
-    np.random.seed(5)
-    for _ in range(200):
-        before = B._global_mt().snap()
-        h = hint(gen)
-        assert B._global_mt().snap() == before
-        assert h == (np.random.rand() < gen.random_fraction)

@@ -2,7 +2,7 @@
     python tools/host_path.py [--reps 400]
 For config #2 (1e5 x 1e3, D = 8) and a 64-candidate get_config against config #3's model: wall time per
 synchronous acquisition through the drop-in (KDEPair.acquire), through the bare native call with every
-argument prepared (hbx_kde_acquire_host), the scoring launch alone (its own start/end stamps), and the
+argument prepared (hbx_kde_acquire_bound), the scoring launch alone (its own start/end stamps), and the
 floor of any one-launch round trip (hbx_fetch of 8 bytes)."""
 import argparse
 import json
@@ -35,9 +35,9 @@ def measure(pair, C, reps):
     ws = torch.empty(pair.workspace_bytes(Nc), dtype=torch.uint8, device=dev)
     drop = per_call(lambda: pair.acquire(C, workspace=ws), reps)
     rec = ctypes.create_string_buffer(64)
-    args = (C.data_ptr(), Nc, pair.good.k_vars, 0) + pair._kde_args + (ws.data_ptr(), ws.numel(), None,
-                                                                        N.stream_handle(None, dev), ctypes.addressof(rec))
-    fn = L.hbx_kde_acquire_host
+    args = (pair._bound, C.data_ptr(), Nc, 0, ws.data_ptr(), ws.numel(), None, None, N.stream_handle(None, dev),
+            ctypes.addressof(rec), None)
+    fn = L.hbx_kde_acquire_bound
     native = per_call(lambda: fn(*args), reps)
     ev = kde.ScoreEvents()
     pair.acquire(C, workspace=ws, events=ev)

@@ -41,7 +41,7 @@ def main():
         t2 = time.perf_counter()
         if s >= 3:
             rows.append((t1 - t0, t2 - t1, t2 - t0, ev.elapsed_ms(True)[0] * 1e-3, e0.elapsed_time(e1) * 1e-3))
-    sync = []  # the drop-in's synchronous call: hbx_kde_acquire_host (the record on the host in one call)
+    sync = []  # the drop-in's synchronous call: hbx_kde_acquire_bound (the record on the host in one call)
     for s in range(a.steps + 3):
         t0 = time.perf_counter()
         r2 = pair.acquire(C, workspace=ws, events=ev)
