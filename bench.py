@@ -1076,7 +1076,7 @@ def kde_result_bytes():
     return kde.RESULT_BYTES
 
 
-PROFILE_SET = "profiles/r05/final"
+PROFILE_SET = "profiles/r06/final"
 
 
 def load_traffic(workload):

@@ -24,7 +24,7 @@ import numpy as np
 import scipy.stats as sps
 
 from .. import _native
-from ..kde import ACQ_DOMAIN_ERR, ObservationStore
+from ..kde import ACQ_DOMAIN_ERR, ObservationStore, mapped_candidates
 from .base import base_config_generator
 from ._cs import ConfigSpace
 
@@ -267,7 +267,7 @@ def ppf_terms_ok():
     return _PPF[0]
 
 
-def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt):
+def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt, out=None):
     """The same draws in one native call on R's own MT19937 state (hbx_bohb_draw, the reference's
     consumption order), then the truncnorm inversion of the call's uniforms and rvs's ``* scale + loc`` --
     the arithmetic rvs applies to each uniform, elementwise, so the values are the per-element path's bit for
@@ -280,7 +280,7 @@ def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt):
     bws = np.ascontiguousarray(kde_good.bw, dtype=np.float64)
     lv = np.ascontiguousarray(levels, dtype=np.int64)
     n, D = data.shape
-    vals = np.empty((num_samples, D))
+    vals = np.empty((num_samples, D)) if out is None else out
     uni = np.empty((num_samples, D))
     need = np.empty((num_samples, D), dtype=np.uint8)
     datum = np.empty(num_samples, dtype=np.int64)
@@ -425,7 +425,7 @@ class BOHB(base_config_generator):
         self._pick_tls = threading.local()  # GPU sampler: this thread's draw / pick buffers (_pick)
 
     # -- candidates ---------------------------------------------------------------------------
-    def sample_candidates(self, kde_good, num_samples, rng=None):
+    def sample_candidates(self, kde_good, num_samples, rng=None, out=None):
         """bohb.py:133-147: around a random good observation, truncnorm per continuous dim (bounds
         from bw, scale bandwidth_factor * bw), keep-or-resample per categorical dim.  Global RNG (or
         ``rng``, a RandomState drawn from in the same order).  One native call for every draw of the call
@@ -443,8 +443,12 @@ class BOHB(base_config_generator):
                 if rng is not None and mt is not None:
                     self._rng_mt = (R, mt)
             if mt is not None:
-                return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt)
-        return _draw_rvs(kde_good, self.vartypes, self.bw_factor, num_samples, R)
+                return _draw_fast(kde_good, self.vartypes, self.bw_factor, num_samples, R, mt, out)
+        c = _draw_rvs(kde_good, self.vartypes, self.bw_factor, num_samples, R)
+        if out is None:
+            return c
+        out[...] = c
+        return out
 
     def get_config(self, budget):
         sample = None
@@ -465,10 +469,11 @@ class BOHB(base_config_generator):
                     self._sample_counter += self.num_samples
                     if res.flags & ACQ_DOMAIN_ERR:
                         raise ValueError("truncnorm domain error: a sampled datum has no valid bounds")
-                else:
-                    cands = self.sample_candidates(pair['good'], self.num_samples)
-                    res = pair.acquire(cands)
-                    best_vector = cands[res.index] if res.index >= 0 else None
+                else:  # drawn into mapped host memory, which the acquisition's kernels read in place
+                    cands = self.sample_candidates(pair['good'], self.num_samples,
+                                                   out=mapped_candidates(self.num_samples, len(self.vartypes)))
+                    res = pair.acquire_mapped(cands)
+                    best_vector = cands[res.index].copy() if res.index >= 0 else None
                 if res.index < 0:
                     self.logger.debug("Sampling based optimization with %i samples failed -> using random configuration"
                                       % self.num_samples)

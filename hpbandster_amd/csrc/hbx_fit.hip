@@ -112,10 +112,13 @@ __global__ __launch_bounds__(256) void seg_argsort_kernel(const double* __restri
   block_sort_segment<false>(loss + s, e - s, tile, lk, li, gk + s, gi + s, gk2 + s, gi2 + s, order + s);
 }
 
-// segments of up to 1024 losses: one wave each, sorted in registers (wave_sort_1024)
+// segments of up to 1024 losses: one wave each, sorted in registers (wave_sort_1024).  list / count (numpy's
+// tie order, nullable): a segment whose sorted keys hold two equal neighbours joins `list` -- the sorted keys
+// are in the wave's registers, so the tie check reads no memory (seg_tie_flag_kernel re-gathered every key)
 __global__ __launch_bounds__(256) void seg_argsort_wave_kernel(const double* __restrict__ loss,
                                                                const int64_t* __restrict__ seg_off, int64_t B,
-                                                               int64_t* __restrict__ order) {
+                                                               int64_t* __restrict__ order, int32_t* list,
+                                                               int32_t* count) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;  // whole wave
@@ -128,6 +131,14 @@ __global__ __launch_bounds__(256) void seg_argsort_wave_kernel(const double* __r
   for (int r = 0; r < PW_PER_LANE; ++r) {
     const int rank = lane * PW_PER_LANE + r;
     if (rank < n) order[s + rank] = pos[r];
+  }
+  if (list) {  // adjacent sorted ranks with equal keys (hbx_d2ord: -0.0 == 0.0, every NaN one key)
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r + 1 < PW_PER_LANE; ++r) tie |= lane * PW_PER_LANE + r + 1 < n && key[r] == key[r + 1];
+    const uint64_t nxt = __shfl_down(key[0], 1);  // the next lane's first rank
+    tie |= lane < 63 && (lane + 1) * PW_PER_LANE < n && key[PW_PER_LANE - 1] == nxt;
+    if (__ballot(tie) && lane == 0) list[atomicAdd(count, 1)] = (int32_t)b;
   }
 }
 
@@ -788,7 +799,8 @@ static int sort_tile(int64_t max_seg) {
 // Stable argsort of each segment's losses (np.argsort order; ties by position).  seg_off: device
 // int64[B+1]; max_seg: host upper bound on segment length; order: device int64[N] (segment-local).
 static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
-                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream);
+                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream,
+                              int32_t* cnt_list = nullptr, bool* flagged = nullptr);
 
 int hbx_seg_argsort(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                     int64_t* order, void* scratch, int64_t scratch_bytes, void* stream) {
@@ -802,15 +814,19 @@ int hbx_seg_argsort_ex(const double* loss, const int64_t* seg_off, int64_t B, in
                        int64_t* order, void* scratch, int64_t scratch_bytes, int32_t order_mode, void* stream) {
   if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
     return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort_ex: order_mode %d", order_mode);
-  int rc = seg_argsort_stable(loss, seg_off, B, max_seg, N, order, scratch, scratch_bytes, stream);
-  if (rc || order_mode == HBX_ORDER_STABLE || B <= 0 || N < 2) return rc;
   int32_t* arrays = (int32_t*)scratch;
+  const bool np = order_mode == HBX_ORDER_NUMPY && B > 0 && N >= 2;
+  bool flagged = false;  // the wave sort flagged its tied segments itself (numpy mode)
+  int rc = seg_argsort_stable(loss, seg_off, B, max_seg, N, order, scratch, scratch_bytes, stream,
+                              np ? arrays + 4 * N : nullptr, &flagged);
+  if (rc || !np) return rc;
   return hbx_np_order_fix(loss, seg_off, B, max_seg, order, nullptr, 0, 1, order, nullptr, arrays, N, 0, arrays + 4 * N,
-                          false, (hipStream_t)stream);
+                          flagged, (hipStream_t)stream);
 }
 
 static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
-                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream) {
+                              int64_t* order, void* scratch, int64_t scratch_bytes, void* stream, int32_t* cnt_list,
+                              bool* flagged) {
   if (!loss || !seg_off || !order || (!scratch && N > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_seg_argsort: null");
   if (B <= 0) return HBX_OK;
   if (scratch_bytes < hbx_sort_scratch_bytes(N)) return hbx_fail(HBX_ERR_ARG, "sort scratch too small");
@@ -818,8 +834,12 @@ static int seg_argsort_stable(const double* loss, const int64_t* seg_off, int64_
   // many short segments: one wave each; a few (a single refit split): the counting rank spreads
   // each segment over many workgroups; longer segments or more of them: LDS tiles + merges
   if (max_seg <= 64 * PW_PER_LANE && (B >= 64 || !rank_ok)) {
+    if (cnt_list) {  // numpy mode: the wave sort flags its tied segments (cnt_list: count, then the list)
+      HBX_HIP(hipMemsetAsync(cnt_list, 0, sizeof(int32_t), (hipStream_t)stream));
+      *flagged = true;
+    }
     hipLaunchKernelGGL(seg_argsort_wave_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                       loss, seg_off, B, order);
+                       loss, seg_off, B, order, cnt_list ? cnt_list + 16 : nullptr, cnt_list);
     HBX_LAUNCH_CHECK();
     return HBX_OK;
   }

@@ -3053,7 +3053,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
   }
   // the candidates: scaled continuous coordinates and codes in registers, pairs of dims packed
   f2 xc[CPT][NB > 0 ? NB : 1], xu[CPT][(NU > 0 && !LUT) ? NU : 1];
-  uint32_t cw[CPT];  // LUT: the candidate's packed codes
+  uint32_t cw[CPT], cw1[CPT];  // LUT: the candidate's packed codes; dims 4-7's field group alone
   bool cbad[CPT];    // LUT: a code outside [0, 3] (or not an integer): the candidate goes to the fp64 pass
   float nx2[CPT];  // sum_k (|x'_k| + xmax_k)^2
 #pragma unroll
@@ -3072,7 +3072,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
       }
       xc[c][q] = f2{v[0], v[1]};
     }
-    cw[c] = 0u;
+    cw[c] = cw1[c] = 0u;
     cbad[c] = false;
     if constexpr (LUT) {
 #pragma unroll
@@ -3083,6 +3083,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
         cbad[c] = cbad[c] || !ok;
         cw[c] |= (ok ? (uint32_t)v : 0u) << (u < 4 ? 2 + 2 * u : 12 + 2 * (u - 4));
       }
+      cw1[c] = (cw[c] >> 10) & 0x3FFu;
     } else {
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
@@ -3149,7 +3150,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
         for (int u = 0; u < DU; ++u)
           w |= (uint32_t)__hiloint2double((int)prc[u], 0) << (u < 4 ? 2 + 2 * u : 12 + 2 * (u - 4));
         xs[b][tid][DC] = __uint_as_float(w);
-        xs[b][tid][DC + 1] = xs[b][tid][DC + 2] = xs[b][tid][DC + 3] = 0.f;
+        xs[b][tid][DC + 1] = __uint_as_float((w >> 10) & 0x3FFu);  // dims 4-7's group alone: one xor per pair
+        xs[b][tid][DC + 2] = xs[b][tid][DC + 3] = 0.f;
       }
     }
   };
@@ -3161,9 +3163,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
   auto term = [&](int c, const float* r) __attribute__((always_inline)) -> float {
     f2 a0 = f2{0.f, 0.f}, a1 = f2{0.f, 0.f};
     if constexpr (LUT) {  // the categorical part: two table reads of the codes' xor
-      const uint32_t x = cw[c] ^ __float_as_uint(r[DC]);
-      const float l0 = *(const float*)((const char*)s_lut + (x & 0x3FFu));
-      const float l1 = DU > 4 ? *(const float*)((const char*)s_lut + 1024 + ((x >> 10) & 0x3FFu)) : 0.f;
+      const uint32_t x0 = (cw[c] ^ __float_as_uint(r[DC])) & 0x3FFu;  // (one v_bitop3)
+      const float l0 = *(const float*)((const char*)s_lut + x0);
+      const float l1 = DU > 4 ? *(const float*)((const char*)s_lut + 1024 + (cw1[c] ^ __float_as_uint(r[DC + 1]))) : 0.f;
       a0 = f2{l0, l1};
     }
 #pragma unroll
@@ -3227,19 +3229,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
       }
     };
     for (int j4 = 0; j4 < jg; j4 += 4) {
-      float tmx[CPT];  // the group's largest exponent per candidate
-#pragma unroll
-      for (int c = 0; c < CPT; ++c) tmx[c] = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float r[W];
         row(j4 + q, r);
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-          const float t = term(c, r);
-          tmx[c] = fmaxf(tmx[c], t);
-          s4[c] += __builtin_amdgcn_exp2f(t - m[c]);
-        }
+        for (int c = 0; c < CPT; ++c) s4[c] += __builtin_amdgcn_exp2f(term(c, r) - m[c]);
       }
       // rare: a term far above the reference point, or NaN (one test per candidate and group of 4): the reference
       // point moves up to ceil of the group's largest exponent (an integer: the rescale is an exact ldexp) and the
@@ -3252,6 +3247,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
         any = any || redo[c];
       }
       if (__builtin_expect(__ballot(any) != 0, 0)) {
+        float tmx[CPT];  // the group's largest exponent per candidate (NaN terms left out)
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) tmx[c] = -INFINITY;
+        for (int q = 0; q < 4; ++q) {
+          float r[W];
+          row(j4 + q, r);
+#pragma unroll
+          for (int c = 0; c < CPT; ++c) tmx[c] = fmaxf(tmx[c], term(c, r));
+        }
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
           const float mn = ceilf(tmx[c]);

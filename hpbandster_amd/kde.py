@@ -77,6 +77,24 @@ def _record_buffer():
     return b
 
 
+def mapped_candidates(n, D):
+    """This thread's device-mapped coherent host buffer of n x D float64 candidates (hbx_host_alloc: the host
+    address is the device's), as a numpy array: the host sampler draws straight into it and the acquisition's
+    kernels read it in place (KDEPair.acquire_mapped) -- no host-to-device copy per get_config.  Reused by
+    every call of the thread (each acquisition on it is synchronous); grown on demand."""
+    import ctypes
+    nbytes = 8 * n * D
+    b = getattr(_pinned_tls, "cands", None)
+    if b is None or b[1] < nbytes:
+        if b is not None:  # (no acquisition of this thread reads the old one any more: they are synchronous)
+            N.check(N.lib().hbx_host_free(b[0]))
+        cap = max(nbytes, 64 * 64 * 8)
+        p = ctypes.c_void_p()
+        N.check(N.lib().hbx_host_alloc(cap, ctypes.addressof(p)))
+        b = _pinned_tls.cands = (p.value, cap)
+    return np.ctypeslib.as_array((ctypes.c_double * (n * D)).from_address(b[0])).reshape(n, D)
+
+
 def fetch_bytes(dev_bytes, stream=None):
     """Bytes of a small device uint8 tensor (a result record) on the host: one native call (hbx_fetch)
     copies them into a per-thread, per-device pinned buffer on ``stream`` (default: the tensor's
@@ -557,6 +575,29 @@ class KDEPair(object):
             if pick is not None:
                 r.index, r.score, r.pdf_l, r.pdf_g = pick[0] - b * seg, pick[1], pick[2], pick[3]
             r.flags |= ACQ_RESOLVED
+
+    def acquire_mapped(self, cands):
+        """acquire(cands) for a host array from mapped_candidates(): the kernels read the candidates in host
+        memory (zero copy), the pick comes back in the same synchronous call (hbx_kde_acquire_bound).  Falls
+        back to acquire() off the fast path's conditions (another current device)."""
+        if self._cur_dev is None or self._raw_stream is None or self._cur_dev() != self._dev_index:
+            return self.acquire(np.array(cands))
+        torch = _torch()
+        Nc = cands.shape[0]
+        wsb = self._wsb.get(Nc)
+        if wsb is None:
+            wsb = self.workspace_bytes(Nc)
+        key = (threading.get_ident(), Nc)
+        workspace = self._ws_cache.get(key)
+        if workspace is None:
+            workspace = self._ws_cache[key] = torch.empty(wsb, dtype=torch.uint8, device=self.good.device)
+        rec = _record_buffer()
+        sh = self._raw_stream(self._dev_index)
+        if sh != self._home:
+            self._order(sh)
+        N.check(self._bound_fn(self._bound, cands.ctypes.data, Nc, 0, workspace.data_ptr(), workspace.numel(), None,
+                               None, sh, rec, None))
+        return AcqResult.from_bytes(rec.raw[:RESULT_BYTES])
 
     def acquire_pick(self, cands, err, workspace, row, sh=None):
         """One synchronous acquisition of ``cands`` (a device [Nc, D] f64 tensor on the model's device) with its

@@ -183,10 +183,11 @@ class _Counter(object):
     def __init__(self, monkeypatch):
         from hpbandster_amd import kde
         self.n = {"acquire": 0, "acquire_batch": 0}
-        for name in self.n:
+        # (acquire_mapped: the host sampler's single call, candidates in mapped host memory)
+        for name, key in (("acquire", "acquire"), ("acquire_mapped", "acquire"), ("acquire_batch", "acquire_batch")):
             orig = getattr(kde.KDEPair, name)
 
-            def wrap(selfp, *a, _orig=orig, _name=name, **k):
+            def wrap(selfp, *a, _orig=orig, _name=key, **k):
                 self.n[_name] += 1
                 return _orig(selfp, *a, **k)
             monkeypatch.setattr(kde.KDEPair, name, wrap)

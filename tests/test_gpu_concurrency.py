@@ -39,13 +39,14 @@ def test_new_result_thread_races_get_config(device, monkeypatch):
     feed(0, 40)  # a first model
     seen = []
     orig = kde.KDEPair.acquire
+    orig_mapped = kde.KDEPair.acquire_mapped  # (the host sampler's call: candidates in mapped host memory)
 
     def recording_acquire(self, cands, *a, **k):
-        res = orig(self, cands, *a, **k)
+        res = orig_mapped(self, cands, *a, **k)
         seen.append((self, np.array(cands, copy=True), res))
         return res
 
-    monkeypatch.setattr(kde.KDEPair, "acquire", recording_acquire)
+    monkeypatch.setattr(kde.KDEPair, "acquire_mapped", recording_acquire)
     errors = []
 
     def dispatcher():
