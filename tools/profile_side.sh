@@ -28,6 +28,6 @@ T=$(ls $OUT/trace/*kernel_trace.csv | head -1)
 python3 tools/side_roofline.py $T $OUT > $OUT/side_roofline.txt || exit 3
 cp $(ls $OUT/trace/*kernel_stats.csv | head -1) $OUT/kernel_stats.csv
 python3 tools/ksteady.py $T --skip 2 > $OUT/kernel_steady.txt || exit 4
-rm -rf $OUT/pmc[0-9]/ $OUT/trace/*kernel_trace.csv
+rm -rf $OUT/pmc[0-9]/
 cat $OUT/side_roofline.txt
 echo side profile done
