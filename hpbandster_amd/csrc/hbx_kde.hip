@@ -2971,7 +2971,7 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 //     Q = -m + 64 + sum_u max(delta_u, 0) + slack bounds their sum_k d_k^2; the others add <= n 2^-63);
 //   the accumulation: chains of NCH fma / add steps, each rounding <= 2^-24 (Q + sum|delta|);
 //   delta_u in fp32: <= 2^-24 sum|delta|; the exponent t' - m: 2^-24 (64 + 1);
-//   exp2: v_exp_f32 within 2 ulp (2^-22 relative); sums: 3 x 2^-24 (fp32 groups of 4) + n 2^-52 (fp64).
+//   exp2: v_exp_f32 within 2 ulp (2^-22 relative); sums: (DD_G - 1) 2^-24 (fp32 groups) + n 2^-52 (fp64).
 // Candidates whose bound stays within 0.99 rtol max(1, |ln p|) are written; the rest go to `list` for the
 // fp64 pass.  KDEs with negative categorical factors, structural NaN or single-level dims: all to `list`.
 // LUT (variant bit 8: <= 8 categorical slots, codes in [0, 3]): the categorical part of a pair is two table
@@ -2982,22 +2982,37 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 #ifndef DD_WPE
 #define DD_WPE(w) ((w) <= 16 ? 4 : (w) <= 40 ? 3 : 2)  // waves per SIMD the register budget is sized for
 #endif
-template <int DC, int DU, int CPT, bool LUT = false>
+// SG (scalar-staged rows): the observation rows are staged ONCE per call into global memory by
+// kde_dd_stage_kernel (the same fp32 values the LDS staging computes, padded with +inf rows to a multiple of
+// DD_G) and read by each wave through the scalar cache into SGPRs, which the packed VALU instructions take as
+// operands: no per-block staging, no barrier per chunk, and no LDS broadcast reads (4 LDS cycles per
+// ds_read_b128) competing with the table reads.  `sg_flag` (scratch header): the stage kernel sets it when the
+// table fit the scratch; the SG kernel runs only then, the LDS kernel of the same call only otherwise.
+#ifndef DD_G
+#define DD_G 4  // terms per fp32 group (its sum's rounding: (DD_G - 1) 2^-24 in the bound)
+#endif
+template <int DC, int DU, int CPT, bool LUT = false, bool SG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC + DU)))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
                                                            const KdeParams* __restrict__ P,
                                                            const double* __restrict__ X,
                                                            const int64_t* __restrict__ rows, double rtol,
                                                            double* __restrict__ out, int32_t* __restrict__ list,
-                                                           int32_t* __restrict__ count) {
+                                                           int32_t* __restrict__ count,
+                                                           const float* __restrict__ stg,
+                                                           const int32_t* __restrict__ sg_flag) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int OB = 64;      // observations per staged chunk
+  constexpr int G = DD_G;
+  static_assert(OB % G == 0, "groups within a chunk");
   // floats per staged row: DC scaled coordinates, then DU codes (LUT: the packed code word and 3 pad slots)
   constexpr int W = LUT ? DC + 4 : DC + DU;
+  static_assert(!SG || W <= 32, "SG: a row in at most 32 SGPRs");
+  if (sg_flag && ((*sg_flag != 0) != SG)) return;  // uniform: the other kernel of the call runs
   constexpr int WC = LUT ? DC : W;  // staged elements per row written by the element loop
   constexpr int NB = DC / 2, NU = DU / 2;  // packed pairs
   static_assert(DC % 4 == 0 && DU % 4 == 0, "pairs of pairs");
   static_assert(!LUT || DU == 4 || DU == 8, "LUT: 4 or 8 categorical slots");
-  __shared__ __align__(16) float xs[2][OB][W];
+  __shared__ __align__(16) float xs[SG ? 1 : 2][SG ? 1 : OB][W];
   __shared__ double s_scale[DC > 0 ? DC : 1], s_mu[DC > 0 ? DC : 1];
   __shared__ int32_t s_col[DC + DU > 0 ? DC + DU : 1];
   __shared__ float s_dl[DU > 0 ? DU : 1];
@@ -3159,45 +3174,69 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     fetch(cc);
     store(cc, b);
   };
-  // exponent t' of the pair (candidate c, staged row r): two packed accumulators (four fma chains)
-  auto term = [&](int c, const float* r) __attribute__((always_inline)) -> float {
-    f2 a0 = f2{0.f, 0.f}, a1 = f2{0.f, 0.f};
-    if constexpr (LUT) {  // the categorical part: two table reads of the codes' xor
-      const uint32_t x0 = (cw[c] ^ __float_as_uint(r[DC])) & 0x3FFu;  // (one v_bitop3)
-      const float l0 = *(const float*)((const char*)s_lut + x0);
-      const float l1 = DU > 4 ? *(const float*)((const char*)s_lut + 1024 + (cw1[c] ^ __float_as_uint(r[DC + 1]))) : 0.f;
-      a0 = f2{l0, l1};
+  // exponents t' of the pairs (every candidate c of the thread, staged row r) into t[c]: two packed accumulators
+  // per candidate (four fma chains), the candidates' steps interleaved so consecutive packed instructions are
+  // independent (each chain's order is that of one candidate alone)
+  auto terms = [&](const float* r, float (&t)[CPT]) __attribute__((always_inline)) {
+    f2 a0[CPT], a1[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      a0[c] = f2{0.f, 0.f};
+      a1[c] = f2{0.f, 0.f};
+      if constexpr (LUT) {  // the categorical part: two table reads of the codes' xor
+        const uint32_t x0 = (cw[c] ^ __float_as_uint(r[DC])) & 0x3FFu;  // (one v_bitop3)
+        const float l0 = *(const float*)((const char*)s_lut + x0);
+        const float l1 =
+            DU > 4 ? *(const float*)((const char*)s_lut + 1024 + (cw1[c] ^ __float_as_uint(r[DC + 1]))) : 0.f;
+        a0[c] = f2{l0, l1};
+      }
     }
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-      const f2 X2 = f2{r[2 * q], r[2 * q + 1]};  // (the row is read as whole 16-byte vectors: see rowv)
-      const f2 d = xc[c][q] - X2;
-      if (q < NB / 2) a0 = __builtin_elementwise_fma(-d, d, a0);
-      else a1 = __builtin_elementwise_fma(-d, d, a1);
+      const f2 X2 = f2{r[2 * q], r[2 * q + 1]};
+      f2 d[CPT];
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) d[c] = xc[c][q] - X2;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        if (q < NB / 2) a0[c] = __builtin_elementwise_fma(-d[c], d[c], a0[c]);
+        else a1[c] = __builtin_elementwise_fma(-d[c], d[c], a1[c]);
+      }
     }
 #pragma unroll
     for (int q = 0; q < (LUT ? 0 : NU); ++q) {
       const f2 E2 = f2{r[DC + 2 * q], r[DC + 2 * q + 1]};
-      const f2 e = xu[c][q] - E2;
-      f2 m;  // [x_u == X_u] = clamp(1 - e^2) for integer code differences e
-      asm("v_pk_fma_f32 %0, %1, %2, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0] clamp" : "=v"(m) : "v"(e), "v"(e));
-      if (q < NU / 2) a0 = __builtin_elementwise_fma(dl2[q], m, a0);
-      else a1 = __builtin_elementwise_fma(dl2[q], m, a1);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const f2 e = xu[c][q] - E2;
+        f2 m;  // [x_u == X_u] = clamp(1 - e^2) for integer code differences e
+        asm("v_pk_fma_f32 %0, %1, %2, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0] clamp" : "=v"(m) : "v"(e), "v"(e));
+        if (q < NU / 2) a0[c] = __builtin_elementwise_fma(dl2[q], m, a0[c]);
+        else a1[c] = __builtin_elementwise_fma(dl2[q], m, a1[c]);
+      }
     }
-    const f2 a = a0 + a1;
-    return a.x + a.y;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const f2 a = a0[c] + a1[c];
+      t[c] = a.x + a.y;
+    }
   };
   const int nch = (n + OB - 1) / OB;
-  stage(0, 0);
-  __syncthreads();
+  if constexpr (!SG) {
+    stage(0, 0);
+    __syncthreads();
+  }
   // m: the largest exponent of chunk 0 (every candidate's sum then has a term 2^0)
   float m[CPT];
 #pragma unroll
   for (int c = 0; c < CPT; ++c) m[c] = -INFINITY;
   const int jn0 = min(OB, n);
   for (int jj = 0; jj < jn0; ++jj) {
+    const float* r0 = SG ? stg + (int64_t)jj * W : &xs[0][SG ? 0 : jj][0];
+    float t[CPT];
+    terms(r0, t);
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) m[c] = fmaxf(m[c], term(c, &xs[0][jj][0]));
+    for (int c = 0; c < CPT; ++c) m[c] = fmaxf(m[c], t[c]);
   }
   double S[CPT];
   float s4[CPT];
@@ -3211,79 +3250,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     ref0[c] = m[c] > -INFINITY;
     m[c] = ref0[c] ? ceilf(m[c]) : 0.f;
   }
-  for (int cc = 0; cc < nch; ++cc) {
-    const int b = cc & 1;
-    if (cc + 1 < nch) fetch(cc + 1);
-    const int jn = min(OB, n - cc * OB);
-    // terms summed in fp32 in groups of 4, the groups into the fp64 sums (a chunk's last group: rows past jn
-    // are the padding rows, whose first coordinate is +inf: exact zeros)
-    const int jg = (jn + 3) & ~3;
-    auto row = [&](int jr, float (&r)[W]) __attribute__((always_inline)) {  // 16-byte vectors (ds_read_b128)
+  // one group of G rows (rowp(q, r): row q of the group into r): terms summed in fp32, the group into the fp64
+  // sums (a chunk's last group: rows past n are the padding rows, whose first coordinate is +inf: exact zeros)
+  auto group = [&](auto rowp) __attribute__((always_inline)) {
 #pragma unroll
-      for (int v = 0; v < W / 4; ++v) {
-        const float4 f = reinterpret_cast<const float4*>(&xs[b][jr][0])[v];
-        r[4 * v] = f.x;
-        r[4 * v + 1] = f.y;
-        r[4 * v + 2] = f.z;
-        r[4 * v + 3] = f.w;
+    for (int q = 0; q < G; ++q) {
+      float r[W], t[CPT];
+      rowp(q, r);
+      terms(r, t);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) s4[c] += __builtin_amdgcn_exp2f(t[c] - m[c]);
+    }
+    // rare: a term far above the reference point, or NaN (one test per candidate and group): the reference
+    // point moves up to ceil of the group's largest exponent (an integer: the rescale is an exact ldexp) and the
+    // group is summed again (a wave-uniform branch; the lanes that need it)
+    bool redo[CPT];
+    bool any = false;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      redo[c] = !(s4[c] < 0x1p100f);
+      any = any || redo[c];
+    }
+    if (__builtin_expect(__ballot(any) != 0, 0)) {
+      float tmx[CPT];  // the group's largest exponent per candidate (NaN terms left out)
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) tmx[c] = -INFINITY;
+      for (int q = 0; q < G; ++q) {
+        float r[W], t[CPT];
+        rowp(q, r);
+        terms(r, t);
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) tmx[c] = fmaxf(tmx[c], t[c]);
       }
-    };
-    for (int j4 = 0; j4 < jg; j4 += 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float r[W];
-        row(j4 + q, r);
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) s4[c] += __builtin_amdgcn_exp2f(term(c, r) - m[c]);
-      }
-      // rare: a term far above the reference point, or NaN (one test per candidate and group of 4): the reference
-      // point moves up to ceil of the group's largest exponent (an integer: the rescale is an exact ldexp) and the
-      // group is summed again (a wave-uniform branch; the lanes that need it)
-      bool redo[CPT];
-      bool any = false;
 #pragma unroll
       for (int c = 0; c < CPT; ++c) {
-        redo[c] = !(s4[c] < 0x1p100f);
-        any = any || redo[c];
-      }
-      if (__builtin_expect(__ballot(any) != 0, 0)) {
-        float tmx[CPT];  // the group's largest exponent per candidate (NaN terms left out)
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) tmx[c] = -INFINITY;
-        for (int q = 0; q < 4; ++q) {
-          float r[W];
-          row(j4 + q, r);
-#pragma unroll
-          for (int c = 0; c < CPT; ++c) tmx[c] = fmaxf(tmx[c], term(c, r));
+        const float mn = ceilf(tmx[c]);
+        if (redo[c] && mn > m[c]) {
+          S[c] = ldexp(S[c], (int)(m[c] - mn));
+          m[c] = mn;
         }
+        if (redo[c]) s4[c] = 0.f;
+      }
+      for (int q = 0; q < G; ++q) {
+        float r[W], t[CPT];
+        rowp(q, r);
+        terms(r, t);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
-          const float mn = ceilf(tmx[c]);
-          if (redo[c] && mn > m[c]) {
-            S[c] = ldexp(S[c], (int)(m[c] - mn));
-            m[c] = mn;
-          }
-          if (redo[c]) s4[c] = 0.f;
+          const float e = __builtin_amdgcn_exp2f(t[c] - m[c]);
+          if (redo[c]) s4[c] += e;
         }
-        for (int q = 0; q < 4; ++q) {
-          float r[W];
-          row(j4 + q, r);
-#pragma unroll
-          for (int c = 0; c < CPT; ++c) {
-            const float e = __builtin_amdgcn_exp2f(term(c, r) - m[c]);
-            if (redo[c]) s4[c] += e;
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CPT; ++c) {
-        S[c] += (double)s4[c];
-        s4[c] = 0.f;
       }
     }
-    // the other buffer is free since the barrier after chunk cc - 1
-    if (cc + 1 < nch) store(cc + 1, b ^ 1);
-    __syncthreads();  // chunk cc + 1 staged; every thread done with chunk cc's buffer
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      S[c] += (double)s4[c];
+      s4[c] = 0.f;
+    }
+  };
+  if constexpr (SG) {
+    const int ngr = (n + G - 1) / G;
+    for (int g = 0; g < ngr; ++g) {
+      const float* base = stg + (int64_t)g * (G * W);  // uniform: scalar loads
+      group([&](int q, float (&r)[W]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) r[k] = base[q * W + k];
+      });
+    }
+  } else {
+    for (int cc = 0; cc < nch; ++cc) {
+      const int b = cc & 1;
+      if (cc + 1 < nch) fetch(cc + 1);
+      const int jn = min(OB, n - cc * OB);
+      const int jg = (jn + G - 1) & ~(G - 1);
+      for (int j4 = 0; j4 < jg; j4 += G) {
+        group([&](int q, float (&r)[W]) __attribute__((always_inline)) {  // 16-byte vectors (ds_read_b128)
+#pragma unroll
+          for (int v = 0; v < W / 4; ++v) {
+            const float4 f = reinterpret_cast<const float4*>(&xs[SG ? 0 : b][SG ? 0 : j4 + q][0])[v];
+            r[4 * v] = f.x;
+            r[4 * v + 1] = f.y;
+            r[4 * v + 2] = f.z;
+            r[4 * v + 3] = f.w;
+          }
+        });
+      }
+      // the other buffer is free since the barrier after chunk cc - 1
+      if (cc + 1 < nch) store(cc + 1, b ^ 1);
+      __syncthreads();  // chunk cc + 1 staged; every thread done with chunk cc's buffer
+    }
   }
   // the bound (log2 units) and the result
   float sdp = 0.f, sda = 0.f;
@@ -3304,7 +3359,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
     const float Et = 2.f * __builtin_sqrtf(Q) * dln + dln * dln + (float)NCH * u24 * (Q + sda) + u24 * sda +
                      65.f * u24 + 0x1p-48f * Q;
     // relative bound of S': 2^Et - 1 per term, the exp, the sums, the terms left out
-    const double rel = exp2((double)Et * (1.0 + 0x1p-20)) - 1.0 + 0x1p-22 + 3.0 * 0x1p-24 + (double)n * 0x1p-52 +
+    const double rel = exp2((double)Et * (1.0 + 0x1p-20)) - 1.0 + 0x1p-22 + (G - 1) * 0x1p-24 + (double)n * 0x1p-52 +
                        (double)n * 0x1p-63;
     const double lnS = log(S[c]) + (double)m[c] * 0.69314718055994531;
     const double lp = lnS + log_c * 0.69314718055994531 + P->log_norm;
@@ -3316,7 +3371,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC +
 }
 
 typedef void (*logpdf_dd_fn)(const double*, int64_t, int32_t, const KdeParams*, const double*, const int64_t*, double,
-                             double*, int32_t*, int32_t*);
+                             double*, int32_t*, int32_t*, const float*, const int32_t*);
+typedef void (*dd_stage_fn)(const KdeParams*, const double*, const int64_t*, int32_t, int64_t, float*, int32_t*);
+
+// the SG kernel's staged rows: row j < n as kde_logpdf_dd_kernel's LDS staging writes it (the DC scaled
+// coordinates in fp32; LUT: the packed two-bit code word, its dims 4-7 group alone, two zeros; else the DU codes),
+// rows n .. n_pad - 1 padding (first coordinate +inf, the rest 0).  Writes only when n_pad W floats fit `cap`
+// bytes, and sets *sg_flag to say so (read by both dd kernels of the call); grid-stride (n is on the device).
+template <int DC, int DU, bool LUT>
+__global__ __launch_bounds__(256) void kde_dd_stage_kernel(const KdeParams* __restrict__ P, const double* __restrict__ X,
+                                                           const int64_t* __restrict__ rows, int32_t D, int64_t cap,
+                                                           float* __restrict__ stg, int32_t* __restrict__ sg_flag) {
+  constexpr int W = LUT ? DC + 4 : DC + DU;
+  const int n = P->n, dc = P->dc, du = P->du;
+  const int64_t n_pad = ((int64_t)n + DD_G - 1) / DD_G * DD_G;
+  const bool fits = n > 0 && n_pad * W * 4 <= cap && !(P->has_neg || P->nan_all || P->nconst);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *sg_flag = fits ? 1 : 0;
+  if (!fits) return;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n_pad * W; e += (int64_t)gridDim.x * 256) {
+    const int j = (int)(e / W), k = (int)(e - (int64_t)j * W);
+    float v = 0.f;
+    if (j < n) {
+      const double* x = X + rows[j] * (int64_t)D;
+      if (k < DC) {
+        if (k < dc) v = (float)(P->cont_scale[k] * (x[P->cont_dim[k]] - P->center[k]));
+      } else if constexpr (LUT) {
+        if (k < DC + 2) {  // codes are integers in [0, 3] (variant bit 8)
+          uint32_t w = 0u;
+#pragma unroll
+          for (int u = 0; u < DU; ++u)
+            if (u < du) w |= (uint32_t)x[P->cat_dim[u]] << (u < 4 ? 2 + 2 * u : 12 + 2 * (u - 4));
+          v = __uint_as_float(k == DC ? w : (w >> 10) & 0x3FFu);
+        }
+      } else {
+        const int u = k - DC;
+        if (u < du) v = cand_code(x[P->cat_dim[u]]);
+      }
+    } else if (k == 0) {
+      v = __builtin_inf();
+    }
+    stg[e] = v;
+  }
+}
+
 // candidates per thread: two share each staged row where both fit the register budget
 #ifndef DD_CPT
 #define DD_CPT 2
@@ -3326,28 +3423,42 @@ constexpr int dd_cpt(int dc, int du) { return DD_CPT; }
 #define DD_CPT_LUT 2
 #endif
 
+struct DdFns {
+  logpdf_dd_fn lds = nullptr, sg = nullptr;
+  dd_stage_fn stage = nullptr;
+};
+template <int DC, int DU, int CPT, bool LUT>
+static DdFns dd_fns() {
+  DdFns f;
+  f.lds = kde_logpdf_dd_kernel<DC, DU, CPT, LUT>;
+  if constexpr ((LUT ? DC + 4 : DC + DU) <= 32) {
+    f.sg = kde_logpdf_dd_kernel<DC, DU, CPT, LUT, true>;
+    f.stage = kde_dd_stage_kernel<DC, DU, LUT>;
+  }
+  return f;
+}
+
 template <int DC>
-static logpdf_dd_fn pick_dd_du(int du_pad, int* cpt, bool lut) {
+static DdFns pick_dd_du(int du_pad, int* cpt, bool lut) {
   if (lut && du_pad == 4) {
     *cpt = DD_CPT_LUT;
-    return kde_logpdf_dd_kernel<DC, 4, DD_CPT_LUT, true>;
+    return dd_fns<DC, 4, DD_CPT_LUT, true>();
   }
   if (lut && du_pad == 8) {
     *cpt = DD_CPT_LUT;
-    return kde_logpdf_dd_kernel<DC, 8, DD_CPT_LUT, true>;
+    return dd_fns<DC, 8, DD_CPT_LUT, true>();
   }
   switch (du_pad) {
-    case 0: *cpt = dd_cpt(DC, 0); return kde_logpdf_dd_kernel<DC, 0, dd_cpt(DC, 0)>;
-    case 4: *cpt = dd_cpt(DC, 4); return kde_logpdf_dd_kernel<DC, 4, dd_cpt(DC, 4)>;
-    case 8: *cpt = dd_cpt(DC, 8); return kde_logpdf_dd_kernel<DC, 8, dd_cpt(DC, 8)>;
-    case 16: *cpt = dd_cpt(DC, 16); return kde_logpdf_dd_kernel<DC, 16, dd_cpt(DC, 16)>;
-    case 32: *cpt = dd_cpt(DC, 32); return kde_logpdf_dd_kernel<DC, 32, dd_cpt(DC, 32)>;
+    case 0: *cpt = dd_cpt(DC, 0); return dd_fns<DC, 0, dd_cpt(DC, 0), false>();
+    case 4: *cpt = dd_cpt(DC, 4); return dd_fns<DC, 4, dd_cpt(DC, 4), false>();
+    case 8: *cpt = dd_cpt(DC, 8); return dd_fns<DC, 8, dd_cpt(DC, 8), false>();
+    case 16: *cpt = dd_cpt(DC, 16); return dd_fns<DC, 16, dd_cpt(DC, 16), false>();
+    case 32: *cpt = dd_cpt(DC, 32); return dd_fns<DC, 32, dd_cpt(DC, 32), false>();
   }
-  return nullptr;
+  return DdFns{};
 }
 
-// the direct-difference fp32 kernel of a bucket (continuous slots rounded up to a multiple of 4)
-static logpdf_dd_fn pick_logpdf_dd(int dc_pad, int du_pad, int* cpt, bool lut) {
+static DdFns pick_logpdf_dd(int dc_pad, int du_pad, int* cpt, bool lut) {
   switch (dc_pad) {
     case 0:
     case 4: return pick_dd_du<4>(du_pad, cpt, lut);
@@ -3356,7 +3467,7 @@ static logpdf_dd_fn pick_logpdf_dd(int dc_pad, int du_pad, int* cpt, bool lut) {
     case 24: return pick_dd_du<24>(du_pad, cpt, lut);
     case 32: return pick_dd_du<32>(du_pad, cpt, lut);
   }
-  return nullptr;  // 64 continuous slots: the estimate + fp64 path
+  return DdFns{};  // 64 continuous slots: the estimate + fp64 path
 }
 
 __global__ __launch_bounds__(256) void kde_logpdf_classify_kernel(const KdeEst* __restrict__ est, int64_t Nc,
@@ -3441,11 +3552,23 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
   int cpt = 1;
   const char* lut_env = getenv("HBX_DD_LUT");  // 0: the packed-match categorical path everywhere (tests)
   const bool lut = ((variant >> 8) & 1) && !(lut_env && atoi(lut_env) == 0);
-  const logpdf_dd_fn dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt, lut) : nullptr;
+  const DdFns dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt, lut) : DdFns{};
+  const char* sg_env = getenv("HBX_DD_SG");  // 0: the LDS-staged dd kernel everywhere (tests)
+  const bool sg = dd.sg && !(sg_env && atoi(sg_env) == 0);
   HBX_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), s));
-  if (dd) {
-    hipLaunchKernelGGL(dd, dim3((unsigned)((Nc + 256 * cpt - 1) / (256 * cpt))), dim3(256), 0, s, cand, Nc, D,
-                       (const KdeParams*)params, X, rows, rtol, out, list, count);
+  if (dd.lds) {
+    const dim3 g((unsigned)((Nc + 256 * cpt - 1) / (256 * cpt)));
+    int32_t* flag = sg ? count + 1 : nullptr;
+    if (sg) {  // rows staged into the (unused here) estimate area when they fit; the flag picks the kernel
+      hipLaunchKernelGGL(dd.stage, dim3(256), dim3(256), 0, s, (const KdeParams*)params, X, rows, D, 16 * Nc,
+                         (float*)est, flag);
+      HBX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(dd.sg, g, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params, X, rows, rtol, out, list,
+                         count, (const float*)est, (const int32_t*)flag);
+      HBX_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(dd.lds, g, dim3(256), 0, s, cand, Nc, D, (const KdeParams*)params, X, rows, rtol, out, list,
+                       count, (const float*)nullptr, (const int32_t*)flag);
     HBX_LAUNCH_CHECK();
   } else {
     if (!exact_only) {  // the estimate (the precise instance: hbx_kde_logpdf's)

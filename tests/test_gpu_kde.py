@@ -639,15 +639,18 @@ def test_capi_logpdf_rtol_contract(device, case, rtol, lut, monkeypatch):
         assert err.max() <= max(rtol, 2e-12), (case, err.max())
 
 
+@pytest.mark.parametrize("sg", ["1", "0"])
 @pytest.mark.parametrize("lut", ["1", "0"])
 @pytest.mark.parametrize("du", [0, 4, 8])
-def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, monkeypatch):
+def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, sg, monkeypatch):
     """Candidates that sit on an observation of a later chunk while every observation of chunk 0 is thousands of
     log2 units away: the group holding that observation overflows the first chunk's reference point, which moves
     up and the group is summed again; candidates with codes outside [0, 3] take the fp64 pass under the tables.
-    Every ln pdf within the contract of the oracle's."""
+    Every ln pdf within the contract of the oracle's.  sg: 5376 candidates (their scratch holds the staged rows:
+    the scalar-staged kernel) or the LDS-staged kernel (HBX_DD_SG=0)."""
     from hpbandster_amd import kde
     monkeypatch.setenv("HBX_DD_LUT", lut)
+    monkeypatch.setenv("HBX_DD_SG", sg)
     rs = np.random.RandomState(41)
     n, dc = 700, 24
     vt = "c" * dc + "u" * du
@@ -666,11 +669,52 @@ def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, monkeypatch):
     k = pair.good
     if du:
         assert (k.variant >> 8) & 1
-    lref = O.log_pdf_many(X, bw, vt, C, nlev)
+    C = np.tile(C, (56, 1))  # 5376 rows: 16 B of scratch each >= 704 staged rows x 28 floats
+    lref = O.log_pdf_many(X, bw, vt, C[:96], nlev)
     got = _capi_logpdf_rtol(k, C)
+    assert np.array_equal(got, np.tile(got[:96], 56))
+    got = got[:96]
     assert np.isfinite(lref).all()
     err = np.abs(got - lref) / np.maximum(1.0, np.abs(lref))
     assert err.max() <= 1e-5, err.max()
+
+
+@pytest.mark.parametrize("lut", ["1", "0"])
+def test_dd_scalar_staged_equals_lds_staged(device, lut, monkeypatch):
+    """The scalar-staged direct-difference kernel (rows staged once into the call's scratch, read through SGPRs)
+    against the LDS-staged one at config #3's dims (24c + 8u, 4 levels; 3000 observations, 20000 candidates:
+    uniform draws, observations' neighbours, an unseen code, a far point): the same fp32 values in the same
+    order, so the ln pdfs are equal bit for bit, and within 1e-5 of the oracle's on a sample (the good KDE's
+    categorical bandwidths exceed 1 here: ln of the reference's signed pdf, NaN where that is negative)."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    monkeypatch.setenv("HBX_DD_LUT", lut)
+    X = S.make_observations(3000, 24, 8, 4, seed=51)
+    Lo = S.make_losses(3000, seed=52)
+    vt = S.var_type_string(24, 8)
+    rs = np.random.RandomState(53)
+    C = S.make_candidates(20000, 24, 8, 4, seed=54)
+    C[:5000] = X[rs.randint(0, 3000, 5000)]
+    C[:5000, :24] += 0.01 * rs.randn(5000, 24)
+    C[7, 30] = 7.0
+    C[11, 2] = 30.0
+    pair = kde.fit_pair(X, Lo, vt, 33, device=device)
+    for k in (pair.good, pair.bad):
+        monkeypatch.setenv("HBX_DD_SG", "1")
+        a = _capi_logpdf_rtol(k, C)
+        monkeypatch.setenv("HBX_DD_SG", "0")
+        b = _capi_logpdf_rtol(k, C)
+        assert np.array_equal(a, b, equal_nan=True)
+        sel = np.r_[np.arange(0, 20000, 40), 7, 11]
+        lref = O.log_pdf_many(k.data, k.bw, vt, C[sel], k.nlev)
+        if k.has_neg:  # a categorical bandwidth above 1: ln of the reference's own (possibly negative) pdf
+            with np.errstate(divide="ignore", invalid="ignore"):
+                lref = np.log(O.pdf_many(k.data, k.bw, vt, C[sel], k.nlev))
+        assert np.array_equal(np.isnan(a[sel]), np.isnan(lref))
+        fin = np.isfinite(lref)
+        assert fin.sum() > 100
+        err = np.abs(a[sel][fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        assert err.max() <= 1e-5, err.max()
 
 
 def test_dd_pass_no_finite_term_in_first_chunk(device):
