@@ -102,7 +102,7 @@ SIGNATURES = {
     "hbx_mt_state_bytes": (c_i64, []),
     "hbx_mt_draw": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp]),
     "hbx_bohb_draw": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, ctypes.c_double, c_i64, c_vp, c_vp, c_vp, c_vp,
-                              c_vp]),
+                              c_vp, c_vp, c_vp]),
 }
 
 # tie order of the sorts (include/hbx.h): numpy's unstable argsort (the reference's) or by position

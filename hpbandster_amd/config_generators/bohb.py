@@ -210,22 +210,23 @@ def _ppf_from_terms(q, lp, mass, left):
     """scipy's truncnorm._ppf at uniforms q from the terms above, the same numpy / scipy.special ufuncs in the
     same order: log_Phi_x = logsumexp([lp, log(q) + mass]) (log1p(-q) on the right), scipy 1.15's
     ``_logsumexp`` for two real rows (the larger one taken out of the sum: (log1p(exp(lo - hi)) + log(m)) + hi,
-    m the number of rows equal to the larger), then ndtri_exp (negated on the right).  Elementwise, so a subset
-    gives the values the whole array would.  Non-finite log_Phi_x inputs come back as None positions
-    (``bad``) for scipy's own _ppf."""
+    m the number of rows equal to the larger), then ndtri_exp (negated on the right).  Formed here as
+    log1p(exp(min - max)) + max: for m = 1, log(m) = 0 adds nothing to log1p(.) >= 0; for m = 2 (the rows
+    equal), exp(0) = 1 and log1p(1) is log(2) (checked by ppf_terms_ok), where scipy adds log(2) to log1p(0) = 0.
+    Elementwise, so a subset gives the values the whole array would.  Non-finite log_Phi_x inputs come back as
+    ``bad`` positions for scipy's own _ppf."""
     import scipy.special as sc
-    if _LOG2[0] is None:
-        _LOG2[0] = np.log(np.array([1.0, 2.0]))
     with np.errstate(all="ignore"):
-        x = np.where(left, np.log(q), np.log1p(-q)) + mass
+        x = np.where(left, np.log(q), np.log1p(-q))
+        x += mass
         hi = np.maximum(lp, x)
-        e0, e1 = lp == hi, x == hi
-        both = e0 & e1
-        lo = np.where(e0, x, lp)
-        s = np.where(both, 0.0, np.exp(lo - hi))
-        out = np.log1p(s) + np.where(both, _LOG2[0][1], _LOG2[0][0]) + hi
-        y = sc.ndtri_exp(out)
-    y = np.where(left, y, -y)
+        s = np.minimum(lp, x)
+        s -= hi
+        np.exp(s, out=s)
+        np.log1p(s, out=s)
+        s += hi
+        y = sc.ndtri_exp(s)
+    np.negative(y, out=y, where=~left)
     return y, ~np.isfinite(hi)
 
 
@@ -258,6 +259,8 @@ def ppf_terms_ok():
             use = t.ok & ~bad
             ok = bool(use.sum() > nr * nd - 3 * nd) and np.array_equal(y[use].view(np.uint64),
                                                                        ref[use].view(np.uint64))
+            one = np.ones(4)  # the equal-rows case of the logsumexp (_ppf_from_terms)
+            ok = ok and np.array_equal(np.log1p(one).view(np.uint64), np.log(one + one).view(np.uint64))
         except Exception:
             ok = False
         _PPF[0] = bool(ok)
@@ -281,23 +284,31 @@ def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt, out=None):
     lv = np.ascontiguousarray(levels, dtype=np.int64)
     n, D = data.shape
     vals = np.empty((num_samples, D)) if out is None else out
-    uni = np.empty((num_samples, D))
-    need = np.empty((num_samples, D), dtype=np.uint8)
+    if not vals.flags.c_contiguous:
+        raise ValueError("_draw_fast: out must be C-contiguous")
+    cap = num_samples * D
+    uni = np.empty(cap)
+    comp = np.empty(2 * cap, dtype=np.int64)
     datum = np.empty(num_samples, dtype=np.int64)
     stop = ctypes.c_int64(-1)
+    nc = ctypes.c_int64(0)
     with mt.lock:
         rc = _native.lib().hbx_bohb_draw(mt.addr, data.ctypes.data, n, D, bws.ctypes.data, lv.ctypes.data,
-                                         float(bw_factor), num_samples, vals.ctypes.data, uni.ctypes.data,
-                                         need.ctypes.data, datum.ctypes.data, ctypes.addressof(stop))
+                                         float(bw_factor), num_samples, vals.ctypes.data, uni.ctypes.data, None,
+                                         datum.ctypes.data, ctypes.addressof(stop), comp.ctypes.data,
+                                         ctypes.addressof(nc))
     if rc == 1:
         raise ValueError("Domain error in arguments (truncnorm bounds of candidate %d, dim %d; bohb.py:141)"
                          % divmod(stop.value, D))
     _native.check(rc)
-    m = need.view(np.bool_)
-    if not m.any():
+    k = nc.value
+    if k == 0:
         return vals
-    h = np.broadcast_to(bws, (num_samples, D))[m]
-    loc = vals[m]
+    # the elements to invert, in draw order: uniform q, element index e, term index ti = datum D + dim
+    q, e, ti = uni[:k], comp[:k], comp[cap:cap + k]
+    flat = vals.reshape(-1)
+    loc = flat.take(e)
+    h = bws.take(ti % D)
     if ppf_terms_ok():
         t = getattr(kde_good, "_tn_terms", None)
         if t is None or t.data is not data or t.bw is not bws or t.lp.shape != (n, D):
@@ -307,15 +318,14 @@ def _draw_fast(kde_good, levels, bw_factor, num_samples, R, mt, out=None):
             except AttributeError:  # (an object that takes no attributes: terms for this call only)
                 pass
         t.fill(datum, np.flatnonzero(lv == 0))
-        ri, di = np.nonzero(m)
-        rr = datum[ri]
-        y, bad = _ppf_from_terms(uni[m], t.lp[rr, di], t.mass[rr, di], t.left[rr, di])
-        rest = bad | ~t.ok[rr, di]
+        y, bad = _ppf_from_terms(q, t.lp.reshape(-1).take(ti), t.mass.reshape(-1).take(ti),
+                                 t.left.reshape(-1).take(ti))
+        rest = bad | ~t.ok.reshape(-1).take(ti)
         if rest.any():
-            y[rest] = sps.truncnorm._ppf(uni[m][rest], -loc[rest] / h[rest], (1 - loc[rest]) / h[rest])
+            y[rest] = sps.truncnorm._ppf(q[rest], -loc[rest] / h[rest], (1 - loc[rest]) / h[rest])
     else:
-        y = sps.truncnorm._ppf(uni[m], -loc / h, (1 - loc) / h)
-    vals[m] = y * (bw_factor * h) + loc
+        y = sps.truncnorm._ppf(q, -loc / h, (1 - loc) / h)
+    flat[e] = y * (bw_factor * h) + loc
     return vals
 
 

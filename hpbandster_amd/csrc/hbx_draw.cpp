@@ -98,10 +98,12 @@ int hbx_mt_draw(void* state, int32_t kind, int64_t n, int64_t high, double* out)
 
 int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const double* bw, const int64_t* levels,
                   double bw_factor, int64_t num_samples, double* vals, double* uni, uint8_t* need_ppf,
-                  int64_t* datum, int64_t* stop) {
-  if (!state || !data || !bw || !levels || !vals || !uni || !need_ppf || !stop || n <= 0 || D <= 0 ||
-      num_samples < 0)
+                  int64_t* datum, int64_t* stop, int64_t* compact, int64_t* n_compact) {
+  if (!state || !data || !bw || !levels || !vals || !uni || (!need_ppf && !compact) || !stop || n <= 0 || D <= 0 ||
+      num_samples < 0 || (compact && !n_compact))
     return hbx_fail(HBX_ERR_ARG, "hbx_bohb_draw: bad arguments");
+  const int64_t cap = num_samples * (int64_t)D;
+  int64_t nc = 0;
   MTState* s = (MTState*)state;
   if (s->pos < 0 || s->pos > kN) return hbx_fail(HBX_ERR_ARG, "hbx_bohb_draw: state position %d", s->pos);
   for (int64_t i = 0; i < num_samples; ++i) {
@@ -111,7 +113,7 @@ int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const d
     for (int32_t d = 0; d < D; ++d) {
       const int64_t e = i * D + d;
       const double m = row[d], h = bw[d];
-      need_ppf[e] = 0;
+      if (need_ppf) need_ppf[e] = 0;
       if (levels[d] == 0) {  // bohb.py:141: truncnorm.rvs(-m/bw, (1-m)/bw, loc=m, scale=bw_factor*bw)
         const double a = -m / h, b = (1. - m) / h, scale = bw_factor * h;
         if (!(a < b) || !(scale >= 0.)) {  // scipy's domain check raises before drawing
@@ -121,9 +123,17 @@ int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const d
         if (scale == 0.) {
           vals[e] = m * 1.0;  // loc * ones(size): no draw
         } else {
-          uni[e] = mt_double(s);  // random_state.uniform(size=()) = 0 + 1 * next_double
+          const double u = mt_double(s);  // random_state.uniform(size=()) = 0 + 1 * next_double
           vals[e] = m;
-          need_ppf[e] = 1;
+          if (compact) {  // the inversion's inputs packed: uniform, element index, term index (datum row, dim)
+            uni[nc] = u;
+            compact[nc] = e;
+            compact[cap + nc] = idx * (int64_t)D + d;
+            ++nc;
+          } else {
+            uni[e] = u;
+            need_ppf[e] = 1;
+          }
         }
       } else {  // bohb.py:144-147
         if (mt_double(s) < (1. - h))
@@ -134,6 +144,7 @@ int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const d
     }
   }
   *stop = -1;
+  if (n_compact) *n_compact = nc;
   return HBX_OK;
 }
 

@@ -406,12 +406,15 @@ int hbx_sh_advance_host(const double* loss, int64_t n, int64_t k, uint8_t* advan
  *   uni[e] with need_ppf[e] = 1 and vals[e] = m (the caller computes truncnorm._ppf(uni, a, b) * scale + m,
  *   the rest of rvs); levels[d] > 0: rand() < 1 - bw keeps m, else randint(levels[d]) (bohb.py:144-147).
  *   vals/uni: host f64[num_samples][D]; need_ppf: host u8[num_samples][D]; datum: host i64[num_samples]
- *   (nullable).  Replaces the scalar draw loop of bohb.py:133-147 (the scoring moved to hbx_kde_acquire). */
+ *   (nullable).  compact (nullable, host i64[2][num_samples D]): instead of need_ppf, the inversion's inputs
+ *   packed in draw order -- uni[j] the j-th uniform, compact[j] its element index i D + d, compact[num_samples
+ *   D + j] its term index datum D + d -- and *n_compact = their count (need_ppf then nullable).
+ *   Replaces the scalar draw loop of bohb.py:133-147 (the scoring moved to hbx_kde_acquire). */
 int64_t hbx_mt_state_bytes(void);
 int hbx_mt_draw(void* state, int32_t kind, int64_t n, int64_t high, double* out);
 int hbx_bohb_draw(void* state, const double* data, int64_t n, int32_t D, const double* bw, const int64_t* levels,
                   double bw_factor, int64_t num_samples, double* vals, double* uni, uint8_t* need_ppf,
-                  int64_t* datum, int64_t* stop);
+                  int64_t* datum, int64_t* stop, int64_t* compact, int64_t* n_compact);
 
 #ifdef __cplusplus
 }
