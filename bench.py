@@ -882,7 +882,7 @@ def precise_line(pair, c_dev, device, rtol=1e-5, reps=5):
     rate = pairs / (t * 1e-3)
     W = 92  # SURVEY 8d algorithmic flops per pair at 24c + 8u
     return {"workload": "kde_logpdf_rtol%g_d32_obs%d_cand%d" % (rtol, pair.good.nobs + pair.bad.nobs, Nc),
-            "value": rate, "unit": "pairs/s", "ms_l_plus_g": t, "rtol": rtol, "kernel": "kde_logpdf_dd_kernel<24,8,2> (fp32 direct differences, packed VALU, a rigorous per-candidate bound)",
+            "value": rate, "unit": "pairs/s", "ms_l_plus_g": t, "rtol": rtol, "kernel": "kde_logpdf_dd_kernel<24,8,2,LUT,SG> (fp32 direct differences, packed VALU, observation rows staged once per call and read through scalar loads, categorical matches through LDS tables, a rigorous per-candidate bound)",
             "fp64_kernel": "kde_logpdf_tiled_kernel (the candidates that bound rejects)", "per_kde": res,
             "roofline": {"bound": "valu", "achieved": W * rate / 1e12, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": W * rate / 1e12 / PEAK_FP32_TFLOPS,

@@ -2991,8 +2991,11 @@ __global__ __launch_bounds__(256) void kde_logpdf_tiled_kernel(const double* __r
 #ifndef DD_G
 #define DD_G 4  // terms per fp32 group (its sum's rounding: (DD_G - 1) 2^-24 in the bound)
 #endif
+#ifndef DD_WPE_SG
+#define DD_WPE_SG 4  // the SG kernel: its rows live in SGPRs, so more waves fit
+#endif
 template <int DC, int DU, int CPT, bool LUT = false, bool SG = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DD_WPE(DC + DU)))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG ? DD_WPE_SG : DD_WPE(DC + DU)))) void kde_logpdf_dd_kernel(const double* __restrict__ pts, int64_t Np, int32_t D,
                                                            const KdeParams* __restrict__ P,
                                                            const double* __restrict__ X,
                                                            const int64_t* __restrict__ rows, double rtol,
@@ -3554,7 +3557,9 @@ int hbx_kde_logpdf_rtol(const double* cand, int64_t Nc, int32_t D, const void* p
   const bool lut = ((variant >> 8) & 1) && !(lut_env && atoi(lut_env) == 0);
   const DdFns dd = (!exact_only && !(variant & 1)) ? pick_logpdf_dd(dc_pad, du_pad, &cpt, lut) : DdFns{};
   const char* sg_env = getenv("HBX_DD_SG");  // 0: the LDS-staged dd kernel everywhere (tests)
-  const bool sg = dd.sg && !(sg_env && atoi(sg_env) == 0);
+  // (small calls: the LDS-staged kernel alone -- the staging launch and a second dd launch would cost more than
+  // the SG kernel saves, and the scratch of a few thousand candidates rarely holds the rows)
+  const bool sg = dd.sg && Nc >= 8192 && !(sg_env && atoi(sg_env) == 0);
   HBX_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), s));
   if (dd.lds) {
     const dim3 g((unsigned)((Nc + 256 * cpt - 1) / (256 * cpt)));

@@ -646,7 +646,7 @@ def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, sg, monkeypatc
     """Candidates that sit on an observation of a later chunk while every observation of chunk 0 is thousands of
     log2 units away: the group holding that observation overflows the first chunk's reference point, which moves
     up and the group is summed again; candidates with codes outside [0, 3] take the fp64 pass under the tables.
-    Every ln pdf within the contract of the oracle's.  sg: 5376 candidates (their scratch holds the staged rows:
+    Every ln pdf within the contract of the oracle's.  sg: 8256 candidates (their scratch holds the staged rows:
     the scalar-staged kernel) or the LDS-staged kernel (HBX_DD_SG=0)."""
     from hpbandster_amd import kde
     monkeypatch.setenv("HBX_DD_LUT", lut)
@@ -669,10 +669,10 @@ def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, sg, monkeypatc
     k = pair.good
     if du:
         assert (k.variant >> 8) & 1
-    C = np.tile(C, (56, 1))  # 5376 rows: 16 B of scratch each >= 704 staged rows x 28 floats
+    C = np.tile(C, (86, 1))  # 8256 rows (the SG kernel runs from 8192 candidates; 16 B of scratch each >= 704 x 28 floats)
     lref = O.log_pdf_many(X, bw, vt, C[:96], nlev)
     got = _capi_logpdf_rtol(k, C)
-    assert np.array_equal(got, np.tile(got[:96], 56))
+    assert np.array_equal(got, np.tile(got[:96], 86))
     got = got[:96]
     assert np.isfinite(lref).all()
     err = np.abs(got - lref) / np.maximum(1.0, np.abs(lref))
