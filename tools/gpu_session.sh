@@ -35,7 +35,7 @@ case $MODE in
   both) run_tests && run_bench ;;
   py) S=$1; shift; timeout -k 10 900 python -u $S "$@" > $OUT/$(basename $S .py).txt 2>&1; rc=$?; tail -40 $OUT/$(basename $S .py).txt; exit $rc ;;
   prof) S=$1; shift; cd /tmp && export TMPDIR=/tmp && cd $R
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u $S "$@" \
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u $S "$@" \
       > $OUT/$(basename $S .py)_prof.txt 2>&1; rc=$?; tail -20 $OUT/$(basename $S .py)_prof.txt; exit $rc ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac

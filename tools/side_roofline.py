@@ -51,6 +51,12 @@ BASES = [
      "config #5: losses read (8 B) + order written (8 B) per configuration", "hbm", B5 * N5 * 16),
     ("sh_select_kernel",
      "config #5: losses read (8 B) + mask written (1 B) per configuration", "hbm", B5 * N5 * 9),
+    # the acquisition's tail after the scoring launch (config #2 when run alone): latency-bound chains, no
+    # roofline -- durations and counters only
+    ("kde_combine_kernel", "acquisition tail: score intervals, segment minima (36 B per candidate)", "lat", 0),
+    ("kde_shortlist_kernel", "acquisition tail: the shortlist predicate per candidate", "lat", 0),
+    ("kde_exact_kernel", "acquisition tail: fp64 re-score of the shortlist (numpy order)", "lat", 0),
+    ("kde_final_kernel", "acquisition tail: argmin, record published to mapped host memory", "lat", 0),
 ]
 
 
@@ -96,7 +102,9 @@ def main():
         c = next((pmc[k] for k in pmc if sub in k), {})
         r = {"kernel": name, "dispatches_traced": len(ds), "dur_us_mean": dur * 1e6,
              "dur_us_median": statistics.median(ds) * 1e6, "basis": basis, "bound": bound}
-        if bound == "hbm":
+        if bound == "lat":
+            r.update(achieved=0.0, peak=None, unit=None, frac=0.0)
+        elif bound == "hbm":
             ach = work / dur / 1e9
             r.update(achieved=ach, peak=HBM, unit="GB/s", frac=ach / HBM, algorithmic_bytes=work)
         else:
