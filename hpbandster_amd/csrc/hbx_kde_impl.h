@@ -206,19 +206,23 @@ __device__ __forceinline__ void stage_rows(const double* __restrict__ src, int64
   if (D <= 64) {  // rows of D <= 64: lane = (row in pass, column), one division per lane instead of one per element
     const int rpp = 64 / D;  // rows per pass (uniform)
     const int lr = lane / D, lc = lane - lr * D;
-    const bool act = lr < rpp;
-    for (int r0 = 0; r0 < (int)nv; r0 += 16 * rpp) {
-      double t[16];
+    if (lr < rpp) {
+      // the whole passes: uniform bases, one per-lane offset, up to 16 loads in flight, no per-element index
+      // arithmetic and only uniform guards; then the ragged last pass (rows past nv masked)
+      const int npf = (int)nv / rpp;
+      const unsigned vo = (unsigned)(lr * D + lc), xo = (unsigned)(lr * DS + lc);
+      const int sq = __builtin_amdgcn_readfirstlane(rpp * D), xq = __builtin_amdgcn_readfirstlane(rpp * DS);
+      for (int p0 = 0; p0 < npf; p0 += 16) {
+        double t[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = r0 + q * rpp + lr;
-        t[q] = (act && row < nv) ? src[row * D + lc] : 0.0;
-      }
+        for (int q = 0; q < 16; ++q)
+          if (p0 + q < npf) t[q] = (src + (int64_t)(p0 + q) * sq)[vo];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = r0 + q * rpp + lr;
-        if (act && row < nv) xs[row * DS + lc] = t[q];
+        for (int q = 0; q < 16; ++q)
+          if (p0 + q < npf) (xs + (p0 + q) * xq)[xo] = t[q];
       }
+      const int row = npf * rpp + lr;
+      if (row < (int)nv) xs[row * DS + lc] = src[row * D + lc];
     }
     return;
   }

@@ -679,6 +679,41 @@ def test_dd_pass_terms_far_above_the_first_chunk(device, du, lut, sg, monkeypatc
     assert err.max() <= 1e-5, err.max()
 
 
+@pytest.mark.parametrize("shape", [(8, 0, 0), (4, 4, 3), (8, 8, 4), (16, 16, 5), (24, 0, 0), (16, 8, 2)])
+def test_dd_scalar_staged_across_buckets(device, shape, monkeypatch):
+    """The SG instance in the other dd buckets it is built for (rows of at most 32 floats: continuous-only,
+    two-bit codes through the tables, wider codes through the packed compare): bit-identical to the
+    LDS-staged kernel on 8192 candidates, within the contract of the oracle on a sample."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    dc, du, lv = shape
+    n = 900
+    X = S.make_observations(n, dc, du, lv, seed=61 + dc + du)
+    Lo = S.make_losses(n, seed=62)
+    vt = S.var_type_string(dc, du)
+    rs = np.random.RandomState(63)
+    C = S.make_candidates(8192, dc, du, lv, seed=64)
+    C[:3000] = X[rs.randint(0, n, 3000)]
+    if dc:
+        C[:3000, :dc] += 0.02 * rs.randn(3000, dc)
+    pair = kde.fit_pair(X, Lo, vt, len(vt) + 1, device=device)
+    sel = np.r_[np.arange(0, 8192, 160), 1, 2]
+    for k in (pair.good, pair.bad):
+        monkeypatch.setenv("HBX_DD_SG", "1")
+        a = _capi_logpdf_rtol(k, C)
+        monkeypatch.setenv("HBX_DD_SG", "0")
+        b = _capi_logpdf_rtol(k, C)
+        assert np.array_equal(a, b, equal_nan=True), shape
+        lref = O.log_pdf_many(k.data, k.bw, vt, C[sel], k.nlev)
+        if k.has_neg:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                lref = np.log(O.pdf_many(k.data, k.bw, vt, C[sel], k.nlev))
+        assert np.array_equal(np.isnan(a[sel]), np.isnan(lref)), shape
+        fin = np.isfinite(lref)
+        err = np.abs(a[sel][fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        assert err.max() <= 1e-5, (shape, err.max())
+
+
 @pytest.mark.parametrize("lut", ["1", "0"])
 def test_dd_scalar_staged_equals_lds_staged(device, lut, monkeypatch):
     """The scalar-staged direct-difference kernel (rows staged once into the call's scratch, read through SGPRs)
