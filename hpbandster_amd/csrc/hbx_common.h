@@ -131,6 +131,9 @@ struct AcqResult {
 __device__ __forceinline__ void hbx_publish_store(uint32_t* dst, uint32_t v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void hbx_publish_store64(uint64_t* dst, uint64_t v) {
+  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void hbx_publish_done(int32_t* done, int32_t seq) {
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1708,11 +1708,8 @@ __device__ __forceinline__ bool near_best(double s, double rp, double best, doub
 }
 
 // A get_config pick published to device-mapped host memory by the final argmin (hbx_kde_acquire_bound with err /
-// row_out): the record, whether any of the call's candidates hit a sampler domain error, the winning row,
-// then the completion word (byte offsets below)
-#define HBX_PICK_ERR 48
-#define HBX_PICK_DONE 52
-#define HBX_PICK_ROW 64
+// row_out): the record, whether any of the call's candidates hit a sampler domain error, the winning row (as
+// tagged 8-byte words: kde_final_body)
 struct PickOut {
   const double* cand;
   const uint8_t* err;  // nullable
@@ -1846,21 +1843,24 @@ __device__ void kde_final_body(const int32_t* __restrict__ list, const int32_t* 
     *res = r;
     rec_sh = r;
   }
-  if (host_res || pick.out) {  // uniform: the record to mapped host memory, then the completion word
+  if (host_res || pick.out) {  // uniform: the record (and a pick's flag and row) to mapped host memory
     static_assert(sizeof(AcqResult) % 4 == 0, "record of whole words");
     __syncthreads();
-    uint32_t* out = pick.out ? (uint32_t*)pick.out : (uint32_t*)host_res;
-    if (threadIdx.x < (int)(sizeof(AcqResult) / 4)) hbx_publish_store(out + threadIdx.x, ((const uint32_t*)&rec_sh)[threadIdx.x]);
-    if (pick.out) {  // a pick: + the domain-error flag and the winning row
-      if (threadIdx.x == 0) hbx_publish_store(out + HBX_PICK_ERR / 4, err_any ? 1u : 0u);
+    // every 32-bit word as one 8-byte system-scope store tagged with the call's sequence number (seq << 32 |
+    // word): the host takes each word only once its tag is the call's, so there is no acknowledgement wait
+    // and no completion word (hbx_pub_wait)
+    uint64_t* out = (uint64_t*)(pick.out ? pick.out : (char*)host_res);
+    const uint64_t tag = (uint64_t)(uint32_t)seq << 32;
+    constexpr int RW = (int)(sizeof(AcqResult) / 4);
+    if (threadIdx.x < RW) hbx_publish_store64(out + threadIdx.x, tag | ((const uint32_t*)&rec_sh)[threadIdx.x]);
+    if (pick.out) {  // a pick: + the domain-error flag (word RW) and the winning row (words RW + 1 ..)
+      if (threadIdx.x == 0) hbx_publish_store64(out + RW, tag | (err_any ? 1u : 0u));
       const int64_t idx = rec_sh.index - index_base;
       if (rec_sh.index >= 0 && idx < pick.Nc)
         for (int w = threadIdx.x; w < 2 * pick.D; w += 256)
-          hbx_publish_store(out + HBX_PICK_ROW / 4 + w, ((const uint32_t*)(pick.cand + idx * pick.D))[w]);
+          hbx_publish_store64(out + RW + 1 + w, tag | ((const uint32_t*)(pick.cand + idx * pick.D))[w]);
     }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words acknowledged
-    __syncthreads();                                       // ... and every wave's
-    if (threadIdx.x == 0) hbx_publish_done(pick.out ? (int32_t*)(pick.out + HBX_PICK_DONE) : done, seq);
+    (void)done;
   }
 }
 
@@ -3634,6 +3634,10 @@ __global__ void fetch_publish_kernel(const uint32_t* __restrict__ src, int32_t w
 }
 
 #define FETCH_MAPPED_BYTES 4096
+// the final kernel's tagged words (hbx_kde_acquire_bound) live past the completion word, apart from hbx_fetch's
+// untagged bytes (whose words could otherwise pass for a later call's tags)
+#define PUB_OFF (FETCH_MAPPED_BYTES + 64)
+#define PUB_BYTES (8 * (16 + 2 * HBX_MAX_D))
 // this thread's device-mapped coherent host buffer: FETCH_MAPPED_BYTES of data, then the completion word
 // (allocated on first use and kept for the thread's lifetime)
 thread_local char* t_mapped = nullptr;
@@ -3641,8 +3645,9 @@ thread_local int32_t t_seq = 0;
 static int mapped_buffer(char** out) {
   if (!t_mapped) {
     void* p = nullptr;
-    HBX_HIP(hipHostMalloc(&p, FETCH_MAPPED_BYTES + 64,
+    HBX_HIP(hipHostMalloc(&p, PUB_OFF + PUB_BYTES,
                           hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    memset(p, 0, PUB_OFF + PUB_BYTES);  // (no stale tag can match: sequence numbers start at 1)
     void* dp = nullptr;
     HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
     if (dp != p) {
@@ -3664,6 +3669,29 @@ static int wait_done(int32_t* done, int32_t seq, hipStream_t s, const char* who)
     HBX_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq)
       return hbx_fail(HBX_ERR_HIP, "%s: the device did not store its completion word", who);
+  }
+  return HBX_OK;
+}
+
+// spin until `n` tagged words (seq << 32 | word, 8 bytes each, stored by the device in any order) all carry
+// this call's sequence number, then take their words (bounded like wait_done)
+static int hbx_pub_wait(const volatile uint64_t* w, int n, int32_t seq, uint32_t* out, hipStream_t s, const char* who) {
+  const uint32_t sq = (uint32_t)seq;
+  int i = 0;
+  for (int64_t it = 0; it < 20000000 && i < n; ++it) {
+    while (i < n) {
+      const uint64_t v = __atomic_load_n((const uint64_t*)(w + i), __ATOMIC_ACQUIRE);
+      if ((uint32_t)(v >> 32) != sq) break;
+      out[i++] = (uint32_t)v;
+    }
+  }
+  if (i < n) {
+    HBX_HIP(hipStreamSynchronize(s));
+    for (; i < n; ++i) {
+      const uint64_t v = __atomic_load_n((const uint64_t*)(w + i), __ATOMIC_ACQUIRE);
+      if ((uint32_t)(v >> 32) != sq) return hbx_fail(HBX_ERR_HIP, "%s: the device did not publish word %d", who, i);
+      out[i] = (uint32_t)v;
+    }
   }
   return HBX_OK;
 }
@@ -3741,21 +3769,32 @@ int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int6
   int rc = mapped_buffer(&mapped);
   if (rc) return rc;
   const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
-  const bool pick = err || row_out;  // (HBX_PICK_ROW + 8 D <= FETCH_MAPPED_BYTES for D <= HBX_MAX_D)
-  int32_t* done = pick ? (int32_t*)(mapped + HBX_PICK_DONE) : (int32_t*)(mapped + FETCH_MAPPED_BYTES);
+  const bool pick = err || row_out;  // (8 (13 + 2 D) <= PUB_BYTES for D <= HBX_MAX_D)
   rc = acquire_impl("hbx_kde_acquire_bound", cand, Nc, Nc > 0 ? Nc : 1, b.D, index_base, b.params_good, b.table_good,
                     b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad, b.variant_bad,
                     b.dc_pad, b.du_pad, b.nmax, nullptr, nullptr, nullptr, workspace, ws_bytes, events, stream,
-                    pick ? nullptr : (AcqResult*)mapped, pick ? nullptr : done, seq,
-                    pick ? PickOut{cand, err, Nc, b.D, mapped} : PickOut{});
+                    pick ? nullptr : (AcqResult*)(mapped + PUB_OFF), nullptr, seq,
+                    pick ? PickOut{cand, err, Nc, b.D, mapped + PUB_OFF} : PickOut{});
   if (rc) return rc;
-  rc = wait_done(done, seq, (hipStream_t)stream, "hbx_kde_acquire_bound");
+  // the final kernel's tagged words: the record, then (a pick) the flag, then the row when there is a winner
+  constexpr int RW = (int)(sizeof(AcqResult) / 4);
+  const volatile uint64_t* w = (const volatile uint64_t*)(mapped + PUB_OFF);
+  uint32_t words[RW];
+  rc = hbx_pub_wait(w, RW, seq, words, (hipStream_t)stream, "hbx_kde_acquire_bound");
   if (rc) return rc;
   AcqResult r;
-  memcpy(&r, mapped, sizeof(AcqResult));
-  if (pick && *(const int32_t*)(mapped + HBX_PICK_ERR)) r.flags |= HBX_ACQ_DOMAIN_ERR;
+  memcpy(&r, words, sizeof(AcqResult));
+  if (pick) {
+    uint32_t e = 0;
+    rc = hbx_pub_wait(w + RW, 1, seq, &e, (hipStream_t)stream, "hbx_kde_acquire_bound");
+    if (rc) return rc;
+    if (e) r.flags |= HBX_ACQ_DOMAIN_ERR;
+    if (row_out && r.index >= 0 && r.index - index_base < Nc) {
+      rc = hbx_pub_wait(w + RW + 1, 2 * b.D, seq, (uint32_t*)row_out, (hipStream_t)stream, "hbx_kde_acquire_bound");
+      if (rc) return rc;
+    }
+  }
   memcpy(rec_out, &r, sizeof(AcqResult));
-  if (row_out && r.index >= 0) memcpy(row_out, mapped + HBX_PICK_ROW, 8 * (size_t)b.D);
   return HBX_OK;
 }
 
