@@ -1177,7 +1177,13 @@ def main():
     xchg = None
     if world > 1:  # one collective per step: RCCL all-gather of the 48-byte records + device reduction
         from hpbandster_amd.distributed import WinnerExchange
-        xchg = WinnerExchange(device, transport="rccl" if a.backend == "nccl" else "records")
+        try:
+            xchg = WinnerExchange(device, transport="rccl" if a.backend == "nccl" else "records")
+        except Exception as e:  # libhbx's communicator refused: the same exchange on torch's process group
+            if a.backend != "nccl":
+                raise
+            log("rank %d: hbx_rccl_comm_init failed (%r): exchanging the records on torch's nccl group" % (rank, e))
+            xchg = WinnerExchange(device, transport="torch")
 
     def step(ev):
         if xchg is None:  # one rank: the acquisition's record reaches the host in the same native call
@@ -1263,7 +1269,9 @@ def main():
                    "parallelism": ("one GPU, no collective (the final argmin kernel publishes the record to the host)"
                                    if world == 1 else "candidate-sharded x%d, %s" % (
                        world, "one collective per step: hbx_argmax_allreduce (RCCL all-gather of result records)"
-                       if a.backend == "nccl" else "gloo all_gather of result records (rehearsal)")),
+                       if xchg.transport == "rccl" else
+                       "one collective per step: all_gather of the device records on torch's nccl group (RCCL)"
+                       if xchg.transport == "torch" else "gloo all_gather of result records (rehearsal)")),
                    "winner": winner[0], "shortlist": last.shortlist,
                    "candidates": "rows [%d, %d) of synthetic.make_candidates_blocked (seed 3) per rank, the first %d "
                                  "rows in all" % (base, base + Nc, pairs_step // (Ng + Nb)),

@@ -97,8 +97,10 @@ class WinnerExchange(object):
 
     ``transport='rccl'``: libhbx's own RCCL communicator (its unique id travels once through
     torch.distributed's default group at construction), ``hbx_argmax_allreduce`` on the device.
-    ``transport='records'``: torch.distributed all_gather of the records (e.g. gloo), then the same
-    device reduction (``hbx_argmax_records``).
+    ``transport='records'``: torch.distributed all_gather of the records through host memory (e.g. gloo),
+    then the same device reduction (``hbx_argmax_records``).
+    ``transport='torch'``: the same all_gather of the device records on torch's own process group (its
+    nccl backend is RCCL as well) -- the fallback when libhbx's communicator cannot be set up.
     """
 
     def __init__(self, device, transport="rccl", group=None):
@@ -131,8 +133,8 @@ class WinnerExchange(object):
             with N.on_device(torch.device("cuda", dev_index)):
                 N.check(L.hbx_rccl_comm_init(ctypes.addressof(h), self.world, N.ptr(idb), self.rank, dev_index))
             self.comm = h.value
-        elif transport != "records":
-            raise ValueError("transport must be 'rccl' or 'records'")
+        elif transport not in ("records", "torch"):
+            raise ValueError("transport must be 'rccl', 'records' or 'torch'")
 
     def exchange(self, rec, stream=None):
         """rec: this rank's device record (48 uint8) -> the global winner's device record (self.out);
@@ -147,7 +149,7 @@ class WinnerExchange(object):
                                                sh))
             else:
                 if self.world > 1:
-                    loc = rec.cpu()
+                    loc = rec.cpu() if self.transport == "records" else rec[:REC_BYTES]
                     parts = [torch.empty_like(loc) for _ in range(self.world)]
                     dist.all_gather(parts, loc, group=self.group)
                     self.gather.copy_(torch.cat(parts))

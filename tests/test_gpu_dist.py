@@ -39,6 +39,18 @@ def test_rccl_exchange_world1_matches_acquire(device):
         x.close()
 
 
+def test_torch_transport_world1_matches_acquire(device):
+    """The fallback exchange (device records all-gathered on torch's process group, then the device reduction)
+    at one rank: the exchanged winner is the local acquisition's record."""
+    from hpbandster_amd.distributed import WinnerExchange, acquire_sharded
+    pair, C = _pair_and_cands(device)
+    want = pair.acquire(C)
+    x = WinnerExchange(device, transport="torch")
+    idx, score, g = acquire_sharded(pair, C, 0, x)
+    assert (idx, score) == (want.index, want.score)
+    assert g.shortlist == want.shortlist
+
+
 def _rec(index, score, rel=1e-13, flags=0):
     from hpbandster_amd.kde import RESULT_FMT
     return struct.pack(RESULT_FMT, index, score, rel, flags, 3, 1, 0.5, 0.25)
