@@ -115,7 +115,10 @@ __global__ __launch_bounds__(256) void seg_argsort_kernel(const double* __restri
 // segments of up to 1024 losses: one wave each, sorted in registers (wave_sort_1024).  list / count (numpy's
 // tie order, nullable): a segment whose sorted keys hold two equal neighbours joins `list` -- the sorted keys
 // are in the wave's registers, so the tie check reads no memory (seg_tie_flag_kernel re-gathered every key)
-__global__ __launch_bounds__(256) void seg_argsort_wave_kernel(const double* __restrict__ loss,
+#ifndef SORT_WPE
+#define SORT_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void seg_argsort_wave_kernel(const double* __restrict__ loss,
                                                                const int64_t* __restrict__ seg_off, int64_t B,
                                                                int64_t* __restrict__ order, int32_t* list,
                                                                int32_t* count) {
@@ -692,8 +695,12 @@ __global__ __launch_bounds__(256) void kde_fit_wave_kernel(
   const int64_t per_set = B * (int64_t)D;
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= 2 * per_set) return;  // (no barriers below)
-  const int set = q >= per_set ? 1 : 0;
-  const int64_t qq = q - set * per_set;
+#ifndef FIT_BAD_FIRST
+#define FIT_BAD_FIRST 1
+#endif
+  // the bad sets' (long) chains first, the good sets' (short) ones filling the tail
+  const int set = (q >= per_set) != (FIT_BAD_FIRST != 0) ? 1 : 0;
+  const int64_t qq = q >= per_set ? q - per_set : q;
   const int64_t b = qq / D;
   const int32_t d = (int32_t)(qq - b * D);
   const int64_t ns = set ? n_bad[b] : n_good[b];
