@@ -684,7 +684,9 @@ __global__ __launch_bounds__(256) void kde_fit_col_kernel(
 // read two batches ahead and the rows one batch ahead of the adds (U loads of each in flight per lane).
 // Level counts: a 128-bit register mask per categorical lane in the mean pass; codes >= 128 (rare) take
 // one more pass per 128-code window.
-#define FIT_WAVE_U 8
+#ifndef FIT_WAVE_U
+#define FIT_WAVE_U 12
+#endif
 __global__ __launch_bounds__(256) void kde_fit_wave_kernel(
     const double* __restrict__ X, int32_t D, const int64_t* __restrict__ seg_off, int64_t B,
     const int64_t* __restrict__ order, const int64_t* __restrict__ n_good, const int64_t* __restrict__ n_bad,
@@ -722,16 +724,18 @@ __global__ __launch_bounds__(256) void kde_fit_wave_kernel(
   auto pass = [&](auto sq_tag, double mean) __attribute__((always_inline)) -> double {
     constexpr bool SQ = decltype(sq_tag)::value;
     double acc = 0.0;
-    int64_t o1[U], o2[U];
+    // the order's entries are segment-local row indices (< 2^31): their low words, one register each
+    const int32_t* ord32 = reinterpret_cast<const int32_t*>(ord);
+    int32_t o1[U], o2[U];
     double v0[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) o1[k] = k < ns ? ord[k] : 0;  // (row 0 past the end: read, unused)
+    for (int k = 0; k < U; ++k) o1[k] = k < ns ? ord32[2 * k] : 0;  // (row 0 past the end: read, unused)
 #pragma unroll
     for (int k = 0; k < U; ++k) v0[k] = Xs[o1[k] * (int64_t)D];
 #pragma unroll
-    for (int k = 0; k < U; ++k) o1[k] = U + k < ns ? ord[U + k] : 0;
+    for (int k = 0; k < U; ++k) o1[k] = U + k < ns ? ord32[2 * (U + k)] : 0;
 #pragma unroll
-    for (int k = 0; k < U; ++k) o2[k] = 2 * U + k < ns ? ord[2 * U + k] : 0;
+    for (int k = 0; k < U; ++k) o2[k] = 2 * U + k < ns ? ord32[2 * (2 * U + k)] : 0;
     for (int64_t i = 0; i < ns; i += U) {
       double v1[U];
 #pragma unroll
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(256) void kde_fit_wave_kernel(
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         o1[k] = o2[k];
-        o2[k] = i + 3 * U + k < ns ? ord[i + 3 * U + k] : 0;  // ranks [i + 3U, i + 4U)
+        o2[k] = i + 3 * U + k < ns ? ord32[2 * (i + 3 * U + k)] : 0;  // ranks [i + 3U, i + 4U)
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
