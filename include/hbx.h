@@ -175,8 +175,9 @@ int hbx_kde_acquire(const double* cand, int64_t Nc, int32_t D, int64_t index_bas
  * the KDEs' device buffers alive while it is in use, and frees it with hbx_kde_pair_free.  NULL on bad
  * arguments (hbx_last_error).
  * hbx_kde_acquire_bound: hbx_kde_acquire (fast scoring instances, no ln-pdf outputs) whose final kernel also
- * stores the 48-byte record into this thread's device-mapped host buffer and a completion word last; the call
- * spins on that word (bounded, then it synchronises `stream`) and copies the record to rec_out (host, 48 bytes;
+ * stores the 48-byte record into this thread's device-mapped host buffer, every 32-bit word as an 8-byte word
+ * tagged with the call's sequence number; the call spins until every word carries its tag (bounded, then it
+ * synchronises `stream`) and copies the record to rec_out (host, 48 bytes;
  * it also stays in the workspace, hbx_kde_result_ptr).  err (nullable, device u8[Nc], the GPU sampler's
  * domain-error flags): HBX_ACQ_DOMAIN_ERR is set in the record when any flag is set.  row_out (nullable, host
  * f64[D]): the winning candidate's row.  Both come with the record from the same final kernel: one wait for
@@ -215,7 +216,8 @@ int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
 /* Copy `bytes` of device memory (e.g. the result record) to host memory on `stream` and wait for it without
  * a blocking synchronisation: up to 4096 bytes go through the calling thread's device-mapped host buffer
- * (allocated on the thread's first call and kept for its lifetime, 4160 bytes) with a completion word the
+ * (allocated on the thread's first call and kept for its lifetime, ~8.4 KB with hbx_kde_acquire_bound's
+ * tagged region) with a completion word the
  * call spins on; larger or unaligned copies poll the stream.  Replaces the caller's copy + synchronise
  * after hbx_kde_acquire (the reference's get_config returns the pick to its caller: bohb.py:166). */
 int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
