@@ -105,3 +105,40 @@ def test_bound_pair_record_equals_the_async_record(device):
     assert rec.flags & kde.ACQ_DOMAIN_ERR and rec.index == r.index - (1 << 33)
     seen = {pair.acquire(C[i * 1000:(i + 1) * 1000]).index for i in range(20)}
     assert len(seen) > 1 and min(seen) >= 0
+
+
+def test_tagged_record_words_interleaved_with_fetches(device):
+    """hbx_kde_acquire_bound's record travels as sequence-tagged words in the thread's mapped buffer, beside
+    hbx_fetch's untagged bytes: 300 calls alternating with fetches on the same thread (their data written where
+    no tag is read), picks with and without rows, varying candidate sets -- every record equals the workspace's
+    record and every row the winner's."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(400, 24, 8, 4, seed=25)
+    pair = kde.fit_pair(X, S.make_losses(400, seed=26), S.var_type_string(24, 8), 33, device=device)
+    C = torch.from_numpy(S.make_candidates(6400, 24, 8, 4, seed=27)).to(device)
+    ws = torch.empty(pair.workspace_bytes(6400), dtype=torch.uint8, device=device)
+    L = N.lib()
+    sh = N.stream_handle(None, device)
+    off = pair.result_offset()
+    err = torch.zeros(6400, dtype=torch.uint8, device=device)
+    junk = torch.randint(0, 256, (4096,), dtype=torch.uint8, device=device)
+    rs = np.random.RandomState(3)
+    for it in range(300):
+        lo = int(rs.randint(0, 6336))
+        n = int(rs.randint(1, 65))
+        dst = ctypes.create_string_buffer(4096)  # a fetch first: arbitrary bytes through the same mapped buffer
+        N.check(L.hbx_fetch(dst, junk.data_ptr(), 4096, sh))
+        a = ctypes.create_string_buffer(64)
+        row = np.full(32, np.nan)
+        pick = it % 2 == 1
+        N.check(L.hbx_kde_acquire_bound(pair._bound, C[lo:].data_ptr(), n, lo, ws.data_ptr(), ws.numel(),
+                                        err.data_ptr() if pick else None, None, sh, a,
+                                        row.ctypes.data if pick else None))
+        w = kde.fetch_bytes(ws[off:off + kde.RESULT_BYTES])
+        assert a.raw[:kde.RESULT_BYTES] == w, it
+        r = kde.AcqResult.from_bytes(w)
+        if pick and r.index >= 0:
+            np.testing.assert_array_equal(row, C[r.index].cpu().numpy())
