@@ -1061,3 +1061,41 @@ def test_exact_scan_equals_the_shortlist_launch(device, monkeypatch, case):
         l = O.pdf_many(pair.good.data, pair.good.bw, vt, C, pair.good.nlev)
         g = O.pdf_many(pair.bad.data, pair.bad.bw, vt, C, pair.bad.nlev)
         assert scan[0][0] == O.select(l, g)[0]
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_dd_scalar_staged_random_shapes(device, case, monkeypatch):
+    """Seeded random shapes for the SG instance (continuous and categorical counts, level counts, observation
+    counts that are not multiples of the group size or of a chunk, fewer than one chunk): bit-identical to the
+    LDS-staged kernel on >= 8192 candidates, within the contract of the oracle on a sample."""
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    rs = np.random.RandomState(700 + case)
+    dc = int(rs.randint(1, 29))
+    du = int(rs.randint(0, 9))
+    lv = int(rs.randint(2, 7))
+    n = int(rs.choice([40, 63, 65, 131, 517, 1003, 2999]))
+    nc = 8192 + int(rs.randint(0, 700))
+    X = S.make_observations(n, dc, du, lv, seed=800 + case)
+    Lo = S.make_losses(n, seed=900 + case)
+    vt = S.var_type_string(dc, du)
+    C = S.make_candidates(nc, dc, du, lv, seed=1000 + case)
+    C[: nc // 3] = X[rs.randint(0, n, nc // 3)]
+    C[: nc // 3, :dc] += 0.02 * rs.randn(nc // 3, dc)
+    pair = kde.fit_pair(X, Lo, vt, min(len(vt) + 1, n - 1), device=device)
+    assert pair is not None, (dc, du, n)
+    sel = np.r_[np.arange(0, nc, 97), 0, 1]
+    for k in (pair.good, pair.bad):
+        monkeypatch.setenv("HBX_DD_SG", "1")
+        a = _capi_logpdf_rtol(k, C)
+        monkeypatch.setenv("HBX_DD_SG", "0")
+        b = _capi_logpdf_rtol(k, C)
+        assert np.array_equal(a, b, equal_nan=True), (dc, du, lv, n)
+        lref = O.log_pdf_many(k.data, k.bw, vt, C[sel], k.nlev)
+        if k.has_neg:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                lref = np.log(O.pdf_many(k.data, k.bw, vt, C[sel], k.nlev))
+        assert np.array_equal(np.isnan(a[sel]), np.isnan(lref)), (dc, du, lv, n)
+        fin = np.isfinite(lref)
+        err = np.abs(a[sel][fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
+        assert err.size == 0 or err.max() <= 1e-5, ((dc, du, lv, n), err.max())
