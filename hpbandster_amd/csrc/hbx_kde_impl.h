@@ -351,3 +351,14 @@ logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
 logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse = false);  // hbx_score_h32.hip
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse = false);
+
+// hbx_kde.hip's pieces the ln-pdf contract (hbx_logpdf.hip, hbx_kde_logpdf_rtol) launches:
+// the precise estimate instance of a bucket (main + rescue into est; HBX_ERR_UNSUPPORTED when it has none) ...
+int hbx_logpdf_estimate(const double* cand, int64_t Nc, int32_t D, const void* params, const float* table,
+                        int32_t dc_pad, int32_t du_pad, int32_t variant, KdeEst* est, hipStream_t s);
+// ... and the fp64 evaluation of the listed candidates list[0 .. *count): per_point = the one-block-per-point
+// log-space kernel (buckets without a tiled instance), then ln of the exact pdf (negative categorical factors,
+// structural NaN; its blocks exit for other KDEs)
+int hbx_logpdf_exact_listed(const double* cand, int64_t Nc, int32_t D, const KdeParams* P, const double* X,
+                            const int64_t* rows, double* out, const int32_t* list, const int32_t* count,
+                            bool per_point, hipStream_t s);
