@@ -70,6 +70,7 @@ SIGNATURES = {
     "hbx_event_elapsed_ms": (c_i32, [c_vp, c_vp, c_vp]),
     "hbx_kde_result_ptr": (c_vp, [c_vp]),
     "hbx_fetch": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
+    "hbx_mapped_host_buffers": (c_i64, []),
     "hbx_kde_ws_offsets": (c_i32, [c_i64, c_i64, c_i64, c_vp]),
     "hbx_np_exp": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "hbx_kde_pdf_scratch_bytes": (c_i64, [c_i64]),

@@ -18,6 +18,7 @@
 #include <string.h>
 #include <stddef.h>
 
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -2362,6 +2363,7 @@ int hbx_kde_refit(double* X, double* loss, int64_t n, int32_t D, const int32_t* 
 // process-wide pool for the next thread (no HIP call from a thread-exit destructor, no pinned memory lost per
 // short-lived result thread).  The sequence number travels with the buffer, so a pooled buffer's old flags
 // never match a new owner's next call.
+static std::atomic<int64_t> g_mapped_live{0};  // device-mapped host buffers allocated (hbx_mapped_host_buffers)
 struct RefitMapped {
   char* p = nullptr;
   int64_t cap = 0;
@@ -2410,6 +2412,7 @@ static int refit_mapped_buffer(int64_t bytes, RefitMapped** out) {
       }
       nb.p = (char*)p;
       nb.cap = cap;
+      g_mapped_live.fetch_add(1, std::memory_order_relaxed);
       for (int i = 0; i < 16; ++i) ((volatile uint64_t*)(nb.p + cap))[i] = 0;  // flagged info words
     }
     if (b.p) {  // the smaller buffer (every call on it completed) back to the pool
@@ -2884,26 +2887,56 @@ __global__ void fetch_publish_kernel(const uint32_t* __restrict__ src, int32_t w
 // untagged bytes (whose words could otherwise pass for a later call's tags)
 #define PUB_OFF (FETCH_MAPPED_BYTES + 64)
 #define PUB_BYTES (8 * (16 + 2 * HBX_MAX_D))
-// this thread's device-mapped coherent host buffer: FETCH_MAPPED_BYTES of data, then the completion word
-// (allocated on first use and kept for the thread's lifetime)
-thread_local char* t_mapped = nullptr;
-thread_local int32_t t_seq = 0;
-static int mapped_buffer(char** out) {
-  if (!t_mapped) {
-    void* p = nullptr;
-    HBX_HIP(hipHostMalloc(&p, PUB_OFF + PUB_BYTES,
-                          hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
-    memset(p, 0, PUB_OFF + PUB_BYTES);  // (no stale tag can match: sequence numbers start at 1)
-    void* dp = nullptr;
-    HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
-    if (dp != p) {
-      (void)hipHostFree(p);
-      return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+// this thread's device-mapped coherent host buffer: FETCH_MAPPED_BYTES of data, the completion word, then the
+// tagged region.  Held for the thread's lifetime and then pooled for the next thread, like the refit buffers
+// (short-lived result threads do not each leave one behind); its sequence number travels with it, so a pooled
+// buffer's old completion word and tags never match a new owner's calls.
+struct AcqMapped {
+  char* p = nullptr;
+  int32_t seq = 0;
+};
+static std::mutex* acq_pool_mu = new std::mutex;                     // never destroyed (as refit_pool)
+static std::vector<AcqMapped>* acq_pool = new std::vector<AcqMapped>;
+struct AcqMappedHolder {
+  AcqMapped b;
+  ~AcqMappedHolder() {
+    if (b.p) {
+      std::lock_guard<std::mutex> g(*acq_pool_mu);
+      acq_pool->push_back(b);
     }
-    t_mapped = (char*)p;
-    *(volatile int32_t*)(t_mapped + FETCH_MAPPED_BYTES) = 0;
   }
-  *out = t_mapped;
+};
+thread_local AcqMappedHolder t_acq;
+// the buffer and this call's sequence number (>= 1)
+static int mapped_buffer(char** out, int32_t* seq) {
+  AcqMapped& b = t_acq.b;
+  if (!b.p) {
+    {
+      std::lock_guard<std::mutex> g(*acq_pool_mu);
+      if (!acq_pool->empty()) {
+        b = acq_pool->back();
+        acq_pool->pop_back();
+      }
+    }
+    if (!b.p) {
+      void* p = nullptr;
+      HBX_HIP(hipHostMalloc(&p, PUB_OFF + PUB_BYTES,
+                            hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+      memset(p, 0, PUB_OFF + PUB_BYTES);  // (no stale tag can match: sequence numbers start at 1)
+      void* dp = nullptr;
+      HBX_HIP(hipHostGetDevicePointer(&dp, p, 0));
+      if (dp != p) {
+        (void)hipHostFree(p);
+        return hbx_fail(HBX_ERR_UNSUPPORTED, "mapped host memory has a different device address");
+      }
+      b.p = (char*)p;
+      b.seq = 0;
+      g_mapped_live.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  b.seq = b.seq == INT32_MAX ? 1 : b.seq + 1;
+  *out = b.p;
+  *seq = b.seq;
   return HBX_OK;
 }
 
@@ -2942,13 +2975,16 @@ static int hbx_pub_wait(const volatile uint64_t* w, int n, int32_t seq, uint32_t
   return HBX_OK;
 }
 
+int64_t hbx_mapped_host_buffers(void) { return g_mapped_live.load(std::memory_order_relaxed); }
+
 int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) {
   if (bytes < 0 || (bytes > 0 && (!host_dst || !dev_src))) return hbx_fail(HBX_ERR_ARG, "hbx_fetch: bad arguments");
   const hipStream_t s = (hipStream_t)stream;
   const bool small = bytes <= FETCH_MAPPED_BYTES && (bytes & 3) == 0 && ((uintptr_t)dev_src & 3) == 0;
   char* mapped = nullptr;
+  int32_t seq = 0;
   if (small) {
-    const int rc = mapped_buffer(&mapped);
+    const int rc = mapped_buffer(&mapped, &seq);
     if (rc) return rc;
   }
   if (!small) {  // larger or unaligned: a copy, then the stream polled to completion
@@ -2960,7 +2996,6 @@ int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream) 
     return HBX_OK;
   }
   int32_t* done = (int32_t*)(mapped + FETCH_MAPPED_BYTES);
-  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
   hipLaunchKernelGGL(fetch_publish_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)dev_src, (int32_t)(bytes / 4),
                      (uint32_t*)mapped, done, seq);
   HBX_LAUNCH_CHECK();
@@ -3012,9 +3047,9 @@ int hbx_kde_acquire_bound(const void* pair, const double* cand, int64_t Nc, int6
   if (!pair || !rec_out || Nc < 0) return hbx_fail(HBX_ERR_ARG, "hbx_kde_acquire_bound: bad arguments");
   const KdePairBinding& b = *(const KdePairBinding*)pair;
   char* mapped = nullptr;
-  int rc = mapped_buffer(&mapped);
+  int32_t seq = 0;
+  int rc = mapped_buffer(&mapped, &seq);
   if (rc) return rc;
-  const int32_t seq = t_seq = t_seq == INT32_MAX ? 1 : t_seq + 1;
   const bool pick = err || row_out;  // (8 (13 + 2 D) <= PUB_BYTES for D <= HBX_MAX_D)
   rc = acquire_impl("hbx_kde_acquire_bound", cand, Nc, Nc > 0 ? Nc : 1, b.D, index_base, b.params_good, b.table_good,
                     b.X_good, b.rows_good, b.variant_good, b.params_bad, b.table_bad, b.X_bad, b.rows_bad, b.variant_bad,

@@ -217,10 +217,16 @@ int hbx_event_elapsed_ms(void* start, void* stop, float* ms);
 /* Copy `bytes` of device memory (e.g. the result record) to host memory on `stream` and wait for it without
  * a blocking synchronisation: up to 4096 bytes go through the calling thread's device-mapped host buffer
  * (allocated on the thread's first call and kept for its lifetime, ~8.4 KB with hbx_kde_acquire_bound's
- * tagged region) with a completion word the
+ * tagged region; when the thread ends it goes back to a process-wide pool for the next thread) with a
+ * completion word the
  * call spins on; larger or unaligned copies poll the stream.  Replaces the caller's copy + synchronise
  * after hbx_kde_acquire (the reference's get_config returns the pick to its caller: bohb.py:166). */
 int hbx_fetch(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
+
+/* Device-mapped host buffers this process has allocated (hbx_fetch / hbx_kde_acquire_bound's and the refits'):
+ * bounded by the threads calling at once, not by the threads that ever called -- a thread's buffer is pooled
+ * when the thread ends.  Diagnostic (tests). */
+int64_t hbx_mapped_host_buffers(void);
 
 /* Device address of the result record inside an acquisition workspace (48 bytes):
  *   {i64 index, f64 score, f32 rel, i32 flags, i32 shortlist, i32 near, f64 pdf_l, f64 pdf_g}

@@ -142,3 +142,55 @@ def test_tagged_record_words_interleaved_with_fetches(device):
         r = kde.AcqResult.from_bytes(w)
         if pick and r.index >= 0:
             np.testing.assert_array_equal(row, C[r.index].cpu().numpy())
+
+
+def test_mapped_buffers_pooled_across_short_lived_threads(device):
+    """Each thread that fetches, acquires or refits holds device-mapped host buffers (include/hbx.h
+    hbx_fetch); when it ends they go back to a process-wide pool with their sequence numbers: 40 short-lived
+    threads one after another, each a fetch, a bound acquisition and a refit, allocate no buffer past the first
+    thread's -- and every record, fetched value and refit is right (a pooled buffer's old completion word and
+    tags never pass for the new owner's)."""
+    import torch
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    Lb = N.lib()
+    X = S.make_observations(340, 6, 2, 3, seed=41)
+    Ls = S.make_losses(340, seed=42)
+    vt = S.var_type_string(6, 2)
+    store = kde.ObservationStore(8, vt, device=device, capacity=400)
+    store.add(X[:300], Ls[:300])
+    C = torch.from_numpy(S.make_candidates(2000, 6, 2, 3, seed=43)).to(device)
+    sh = N.stream_handle(None, device)
+    out, errors = [], []
+
+    def run(i):
+        try:
+            torch.cuda.set_device(device)
+            src = torch.full((12,), i, dtype=torch.int32, device=device)
+            dst = ctypes.create_string_buffer(48)
+            N.check(Lb.hbx_fetch(dst, src.data_ptr(), 48, sh))
+            assert (np.frombuffer(dst.raw, dtype=np.int32) == i).all()
+            store.add(X[300 + i:301 + i], Ls[300 + i:301 + i])
+            pair = store.refit(9)
+            ref = kde.fit_pair(X[:301 + i], Ls[:301 + i], vt, 9, device=device)
+            r = pair.acquire(C)
+            r_ref = ref.acquire(C)
+            out.append((i, r.index, r.score, r_ref.index, r_ref.score))
+        except Exception as e:  # noqa: BLE001 (re-raised on the main thread)
+            errors.append((i, e))
+
+    def one(i):
+        t = threading.Thread(target=run, args=(i,))
+        t.start()
+        t.join()
+
+    one(0)
+    base = int(Lb.hbx_mapped_host_buffers())
+    for i in range(1, 40):
+        one(i)
+    assert not errors, errors
+    assert int(Lb.hbx_mapped_host_buffers()) == base
+    assert len(out) == 40
+    for i, a, sa, b, sb in out:
+        assert (a, sa) == (b, sb), i
