@@ -1,0 +1,163 @@
+"""Seeded random acquisitions end to end against the oracle: the refit (good/bad rows in numpy's argsort
+order, normal-reference bandwidths, level counts) and the pick (bohb.py:124-166: the first index of the
+smallest max(1e-8, g) / max(l, 1e-8), the winner's fp64 pdfs) over shapes no fixture holds -- 1 to 46 dims of
+mixed kinds, 1 to 6 levels (a single observed level makes that KDE's pdf NaN, SM:kernels.py:62-64), constant
+and quantised continuous columns, tied and crashed (+inf) losses, duplicate / perturbed / far candidates
+(exact score ties, pdfs that underflow to 0 so both factors clamp).  Per case also: the batched
+acquisition (one pick per segment of the candidate set, HB_iteration.py:136-138 requests served at once) and
+the ln-pdf contract (hbx_kde_logpdf_rtol: within 1e-5 * max(1, |ln p|) of the fp64 log-space oracle, NaN and
+-inf where it has them; ln of the reference's own signed fp64 pdf for KDEs with negative factors) on the first
+256 candidates.
+
+The pick must be the oracle's bit for bit: c_oracle.kde_pdf(exact=True) restates the pinned reference's
+float64 arithmetic (numpy 1.26.4's exp and pairwise sums), pinned against the reference's own outputs by
+tests/test_oracle_golden.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import kde_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = list(range(120))
+
+
+def _case(seed):
+    rs = np.random.RandomState(1000 + seed)
+    dc = int(rs.choice([0, 1, 2, 3, 5, 8, 13, 24, 32, 40]))
+    du = int(rs.choice([0, 0, 1, 2, 3, 6, 8])) if dc < 40 else int(rs.randint(0, 7))
+    if dc + du == 0:
+        dc = 1
+    D = dc + du
+    n = int(rs.randint(D + 2, max(D + 3, 2000)))
+    levels = rs.randint(2, 7, size=du)
+    X = np.empty((n, D))
+    X[:, :dc] = rs.rand(n, dc)
+    for d in range(dc):
+        r = rs.rand()
+        if r < 0.17:
+            X[:, d] = np.round(X[:, d] * 8) / 8  # quantised: tied values
+        elif r < 0.4:
+            X[:, d] = 0.5 + 0.02 * rs.randn(n)  # clustered
+    for u in range(du):
+        X[:, dc + u] = rs.randint(0, levels[u], size=n)
+    special = rs.rand()
+    if special < 0.08 and dc:
+        X[:, rs.randint(dc)] = 0.25  # a constant column: bandwidth 0, both pdfs NaN
+    elif special < 0.16 and du:
+        X[:, dc + rs.randint(du)] = 1.0  # one observed level: h / (c - 1) is NaN
+    vt = "c" * dc + "u" * du
+    losses = rs.rand(n)
+    if rs.rand() < 0.4:
+        losses = np.round(losses * 20) / 20  # ties: numpy's unstable argsort order decides the split
+    if rs.rand() < 0.3:
+        losses[rs.rand(n) < 0.1] = np.inf  # crashed runs
+    nc = int(rs.choice([1, 7, 64, 700, 3000, 20000]))
+    C = np.empty((nc, D))
+    C[:, :dc] = rs.rand(nc, dc)
+    for u in range(du):
+        C[:, dc + u] = rs.randint(0, levels[u], size=nc)
+    k = rs.rand(nc)
+    src = X[rs.randint(0, n, size=nc)]
+    cp = k < 0.2
+    C[cp] = src[cp]  # observation rows as candidates
+    pt = (k >= 0.2) & (k < 0.5)
+    C[pt, :dc] = src[pt, :dc] + 0.01 * rs.randn(int(pt.sum()), dc)
+    C[pt, dc:] = src[pt, dc:]
+    far = (k >= 0.5) & (k < 0.6)
+    C[far, :dc] = 4.0 + rs.rand(int(far.sum()), dc)  # pdfs underflow to 0
+    if nc > 4:
+        C[nc // 2] = C[nc // 4]  # a duplicate: an exact score tie
+    return X, losses, vt, C, D + 1
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_acquisition_matches_oracle(device, seed):
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    n, D = X.shape
+    pair = kde.fit_pair(X, losses, vt, mp, device=device)
+    g_idx, b_idx = O.bohb_split(X, losses, mp)
+    if pair is None:  # the reference builds no model either (too few rows for a KDE)
+        assert len(g_idx) <= D or len(b_idx) <= D
+        return
+    np.testing.assert_array_equal(pair.good.rows_dev.cpu().numpy(), g_idx)
+    np.testing.assert_array_equal(pair.bad.rows_dev.cpu().numpy(), b_idx)
+    with np.errstate(all="ignore"):
+        np.testing.assert_array_equal(pair.good.bw, O.normal_reference_bw(X[g_idx]))
+        np.testing.assert_array_equal(pair.bad.bw, O.normal_reference_bw(X[b_idx]))
+    np.testing.assert_array_equal(pair.good.nlev, O.num_levels(X[g_idx], vt))
+    np.testing.assert_array_equal(pair.bad.nlev, O.num_levels(X[b_idx], vt))
+    with np.errstate(all="ignore"):
+        l = c_oracle.kde_pdf(X[g_idx], pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(X[b_idx], pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    want, _ = O.select(l, g)
+    res = pair.acquire(C)
+    assert res.index == want, (seed, res.index, want, res.flags)
+    if want >= 0:
+        assert (res.pdf_l, res.pdf_g) == (l[want], g[want]) or (
+            np.isnan(l[want]) and np.isnan(res.pdf_l) and res.pdf_g == g[want]), seed
+
+
+def _pick(l, g):
+    want, _ = O.select(l, g)
+    return want
+
+
+@pytest.mark.parametrize("seed", SEEDS[::3])
+def test_random_batch_acquisition_matches_oracle(device, seed):
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    pair = kde.fit_pair(X, losses, vt, mp, device=device)
+    if pair is None:
+        return
+    with np.errstate(all="ignore"):
+        l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    nc = len(C)
+    for seg in sorted({1, max(1, nc // 3), 64, nc}):
+        if nc // seg > 4096:
+            continue
+        recs = pair.acquire_batch(C, seg)
+        assert len(recs) == (nc + seg - 1) // seg
+        for b, r in enumerate(recs):
+            lo, hi = b * seg, min(nc, (b + 1) * seg)
+            want = _pick(l[lo:hi], g[lo:hi])
+            assert r.index == want, (seed, seg, b, r.index, want, r.flags)
+            if want >= 0:
+                assert r.pdf_g == g[lo + want], (seed, seg, b)
+
+
+@pytest.mark.parametrize("seed", SEEDS[1::3])
+def test_random_logpdf_contract(device, seed):
+    """KDEs whose categorical factors are all positive: within 1e-5 of the fp64 log-space oracle.  KDEs with
+    a negative match factor (bandwidth > 1, SM:kernels.py:62-64): the reference's own pdf is a signed sum
+    whose fp64 value can cancel or underflow to <= 0, so its ln is ln of that exact value -- NaN below 0,
+    -inf at 0 -- and the engine's must have the same NaN / -inf entries and be within the same 1e-5 of it elsewhere
+(its signed fp32 estimate where the bound allows, else ln of the bit-exact fp64 pdf)."""
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    pair = kde.fit_pair(X, losses, vt, mp, device=device)
+    if pair is None:
+        return
+    C = C[:256]
+    cat = np.array([v == "u" for v in vt])
+    for k in (pair.good, pair.bad):
+        lp = k.logpdf(C)
+        signed = bool(np.any((k.bw[cat] > 1.0) & (np.asarray(k.nlev)[cat] > 1)))
+        if signed:
+            with np.errstate(all="ignore"):
+                ref = np.log(c_oracle.kde_pdf(k.data, k.bw, vt, k.nlev, C, exact=True))
+        else:
+            ref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        np.testing.assert_array_equal(np.isnan(lp), np.isnan(ref))
+        ninf = np.isneginf(ref)
+        assert np.all(np.isneginf(lp[ninf])), seed
+        fin = np.isfinite(ref)
+        assert np.all(np.isfinite(lp[fin])), seed
+        err = np.abs(lp[fin] - ref[fin]) / np.maximum(1.0, np.abs(ref[fin]))
+        assert err.max(initial=0.0) <= 1e-5, (seed, signed, err.max())
