@@ -821,8 +821,9 @@ class ObservationStore(object):
         return self._lh[:self.nh]
 
     def refit(self, min_points, top_n_percent=15, split_rule="bohb", stream=None):
-        """Refit on every row added so far.  Returns a KDEPair, or None where the reference builds no
-        model (too few rows for a KDE)."""
+        """Refit on every row added so far (bohb.py:220-251).  Returns a KDEPair, or None where the reference
+        builds no model (too few rows for a KDE, bohb.py:234-237).  The row-count gate before it
+        (``len <= min_points + 1``: no refit, bohb.py:216-217) is the caller's, as in new_result."""
         n = self.nh
         sizes = split_sizes(n, self.D, min_points, top_n_percent, split_rule)
         if sizes is None:

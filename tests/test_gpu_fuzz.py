@@ -79,10 +79,11 @@ def test_random_acquisition_matches_oracle(device, seed):
     X, losses, vt, C, mp = _case(seed)
     n, D = X.shape
     pair = kde.fit_pair(X, losses, vt, mp, device=device)
-    g_idx, b_idx = O.bohb_split(X, losses, mp)
-    if pair is None:  # the reference builds no model either (too few rows for a KDE)
-        assert len(g_idx) <= D or len(b_idx) <= D
+    sp = O.bohb_split(X, losses, mp)
+    if sp is None:  # the reference builds no model (too few rows for a KDE)
+        assert pair is None
         return
+    g_idx, b_idx = sp
     np.testing.assert_array_equal(pair.good.rows_dev.cpu().numpy(), g_idx)
     np.testing.assert_array_equal(pair.bad.rows_dev.cpu().numpy(), b_idx)
     with np.errstate(all="ignore"):
@@ -161,3 +162,43 @@ def test_random_logpdf_contract(device, seed):
         assert np.all(np.isfinite(lp[fin])), seed
         err = np.abs(lp[fin] - ref[fin]) / np.maximum(1.0, np.abs(ref[fin]))
         assert err.max(initial=0.0) <= 1e-5, (seed, signed, err.max())
+
+
+@pytest.mark.parametrize("seed", SEEDS[2::3])
+def test_random_incremental_refits_match_oracle(device, seed):
+    """new_result's refit (bohb.py:171-251) after rows arrive in random batches, at a random top_n_percent:
+    after every batch the rows, bandwidths and level counts equal the oracle's on the prefix (None where
+    the reference builds no model), and the last model's pick equals the oracle's."""
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    n, D = X.shape
+    rs = np.random.RandomState(7 + seed)
+    top = int(rs.choice([10, 15, 33, 50]))
+    store = kde.ObservationStore(D, vt, device=device, capacity=int(rs.randint(8, 64)))
+    m, pair = 0, None
+    while m < n:
+        step = int(min(n - m, rs.choice([1, 3, 17, 200])))
+        store.add(X[m:m + step], losses[m:m + step])
+        m += step
+        if m <= mp + 1:  # new_result returns before the refit (bohb.py:216-217), as the generator does
+            continue
+        pair = store.refit(mp, top_n_percent=top)
+        sp = O.bohb_split(X[:m], losses[:m], mp, top_n_percent=top)
+        if sp is None:
+            assert pair is None, (seed, m)
+            continue
+        g_idx, b_idx = sp
+        assert pair is not None, (seed, m)
+        np.testing.assert_array_equal(pair.good.rows_dev.cpu().numpy(), g_idx)
+        np.testing.assert_array_equal(pair.bad.rows_dev.cpu().numpy(), b_idx)
+        with np.errstate(all="ignore"):
+            np.testing.assert_array_equal(pair.good.bw, O.normal_reference_bw(X[g_idx]))
+            np.testing.assert_array_equal(pair.bad.bw, O.normal_reference_bw(X[b_idx]))
+        np.testing.assert_array_equal(pair.good.nlev, O.num_levels(X[g_idx], vt))
+        np.testing.assert_array_equal(pair.bad.nlev, O.num_levels(X[b_idx], vt))
+    if pair is not None:
+        with np.errstate(all="ignore"):
+            l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+            g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+        assert pair.acquire(C).index == _pick(l, g), seed
