@@ -403,17 +403,21 @@ int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_
 int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                       const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                       int64_t scratch_bytes, int32_t order_mode, void* events, void* stream) {
-  if (!loss || !seg_off || !k || !advance) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
+  if (((!loss || !advance) && N > 0) || !seg_off || !k) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
   if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
     return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_ex: order_mode %d", order_mode);
   if (B <= 0) return HBX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (N <= 0) {  // every bracket empty: nothing advances (process_results over no results)
+    if (n_advance) HBX_HIP(hipMemsetAsync(n_advance, 0, sizeof(int64_t) * B, st));
+    return HBX_OK;
+  }
   const bool np = order_mode == HBX_ORDER_NUMPY;
   const bool want_order = order != nullptr;
   const int64_t need = hbx_sh_promote_scratch_bytes(B, max_seg, N, want_order, order_mode);
   if (need > 0 && (!scratch || scratch_bytes < need))
     return hbx_fail(HBX_ERR_ARG, "promotion scratch too small: %lld < %lld bytes", (long long)scratch_bytes,
                     (long long)need);
-  hipStream_t st = (hipStream_t)stream;
   if (max_seg <= 64 * PW_PER_LANE && !order) {  // mask only: O(n) selection
     int32_t* pool = (int32_t*)scratch;
     const int64_t slots = (int64_t)NPS_POOL * max_seg;

@@ -347,7 +347,8 @@ int hbx_argmax_records(const void* all, int32_t nranks, void* out, void* stream)
  * order: device i64[N] (sorted positions per bracket, output) or NULL when only the mask is wanted --
  * brackets of <= 1024 configurations then take an O(n) selection of the k-th loss and need no
  * scratch (scratch may be NULL); advance: device u8[N]; n_advance: device i64[B], nullable.
- * scratch: hbx_sort_scratch_bytes(N) bytes when order is requested or a bracket exceeds 1024. */
+ * scratch: hbx_sort_scratch_bytes(N) bytes when order is requested or a bracket exceeds 1024.
+ * N = 0 (every bracket empty): loss, order and advance may be NULL; n_advance is zeroed. */
 int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                    const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                    int64_t scratch_bytes, void* stream);

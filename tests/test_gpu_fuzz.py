@@ -202,3 +202,31 @@ def test_random_incremental_refits_match_oracle(device, seed):
             l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
             g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
         assert pair.acquire(C).index == _pick(l, g), seed
+
+
+@pytest.mark.parametrize("seed", SEEDS[::4])
+def test_random_promotion_matches_oracle(device, seed):
+    """process_results' promotion (HB_iteration.py:179-182, 239-242) over ragged brackets: empty ones, every
+    loss tied or crashed, quantised losses whose tie order numpy's argsort decides, k of 0, fractional k
+    (SuccessiveResampling's max(1, n * 0.5)) and k past the bracket size -- every mask the oracle's."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(5000 + seed)
+    B = int(rs.choice([1, 3, 40, 700]))
+    n = int(rs.choice([1, 5, 81, 1000, 3000]))
+    lens = rs.randint(0, n + 1, size=B)
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    loss = rs.rand(int(seg[-1]))
+    q = int(rs.choice([0, 4, 50, 1000]))
+    if q:
+        loss = np.round(loss * q) / q
+    loss[rs.rand(loss.size) < rs.choice([0.0, 0.05, 0.5])] = np.inf
+    if B > 2 and lens[1] > 0:
+        loss[seg[1]:seg[2]] = 0.25  # one bracket all tied
+    k = np.floor(lens * rs.choice([0.0, 1 / 3, 0.5, 1.0, 1.5], size=B))
+    sr = rs.rand(B) < 0.2
+    k[sr] = np.maximum(1.0, lens[sr] * 0.5)  # SuccessiveResampling: max(1, n * 0.5)
+    k[rs.rand(B) < 0.1] += 0.5
+    adv = promote.promote_segments(loss, seg, k, device=device)
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        np.testing.assert_array_equal(adv[s:e], O.sh_advance(loss[s:e], k[b]), err_msg="bracket %d" % b)
