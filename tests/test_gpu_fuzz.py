@@ -230,3 +230,22 @@ def test_random_promotion_matches_oracle(device, seed):
     for b in range(B):
         s, e = seg[b], seg[b + 1]
         np.testing.assert_array_equal(adv[s:e], O.sh_advance(loss[s:e], k[b]), err_msg="bracket %d" % b)
+
+
+@pytest.mark.parametrize("policy", ["gpu", "auto"])
+def test_random_single_bracket_promotion(device, policy):
+    """advance_mask (one process_results call, HB_iteration.py:179-182) on 300 random brackets of 0-1500
+    configurations -- tied, crashed and quantised losses, k from 0 past n, fractional k -- on the device
+    path and the size policy: every mask the oracle's."""
+    from hpbandster_amd import promote
+    rs = np.random.RandomState(77)
+    for t in range(300):
+        n = int(rs.choice([0, 1, 2, 9, 81, 700, 1500]))
+        loss = rs.rand(n)
+        q = int(rs.choice([0, 3, 40]))
+        if q:
+            loss = np.round(loss * q) / q
+        loss[rs.rand(n) < rs.choice([0.0, 0.1, 0.9])] = np.inf
+        k = float(np.floor(n * rs.choice([0.0, 1 / 3, 0.5, 1.0, 2.0])) + rs.choice([0.0, 0.0, 0.5]))
+        got = promote.advance_mask(loss, k, device=device, policy=policy)
+        np.testing.assert_array_equal(got, O.sh_advance(loss, k), err_msg="bracket %d (n=%d, k=%g)" % (t, n, k))
