@@ -249,3 +249,42 @@ def test_random_single_bracket_promotion(device, policy):
         k = float(np.floor(n * rs.choice([0.0, 1 / 3, 0.5, 1.0, 2.0])) + rs.choice([0.0, 0.0, 0.5]))
         got = promote.advance_mask(loss, k, device=device, policy=policy)
         np.testing.assert_array_equal(got, O.sh_advance(loss, k), err_msg="bracket %d (n=%d, k=%g)" % (t, n, k))
+
+
+@pytest.mark.parametrize("seed", SEEDS[::5])
+def test_random_kde_ei_refit_and_pick(device, seed):
+    """KDEEI.new_result's split (kde_ei.py:187-207: n_good = int(max(top% N / 100., mp)), numpy's argsort,
+    rows >= D) on the continuous part of the random cases at a random top_n_percent: rows, bandwidths and the
+    pick equal the oracle's; rows == D raises as KDEMultivariate does (kernel_density.py:107-109)."""
+    from oracle import c_oracle, np_argsort
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    dc = vt.count("c")
+    if dc == 0:
+        return
+    X, C, vt = X[:, :dc], C[:, :dc], "c" * dc
+    rs = np.random.RandomState(9 + seed)
+    top = int(rs.choice([10, 15, 33]))
+    mp = int(rs.choice([dc - 1, dc, dc + 1, 3])) if dc > 1 else 2
+    n = X.shape[0]
+    n_good = int(max(top * n / 100., mp))
+    n_bad = int(max((100 - top) * n / 100., mp))
+    ng, nb = min(n_good, n), min(n_bad, n)
+    if ng < dc or nb < dc:
+        assert kde.fit_pair(X, losses, vt, mp, top_n_percent=top, device=device, split_rule="kde_ei") is None
+        return
+    if ng == dc or nb == dc:
+        with pytest.raises(ValueError):
+            kde.fit_pair(X, losses, vt, mp, top_n_percent=top, device=device, split_rule="kde_ei")
+        return
+    pair = kde.fit_pair(X, losses, vt, mp, top_n_percent=top, device=device, split_rule="kde_ei")
+    idx = np_argsort.argsort(losses)
+    g_idx, b_idx = idx[:n_good], idx[-n_bad:]
+    np.testing.assert_array_equal(pair.good.rows_dev.cpu().numpy(), g_idx)
+    np.testing.assert_array_equal(pair.bad.rows_dev.cpu().numpy(), b_idx)
+    with np.errstate(all="ignore"):
+        np.testing.assert_array_equal(pair.good.bw, O.normal_reference_bw(X[g_idx]))
+        np.testing.assert_array_equal(pair.bad.bw, O.normal_reference_bw(X[b_idx]))
+        l = c_oracle.kde_pdf(X[g_idx], pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(X[b_idx], pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    assert pair.acquire(C).index == _pick(l, g), seed
