@@ -23,6 +23,27 @@ def test_hb_budgets_and_brackets_match_reference():
             assert ns == it["num_configs"]
 
 
+def test_hb_budgets_random_bit_identical_to_oracle():
+    """Budgets are dict keys in the reference (float equality matters, HB_master.py:93-94): 4000 random
+    (eta, min_budget, max_budget) give the oracle's restatement of the reference expressions bit for bit,
+    and every bracket's num_configs (HB_master.py:161-168)."""
+    rs = np.random.RandomState(0)
+    done = 0
+    while done < 4000:
+        eta = float(rs.choice([2, 3, 4, 2.5, 1.5, 5, 10]))
+        mx = float(rs.choice([1, 9, 27, 81, 100, 243, 1000, 3.7, 64])) * 10.0 ** rs.randint(-3, 3)
+        mn = mx / eta ** rs.randint(0, 8) * float(rs.choice([1, 1, 0.9, 1.1, 0.5]))
+        if not 0 < mn <= mx:
+            continue
+        done += 1
+        m, budgets = M.hb_budgets(eta, mn, mx)
+        mo, bo = O.hb_budgets(eta, mn, mx)
+        assert m == mo
+        assert np.array_equal(budgets, bo) and budgets.tobytes() == bo.tobytes(), (eta, mn, mx)
+        for it in range(2 * m):
+            assert M.hb_bracket(it, eta, m) == O.hb_bracket(it, eta, m)
+
+
 class _Job(object):
     def __init__(self, cid, cfg, b, loss):
         self.id, self.kwargs, self.timestamps = cid, {"config": cfg, "budget": b}, {}
