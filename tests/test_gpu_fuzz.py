@@ -288,3 +288,44 @@ def test_random_kde_ei_refit_and_pick(device, seed):
         l = c_oracle.kde_pdf(X[g_idx], pair.good.bw, vt, pair.good.nlev, C, exact=True)
         g = c_oracle.kde_pdf(X[b_idx], pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
     assert pair.acquire(C).index == _pick(l, g), seed
+
+
+@pytest.mark.parametrize("seed", SEEDS[::4])
+def test_random_sharded_picks_match_oracle(device, seed):
+    """SURVEY 8e's sharding: the candidates split over 2-7 ranks (contiguous shards, global indices via
+    index_base), each shard's record reduced by the exchange's rule -- on the device (hbx_argmax_records, what
+    the RCCL all-gather feeds) and on the host -- is the oracle's single pick over all candidates, ties across
+    shards to the first global index."""
+    import torch
+    from oracle import c_oracle
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    from hpbandster_amd.distributed import reduce_records_host, shard_range
+    X, losses, vt, C, mp = _case(seed)
+    pair = kde.fit_pair(X, losses, vt, mp, device=device)
+    if pair is None or len(C) < 2:
+        return
+    with np.errstate(all="ignore"):
+        l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    want = _pick(l, g)
+    world = int(np.random.RandomState(seed).randint(2, 8))
+    Cd = torch.from_numpy(C).to(device)
+    raw = []
+    for r in range(world):
+        lo, hi = shard_range(len(C), r, world)
+        if hi > lo:
+            raw.append(pair.acquire(Cd[lo:hi], index_base=lo))
+    best, _ = reduce_records_host(raw)
+    assert (raw[best].index if best >= 0 else -1) == want, (seed, world)
+    blob = b"".join(_acq_bytes(r) for r in raw)
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
+    out = torch.empty(kde.RESULT_BYTES, dtype=torch.uint8, device=device)
+    N.check(N.lib().hbx_argmax_records(N.ptr(d), len(raw), N.ptr(out), N.stream_handle(None, device)))
+    assert kde.AcqResult.from_bytes(out.cpu().numpy().tobytes()).index == want, (seed, world)
+
+
+def _acq_bytes(r):
+    import struct
+    from hpbandster_amd.kde import RESULT_FMT
+    return struct.pack(RESULT_FMT, r.index, r.score, r.rel, r.flags, r.shortlist, r.near, r.pdf_l, r.pdf_g)
