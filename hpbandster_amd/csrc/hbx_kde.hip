@@ -2805,7 +2805,8 @@ int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax) { return 256; }
 int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                       const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
                       void* stream) {
-  if (!pts || !params || !X || !rows || !out || !scratch) return hbx_fail(HBX_ERR_ARG, "hbx_kde_pdf_exact: null");
+  if (((!pts || !out) && Np > 0) || !params || !X || !rows || !scratch)
+    return hbx_fail(HBX_ERR_ARG, "hbx_kde_pdf_exact: null");
   if (scratch_bytes < hbx_kde_pdf_scratch_bytes(n)) return hbx_fail(HBX_ERR_ARG, "pdf scratch too small");
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);
@@ -2819,7 +2820,7 @@ int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* para
 // KDE has negative categorical factors or structural NaNs (use hbx_kde_pdf_exact there).
 int hbx_kde_logpdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                          const int64_t* rows, double* out, void* stream) {
-  if (!pts || !params || !X || !rows || !out) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_exact: null");
+  if (((!pts || !out) && Np > 0) || !params || !X || !rows) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_exact: null");
   if (D < 1 || D > HBX_MAX_D) return hbx_fail(HBX_ERR_ARG, "hbx_kde_logpdf_exact: D=%d", D);
   if (Np <= 0) return HBX_OK;
   const unsigned grid = (unsigned)(Np < EXACT_GRID ? Np : EXACT_GRID);

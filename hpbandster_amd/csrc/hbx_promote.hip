@@ -403,7 +403,7 @@ int hbx_sh_promote(const double* loss, const int64_t* seg_off, int64_t B, int64_
 int hbx_sh_promote_ex(const double* loss, const int64_t* seg_off, int64_t B, int64_t max_seg, int64_t N,
                       const double* k, int64_t* order, uint8_t* advance, int64_t* n_advance, void* scratch,
                       int64_t scratch_bytes, int32_t order_mode, void* events, void* stream) {
-  if (((!loss || !advance) && N > 0) || !seg_off || !k) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
+  if (((!loss || !advance) && N > 0) || !seg_off || (!k && B > 0)) return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote: null pointer");
   if (order_mode != HBX_ORDER_NUMPY && order_mode != HBX_ORDER_STABLE)
     return hbx_fail(HBX_ERR_ARG, "hbx_sh_promote_ex: order_mode %d", order_mode);
   if (B <= 0) return HBX_OK;

@@ -251,7 +251,8 @@ int64_t hbx_kde_pdf_scratch_bytes(int64_t nmax);
 
 /* Exact fp64 pdf of one prepared KDE at Np points (device f64[Np][D]) -> out (device f64[Np]).  Same
  * float64 operations in the same order as statsmodels 0.12.2 on the pinned numpy 1.26.4 (its SVML exp
- * restated bit for bit, numpy's pairwise sums): bit-identical to the reference's KDEMultivariate.pdf. */
+ * restated bit for bit, numpy's pairwise sums): bit-identical to the reference's KDEMultivariate.pdf.
+ * Np = 0: nothing to do (pts / out may be NULL); likewise hbx_kde_logpdf_exact. */
 int hbx_kde_pdf_exact(const double* pts, int64_t Np, int32_t D, const void* params, const double* X,
                       const int64_t* rows, int64_t n, double* out, void* scratch, int64_t scratch_bytes,
                       void* stream);

@@ -329,3 +329,31 @@ def _acq_bytes(r):
     import struct
     from hpbandster_amd.kde import RESULT_FMT
     return struct.pack(RESULT_FMT, r.index, r.score, r.rel, r.flags, r.shortlist, r.near, r.pdf_l, r.pdf_g)
+
+
+def test_empty_and_single_inputs(device):
+    """The entry points on empty and one-element inputs (cases the fuzz above turned up): no candidates ->
+    no pick (index -1) and empty outputs, one candidate -> that candidate, empty pdf / ln-pdf calls ->
+    empty arrays, promotion over zero brackets or only empty ones -> empty masks; a wrong row width raises."""
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde, promote
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(300, 6, 2, 3, seed=1)
+    pair = kde.fit_pair(X, S.make_losses(300, seed=2), S.var_type_string(6, 2), 9, device=device)
+    E = np.empty((0, 8))
+    assert pair.acquire(E).index == -1
+    r, ll, lg = pair.acquire(E, logs=True)
+    assert r.index == -1 and ll.size == 0 and lg.size == 0
+    assert pair.acquire_batch(E, 4) == []
+    assert pair.good.logpdf(E).size == 0
+    assert np.asarray(pair.good.pdf(E)).size == 0
+    one = S.make_candidates(1, 6, 2, 3)
+    r1 = pair.acquire(one)
+    assert r1.index == 0 and r1.pdf_l == float(np.asarray(pair.good.pdf(one)).reshape(-1)[0])
+    three = S.make_candidates(3, 6, 2, 3)
+    rb = pair.acquire_batch(three, 10)  # one segment longer than the set
+    assert len(rb) == 1 and rb[0].index == pair.acquire(three).index
+    with pytest.raises(N.HbxError):
+        pair.acquire(np.zeros((4, 7)))
+    assert promote.promote_segments(np.zeros(0), np.zeros(1, np.int64), np.zeros(0), device=device).size == 0
+    assert promote.promote_segments(np.zeros(0), np.zeros(4, np.int64), np.ones(3), device=device).size == 0
