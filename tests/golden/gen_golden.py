@@ -337,9 +337,10 @@ class _PdfRecorder(object):
         return v
 
 
-def gen_get_config(ref):
+def gen_get_config(ref, cases=None):
     S = ref.synth
-    cases = [("d8c", 8, 0, 2, 200), ("mixed", 5, 3, [2, 3, 5], 150), ("hgt1", 2, 3, 10, 40)]
+    if cases is None:
+        cases = [("d8c", 8, 0, 2, 200), ("mixed", 5, 3, [2, 3, 5], 150), ("hgt1", 2, 3, 10, 40)]
     for name, dc, du, lv, n in cases:
         X = S.make_observations(n, dc, du, lv)
         L = S.make_losses(n)
@@ -374,6 +375,13 @@ def gen_get_config(ref):
         np.savez_compressed(path, **out)
         print("wrote %s  model-based picks %d/%d" % (
             os.path.basename(path), sum(r["model_based"] for r in records), len(records)))
+
+
+def gen_get_config_more(ref):
+    """Round 6: one continuous dim (config #1's shape), categorical dims only (2-7 levels), and a wider
+    mixed space with more observations -- the same recording as gen_get_config."""
+    gen_get_config(ref, [("d1", 1, 0, 2, 24), ("cat6", 0, 6, [2, 3, 4, 5, 6, 7], 90),
+                         ("d24m", 16, 8, 4, 400)])
 
 
 # ----------------------------------------------------------------------------------------
@@ -711,7 +719,7 @@ def gen_np_argsort(ref):
     print("wrote np_argsort.npz (%d arrays, %d values, numpy %s)" % (len(xs), offs[-1], np.__version__))
 
 
-GENERATORS = ["kde", "neartie", "getcfg", "sh", "brackets", "e2e", "npexp", "kdeei", "ties", "shties", "npargsort"]
+GENERATORS = ["kde", "neartie", "getcfg", "getcfg_more", "sh", "brackets", "e2e", "npexp", "kdeei", "ties", "shties", "npargsort"]
 
 
 def main():
@@ -722,7 +730,8 @@ def main():
     t0 = time.time()
     ref = load_reference()
     todo = a.only or GENERATORS
-    fns = {"kde": gen_kde_cases, "neartie": gen_neartie_cases, "getcfg": gen_get_config, "sh": gen_sh,
+    fns = {"kde": gen_kde_cases, "neartie": gen_neartie_cases, "getcfg": gen_get_config,
+           "getcfg_more": gen_get_config_more, "sh": gen_sh,
            "brackets": gen_brackets, "e2e": gen_e2e, "npexp": gen_npexp,
            "kdeei": gen_kdeei, "ties": gen_tie_cases, "shties": gen_sh_ties, "npargsort": gen_np_argsort}
     for name in todo:
