@@ -1080,7 +1080,7 @@ def kde_result_bytes():
     return kde.RESULT_BYTES
 
 
-PROFILE_SET = "profiles/r06/final3"
+PROFILE_SET = "profiles/r06/final4"
 
 
 def load_traffic(workload):
