@@ -2017,6 +2017,7 @@ struct ScoreFns {
   bool split_ok = false;  // the pair kernel takes observation splits and initialises a single acquisition's
                           // state (the 32x32-tile instances)
   combine_fn combine_rescue = nullptr;  // the combine kernel doing the rescue pass of this instance
+  logpdf_pair_fn pair1 = nullptr;       // the coarse pair kernel with one column tile per wave (launch_score2)
 };
 
 // Observation splits of a pair launch with `tiles` candidate tiles per KDE over <= nmax observations: a
@@ -2045,6 +2046,13 @@ static int obs_splits(unsigned tiles, int64_t nmax, bool ws_sizing = false) {
 // HBX_SCORE_PAIR=0 keeps two launches (read per call: tests switch it in-process)
 static bool pair_enabled() {
   const char* e = getenv("HBX_SCORE_PAIR");
+  return !(e && atoi(e) == 0);
+}
+
+// the coarse pair launch with one column tile per wave where it fits one round (launch_score2); HBX_PAIR1=0:
+// always the H32C_CT-tile kernel (read per call: tests switch it in-process)
+static bool pair1_enabled() {
+  const char* e = getenv("HBX_PAIR1");
   return !(e && atoi(e) == 0);
 }
 
@@ -2094,10 +2102,12 @@ static ScoreFns pick_logpdf(int dc_pad, int du_pad, int variant, bool fast = fal
     const bool co = fast && !sg && ((variant >> 7) & 1);  // the acquisition's coarse pre-screen instance
     const bool fa = fast && kp > 0;
     const int hw = co ? H32C_WAVES : H16_WAVES;
-    return {hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
-            hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
-            sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true,
-            sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>};
+    ScoreFns f{hbx_pick_h32(nsc_of(dc_pad), kp, sg, fa, co), r, 32 * hw * (co ? H32C_CT : 1), 64 * hw,
+               hbx_pick_h32_pair(nsc_of(dc_pad), kp, sg, fa, co),
+               sg ? pick_rescue_pair<true>(dc_pad) : pick_rescue_pair<false>(dc_pad), true,
+               sg ? kde_combine_kernel<true, true> : kde_combine_kernel<false, true>};
+    if (co && H32C_CT > 1) f.pair1 = hbx_pick_h32_pair1(nsc_of(dc_pad), kp);
+    return f;
   }
   if (hm) {
     if (dc_pad < 8) return {nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -2135,6 +2145,13 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
   if (ev && !pair) HBX_HIP(hipEventRecord(ev[0], s));
   if (pair) {
     unsigned gm = (unsigned)((Nc + f0.cands_per_block - 1) / f0.cands_per_block);
+    logpdf_pair_fn pk = f0.pair;
+    // both KDEs' blocks within one round of the chip's slots (two per CU): one column tile per wave instead,
+    // twice the waves (config #2: 52 instead of 53.5 us per acquisition; profiles/r06/ct1/)
+    if (f0.pair1 && f0.pair1 == f1.pair1 && 2 * gm <= 512 && pair1_enabled()) {
+      pk = f0.pair1;
+      gm = (unsigned)((Nc + f0.cands_per_block / H32C_CT - 1) / (f0.cands_per_block / H32C_CT));
+    }
     const unsigned gr = (unsigned)((Nc + 255) / 256);
     if ((uint64_t)gr * 2 > 0x7fffffffu) return hbx_fail(HBX_ERR_ARG, "too many candidates for one pair launch");
     const bool can = f0.split_ok && nsplit_out && nmax > 0;
@@ -2142,7 +2159,6 @@ static int launch_score2(ScoreFns f0, const void* params0, const float* table0, 
     // blocks -- splitting only the bad KDE's longer walks in two measured 3-5 us slower, like splitting
     // both: each range repeats the block's prologue, and the merge reads twice the estimates.)
     const int ns0 = can ? obs_splits(gm, nmax) : 1, ns1 = ns0;
-    logpdf_pair_fn pk = f0.pair;
     KdePairArgs a{(const KdeParams*)params1, (const KdeParams*)params0, table1, table0, est1, est0, gm * ns0,
                   rescue_cnt, {}};
     a.tiles = gm;

@@ -43,7 +43,9 @@
 #endif
 // ... and its candidate column tiles per wave: 2 = 64 candidates per wave, each A fragment read from LDS
 // feeding both tiles' matrix instructions (half the LDS reads per pair)
+#ifndef H32C_CT
 #define H32C_CT 2  // phases in snake order (hbx_score_h32.hip chunk2s); 1 / 3 / 4 measured no faster
+#endif
 
 // Observation table, chunked for the MFMA scoring kernel.  Chunk c holds observations 64c..64c+63:
 //   [KP k-rows][KROW]   B operand, k-major: k=0 -> C_j, k=1 -> 1, k=2+c -> X'_jc, rest 0
@@ -351,6 +353,7 @@ logpdf_fn hbx_pick_h(int nsc, int kc, bool sg);            // hbx_score_h.hip
 logpdf_pair_fn hbx_pick_h_pair(int nsc, int kc, bool sg);  // hbx_score_h.hip (l + g in one launch)
 logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse = false);  // hbx_score_h32.hip
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse = false);
+logpdf_pair_fn hbx_pick_h32_pair1(int nsc, int kp);  // the coarse pair kernel, one column tile per wave
 
 // hbx_kde.hip's pieces the ln-pdf contract (hbx_logpdf.hip, hbx_kde_logpdf_rtol) launches:
 // the precise estimate instance of a bucket (main + rescue into est; HBX_ERR_UNSUPPORTED when it has none) ...

@@ -536,6 +536,25 @@ __global__ __launch_bounds__(64 * (CO ? H32C_WAVES : H16_WAVES)) __attribute__((
                                                 second ? a.out1 : a.out0, tile, a.rescue, split, ns);
 }
 
+// the coarse pair kernel with ONE candidate column tile per wave (32 candidates, half a block's): for launches
+// whose two KDEs' H32C_CT-tile blocks fit one round of the chip's block slots (config #2: 2 x 196 blocks), twice
+// the waves, each walking its chunks with half the matrix work -- more waves per SIMD to hide the ring refills
+template <int NSC, int KP>
+__global__ __launch_bounds__(64 * H32C_WAVES) __attribute__((amdgpu_waves_per_eu(H32C_EU))) void kde_logpdf_h32_pair1_kernel(
+    const double* __restrict__ cand, int64_t Nc, int32_t D, KdePairArgs a) {
+#if HBX_PAIR_INIT
+  if (a.init.U && blockIdx.x == 0 && threadIdx.x == 0)
+    acq_init_state(a.init.U, a.init.count, a.init.flags, a.init.first1, a.init.res);
+#endif
+  const bool second = blockIdx.x >= a.nblk0;
+  const unsigned loc = second ? blockIdx.x - a.nblk0 : blockIdx.x;
+  const int ns = second ? a.nsplit1 : a.nsplit0;
+  const unsigned tile = ns > 1 ? loc % a.tiles : loc;
+  const int split = ns > 1 ? (int)(loc / a.tiles) : 0;
+  kde_logpdf_h32_body<NSC, KP, false, false, true, 1>(cand, Nc, D, second ? a.P1 : a.P0, second ? a.table1 : a.table0,
+                                                       second ? a.out1 : a.out0, tile, a.rescue, split, ns);
+}
+
 // signed sums (the parity product and its accumulators): one 8-wave block per CU, so 2 waves per SIMD
 // and a 256-register budget
 template <int NSC, int KP, bool FAST>
@@ -609,4 +628,24 @@ logpdf_fn hbx_pick_h32(int nsc, int kp, bool sg, bool fast, bool coarse) {
 
 logpdf_pair_fn hbx_pick_h32_pair(int nsc, int kp, bool sg, bool fast, bool coarse) {
   return sg ? pick32<true, true>(nsc, kp, fast, false) : pick32<false, true>(nsc, kp, fast, coarse);
+}
+
+template <int NSC>
+static logpdf_pair_fn pick32_pair1_kp(int kp) {
+  switch (kp) {
+    case 0: if constexpr (h32_ok(NSC, 0, false)) return kde_logpdf_h32_pair1_kernel<NSC, 0>; break;
+    case 1: if constexpr (h32_ok(NSC, 1, false)) return kde_logpdf_h32_pair1_kernel<NSC, 1>; break;
+    case 2: if constexpr (h32_ok(NSC, 2, false)) return kde_logpdf_h32_pair1_kernel<NSC, 2>; break;
+  }
+  return nullptr;
+}
+
+logpdf_pair_fn hbx_pick_h32_pair1(int nsc, int kp) {
+  switch (nsc) {
+    case 1: return pick32_pair1_kp<1>(kp);
+    case 2: return pick32_pair1_kp<2>(kp);
+    case 3: return pick32_pair1_kp<3>(kp);
+    case 4: return pick32_pair1_kp<4>(kp);
+  }
+  return nullptr;
 }

@@ -1099,3 +1099,28 @@ def test_dd_scalar_staged_random_shapes(device, case, monkeypatch):
         fin = np.isfinite(lref)
         err = np.abs(a[sel][fin] - lref[fin]) / np.maximum(1.0, np.abs(lref[fin]))
         assert err.size == 0 or err.max() <= 1e-5, ((dc, du, lv, n), err.max())
+
+
+@pytest.mark.parametrize("nc,dc,du,n", [(100000, 8, 0, 1000), (20000, 24, 8, 3000), (700, 16, 0, 500),
+                                        (64, 24, 8, 10000), (131072, 8, 0, 1000)])
+def test_one_tile_pair_kernel_same_records(device, nc, dc, du, n, monkeypatch):
+    """Launches whose two KDEs' blocks fit one round of the chip's slots take the coarse pair kernel with one
+    candidate column tile per wave (kde_logpdf_h32_pair1_kernel); HBX_PAIR1=0 keeps the two-tile kernel.  Same
+    record either way (index, score, shortlist, near, flags) -- the winner the C oracle's."""
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    from hpbandster_amd import synthetic as S
+    X = S.make_observations(n, dc, du, 4)
+    vt = S.var_type_string(dc, du)
+    pair = kde.fit_pair(X, S.make_losses(n), vt, dc + du + 1, device=device)
+    C = S.make_candidates(nc, dc, du, 4, seed=9)
+    recs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("HBX_PAIR1", v)
+        r = pair.acquire(C)
+        recs.append((r.index, r.score, r.shortlist, r.near, r.flags, r.pdf_l, r.pdf_g))
+    assert recs[0] == recs[1]
+    if nc <= 20000:
+        l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+        assert recs[0][0] == O.select(l, g)[0]
