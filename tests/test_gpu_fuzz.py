@@ -357,3 +357,62 @@ def test_empty_and_single_inputs(device):
         pair.acquire(np.zeros((4, 7)))
     assert promote.promote_segments(np.zeros(0), np.zeros(1, np.int64), np.zeros(0), device=device).size == 0
     assert promote.promote_segments(np.zeros(0), np.zeros(4, np.int64), np.ones(3), device=device).size == 0
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_batched_bracket_refits(device, seed):
+    """Config #5's batched refit over ragged brackets (hbx_seg_argsort_ex in numpy's order, then hbx_kde_fit):
+    bracket sizes 1-1500 with tied, quantised and crashed losses, per-bracket split sizes (0 = skipped) --
+    every bracket's order, bandwidths and level counts equal to the oracle's (bohb.py:220-246)."""
+    import torch
+    from oracle import np_argsort as NA
+    from hpbandster_amd import _native as N
+    from hpbandster_amd import kde
+    rs = np.random.RandomState(300 + seed)
+    B = int(rs.choice([1, 7, 60]))
+    dc, du = int(rs.choice([1, 4, 24])), int(rs.choice([0, 2, 8]))
+    D = dc + du
+    lens = rs.randint(1, int(rs.choice([40, 400, 1500])) + 1, size=B)
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    Ntot = int(seg[-1])
+    losses = rs.rand(Ntot)
+    q = int(rs.choice([0, 5, 100]))
+    if q:
+        losses = np.round(losses * q) / q
+    losses[rs.rand(Ntot) < 0.05] = np.inf
+    X = np.hstack([rs.rand(Ntot, dc), rs.randint(0, 5, (Ntot, du)).astype(np.float64)])
+    sizes = [kde.bohb_split_sizes(int(m), D + 1) for m in lens]
+    skip = np.array([min(a, m) <= D or min(b, m) <= D for (a, b), m in zip(sizes, lens)])
+    ng = np.array([0 if s else min(a, m) for (a, b), m, s in zip(sizes, lens, skip)], dtype=np.int64)
+    nb = np.array([0 if s else min(b, m) for (a, b), m, s in zip(sizes, lens, skip)], dtype=np.int64)
+    fg = np.array([kde.bandwidth_factor(int(v), D) if v else 0.0 for v in ng])
+    fb = np.array([kde.bandwidth_factor(int(v), D) if v else 0.0 for v in nb])
+    L = N.lib()
+    ld, segd, Xd, ngd, nbd, fgd, fbd = (torch.from_numpy(np.ascontiguousarray(a)).to(device)
+                                        for a in (losses, seg, X, ng, nb, fg, fb))
+    order = torch.empty(Ntot, dtype=torch.int64, device=device)
+    sb = int(L.hbx_sort_scratch_bytes(Ntot))
+    scr = torch.empty(sb, dtype=torch.uint8, device=device)
+    N.call("hbx_seg_argsort_ex", N.ptr(ld), N.ptr(segd), B, int(lens.max()), Ntot, N.ptr(order), N.ptr(scr), sb,
+           N.ORDER_NUMPY, N.stream_handle())
+    vt = torch.tensor([0] * dc + [1] * du, dtype=torch.int32, device=device)
+    outs = [torch.zeros((B, D), dtype=torch.float64, device=device) for _ in range(2)] + \
+           [torch.zeros((B, D), dtype=torch.int32, device=device) for _ in range(2)]
+    N.call("hbx_kde_fit", N.ptr(Xd), D, N.ptr(segd), B, N.ptr(order), N.ptr(ngd), N.ptr(nbd), N.ptr(fgd),
+           N.ptr(fbd), N.ptr(vt), *[N.ptr(o) for o in outs], N.stream_handle())
+    bwg, bwb, nlg, nlb = (o.cpu().numpy() for o in outs)
+    o = order.cpu().numpy()
+    vts = "c" * dc + "u" * du
+    for b in range(B):
+        s, e = seg[b], seg[b + 1]
+        rows = NA.argsort(losses[s:e])
+        np.testing.assert_array_equal(o[s:e], rows, err_msg="bracket %d" % b)
+        if skip[b]:
+            continue
+        Xb = X[s:e]
+        good, bad = Xb[rows[:ng[b]]], Xb[rows[-nb[b]:]]
+        with np.errstate(all="ignore"):
+            np.testing.assert_array_equal(bwg[b], O.normal_reference_bw(good), err_msg="bracket %d" % b)
+            np.testing.assert_array_equal(bwb[b], O.normal_reference_bw(bad), err_msg="bracket %d" % b)
+        np.testing.assert_array_equal(nlg[b], O.num_levels(good, vts))
+        np.testing.assert_array_equal(nlb[b], O.num_levels(bad, vts))
