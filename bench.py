@@ -925,7 +925,9 @@ def config2_line(device, reps=50):
             "scoring_launch_ms": lm, "step_minus_scoring_ms": el * 1e3 - lm,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": tf / PEAK_F16_MFMA_TFLOPS, "flops_per_pair": fpp,
-                         "kernel": "kde_logpdf_h32_pair_kernel<1,0,false,true> (l and g in one launch)",
+                         "kernel": ("kde_logpdf_h32_pair1_kernel<1,0> (l and g in one launch, one candidate column "
+                                    "tile per wave)" if os.environ.get("HBX_PAIR1", "1") != "0" else
+                                    "kde_logpdf_h32_pair_kernel<1,0,false,true> (l and g in one launch)"),
                          "timing": "median of 20 launches' start/end events"}}
 
 

@@ -1,5 +1,5 @@
 """The secondary kernels' workloads alone (GPU box), for rocprofv3 kernel traces and PMC passes
-(tools/profile_side.sh): config #2's acquisition (kde_logpdf_h32_pair_kernel<1,0,false,true>), the ln-pdf
+(tools/profile_side.sh): config #2's acquisition (kde_logpdf_h32_pair1_kernel<1,0>), the ln-pdf
 contract at config #3 (kde_logpdf_dd_kernel<24,8,2>), the GPU sampler (kde_sample_pair_kernel), config #5's
 refit of every bracket (seg_argsort_wave_kernel + kde_fit_wave_kernel) and its promotion (sh_select_kernel).
 Each workload is bench.py's own side line with fewer repetitions; the JSON lines it prints are that line.

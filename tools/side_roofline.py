@@ -34,8 +34,11 @@ NC3, NG3, NB3 = 1_000_000, 1500, 8500          # config #3
 B5, N5, D5 = 10_000, 1000, 32                  # config #5
 NG5, NB5 = 150, 850                            # bohb_split_sizes(1000, 33)
 BASES = [
+    ("kde_logpdf_h32_pair1_kernel<1, 0>",
+     "config #2: 28 flops/pair (SURVEY 8d, 3 Dc + 4) x 1e5 x 1e3 pairs (one column tile per wave)", "mfma",
+     28.0 * NC2 * NOBS2),
     ("kde_logpdf_h32_pair_kernel<1, 0, false, true>",
-     "config #2: 28 flops/pair (SURVEY 8d, 3 Dc + 4) x 1e5 x 1e3 pairs", "mfma", 28.0 * NC2 * NOBS2),
+     "config #2 with HBX_PAIR1=0: 28 flops/pair x 1e5 x 1e3 pairs", "mfma", 28.0 * NC2 * NOBS2),
     ("kde_logpdf_h32_pair_kernel<3, 1, false, true>",
      "config #3 headline: 92 flops/pair x 1e6 x 1e4 pairs", "mfma", 92.0 * NC3 * (NG3 + NB3)),
     ("kde_logpdf_dd_kernel<24, 8, 2",
