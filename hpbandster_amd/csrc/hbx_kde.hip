@@ -539,10 +539,13 @@ __device__ __forceinline__ void kde_table_body(const double* __restrict__ x, con
     for (int k = (16 * nd32 + 32 * h32_kp(P->kc) + 2 * h32_ixw(h32_kp(P->kc))) & ~7; k < KTP; k += 8)
       *(h8*)(hrow + k) = z8;
   if (P->kc == 0) {
-    for (int u = 0; u < dup; ++u) {
-      const float v = (ok && u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
-      if (slot) ch[KP * KROW + jj * dup + u] = v;
-    }
+    // the f32 layout's code block only: a matrix-core layout with kc == 0 has no active categorical dim (hm_ok),
+    // and du_pad > 0 there means single-level dims alone -- writing their codes would overwrite row data
+    if (hm == 0)
+      for (int u = 0; u < dup; ++u) {
+        const float v = (ok && u < du) ? (float)x[P->cat_dim[u]] : -2.0f;
+        if (slot) ch[KP * KROW + jj * dup + u] = v;
+      }
   } else if (slot && hm == 2) {
     // 2:4-compressed one-hot (h32 layout, hbx_kde_impl.h): per step s and group g (positions t0 = 32s + 4g
     // .. t0 + 3) the f16 hi / lo of delta_u for the observation's level in the pair (t0, t0+1) and in

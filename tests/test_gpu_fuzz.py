@@ -22,8 +22,10 @@ from oracle import kde_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# HBX_FUZZ_SEEDS=N widens every seeded test here to N cases (a long search run on a GPU box); default 120
-SEEDS = list(range(int(os.environ.get("HBX_FUZZ_SEEDS", "120"))))
+# HBX_FUZZ_SEEDS=N widens every seeded test here to N cases (a long search run on a GPU box; HBX_FUZZ_SEED0 shifts
+# the range); default 120 from 0
+_S0 = int(os.environ.get("HBX_FUZZ_SEED0", "0"))
+SEEDS = list(range(_S0, _S0 + int(os.environ.get("HBX_FUZZ_SEEDS", "120"))))
 
 
 def _case(seed):
@@ -439,3 +441,29 @@ def test_random_batched_bracket_refits(device, seed):
             np.testing.assert_array_equal(bwb[b], O.normal_reference_bw(bad), err_msg="bracket %d" % b)
         np.testing.assert_array_equal(nlg[b], O.num_levels(good, vts))
         np.testing.assert_array_equal(nlb[b], O.num_levels(bad, vts))
+
+
+@pytest.mark.parametrize("seed,top", [(2687, 10), (2687, 15)])
+def test_single_level_dim_matrix_core_table(device, seed, top):
+    """Regression (found by the 1500-seed search): a KDE whose only categorical dim has a single observed level
+    (du_pad 4, no active categorical dim) prepared for the f16 matrix-core kernel -- the table build wrote the f32
+    layout's code block into the matrix-core rows, so some candidates' estimates left their bounds and the pick
+    missed the oracle's.  Every estimate within its bound, the pick the oracle's."""
+    import torch
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    X, losses, vt, C, mp = _case(seed)
+    pair = kde.fit_pair(X, losses, vt, mp, top_n_percent=top, device=device)
+    assert pair.good.du_pad > 0 and (pair.good.variant >> 4) & 1  # the matrix-core path with the padded dims
+    cd = torch.from_numpy(C).to(device)
+    for k in (pair.good, pair.bad):
+        lp, ln, er = k.logpdf_est(cd)
+        ref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        fin = np.isfinite(ref)
+        with np.errstate(all="ignore"):
+            est = np.where(ln > -np.inf, lp + np.log1p(-np.exp(ln - lp)), lp)
+        assert np.all(np.abs(est[fin] - ref[fin]) <= 2.0 * er[fin] * np.maximum(1.0, np.abs(ref[fin])) + 1e-6)
+    with np.errstate(all="ignore"):
+        l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    assert pair.acquire(C).index == _pick(l, g)
