@@ -467,3 +467,36 @@ def test_single_level_dim_matrix_core_table(device, seed, top):
         l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
         g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
     assert pair.acquire(C).index == _pick(l, g)
+
+
+@pytest.mark.parametrize("dc", [8, 16, 24, 32, 40])
+@pytest.mark.parametrize("nconst", [1, 2])
+def test_single_level_dims_every_bucket(device, dc, nconst):
+    """The same shape at every continuous bucket (the 32x32 and 16x16 matrix-core tables and their coarse
+    tables): dc continuous dims and nconst categorical dims with one observed level; candidates at that level
+    (the others' pdf is NaN).  Estimates within their bounds, the pick the oracle's."""
+    import torch
+    from oracle import c_oracle
+    from hpbandster_amd import kde
+    rs = np.random.RandomState(dc * 10 + nconst)
+    n, nc = 700, 3000
+    X = np.hstack([rs.rand(n, dc), np.full((n, nconst), 2.0)])
+    C = np.hstack([rs.rand(nc, dc), np.full((nc, nconst), 2.0)])
+    C[: nc // 5, :dc] = X[rs.randint(0, n, nc // 5), :dc] + 0.01 * rs.randn(nc // 5, dc)
+    vt = "c" * dc + "u" * nconst
+    pair = kde.fit_pair(X, rs.rand(n), vt, dc + nconst + 1, device=device)
+    cd = torch.from_numpy(C).to(device)
+    for k in (pair.good, pair.bad):
+        lp, ln, er = k.logpdf_est(cd)
+        ref = O.log_pdf_many(k.data, k.bw, vt, C, k.nlev)
+        fin = np.isfinite(ref)
+        assert fin.all()
+        with np.errstate(all="ignore"):
+            est = np.where(ln > -np.inf, lp + np.log1p(-np.exp(ln - lp)), lp)
+        ok = np.abs(est - ref) <= 2.0 * er * np.maximum(1.0, np.abs(ref)) + 1e-6
+        ok |= er < 0  # rescue markers: re-scored later
+        assert ok.all(), (dc, nconst, np.nonzero(~ok)[0][:8])
+    with np.errstate(all="ignore"):
+        l = c_oracle.kde_pdf(pair.good.data, pair.good.bw, vt, pair.good.nlev, C, exact=True)
+        g = c_oracle.kde_pdf(pair.bad.data, pair.bad.bw, vt, pair.bad.nlev, C, exact=True)
+    assert pair.acquire(C).index == _pick(l, g)
