@@ -28,15 +28,24 @@ _S0 = int(os.environ.get("HBX_FUZZ_SEED0", "0"))
 SEEDS = list(range(_S0, _S0 + int(os.environ.get("HBX_FUZZ_SEEDS", "120"))))
 
 
+# HBX_FUZZ_WIDE=1 (search runs): wider shapes -- up to 90 continuous dims (past the 64-slot bucket: the exact-only
+# path), up to 40 categorical dims of up to 24 levels (one-hot widths past the matrix-core limit)
+_WIDE = os.environ.get("HBX_FUZZ_WIDE", "0") not in ("", "0")
+
+
 def _case(seed):
     rs = np.random.RandomState(1000 + seed)
-    dc = int(rs.choice([0, 1, 2, 3, 5, 8, 13, 24, 32, 40]))
-    du = int(rs.choice([0, 0, 1, 2, 3, 6, 8])) if dc < 40 else int(rs.randint(0, 7))
+    if _WIDE:
+        dc = int(rs.choice([0, 4, 16, 33, 48, 64, 65, 90]))
+        du = int(rs.choice([0, 1, 5, 12, 33, 40]))
+    else:
+        dc = int(rs.choice([0, 1, 2, 3, 5, 8, 13, 24, 32, 40]))
+        du = int(rs.choice([0, 0, 1, 2, 3, 6, 8])) if dc < 40 else int(rs.randint(0, 7))
     if dc + du == 0:
         dc = 1
     D = dc + du
     n = int(rs.randint(D + 2, max(D + 3, 2000)))
-    levels = rs.randint(2, 7, size=du)
+    levels = rs.randint(2, 25 if _WIDE else 7, size=du)
     X = np.empty((n, D))
     X[:, :dc] = rs.rand(n, dc)
     for d in range(dc):
